@@ -1,0 +1,75 @@
+"""Loader for the in-tree native extension ``pytorch_distributed_rnn_amd._C``.
+
+Policy (so that GPU runs never silently fall back to eager PyTorch):
+
+* On a machine with a visible GPU the HIP kernels ARE the compute path.  If the
+  extension cannot be imported there, :func:`native` raises with the import
+  error, unless ``PDRNN_ALLOW_FALLBACK=1`` is set explicitly.
+* On a CPU-only machine (this container, CI) the torch reference path is used
+  and :func:`native` returns ``None``.
+* ``PDRNN_KERNELS=torch`` forces the reference path everywhere (testing aid,
+  mirrors the ``--kernel torch`` CLI flag).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+from typing import Optional
+
+import torch
+
+_C = None
+_IMPORT_ERROR: Optional[BaseException] = None
+_TRIED = False
+
+
+def _try_import():
+    global _C, _IMPORT_ERROR, _TRIED
+    if _TRIED:
+        return _C
+    _TRIED = True
+    try:
+        _C = importlib.import_module("pytorch_distributed_rnn_amd._C")
+    except BaseException as e:  # noqa: BLE001 - report any loader failure verbatim
+        _IMPORT_ERROR = e
+        _C = None
+    return _C
+
+
+def kernels_mode() -> str:
+    return os.environ.get("PDRNN_KERNELS", "hip").lower()
+
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available()
+
+
+def extension():
+    """Return the imported extension module (or None) regardless of device."""
+    return _try_import()
+
+
+def native(device: Optional[torch.device] = None):
+    """The native module if HIP kernels should run for ``device``; else None."""
+    if kernels_mode() == "torch":
+        return None
+    if device is not None and torch.device(device).type != "cuda":
+        return None
+    if not gpu_available():
+        return None
+    mod = _try_import()
+    if mod is None and os.environ.get("PDRNN_ALLOW_FALLBACK", "0") != "1":
+        raise RuntimeError(
+            "pytorch_distributed_rnn_amd: GPU present but the native extension failed to load "
+            f"({_IMPORT_ERROR!r}). Build it with `python -m pytorch_distributed_rnn_amd._build` "
+            "or set PDRNN_ALLOW_FALLBACK=1 to run the (slow) torch reference path."
+        )
+    return mod
+
+
+def require():
+    """Import the extension or raise (used by build checks and GPU tests)."""
+    mod = _try_import()
+    if mod is None:
+        raise RuntimeError(f"native extension not importable: {_IMPORT_ERROR!r}")
+    return mod

@@ -1,0 +1,333 @@
+// torch <-> native bindings for pytorch_distributed_rnn_amd._C
+//
+// Thin host glue: validates tensors, allocates outputs/workspaces through the
+// torch caching allocator, fills the POD argument structs of pdrnn/api.h and
+// launches on torch's current HIP stream.  All math lives in csrc/kernels.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "pdrnn/api.h"
+#include "pdrnn/runtime.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+#define CHECK_HIP_TENSOR(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define HIP_LAUNCH_CHECK(expr)                                                               \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    TORCH_CHECK(_e == hipSuccess, "HIP launch failed: ", hipGetErrorString(_e), " @ " #expr); \
+  } while (0)
+
+const float* opt_ptr(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+// Parameter layout of one fused LSTM stack, in nn.LSTM parameter order:
+// per layer weight_ih, weight_hh, bias_ih, bias_hh (biases optional).
+struct StackLayout {
+  int64_t P = 0;
+  int64_t off_wih[PDRNN_MAX_LAYERS], off_whh[PDRNN_MAX_LAYERS];
+  int64_t off_bih[PDRNN_MAX_LAYERS], off_bhh[PDRNN_MAX_LAYERS];
+};
+
+StackLayout stack_layout(const std::vector<Tensor>& w, int64_t NL, bool has_bias) {
+  StackLayout L;
+  int64_t off = 0;
+  for (int64_t l = 0; l < NL; ++l) {
+    L.off_wih[l] = off; off += w[l * 4 + 0].numel();
+    L.off_whh[l] = off; off += w[l * 4 + 1].numel();
+    if (has_bias) {
+      L.off_bih[l] = off; off += w[l * 4 + 2].numel();
+      L.off_bhh[l] = off; off += w[l * 4 + 3].numel();
+    } else {
+      L.off_bih[l] = L.off_bhh[l] = -1;
+    }
+  }
+  L.P = off;
+  return L;
+}
+
+void check_stack(const std::vector<Tensor>& w, int64_t NL, int64_t H, int64_t I, bool& has_bias) {
+  TORCH_CHECK((int64_t)w.size() == 4 * NL, "expected 4 tensors per layer (w_ih, w_hh, b_ih, b_hh)");
+  TORCH_CHECK(NL >= 1 && NL <= PDRNN_MAX_LAYERS, "1..4 layers supported by the fused small-H LSTM");
+  TORCH_CHECK(pdrnn_lstm_small_supported((int)H, (int)I, (int)NL), "fused small-H LSTM: unsupported (H=", H,
+              ", I=", I, ", layers=", NL, ")");
+  has_bias = w[2].defined();
+  for (int64_t l = 0; l < NL; ++l) {
+    const int64_t Iin = l == 0 ? I : H;
+    const Tensor& wih = w[l * 4 + 0];
+    const Tensor& whh = w[l * 4 + 1];
+    CHECK_HIP_TENSOR(wih); CHECK_F32(wih); CHECK_F32(whh);
+    TORCH_CHECK(wih.is_contiguous() && whh.is_contiguous(), "LSTM weights must be contiguous");
+    TORCH_CHECK(wih.size(0) == 4 * H && wih.size(1) == Iin, "weight_ih_l", l, " shape mismatch");
+    TORCH_CHECK(whh.size(0) == 4 * H && whh.size(1) == H, "weight_hh_l", l, " shape mismatch");
+    if (has_bias) {
+      TORCH_CHECK(w[l * 4 + 2].defined() && w[l * 4 + 3].defined(), "bias presence must be uniform");
+      TORCH_CHECK(w[l * 4 + 2].is_contiguous() && w[l * 4 + 3].is_contiguous());
+    }
+  }
+}
+
+// Returns {out_or_hseq, hn, cn, act}.  x: [B,T,I] (batch_first) or [T,B,I];
+// with idx, x is a [N,T,I] source table and B = len(idx).
+std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx, const std::vector<Tensor>& w,
+                                   const optional<Tensor>& h0, const optional<Tensor>& c0, int64_t H, int64_t NL,
+                                   bool batch_first, bool save, bool need_out, int64_t nb) {
+  CHECK_HIP_TENSOR(x); CHECK_F32(x);
+  TORCH_CHECK(x.dim() == 3, "x must be 3-D");
+  TORCH_CHECK(x.stride(2) == 1, "x innermost dim must be contiguous");
+  const c10::DeviceGuard guard(x.device());
+  const int64_t I = x.size(2);
+  bool has_bias = false;
+  check_stack(w, NL, H, I, has_bias);
+  int64_t B, T, x_sb, x_st;
+  if (idx.has_value() && idx->defined()) {
+    TORCH_CHECK(batch_first, "gathered input requires batch_first");
+    TORCH_CHECK(idx->scalar_type() == at::kLong && idx->is_contiguous());
+    B = idx->size(0); T = x.size(1); x_sb = x.stride(0); x_st = x.stride(1);
+  } else if (batch_first) {
+    B = x.size(0); T = x.size(1); x_sb = x.stride(0); x_st = x.stride(1);
+  } else {
+    T = x.size(0); B = x.size(1); x_sb = x.stride(1); x_st = x.stride(0);
+  }
+  auto opts = x.options();
+  Tensor hn = at::empty({NL, B, H}, opts), cn = at::empty({NL, B, H}, opts);
+  Tensor hseq, act, out;
+  PdrnnLstmSmallFwdArgs a{};
+  a.x = x.data_ptr<float>();
+  a.idx = (idx.has_value() && idx->defined()) ? idx->data_ptr<int64_t>() : nullptr;
+  a.x_sb = x_sb; a.x_st = x_st;
+  for (int64_t l = 0; l < NL; ++l) {
+    a.w_ih[l] = w[l * 4 + 0].data_ptr<float>();
+    a.w_hh[l] = w[l * 4 + 1].data_ptr<float>();
+    a.b_ih[l] = has_bias ? w[l * 4 + 2].data_ptr<float>() : nullptr;
+    a.b_hh[l] = has_bias ? w[l * 4 + 3].data_ptr<float>() : nullptr;
+  }
+  if (h0.has_value() && h0->defined()) TORCH_CHECK(h0->is_contiguous() && h0->numel() == NL * B * H, "h0 shape");
+  if (c0.has_value() && c0->defined()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == NL * B * H, "c0 shape");
+  a.h0 = opt_ptr(h0); a.c0 = opt_ptr(c0);
+  if (save) {
+    hseq = at::empty({NL, B, T, H}, opts);
+    act = at::empty({NL, B, T, 5, H}, opts);
+    a.hseq = hseq.data_ptr<float>();
+    a.act = act.data_ptr<float>();
+    out = hseq;
+  } else if (need_out) {
+    out = batch_first ? at::empty({B, T, H}, opts) : at::empty({T, B, H}, opts);
+    a.out = out.data_ptr<float>();
+    a.o_sb = batch_first ? T * H : H;
+    a.o_st = batch_first ? H : B * H;
+  }
+  a.hn = hn.data_ptr<float>(); a.cn = cn.data_ptr<float>();
+  a.B = (int)B; a.T = (int)T; a.I = (int)I; a.NL = (int)NL;
+  if (B > 0 && T > 0) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&a, (int)H, (int)nb, save ? 1 : 0, cur_stream()));
+  return {out, hn, cn, act};
+}
+
+// Returns {dparams_flat[P] (nn.LSTM parameter order), dx, dh0, dc0}.
+std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx, const std::vector<Tensor>& w,
+                                   const optional<Tensor>& h0, const optional<Tensor>& c0, const Tensor& hseq,
+                                   const Tensor& act, const optional<Tensor>& dout, const optional<Tensor>& dhn,
+                                   const optional<Tensor>& dcn, int64_t H, int64_t NL, bool batch_first,
+                                   bool need_dx, bool need_dh0, int64_t nb, const optional<Tensor>& grad_accum) {
+  CHECK_HIP_TENSOR(x);
+  const c10::DeviceGuard guard(x.device());
+  const int64_t I = x.size(2);
+  bool has_bias = false;
+  check_stack(w, NL, H, I, has_bias);
+  const bool gathered = idx.has_value() && idx->defined();
+  int64_t B, T, x_sb, x_st;
+  if (gathered) {
+    B = idx->size(0); T = x.size(1); x_sb = x.stride(0); x_st = x.stride(1);
+  } else if (batch_first) {
+    B = x.size(0); T = x.size(1); x_sb = x.stride(0); x_st = x.stride(1);
+  } else {
+    T = x.size(0); B = x.size(1); x_sb = x.stride(1); x_st = x.stride(0);
+  }
+  TORCH_CHECK(hseq.is_contiguous() && act.is_contiguous());
+  StackLayout L = stack_layout(w, NL, has_bias);
+  auto opts = x.options();
+  const int grid = pdrnn_lstm_small_grid((int)H, (int)B, (int)nb);
+  Tensor slab = at::empty({std::max(grid, 1), L.P}, opts);
+  Tensor dx, dh0, dc0;
+  PdrnnLstmSmallBwdArgs a{};
+  a.x = x.data_ptr<float>();
+  a.idx = gathered ? idx->data_ptr<int64_t>() : nullptr;
+  a.x_sb = x_sb; a.x_st = x_st;
+  for (int64_t l = 0; l < NL; ++l) {
+    a.w_ih[l] = w[l * 4 + 0].data_ptr<float>();
+    a.w_hh[l] = w[l * 4 + 1].data_ptr<float>();
+    a.off_wih[l] = L.off_wih[l]; a.off_whh[l] = L.off_whh[l];
+    a.off_bih[l] = L.off_bih[l]; a.off_bhh[l] = L.off_bhh[l];
+  }
+  a.h0 = opt_ptr(h0); a.c0 = opt_ptr(c0);
+  a.hseq = hseq.data_ptr<float>(); a.act = act.data_ptr<float>();
+  if (dout.has_value() && dout->defined()) {
+    CHECK_F32(*dout);
+    TORCH_CHECK(dout->stride(2) == 1, "dout innermost dim must be contiguous");
+    a.dout = dout->data_ptr<float>();
+    if (batch_first || gathered) { a.d_sb = dout->stride(0); a.d_st = dout->stride(1); }
+    else { a.d_sb = dout->stride(1); a.d_st = dout->stride(0); }
+  }
+  if (dhn.has_value() && dhn->defined()) TORCH_CHECK(dhn->is_contiguous(), "dhn must be contiguous");
+  if (dcn.has_value() && dcn->defined()) TORCH_CHECK(dcn->is_contiguous(), "dcn must be contiguous");
+  a.dhn = opt_ptr(dhn); a.dcn = opt_ptr(dcn);
+  if (need_dx) {
+    TORCH_CHECK(!gathered, "input gradient of a gathered batch is not supported");
+    dx = at::zeros_like(x);
+    a.dx = dx.data_ptr<float>();
+    a.dx_sb = batch_first ? dx.stride(0) : dx.stride(1);
+    a.dx_st = batch_first ? dx.stride(1) : dx.stride(0);
+  }
+  if (need_dh0) {
+    dh0 = at::empty({NL, B, H}, opts);
+    dc0 = at::empty({NL, B, H}, opts);
+    a.dh0 = dh0.data_ptr<float>(); a.dc0 = dc0.data_ptr<float>();
+  }
+  a.slab = slab.data_ptr<float>();
+  a.P = L.P;
+  a.B = (int)B; a.T = (int)T; a.I = (int)I; a.NL = (int)NL;
+  Tensor dparams;
+  float beta = 0.f;
+  if (grad_accum.has_value() && grad_accum->defined()) {
+    TORCH_CHECK(grad_accum->numel() == L.P && grad_accum->is_contiguous(), "grad_accum must be flat [P]");
+    dparams = *grad_accum;
+    beta = 1.f;
+  } else {
+    dparams = at::empty({L.P}, opts);
+  }
+  if (B > 0 && T > 0) {
+    HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&a, (int)H, (int)nb, cur_stream()));
+    const int split = std::min<int>(64, std::max<int>(1, grid / 16));
+    Tensor work = at::empty({split, L.P}, opts);
+    HIP_LAUNCH_CHECK(pdrnn_slab_reduce(slab.data_ptr<float>(), grid, L.P, dparams.data_ptr<float>(), beta,
+                                       work.data_ptr<float>(), split, cur_stream()));
+  } else if (beta == 0.f) {
+    dparams.zero_();
+  }
+  return {dparams, dx, dh0, dc0};
+}
+
+std::vector<Tensor> xent_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore_index, bool need_grad) {
+  CHECK_HIP_TENSOR(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, C] with contiguous rows");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == logits.size(0));
+  const c10::DeviceGuard guard(logits.device());
+  const int64_t N = logits.size(0), C = logits.size(1);
+  auto f32 = logits.options().dtype(at::kFloat);
+  PdrnnXentArgs a{};
+  a.logits = logits.data_ptr();
+  a.ld = logits.stride(0);
+  switch (logits.scalar_type()) {
+    case at::kFloat: a.dtype = 0; break;
+    case at::kBFloat16: a.dtype = 1; break;
+    case at::kHalf: a.dtype = 2; break;
+    default: TORCH_CHECK(false, "xent: unsupported logits dtype");
+  }
+  a.labels = labels.data_ptr<int64_t>();
+  a.N = N; a.C = C; a.ignore_index = ignore_index;
+  Tensor dlogits;
+  if (need_grad) { dlogits = at::empty({N, C}, f32); a.dlogits = dlogits.data_ptr<float>(); }
+  const int nblocks = std::max(1, pdrnn_xent_partial_blocks(N, C));
+  Tensor partial = at::empty({nblocks, 3}, f32);
+  Tensor stats = at::empty({3}, f32);
+  a.partial = partial.data_ptr<float>();
+  a.out = stats.data_ptr<float>();
+  HIP_LAUNCH_CHECK(pdrnn_xent_fwd(&a, cur_stream()));
+  return {stats, dlogits};
+}
+
+Tensor xent_bwd(const Tensor& dlogits, const Tensor& grad_out, const Tensor& stats) {
+  CHECK_HIP_TENSOR(dlogits);
+  const c10::DeviceGuard guard(dlogits.device());
+  Tensor g = grad_out.to(at::kFloat).contiguous();
+  Tensor out = at::empty_like(dlogits);
+  HIP_LAUNCH_CHECK(pdrnn_xent_bwd(dlogits.data_ptr<float>(), g.data_ptr<float>(), stats.data_ptr<float>(),
+                                  out.data_ptr<float>(), dlogits.numel(), cur_stream()));
+  return out;
+}
+
+void adam_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_sq,
+               const optional<Tensor>& max_exp_avg_sq, double lr, double beta1, double beta2, double eps,
+               double weight_decay, double step, double grad_scale, bool decoupled, bool maximize,
+               const optional<Tensor>& lr_t, const optional<Tensor>& step_t) {
+  CHECK_HIP_TENSOR(param);
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&param, &grad, &exp_avg, &exp_avg_sq}) {
+    CHECK_F32(*t);
+    TORCH_CHECK(t->is_contiguous() && t->numel() == param.numel(), "adam_flat: flat contiguous buffers expected");
+  }
+  const c10::DeviceGuard guard(param.device());
+  PdrnnAdamArgs a{};
+  a.param = param.data_ptr<float>();
+  a.grad = grad.data_ptr<float>();
+  a.exp_avg = exp_avg.data_ptr<float>();
+  a.exp_avg_sq = exp_avg_sq.data_ptr<float>();
+  a.max_exp_avg_sq = (max_exp_avg_sq.has_value() && max_exp_avg_sq->defined()) ? max_exp_avg_sq->data_ptr<float>() : nullptr;
+  a.n = param.numel();
+  a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay;
+  a.bias_correction1 = (float)(1.0 - std::pow(beta1, step));
+  a.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(beta2, step));
+  a.grad_scale = (float)grad_scale;
+  a.decoupled = decoupled ? 1 : 0;
+  a.maximize = maximize ? 1 : 0;
+  a.lr_ptr = opt_ptr(lr_t);
+  a.step_ptr = opt_ptr(step_t);
+  HIP_LAUNCH_CHECK(pdrnn_adam_flat(&a, cur_stream()));
+}
+
+Tensor embedding_fwd(const Tensor& weight, const Tensor& idx) {
+  CHECK_HIP_TENSOR(weight); CHECK_F32(weight);
+  TORCH_CHECK(weight.is_contiguous() && weight.dim() == 2);
+  TORCH_CHECK(idx.scalar_type() == at::kLong);
+  const c10::DeviceGuard guard(weight.device());
+  Tensor flat = idx.contiguous().view({-1});
+  std::vector<int64_t> shape(idx.sizes().begin(), idx.sizes().end());
+  shape.push_back(weight.size(1));
+  Tensor out = at::empty(shape, weight.options());
+  HIP_LAUNCH_CHECK(pdrnn_embedding_fwd(weight.data_ptr<float>(), flat.data_ptr<int64_t>(), out.data_ptr<float>(),
+                                       flat.numel(), weight.size(1), weight.size(0), cur_stream()));
+  return out;
+}
+
+Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddings, int64_t padding_idx) {
+  CHECK_HIP_TENSOR(dout);
+  const c10::DeviceGuard guard(dout.device());
+  const int64_t dim = dout.size(-1);
+  Tensor g = dout.to(at::kFloat).contiguous().view({-1, dim});
+  Tensor flat = idx.contiguous().view({-1});
+  flat = at::where(flat < 0, flat + num_embeddings, flat);
+  auto sorted = at::sort(flat, /*stable=*/true, /*dim=*/0, /*descending=*/false);
+  Tensor vals = std::get<0>(sorted), perm = std::get<1>(sorted).contiguous();
+  Tensor bounds = at::arange(num_embeddings + 1, flat.options());
+  Tensor offsets = at::searchsorted(vals, bounds).contiguous();
+  Tensor dw = at::empty({num_embeddings, dim}, dout.options().dtype(at::kFloat));
+  HIP_LAUNCH_CHECK(pdrnn_embedding_bwd_csr(g.data_ptr<float>(), perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(),
+                                           dw.data_ptr<float>(), num_embeddings, dim, padding_idx, cur_stream()));
+  return dw;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "pytorch_distributed_rnn_amd native runtime (gfx950 HIP kernels + RCCL runtime)";
+  m.def("lstm_small_fwd", &lstm_small_fwd, "fused small-H LSTM stack forward");
+  m.def("lstm_small_bwd", &lstm_small_bwd, "fused small-H LSTM stack BPTT backward");
+  m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
+    return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
+  });
+  m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
+  m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
+  m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer");
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.attr("offload_arch") = "gfx950";
+  pdrnn::register_runtime(m);
+}

@@ -1,0 +1,132 @@
+// C ABI between the hipcc-compiled kernels (csrc/kernels/*.hip) and the
+// g++-compiled host runtime / torch bindings (csrc/bindings.cpp).
+//
+// Every launcher takes plain pointers plus a hipStream_t and returns the HIP
+// error of the launch.  Argument structs are POD so that both compilers agree
+// on their layout.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDRNN_MAX_LAYERS 4
+
+// ----------------------------------------------------------------------------
+// Fused small-hidden LSTM stack (H <= 64, input size <= H): every layer of the
+// stack runs inside ONE launch, layer l working on timestep t-l while layer 0
+// works on t (wavefront pipeline); one workgroup owns NB sequences for all T.
+// ----------------------------------------------------------------------------
+typedef struct {
+  const float* x;            // input, element (b,t,i) at b*x_sb + t*x_st + i
+  const int64_t* idx;        // optional gather: batch row b reads x sequence idx[b]
+  int64_t x_sb, x_st;
+  const float* w_ih[PDRNN_MAX_LAYERS];  // [4H, I_l]   gate order i,f,g,o
+  const float* w_hh[PDRNN_MAX_LAYERS];  // [4H, H]
+  const float* b_ih[PDRNN_MAX_LAYERS];  // [4H] or NULL
+  const float* b_hh[PDRNN_MAX_LAYERS];  // [4H] or NULL
+  const float* h0;           // [NL, B, H] or NULL (zeros)
+  const float* c0;           // [NL, B, H] or NULL
+  float* hseq;               // training: [NL, B, T, H] every layer's h_t
+  float* act;                // training: [NL, B, T, 5, H] post-activation i,f,g,o and c_t
+  float* out;                // inference: top-layer output (may be NULL), (b,t,j) at b*o_sb+t*o_st+j
+  int64_t o_sb, o_st;
+  float* hn;                 // [NL, B, H]
+  float* cn;                 // [NL, B, H]
+  int B, T, I, NL;
+} PdrnnLstmSmallFwdArgs;
+
+typedef struct {
+  const float* x;
+  const int64_t* idx;
+  int64_t x_sb, x_st;
+  const float* w_ih[PDRNN_MAX_LAYERS];
+  const float* w_hh[PDRNN_MAX_LAYERS];
+  const float* h0;
+  const float* c0;
+  const float* hseq;         // saved by the forward
+  const float* act;          // saved by the forward
+  const float* dout;         // grad of top-layer output, (b,t,j) at b*d_sb+t*d_st+j; NULL = 0
+  int64_t d_sb, d_st;
+  const float* dhn;          // [NL,B,H] or NULL
+  const float* dcn;          // [NL,B,H] or NULL
+  float* dx;                 // (b,t,i) at b*dx_sb+t*dx_st+i, or NULL (input grad not needed)
+  int64_t dx_sb, dx_st;
+  float* dh0;                // [NL,B,H] or NULL
+  float* dc0;                // [NL,B,H] or NULL
+  float* slab;               // [grid, P] per-workgroup partial parameter gradients
+  int64_t P;
+  int64_t off_wih[PDRNN_MAX_LAYERS], off_whh[PDRNN_MAX_LAYERS];
+  int64_t off_bih[PDRNN_MAX_LAYERS], off_bhh[PDRNN_MAX_LAYERS];  // -1 = no bias
+  int B, T, I, NL;
+} PdrnnLstmSmallBwdArgs;
+
+// Query the launch geometry chosen for (H, B): returns grid size (number of slab rows).
+int pdrnn_lstm_small_grid(int H, int B, int nb);
+int pdrnn_lstm_small_supported(int H, int I, int NL);
+hipError_t pdrnn_lstm_small_fwd(const PdrnnLstmSmallFwdArgs* a, int H, int nb, int save,
+                                hipStream_t stream);
+hipError_t pdrnn_lstm_small_bwd(const PdrnnLstmSmallBwdArgs* a, int H, int nb, hipStream_t stream);
+
+// Column sums of a [rows, P] fp32 slab into out[P] (out = beta*out + sum).
+// Two deterministic passes through `work` ([split, P] floats, split <= 64).
+hipError_t pdrnn_slab_reduce(const float* slab, int64_t rows, int64_t P, float* out, float beta,
+                             float* work, int split, hipStream_t stream);
+
+// ----------------------------------------------------------------------------
+// Fused cross-entropy (+ accuracy): mean loss over valid rows, dlogits saved.
+// ----------------------------------------------------------------------------
+typedef struct {
+  const void* logits;        // [N, C] fp32/bf16/fp16 (row stride ld)
+  int64_t ld;
+  int dtype;                 // 0 fp32, 1 bf16, 2 fp16
+  const int64_t* labels;     // [N]
+  int64_t N, C;
+  int64_t ignore_index;
+  float* row_loss;           // [N] scratch
+  float* dlogits;            // [N, C] fp32 (softmax - onehot) / n_valid, or NULL
+  float* partial;            // [nblocks, 3]  (loss sum, n_valid, n_correct)
+  float* out;                // [3] loss mean, n_valid, n_correct
+} PdrnnXentArgs;
+hipError_t pdrnn_xent_fwd(const PdrnnXentArgs* a, hipStream_t stream);
+int pdrnn_xent_partial_blocks(int64_t N, int64_t C);
+// dst = dlogits * (grad_out[0] / stats[1])   (stats = PdrnnXentArgs.out)
+hipError_t pdrnn_xent_bwd(const float* dlogits, const float* grad_out, const float* stats, float* dst,
+                          int64_t n, hipStream_t stream);
+
+// ----------------------------------------------------------------------------
+// Fused Adam / AdamW over flat fp32 buffers (torch.optim.Adam semantics).
+// ----------------------------------------------------------------------------
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* max_exp_avg_sq;     // amsgrad only, else NULL
+  int64_t n;
+  float lr, beta1, beta2, eps, weight_decay;
+  float bias_correction1, bias_correction2_sqrt;
+  float grad_scale;          // multiply grads (e.g. 1/world for a sum all-reduce)
+  int decoupled;             // AdamW
+  int maximize;
+  const float* lr_ptr;       // optional device lr (graph-capturable); overrides lr
+  const float* step_ptr;     // optional device step count for bias correction (capturable)
+} PdrnnAdamArgs;
+hipError_t pdrnn_adam_flat(const PdrnnAdamArgs* a, hipStream_t stream);
+
+// ----------------------------------------------------------------------------
+// Embedding gather / deterministic CSR backward (perm = stable argsort of idx,
+// offsets[v] = first position of vocabulary row v in the sorted order).
+// ----------------------------------------------------------------------------
+hipError_t pdrnn_embedding_fwd(const float* weight, const int64_t* idx, float* out, int64_t n_idx,
+                               int64_t dim, int64_t num_embeddings, hipStream_t stream);
+hipError_t pdrnn_embedding_bwd_csr(const float* dout, const int64_t* perm, const int64_t* offsets,
+                                   float* dweight, int64_t num_embeddings, int64_t dim,
+                                   int64_t padding_idx, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif

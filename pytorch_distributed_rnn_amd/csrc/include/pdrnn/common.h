@@ -1,0 +1,88 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of pytorch_distributed_rnn_amd.
+//
+// Everything here is written for wave64 CDNA4: cross-lane reductions use DPP
+// quad permutes (no LDS round trip), transcendental helpers map to the hardware
+// v_exp_f32 / v_rcp_f32 instructions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PDRNN_HOST_DEVICE __host__ __device__
+#define PDRNN_DEVICE __device__ __forceinline__
+
+namespace pdrnn {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------
+// Cross-lane helpers (DPP, wave64).  quad_perm control words:
+//   [1,0,3,2] = 0xB1  (swap neighbours)      [2,3,0,1] = 0x4E (swap pairs)
+// ---------------------------------------------------------------------------
+PDRNN_DEVICE float dpp_swap1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+PDRNN_DEVICE float dpp_swap2(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+// row_half_mirror (lane i of an 8-lane half-row reads lane 7-i) and row_mirror
+// (lane i of a 16-lane row reads lane 15-i): after the quad sums these pair
+// each quad with the other quad of the 8-group / each 8-group with the other
+// half of the row, which completes the 8- and 16-lane butterflies.
+PDRNN_DEVICE float dpp_half_mirror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+}
+PDRNN_DEVICE float dpp_mirror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+}
+
+// Sum over groups of S adjacent lanes (S in {1,2,4,8,16}); every lane of the
+// group receives the group total.
+template <int S>
+PDRNN_DEVICE float group_sum(float v) {
+  if constexpr (S >= 2) v += dpp_swap1(v);
+  if constexpr (S >= 4) v += dpp_swap2(v);
+  if constexpr (S >= 8) v += dpp_half_mirror(v);
+  if constexpr (S >= 16) v += dpp_mirror(v);
+  return v;
+}
+
+PDRNN_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+PDRNN_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Activations (fp32).  sigmoid via v_exp_f32 + v_rcp_f32; tanh from exp(-2|x|)
+// so that small arguments keep their relative accuracy.
+// ---------------------------------------------------------------------------
+PDRNN_DEVICE float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+PDRNN_DEVICE float sigmoidf_fast(float x) { return fast_rcp(1.f + __expf(-x)); }
+PDRNN_DEVICE float tanhf_fast(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  const float t = (1.f - e) * fast_rcp(1.f + e);
+  return copysignf(t, x);
+}
+
+// bf16 <-> f32 (round to nearest even; NaN preserved by the hardware cvt).
+PDRNN_DEVICE float bf16_to_f32(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
+PDRNN_DEVICE uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+}  // namespace pdrnn
+
+#define PDRNN_HIP_CHECK(expr)                                                   \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) return _e;                                            \
+  } while (0)

@@ -1,0 +1,98 @@
+// Fused Adam / AdamW step over ONE flat fp32 parameter buffer.
+//
+// Replaces torch 1.4's per-parameter Python loop of ATen ops that the
+// reference runs every step (reference: src/motion/trainer/base.py:43,117;
+// SURVEY.md §2b N5).  Models built by this framework keep all parameters,
+// gradients and optimizer moments in contiguous flat buffers, so the whole
+// optimizer step is a single streaming launch (16 B per lane, grid-stride).
+// The update follows torch.optim.Adam's single-tensor formula term by term
+// (lerp for exp_avg, addcmul for exp_avg_sq, sqrt(v)/sqrt(bc2)+eps,
+// addcdiv by lr/bc1).  `grad_scale` folds the 1/world average of a sum
+// all-reduce into the read of the gradient.
+#include "pdrnn/api.h"
+#include "pdrnn/common.h"
+
+namespace pdrnn {
+namespace {
+
+struct AdamScalars {
+  float lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale;
+  int decoupled, maximize, amsgrad;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float* vmax,
+                                          const AdamScalars& s) {
+  g *= s.gscale;
+  if (s.maximize) g = -g;
+  if (s.wd != 0.f) {
+    if (s.decoupled) p *= 1.f - s.lr * s.wd;
+    else g = fmaf(s.wd, p, g);
+  }
+  // exp_avg.lerp_(grad, 1 - beta1)   (weight < 0.5 branch of torch's lerp)
+  m = m + (1.f - s.b1) * (g - m);
+  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1-beta2)
+  v = v * s.b2 + (1.f - s.b2) * (g * g);
+  float vv = v;
+  if (s.amsgrad) { *vmax = fmaxf(*vmax, v); vv = *vmax; }
+  const float denom = sqrtf(vv) / s.bc2_sqrt + s.eps;
+  const float step_size = s.lr / s.bc1;
+  p = p - step_size * (m / denom);
+}
+
+__global__ void __launch_bounds__(256) adam_flat_kernel(PdrnnAdamArgs a) {
+  AdamScalars s;
+  s.lr = a.lr_ptr ? *a.lr_ptr : a.lr;
+  s.b1 = a.beta1; s.b2 = a.beta2; s.eps = a.eps; s.wd = a.weight_decay;
+  if (a.step_ptr) {
+    const float st = *a.step_ptr;
+    s.bc1 = 1.f - powf(a.beta1, st);
+    s.bc2_sqrt = sqrtf(1.f - powf(a.beta2, st));
+  } else {
+    s.bc1 = a.bias_correction1;
+    s.bc2_sqrt = a.bias_correction2_sqrt;
+  }
+  s.gscale = a.grad_scale; s.decoupled = a.decoupled; s.maximize = a.maximize;
+  s.amsgrad = a.max_exp_avg_sq != nullptr;
+
+  const int64_t n = a.n;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(a.param) | reinterpret_cast<uintptr_t>(a.grad) |
+                         reinterpret_cast<uintptr_t>(a.exp_avg) | reinterpret_cast<uintptr_t>(a.exp_avg_sq)) & 15) == 0 &&
+                       !s.amsgrad;
+  int64_t done = 0;
+  if (aligned) {
+    const int64_t n4 = n / 4;
+    float4* P = reinterpret_cast<float4*>(a.param);
+    const float4* Gr = reinterpret_cast<const float4*>(a.grad);
+    float4* M = reinterpret_cast<float4*>(a.exp_avg);
+    float4* V = reinterpret_cast<float4*>(a.exp_avg_sq);
+    for (int64_t i = tid; i < n4; i += stride) {
+      float4 p = P[i], m = M[i], v = V[i];
+      const float4 g = Gr[i];
+      adam_elem(p.x, g.x, m.x, v.x, nullptr, s);
+      adam_elem(p.y, g.y, m.y, v.y, nullptr, s);
+      adam_elem(p.z, g.z, m.z, v.z, nullptr, s);
+      adam_elem(p.w, g.w, m.w, v.w, nullptr, s);
+      P[i] = p; M[i] = m; V[i] = v;
+    }
+    done = n4 * 4;
+  }
+  for (int64_t i = done + tid; i < n; i += stride) {
+    float p = a.param[i], m = a.exp_avg[i], v = a.exp_avg_sq[i];
+    adam_elem(p, a.grad[i], m, v, s.amsgrad ? a.max_exp_avg_sq + i : nullptr, s);
+    a.param[i] = p; a.exp_avg[i] = m; a.exp_avg_sq[i] = v;
+  }
+}
+
+}  // namespace
+}  // namespace pdrnn
+
+extern "C" hipError_t pdrnn_adam_flat(const PdrnnAdamArgs* a, hipStream_t stream) {
+  if (a->n <= 0) return hipSuccess;
+  int64_t blocks = (a->n / 4 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pdrnn::adam_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, *a);
+  return hipGetLastError();
+}

@@ -1,0 +1,85 @@
+// Embedding lookup (gather) and deterministic backward (CSR segmented sum).
+//
+// New capability required by BASELINE config 4 (char-LM); the reference has no
+// embedding (SURVEY.md §0 discrepancies table).  Forward: one wave per output
+// row, 16 B per lane.  Backward: instead of float atomics (order-dependent
+// rounding, ~1.3 TB/s chip-wide cap) the indices are stably sorted once on
+// the host side of the op and each vocabulary row sums its contribution rows
+// in a fixed order -> bitwise reproducible gradients, plain coalesced loads.
+#include "pdrnn/api.h"
+#include "pdrnn/common.h"
+
+namespace pdrnn {
+namespace {
+
+__global__ void __launch_bounds__(256) emb_fwd_kernel(const float* __restrict__ w, const int64_t* __restrict__ idx,
+                                                      float* __restrict__ out, int64_t n, int64_t dim,
+                                                      int64_t V) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const bool vec = (dim % 4) == 0;
+  for (int64_t r = wave; r < n; r += nwaves) {
+    int64_t v = idx[r];
+    if (v < 0) v += V;
+    const float* src = w + v * dim;
+    float* dst = out + r * dim;
+    if (vec) {
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(dst);
+      for (int64_t c = lane; c < dim / 4; c += 64) d4[c] = s4[c];
+    } else {
+      for (int64_t c = lane; c < dim; c += 64) dst[c] = src[c];
+    }
+  }
+}
+
+// dweight[v] = sum over j in [off[v], off[v+1]) of dout[perm[j]]; padding row -> 0.
+__global__ void __launch_bounds__(256) emb_bwd_csr_kernel(const float* __restrict__ dout,
+                                                          const int64_t* __restrict__ perm,
+                                                          const int64_t* __restrict__ off,
+                                                          float* __restrict__ dw, int64_t V, int64_t dim,
+                                                          int64_t padding_idx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t v = wave; v < V; v += nwaves) {
+    const int64_t j0 = off[v], j1 = off[v + 1];
+    float* dst = dw + v * dim;
+    for (int64_t c = lane; c < dim; c += 64) {
+      float acc = 0.f;
+      if (v != padding_idx)
+        for (int64_t j = j0; j < j1; ++j) acc += dout[perm[j] * dim + c];
+      dst[c] = acc;
+    }
+  }
+}
+
+int blocks_for(int64_t rows) {
+  int64_t b = (rows + 3) / 4;  // 4 waves per block, one row per wave
+  if (b < 1) b = 1;
+  if (b > 8192) b = 8192;
+  return (int)b;
+}
+
+}  // namespace
+}  // namespace pdrnn
+
+extern "C" {
+
+hipError_t pdrnn_embedding_fwd(const float* weight, const int64_t* idx, float* out, int64_t n_idx, int64_t dim,
+                               int64_t num_embeddings, hipStream_t stream) {
+  if (n_idx <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pdrnn::emb_fwd_kernel, dim3(pdrnn::blocks_for(n_idx)), dim3(256), 0, stream, weight, idx, out,
+                     n_idx, dim, num_embeddings);
+  return hipGetLastError();
+}
+
+hipError_t pdrnn_embedding_bwd_csr(const float* dout, const int64_t* perm, const int64_t* offsets, float* dweight,
+                                   int64_t num_embeddings, int64_t dim, int64_t padding_idx, hipStream_t stream) {
+  hipLaunchKernelGGL(pdrnn::emb_bwd_csr_kernel, dim3(pdrnn::blocks_for(num_embeddings)), dim3(256), 0, stream, dout,
+                     perm, offsets, dweight, num_embeddings, dim, padding_idx);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,322 @@
+// Gradient synchronisation engines + pybind registration of the runtime.
+//
+// GradReducer   -- replaces the C++ DDP Reducer of torch 1.4 that the reference
+//                  gets from DistributedDataParallel (reference:
+//                  src/motion/trainer/ddp.py:19).
+//   * parameters are packed, in REVERSE registration order (the order BPTT
+//     produces their gradients), into flat per-dtype buckets capped at
+//     `bucket_cap_bytes`; every param.grad is a view into its bucket, so the
+//     autograd engine / fused backward kernels accumulate straight into the
+//     communication buffer (no pack copy),
+//   * a bucket is launched as ONE all-reduce as soon as all of its params are
+//     ready, strictly in bucket order (identical collective order on every
+//     rank), on the communicator's own stream -> it overlaps the backward
+//     kernels of the layers below,
+//   * finalize() (queued at the end of backward) launches the stragglers and
+//     makes the compute stream wait; averaging is done on the wire (ncclAvg)
+//     or by one scale per bucket.
+// FusionReducer -- replaces Horovod's tensor-fusion all-reduce that the
+//                  reference uses through hvd.DistributedOptimizer (reference:
+//                  src/motion/trainer/horovod.py:33-35):
+//   per-tensor readiness from optimizer-side hooks, ready tensors are copied
+//   (in canonical order) into a fusion buffer of `fusion_bytes`, one all-reduce
+//   per full buffer, results copied back at synchronize().
+#include <algorithm>
+#include <map>
+
+#include "pdrnn/runtime.h"
+
+namespace pdrnn {
+namespace py = pybind11;
+
+class GradReducer {
+ public:
+  GradReducer(std::vector<at::Tensor> params, std::shared_ptr<Comm> comm, int64_t bucket_cap_bytes,
+              int64_t first_bucket_cap_bytes, bool average)
+      : params_(std::move(params)), comm_(std::move(comm)), average_(average) {
+    const int64_t n = (int64_t)params_.size();
+    loc_.resize(n);
+    // Reverse order bucketing, split on dtype/device change or cap.
+    std::vector<int64_t> cur;
+    int64_t cur_bytes = 0;
+    at::ScalarType cur_dtype = at::kFloat;
+    c10::Device cur_dev = at::kCPU;
+    auto close = [&]() {
+      if (cur.empty()) return;
+      buckets_idx_.push_back(cur);
+      cur.clear();
+      cur_bytes = 0;
+    };
+    for (int64_t i = n - 1; i >= 0; --i) {
+      const auto& p = params_[i];
+      const int64_t cap = buckets_idx_.empty() ? first_bucket_cap_bytes : bucket_cap_bytes;
+      const int64_t bytes = p.numel() * p.element_size();
+      if (!cur.empty() && (p.scalar_type() != cur_dtype || p.device() != cur_dev || cur_bytes + bytes > cap)) close();
+      if (cur.empty()) { cur_dtype = p.scalar_type(); cur_dev = p.device(); }
+      cur.push_back(i);
+      cur_bytes += bytes;
+    }
+    close();
+    for (size_t b = 0; b < buckets_idx_.size(); ++b) {
+      int64_t total = 0;
+      for (int64_t i : buckets_idx_[b]) total += params_[i].numel();
+      auto flat = at::zeros({total}, params_[buckets_idx_[b][0]].options().requires_grad(false));
+      int64_t off = 0;
+      for (int64_t i : buckets_idx_[b]) {
+        loc_[i] = {(int64_t)b, off};
+        off += params_[i].numel();
+      }
+      buckets_.push_back(flat);
+    }
+    views_.resize(n);
+    for (int64_t i = 0; i < n; ++i) {
+      const auto& p = params_[i];
+      views_[i] = buckets_[loc_[i].first].narrow(0, loc_[i].second, p.numel()).view(p.sizes());
+    }
+    pending_.resize(buckets_.size());
+    ready_.assign(n, 0);
+    reset();
+  }
+
+  const std::vector<at::Tensor>& grad_views() const { return views_; }
+  const std::vector<at::Tensor>& buckets() const { return buckets_; }
+  const std::vector<std::vector<int64_t>>& bucket_indices() const { return buckets_idx_; }
+
+  void reset() {
+    for (size_t b = 0; b < buckets_.size(); ++b) pending_[b] = (int64_t)buckets_idx_[b].size();
+    std::fill(ready_.begin(), ready_.end(), 0);
+    next_ = 0;
+    launched_ = 0;
+  }
+
+  // Returns true when the caller must re-point param.grad to grad_views()[i]
+  // (the autograd engine produced a fresh tensor, which was copied in).
+  bool mark_ready(int64_t i, const at::Tensor& grad) {
+    TORCH_CHECK(i >= 0 && i < (int64_t)params_.size(), "bad parameter index");
+    bool repoint = false;
+    if (grad.defined() && grad.data_ptr() != views_[i].data_ptr()) {
+      views_[i].copy_(grad);
+      repoint = true;
+    }
+    if (ready_[i]) return repoint;  // grad accumulated twice in one backward (shared weight)
+    ready_[i] = 1;
+    const int64_t b = loc_[i].first;
+    if (--pending_[b] == 0) launch_ready();
+    return repoint;
+  }
+
+  void finalize() {
+    // Params that received no gradient this iteration contribute zeros.
+    for (size_t b = 0; b < buckets_.size(); ++b) {
+      for (int64_t i : buckets_idx_[b]) {
+        if (!ready_[i]) {
+          ready_[i] = 1;
+          --pending_[b];
+        }
+      }
+    }
+    launch_ready();
+    comm_->wait();
+    if (average_ && !comm_->native_avg() && comm_->world() > 1) {
+      for (auto& f : buckets_) f.div_((double)comm_->world());
+    }
+    reset();
+  }
+
+  void zero_() {
+    for (auto& f : buckets_) f.zero_();
+  }
+
+  // Synchronous all-reduce of every bucket (used by no-hook fallbacks / tests).
+  void all_reduce_now() {
+    for (size_t b = 0; b < buckets_.size(); ++b) comm_->all_reduce(buckets_[b], op());
+    comm_->wait();
+    if (average_ && !comm_->native_avg() && comm_->world() > 1)
+      for (auto& f : buckets_) f.div_((double)comm_->world());
+  }
+
+  int64_t launched() const { return launched_; }
+
+ private:
+  RedOp op() const { return (average_ && comm_->native_avg()) ? RedOp::kAvg : RedOp::kSum; }
+  void launch_ready() {
+    while (next_ < (int64_t)buckets_.size() && pending_[next_] == 0) {
+      comm_->all_reduce(buckets_[next_], op());
+      ++next_;
+      ++launched_;
+    }
+  }
+
+  std::vector<at::Tensor> params_;
+  std::shared_ptr<Comm> comm_;
+  bool average_;
+  std::vector<std::vector<int64_t>> buckets_idx_;
+  std::vector<at::Tensor> buckets_;
+  std::vector<at::Tensor> views_;
+  std::vector<std::pair<int64_t, int64_t>> loc_;
+  std::vector<int64_t> pending_;
+  std::vector<char> ready_;
+  int64_t next_ = 0;
+  int64_t launched_ = 0;
+};
+
+class FusionReducer {
+ public:
+  FusionReducer(std::shared_ptr<Comm> comm, int64_t fusion_bytes, bool average)
+      : comm_(std::move(comm)), fusion_bytes_(std::max<int64_t>(fusion_bytes, 1024)), average_(average) {}
+
+  // Register a tensor slot in canonical order; returns its handle.
+  int64_t register_tensor(const std::string& name, const at::Tensor& like) {
+    names_.push_back(name);
+    entries_.push_back({at::Tensor(), false});
+    (void)like;
+    return (int64_t)names_.size() - 1;
+  }
+
+  // A gradient is ready: remember it; pack every ready tensor at the head of
+  // the canonical order into the fusion buffer, all-reducing full buffers.
+  void enqueue(int64_t h, const at::Tensor& grad) {
+    TORCH_CHECK(h >= 0 && h < (int64_t)entries_.size(), "bad handle");
+    entries_[h] = {grad, true};
+    advance(false);
+  }
+
+  // Flush everything (missing tensors are skipped consistently: a rank only
+  // skips what every rank skips when the model is identical), wait, unpack.
+  void synchronize() {
+    advance(true);
+    flush();
+    comm_->wait();
+    for (auto& f : inflight_) unpack(f);
+    inflight_.clear();
+    for (auto& e : entries_) e = {at::Tensor(), false};
+    cursor_ = 0;
+  }
+
+  int64_t collectives() const { return collectives_; }
+  int64_t num_registered() const { return (int64_t)names_.size(); }
+
+ private:
+  struct Fused {
+    at::Tensor buf;
+    std::vector<std::pair<at::Tensor, int64_t>> members;  // (grad, offset)
+  };
+  RedOp op() const { return (average_ && comm_->native_avg()) ? RedOp::kAvg : RedOp::kSum; }
+
+  void advance(bool final_pass) {
+    while (cursor_ < (int64_t)entries_.size()) {
+      auto& e = entries_[cursor_];
+      if (!e.second) {
+        if (!final_pass) return;
+        ++cursor_;
+        continue;
+      }
+      const at::Tensor& g = e.first;
+      const int64_t bytes = g.numel() * g.element_size();
+      if (!cur_.members.empty() &&
+          (cur_used_ * cur_esize_ + bytes > fusion_bytes_ || g.scalar_type() != cur_dtype_ || g.device() != cur_dev_))
+        flush();
+      if (cur_.members.empty()) {
+        cur_dtype_ = g.scalar_type();
+        cur_dev_ = g.device();
+        cur_esize_ = g.element_size();
+        const int64_t cap = std::max<int64_t>(fusion_bytes_ / cur_esize_, g.numel());
+        cur_.buf = at::empty({cap}, g.options());
+        cur_used_ = 0;
+      }
+      cur_.buf.narrow(0, cur_used_, g.numel()).copy_(g.reshape({-1}));
+      cur_.members.push_back({g, cur_used_});
+      cur_used_ += g.numel();
+      ++cursor_;
+    }
+  }
+
+  void flush() {
+    if (cur_.members.empty()) return;
+    auto view = cur_.buf.narrow(0, 0, cur_used_);
+    comm_->all_reduce(view, op());
+    ++collectives_;
+    inflight_.push_back(std::move(cur_));
+    cur_ = Fused();
+    cur_used_ = 0;
+  }
+
+  void unpack(Fused& f) {
+    const bool div = average_ && !comm_->native_avg() && comm_->world() > 1;
+    for (auto& m : f.members) {
+      auto src = f.buf.narrow(0, m.second, m.first.numel()).view(m.first.sizes());
+      if (div) m.first.copy_(src / (double)comm_->world());
+      else m.first.copy_(src);
+    }
+  }
+
+  std::shared_ptr<Comm> comm_;
+  int64_t fusion_bytes_;
+  bool average_;
+  std::vector<std::string> names_;
+  std::vector<std::pair<at::Tensor, bool>> entries_;
+  int64_t cursor_ = 0;
+  Fused cur_;
+  int64_t cur_used_ = 0;
+  int64_t cur_esize_ = 4;
+  at::ScalarType cur_dtype_ = at::kFloat;
+  c10::Device cur_dev_ = at::kCPU;
+  std::vector<Fused> inflight_;
+  int64_t collectives_ = 0;
+};
+
+static RedOp parse_op(const std::string& s) {
+  if (s == "sum") return RedOp::kSum;
+  if (s == "avg" || s == "mean") return RedOp::kAvg;
+  if (s == "max") return RedOp::kMax;
+  if (s == "min") return RedOp::kMin;
+  TORCH_CHECK(false, "unknown reduce op ", s);
+}
+
+void register_runtime(py::module_& m) {
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world", &Comm::world)
+      .def_property_readonly("native_avg", &Comm::native_avg)
+      .def("all_reduce", [](Comm& c, at::Tensor t, const std::string& op) { c.all_reduce(t, parse_op(op)); },
+           py::arg("tensor"), py::arg("op") = "sum")
+      .def("broadcast", [](Comm& c, at::Tensor t, int root) { c.broadcast(t, root); })
+      .def("all_gather", [](Comm& c, at::Tensor out, const at::Tensor& in) { c.all_gather(out, in); })
+      .def("reduce_scatter", [](Comm& c, at::Tensor out, const at::Tensor& in, const std::string& op) {
+             c.reduce_scatter(out, in, parse_op(op));
+           }, py::arg("out"), py::arg("input"), py::arg("op") = "sum")
+      .def("all_to_all", [](Comm& c, at::Tensor out, const at::Tensor& in) { c.all_to_all(out, in); })
+      .def("send", &Comm::send)
+      .def("recv", [](Comm& c, at::Tensor t, int peer) { c.recv(t, peer); })
+      .def("wait", &Comm::wait)
+      .def("barrier", &Comm::barrier);
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("make_rccl_comm", [](py::bytes uid, int rank, int world, int device, bool high_priority) {
+    return make_rccl_comm(std::string(uid), rank, world, device, high_priority);
+  }, py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("high_priority") = true);
+  m.def("make_pg_comm", &make_pg_comm, py::arg("process_group"));
+
+  py::class_<GradReducer, std::shared_ptr<GradReducer>>(m, "GradReducer")
+      .def(py::init<std::vector<at::Tensor>, std::shared_ptr<Comm>, int64_t, int64_t, bool>(), py::arg("params"),
+           py::arg("comm"), py::arg("bucket_cap_bytes"), py::arg("first_bucket_cap_bytes"), py::arg("average") = true)
+      .def("grad_views", &GradReducer::grad_views)
+      .def("buckets", &GradReducer::buckets)
+      .def("bucket_indices", &GradReducer::bucket_indices)
+      .def("mark_ready", &GradReducer::mark_ready)
+      .def("finalize", &GradReducer::finalize)
+      .def("reset", &GradReducer::reset)
+      .def("zero_", &GradReducer::zero_)
+      .def("all_reduce_now", &GradReducer::all_reduce_now)
+      .def_property_readonly("launched", &GradReducer::launched);
+
+  py::class_<FusionReducer, std::shared_ptr<FusionReducer>>(m, "FusionReducer")
+      .def(py::init<std::shared_ptr<Comm>, int64_t, bool>(), py::arg("comm"), py::arg("fusion_bytes"),
+           py::arg("average") = true)
+      .def("register_tensor", &FusionReducer::register_tensor)
+      .def("enqueue", &FusionReducer::enqueue)
+      .def("synchronize", &FusionReducer::synchronize)
+      .def_property_readonly("collectives", &FusionReducer::collectives)
+      .def_property_readonly("num_registered", &FusionReducer::num_registered);
+}
+
+}  // namespace pdrnn

@@ -1,0 +1,195 @@
+"""LSTM stack operator: fused HIP kernels on MI355X, torch reference elsewhere.
+
+The reference framework runs ``nn.LSTM`` (ATen CPU kernels) inside
+``MotionModel`` (reference: src/motion/model.py:9,14).  Here the whole stack
+(all layers, all timesteps, forward and BPTT) is one HIP launch each way for
+small hidden sizes (H in {16, 32, 64}, input <= H) -- see
+``csrc/kernels/lstm_small.hip`` -- and a per-timestep MFMA path for large
+hidden sizes (``ops/lstm_large.py``).
+
+Gate order and parameter layout are exactly nn.LSTM's (i, f, g, o; weight_ih_l*,
+weight_hh_l*, bias_ih_l*, bias_hh_l*), so checkpoints interoperate with stock
+PyTorch.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+from torch import Tensor
+
+from .. import _ext
+
+
+def _env_int(name: str, default: int) -> int:
+    try:
+        return int(os.environ.get(name, default))
+    except ValueError:
+        return default
+
+
+def small_launch_config(batch: int, hidden: int) -> Tuple[int, int]:
+    """(sequences per workgroup) for forward and backward.
+
+    Forward: one sequence per workgroup until the grid already over-fills the
+    chip (256 CUs x ~3 resident workgroups), then two.  Backward keeps one
+    sequence per workgroup (register-bound)."""
+    nb_fwd = _env_int("PDRNN_LSTM_NB_FWD", 0)
+    nb_bwd = _env_int("PDRNN_LSTM_NB_BWD", 0)
+    if nb_fwd not in (1, 2, 4):
+        nb_fwd = 2 if batch >= 2048 else 1
+    if nb_bwd not in (1, 2, 4):
+        nb_bwd = 1
+    return nb_fwd, nb_bwd
+
+
+def fused_small_supported(x: Tensor, hidden: int, num_layers: int, bidirectional: bool,
+                          proj_size: int = 0) -> bool:
+    if bidirectional or proj_size:
+        return False
+    if x.dtype != torch.float32 or x.dim() != 3:
+        return False
+    mod = _ext.native(x.device)
+    if mod is None:
+        return False
+    return bool(mod.lstm_small_supported(hidden, x.shape[-1], num_layers))
+
+
+class _FusedSmallLSTM(torch.autograd.Function):
+    """Autograd node for the fused small-H LSTM stack.
+
+    forward inputs: x, idx, h0, c0, config tuple, *weights (4 per layer)."""
+
+    @staticmethod
+    def forward(ctx, x, idx, h0, c0, cfg, *weights):
+        hidden, num_layers, batch_first, need_out = cfg
+        mod = _ext.native(x.device)
+        nb_fwd, nb_bwd = small_launch_config(x.shape[0] if batch_first else x.shape[1], hidden)
+        h0c = h0.contiguous() if h0 is not None else None
+        c0c = c0.contiguous() if c0 is not None else None
+        out, hn, cn, act = mod.lstm_small_fwd(
+            x, idx, list(weights), h0c, c0c, hidden, num_layers, batch_first, True, need_out, nb_fwd)
+        ctx.set_materialize_grads(False)
+        ctx.cfg = (hidden, num_layers, batch_first, nb_bwd)
+        ctx.save_for_backward(x, idx, h0c, c0c, out, act, *weights)
+        top = out[num_layers - 1]  # [B, T, H]
+        if not batch_first:
+            top = top.transpose(0, 1)
+        return top, hn, cn
+
+    @staticmethod
+    def backward(ctx, dout, dhn, dcn):
+        x, idx, h0, c0, hseq, act, *weights = ctx.saved_tensors
+        hidden, num_layers, batch_first, nb_bwd = ctx.cfg
+        mod = _ext.native(x.device)
+        need_dx = ctx.needs_input_grad[0]
+        need_dh0 = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        if dout is not None and dout.stride(-1) != 1:
+            dout = dout.contiguous()
+        dhn = dhn.contiguous() if dhn is not None else None
+        dcn = dcn.contiguous() if dcn is not None else None
+        dparams, dx, dh0, dc0 = mod.lstm_small_bwd(
+            x, idx, list(weights), h0, c0, hseq, act, dout, dhn, dcn, hidden, num_layers,
+            batch_first, need_dx, need_dh0, nb_bwd, None)
+        grads = []
+        off = 0
+        for w in weights:
+            n = w.numel()
+            grads.append(dparams[off:off + n].view_as(w))
+            off += n
+        return (dx if need_dx else None, None,
+                dh0 if ctx.needs_input_grad[2] else None,
+                dc0 if ctx.needs_input_grad[3] else None, None, *grads)
+
+
+def _flat_weights(weights: Sequence[Optional[Tensor]], num_layers: int, hidden: int,
+                  like: Tensor) -> List[Tensor]:
+    out = []
+    for l in range(num_layers):
+        w_ih, w_hh, b_ih, b_hh = weights[4 * l:4 * l + 4]
+        if b_ih is None:
+            b_ih = like.new_zeros(4 * hidden)
+        if b_hh is None:
+            b_hh = like.new_zeros(4 * hidden)
+        out += [w_ih.contiguous(), w_hh.contiguous(), b_ih.contiguous(), b_hh.contiguous()]
+    return out
+
+
+def lstm_reference(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor],
+                   c0: Optional[Tensor], hidden: int, num_layers: int, batch_first: bool,
+                   dropout: float = 0.0, training: bool = False,
+                   bidirectional: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
+    """Stock ATen LSTM (CPU / MIOpen) -- the torch reference path for tests."""
+    dirs = 2 if bidirectional else 1
+    has_bias = weights[2] is not None
+    flat = [w for w in weights if w is not None]
+    if h0 is None:
+        b = x.shape[0] if batch_first else x.shape[1]
+        h0 = x.new_zeros(num_layers * dirs, b, hidden)
+        c0 = x.new_zeros(num_layers * dirs, b, hidden)
+    out, hn, cn = torch._VF.lstm(x, (h0, c0), flat, has_bias, num_layers, dropout, training,
+                                 bidirectional, batch_first)
+    return out, hn, cn
+
+
+def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor] = None,
+                 c0: Optional[Tensor] = None, *, hidden: int, num_layers: int,
+                 batch_first: bool = False, need_out: bool = True, idx: Optional[Tensor] = None,
+                 dropout: float = 0.0, training: bool = False,
+                 bidirectional: bool = False) -> Tuple[Optional[Tensor], Tensor, Tensor]:
+    """LSTM stack forward.  Returns (out, h_n, c_n) like nn.LSTM.
+
+    ``idx`` (optional) gathers batch rows from ``x`` (a device-resident dataset)
+    inside the kernel; ``need_out=False`` lets inference skip the per-timestep
+    output stream when only h_n is consumed."""
+    if (not bidirectional and dropout == 0.0
+            and fused_small_supported(x, hidden, num_layers, bidirectional)):
+        flat = _flat_weights(weights, num_layers, hidden, x)
+        needs_grad = torch.is_grad_enabled() and (
+            x.requires_grad or any(w.requires_grad for w in flat)
+            or (h0 is not None and h0.requires_grad) or (c0 is not None and c0.requires_grad))
+        if needs_grad:
+            out, hn, cn = _FusedSmallLSTM.apply(
+                x, idx, h0, c0, (hidden, num_layers, batch_first, need_out), *flat)
+            return out, hn, cn
+        mod = _ext.native(x.device)
+        nb_fwd, _ = small_launch_config(idx.numel() if idx is not None else
+                                        (x.shape[0] if batch_first else x.shape[1]), hidden)
+        out, hn, cn, _ = mod.lstm_small_fwd(
+            x, idx, flat, h0.contiguous() if h0 is not None else None,
+            c0.contiguous() if c0 is not None else None, hidden, num_layers, batch_first, False,
+            need_out, nb_fwd)
+        return out, hn, cn
+    from . import lstm_large
+    if lstm_large.supported(x, hidden, num_layers):
+        return lstm_large.lstm_large_forward(x, weights, h0, c0, hidden=hidden,
+                                             num_layers=num_layers, batch_first=batch_first,
+                                             bidirectional=bidirectional)
+    if idx is not None:
+        x = x.index_select(0, idx)
+    return lstm_reference(x, weights, h0, c0, hidden, num_layers, batch_first, dropout, training,
+                          bidirectional)
+
+
+def lstm_bidirectional_forward(x: Tensor, all_weights: Sequence[Tensor], h0: Optional[Tensor],
+                               c0: Optional[Tensor], *, hidden: int, num_layers: int,
+                               batch_first: bool, dropout: float = 0.0,
+                               training: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
+    """Stacked bidirectional LSTM (nn.LSTM(bidirectional=True) parameter order:
+    per layer [fwd: w_ih, w_hh, b_ih, b_hh, bwd: w_ih, w_hh, b_ih, b_hh])."""
+    from . import lstm_large
+    if lstm_large.supported(x, hidden, num_layers, bidirectional=True):
+        return lstm_large.lstm_large_forward(x, all_weights, h0, c0, hidden=hidden,
+                                             num_layers=num_layers, batch_first=batch_first,
+                                             bidirectional=True)
+    has_bias = len(all_weights) == 8 * num_layers
+    ws: List[Optional[Tensor]] = []
+    per = 4 if has_bias else 2
+    for l in range(num_layers * 2):
+        chunk = list(all_weights[l * per:(l + 1) * per])
+        if not has_bias:
+            chunk += [None, None]
+        ws += chunk
+    return lstm_reference(x, ws, h0, c0, hidden, num_layers, batch_first, dropout, training,
+                          bidirectional=True)

@@ -1,0 +1,137 @@
+"""Numerics of the HIP kernels vs plain PyTorch fp64/fp32 references (GPU only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    from pytorch_distributed_rnn_amd import _ext
+    return _ext.require()
+
+
+def _make_lstm(I, H, NL, seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.LSTM(I, H, NL, batch_first=True)
+
+
+@pytest.mark.parametrize("H,NL,I", [(32, 2, 9), (32, 1, 32), (16, 3, 5), (64, 1, 40), (32, 4, 32)])
+@pytest.mark.parametrize("B,T", [(3, 7), (180, 128)])
+def test_lstm_small_fwd_bwd_matches_torch(H, NL, I, B, T):
+    from pytorch_distributed_rnn_amd.ops.lstm import lstm_forward
+    ref = _make_lstm(I, H, NL).double()
+    x = torch.randn(B, T, I, dtype=torch.float64)
+    out_ref, (hn_ref, cn_ref) = ref(x)
+    g_out = torch.randn_like(out_ref)
+    g_hn = torch.randn_like(hn_ref)
+    (out_ref * g_out).sum().add_((hn_ref * g_hn).sum()).backward()
+
+    dev = torch.device("cuda")
+    ws = [p.detach().float().to(dev).requires_grad_() for p in ref.parameters()]
+    xg = x.float().to(dev)
+    out, hn, cn = lstm_forward(xg, ws, hidden=H, num_layers=NL, batch_first=True)
+    assert torch.allclose(out.double().cpu(), out_ref, atol=2e-5, rtol=1e-4)
+    assert torch.allclose(hn.double().cpu(), hn_ref, atol=2e-5, rtol=1e-4)
+    assert torch.allclose(cn.double().cpu(), cn_ref, atol=2e-5, rtol=1e-4)
+    loss = (out * g_out.float().to(dev)).sum() + (hn * g_hn.float().to(dev)).sum()
+    loss.backward()
+    for w, p in zip(ws, ref.parameters()):
+        scale = p.grad.abs().max().item() + 1e-6
+        err = (w.grad.double().cpu() - p.grad).abs().max().item()
+        assert err / scale < 2e-4, (err, scale)
+
+
+def test_lstm_small_seq_first_and_states():
+    from pytorch_distributed_rnn_amd.ops.lstm import lstm_forward
+    H, NL, I, B, T = 32, 2, 9, 5, 11
+    ref = torch.nn.LSTM(I, H, NL).double()
+    x = torch.randn(T, B, I, dtype=torch.float64, requires_grad=True)
+    h0 = torch.randn(NL, B, H, dtype=torch.float64, requires_grad=True)
+    c0 = torch.randn(NL, B, H, dtype=torch.float64, requires_grad=True)
+    out_ref, (hn_ref, cn_ref) = ref(x, (h0, c0))
+    (out_ref.sum() + hn_ref.pow(2).sum() + cn_ref.sum()).backward()
+    dev = torch.device("cuda")
+    ws = [p.detach().float().to(dev).requires_grad_() for p in ref.parameters()]
+    xg = x.detach().float().to(dev).requires_grad_()
+    h0g = h0.detach().float().to(dev).requires_grad_()
+    c0g = c0.detach().float().to(dev).requires_grad_()
+    out, hn, cn = lstm_forward(xg, ws, h0g, c0g, hidden=H, num_layers=NL, batch_first=False)
+    assert torch.allclose(out.double().cpu(), out_ref, atol=2e-5)
+    (out.sum() + hn.pow(2).sum() + cn.sum()).backward()
+    assert torch.allclose(xg.grad.double().cpu(), x.grad, atol=1e-4)
+    assert torch.allclose(h0g.grad.double().cpu(), h0.grad, atol=1e-4)
+    assert torch.allclose(c0g.grad.double().cpu(), c0.grad, atol=1e-4)
+
+
+def test_lstm_small_gather_index():
+    from pytorch_distributed_rnn_amd.ops.lstm import lstm_forward
+    H, NL, I = 32, 2, 9
+    ref = torch.nn.LSTM(I, H, NL, batch_first=True)
+    data = torch.randn(50, 16, I)
+    idx = torch.randperm(50)[:20]
+    out_ref, (hn_ref, _) = ref(data[idx])
+    dev = torch.device("cuda")
+    ws = [p.detach().to(dev) for p in ref.parameters()]
+    with torch.no_grad():
+        out, hn, cn = lstm_forward(data.to(dev), ws, hidden=H, num_layers=NL, batch_first=True,
+                                   idx=idx.to(dev))
+    assert torch.allclose(out.cpu(), out_ref.detach(), atol=2e-5)
+    assert torch.allclose(hn.cpu(), hn_ref.detach(), atol=2e-5)
+
+
+@pytest.mark.parametrize("N,C", [(1440, 6), (37, 1000), (4096, 256)])
+def test_xent_matches_torch(N, C):
+    from pytorch_distributed_rnn_amd.ops.xent import cross_entropy_with_stats
+    logits = torch.randn(N, C, dtype=torch.float64) * 3
+    labels = torch.randint(0, C, (N,))
+    labels[::7] = -100
+    lr = logits.clone().requires_grad_()
+    ref = F.cross_entropy(lr, labels, ignore_index=-100)
+    ref.backward()
+    lg = logits.float().cuda().requires_grad_()
+    loss, stats = cross_entropy_with_stats(lg, labels.cuda(), -100)
+    loss.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5
+    valid = labels != -100
+    assert stats[1].item() == valid.sum().item()
+    assert stats[2].item() == ((logits.argmax(1) == labels) & valid).sum().item()
+    assert torch.allclose(lg.grad.double().cpu(), lr.grad, atol=1e-7)
+
+
+def test_fused_adam_matches_torch():
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    from pytorch_distributed_rnn_amd.utils.flat import FlatParameters
+    torch.manual_seed(0)
+    m_ref = torch.nn.Sequential(torch.nn.Linear(9, 32), torch.nn.Linear(32, 6))
+    m = torch.nn.Sequential(torch.nn.Linear(9, 32), torch.nn.Linear(32, 6)).cuda()
+    m.load_state_dict(m_ref.state_dict())
+    flat = FlatParameters(list(m.parameters()))
+    opt_ref = torch.optim.Adam(m_ref.parameters(), lr=2.5e-3)
+    opt = FusedAdam(m.parameters(), lr=2.5e-3)
+    for _ in range(5):
+        x = torch.randn(16, 9)
+        opt_ref.zero_grad()
+        m_ref(x).pow(2).mean().backward()
+        opt_ref.step()
+        opt.zero_grad()
+        m(x.cuda()).pow(2).mean().backward()
+        assert flat.grads_attached()
+        opt.step()
+    for p, q in zip(m.parameters(), m_ref.parameters()):
+        assert torch.allclose(p.detach().cpu(), q.detach(), atol=1e-6, rtol=1e-5)
+    sd = opt.state_dict()
+    assert set(sd["state"][0].keys()) >= {"step", "exp_avg", "exp_avg_sq"}
+
+
+def test_embedding_matches_torch():
+    C = _C()
+    V, D, N = 97, 64, 5000
+    w = torch.randn(V, D)
+    idx = torch.randint(0, V, (N,))
+    out = C.embedding_fwd(w.cuda(), idx.cuda())
+    assert torch.equal(out.cpu(), w[idx])
+    g = torch.randn(N, D)
+    dw = C.embedding_bwd(g.cuda(), idx.cuda(), V, -1)
+    ref = torch.zeros(V, D, dtype=torch.float64).index_add_(0, idx, g.double())
+    assert torch.allclose(dw.double().cpu(), ref, atol=1e-4)
