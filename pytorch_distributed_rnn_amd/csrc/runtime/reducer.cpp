@@ -31,9 +31,24 @@ namespace py = pybind11;
 
 class GradReducer {
  public:
+  // flat_grad (optional): an existing flat gradient buffer in which the
+  // params' gradients are laid out back to back in registration order (see
+  // utils/flat.py).  Buckets then are plain slices of it -- zero copies.
   GradReducer(std::vector<at::Tensor> params, std::shared_ptr<Comm> comm, int64_t bucket_cap_bytes,
-              int64_t first_bucket_cap_bytes, bool average)
+              int64_t first_bucket_cap_bytes, bool average, c10::optional<at::Tensor> flat_grad)
       : params_(std::move(params)), comm_(std::move(comm)), average_(average) {
+    const bool use_flat = flat_grad.has_value() && flat_grad->defined();
+    std::vector<int64_t> flat_off;
+    if (use_flat) {
+      int64_t off = 0;
+      for (const auto& p : params_) {
+        TORCH_CHECK(p.scalar_type() == flat_grad->scalar_type() && p.device() == flat_grad->device(),
+                    "flat_grad dtype/device must match every parameter");
+        flat_off.push_back(off);
+        off += p.numel();
+      }
+      TORCH_CHECK(off == flat_grad->numel() && flat_grad->is_contiguous(), "flat_grad size mismatch");
+    }
     const int64_t n = (int64_t)params_.size();
     loc_.resize(n);
     // Reverse order bucketing, split on dtype/device change or cap.
@@ -60,13 +75,21 @@ class GradReducer {
     for (size_t b = 0; b < buckets_idx_.size(); ++b) {
       int64_t total = 0;
       for (int64_t i : buckets_idx_[b]) total += params_[i].numel();
-      auto flat = at::zeros({total}, params_[buckets_idx_[b][0]].options().requires_grad(false));
-      int64_t off = 0;
-      for (int64_t i : buckets_idx_[b]) {
-        loc_[i] = {(int64_t)b, off};
-        off += params_[i].numel();
+      if (use_flat) {
+        // reverse-ordered bucket = descending contiguous index range
+        const int64_t lo = buckets_idx_[b].back();
+        const int64_t start = flat_off[lo];
+        buckets_.push_back(flat_grad->narrow(0, start, total));
+        for (int64_t i : buckets_idx_[b]) loc_[i] = {(int64_t)b, flat_off[i] - start};
+      } else {
+        auto flat = at::zeros({total}, params_[buckets_idx_[b][0]].options().requires_grad(false));
+        int64_t off = 0;
+        for (int64_t i : buckets_idx_[b]) {
+          loc_[i] = {(int64_t)b, off};
+          off += params_[i].numel();
+        }
+        buckets_.push_back(flat);
       }
-      buckets_.push_back(flat);
     }
     views_.resize(n);
     for (int64_t i = 0; i < n; ++i) {
@@ -297,8 +320,9 @@ void register_runtime(py::module_& m) {
   m.def("make_pg_comm", &make_pg_comm, py::arg("process_group"));
 
   py::class_<GradReducer, std::shared_ptr<GradReducer>>(m, "GradReducer")
-      .def(py::init<std::vector<at::Tensor>, std::shared_ptr<Comm>, int64_t, int64_t, bool>(), py::arg("params"),
-           py::arg("comm"), py::arg("bucket_cap_bytes"), py::arg("first_bucket_cap_bytes"), py::arg("average") = true)
+      .def(py::init<std::vector<at::Tensor>, std::shared_ptr<Comm>, int64_t, int64_t, bool, c10::optional<at::Tensor>>(),
+           py::arg("params"), py::arg("comm"), py::arg("bucket_cap_bytes"), py::arg("first_bucket_cap_bytes"),
+           py::arg("average") = true, py::arg("flat_grad") = py::none())
       .def("grad_views", &GradReducer::grad_views)
       .def("buckets", &GradReducer::buckets)
       .def("bucket_indices", &GradReducer::bucket_indices)

@@ -32,7 +32,7 @@ class FusedAdam(torch.optim.Adam):
             super().__init__(params, **kw)
             for g in self.param_groups:
                 g["decoupled_weight_decay"] = decoupled_weight_decay
-        self.grad_scale = grad_scale
+        self._pdrnn_grad_scale = grad_scale
         self._flat_state = {}
 
     # -- flat state -------------------------------------------------------
@@ -104,7 +104,7 @@ class FusedAdam(torch.optim.Adam):
             step = float(fs["step"])
             mod.adam_flat(fs["flat_p"], gflat, fs["exp_avg"], fs["exp_avg_sq"], fs["max_sq"],
                           float(group["lr"]), beta1, beta2, group["eps"], group["weight_decay"],
-                          step, self.grad_scale, bool(group.get("decoupled_weight_decay", False)),
+                          step, self._pdrnn_grad_scale, bool(group.get("decoupled_weight_decay", False)),
                           bool(group.get("maximize", False)), None, None)
         return loss
 
@@ -120,10 +120,10 @@ class FusedAdam(torch.optim.Adam):
         saved = self.param_groups
         self.param_groups = [group]
         try:
-            if self.grad_scale != 1.0:
+            if self._pdrnn_grad_scale != 1.0:
                 for p in group["params"]:
                     if p.grad is not None:
-                        p.grad.mul_(self.grad_scale)
+                        p.grad.mul_(self._pdrnn_grad_scale)
             super().step()
         finally:
             self.param_groups = saved

@@ -1,0 +1,85 @@
+"""Native communicator factory.
+
+``get_comm(group)`` returns the framework's C++ communicator for a process
+group:
+
+* GPU + RCCL group -> :class:`RcclComm` (csrc/runtime/comm.cpp): its own
+  ncclComm created from a unique id that rank 0 draws and every rank receives
+  through the already-initialised torch.distributed group (TCPStore
+  rendezvous), its own high-priority HIP stream;
+* otherwise (gloo / CPU plumbing) -> the same interface over torch.distributed.
+
+Communicators are cached per group.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import _ext
+
+_CACHE: Dict[int, object] = {}
+
+
+class _PyComm:
+    """Pure-Python fallback with the Comm interface (no native extension)."""
+
+    def __init__(self, group):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.native_avg = dist.get_backend(group) == "nccl"
+        self._works = []
+
+    def all_reduce(self, t, op="sum"):
+        o = {"sum": dist.ReduceOp.SUM, "avg": dist.ReduceOp.AVG, "max": dist.ReduceOp.MAX,
+             "min": dist.ReduceOp.MIN}[op]
+        self._works.append(dist.all_reduce(t, op=o, group=self.group, async_op=True))
+
+    def broadcast(self, t, root):
+        self._works.append(dist.broadcast(t, dist.get_global_rank(self.group, root), group=self.group,
+                                          async_op=True))
+
+    def all_gather(self, out, inp):
+        self._works.append(dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True))
+
+    def wait(self):
+        for w in self._works:
+            w.wait()
+        self._works.clear()
+
+    def barrier(self):
+        self.wait()
+        dist.barrier(group=self.group)
+
+
+def get_comm(group=None, prefer_native: bool = True):
+    if not dist.is_initialized():
+        raise RuntimeError("init_distributed() first")
+    g = group if group is not None else dist.group.WORLD
+    key = id(g)
+    if key in _CACHE:
+        return _CACHE[key]
+    backend = dist.get_backend(g)
+    mod = _ext.extension()
+    use_rccl = (prefer_native and backend == "nccl" and torch.cuda.is_available() and mod is not None
+                and os.environ.get("PDRNN_COMM", "rccl") == "rccl")
+    if use_rccl:
+        rank = dist.get_rank(g)
+        world = dist.get_world_size(g)
+        uid = [mod.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=dist.get_global_rank(g, 0), group=g)
+        comm = mod.make_rccl_comm(uid[0], rank, world, torch.cuda.current_device(), True)
+    elif mod is not None:
+        comm = mod.make_pg_comm(g)
+    else:
+        comm = _PyComm(g)
+    _CACHE[key] = comm
+    return comm
+
+
+def reset_comms() -> None:
+    _CACHE.clear()

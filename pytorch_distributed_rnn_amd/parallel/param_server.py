@@ -1,0 +1,284 @@
+"""Parameter-server training over torch RPC (TensorPipe) + distributed autograd.
+
+Capability parity with the reference PS mode (reference:
+src/motion/param_server/__init__.py:11-73, master.py:9-59, worker.py:17-112,
+util.py:11-25): rank 0 hosts the ONLY model instance (created lazily, once,
+under a lock, by the first worker's RPC); ranks 1..W-1 are trainers whose model
+is a proxy (``RemoteModel``) that runs forward AND backward on the server
+through ``rpc_sync`` inside a ``dist_autograd.context``; each trainer steps its
+own ``DistributedOptimizer(Adam)`` over the server's parameter RRefs, applying
+its gradients immediately (asynchronous, Hogwild-style -- no averaging).
+
+MI355X-native differences:
+
+* the server keeps the model (and the fused HIP LSTM kernels) on its GPU; the
+  RPC payloads stay host tensors (batch in, logits out) so the transport works
+  with any TensorPipe channel;
+* fixes of reference quirks, each behind a flag: trainers
+  shard the data over the W-1 trainers (``--ps-legacy-sharding`` restores the
+  reference's ``num_replicas=W`` sharding that never trains on shard 0);
+  trainer 1 asks the server to write the checkpoint at the end (the reference
+  never saves in PS mode); log lines go through ``logging`` at ``--log``
+  level (the reference's PS path silently drops them).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+from datetime import timedelta
+from pathlib import Path
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+PS_NAME = "parameter_server"
+RPC_TIMEOUT_S = float(os.environ.get("PDRNN_RPC_TIMEOUT", 60))
+
+_server_model = None
+_server_lock = threading.Lock()
+
+
+# --------------------------------------------------------------------------- helpers
+def call_method(method, rref, *args, **kwargs):
+    """Run ``method(rref.local_value(), ...)`` on the owner of ``rref``."""
+    return method(rref.local_value(), *args, **kwargs)
+
+
+def remote_method(method, rref, *args, **kwargs):
+    import torch.distributed.rpc as rpc
+    return rpc.rpc_sync(rref.owner(), call_method, args=[method, rref] + list(args), kwargs=kwargs)
+
+
+# --------------------------------------------------------------------------- server
+class ServerModel:
+    """The single model instance living on the parameter server."""
+
+    def __init__(self, input_dim: int, hidden_dim: int, layer_dim: int, output_dim: int,
+                 cell: str = "lstm"):
+        from ..models.motion import MotionModel
+        self.device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+            else torch.device("cpu")
+        self.model = MotionModel(input_dim, hidden_dim, layer_dim, output_dim, cell=cell).to(self.device)
+        self.lock = threading.Lock()
+        self.step_lock = threading.Lock()
+
+    def begin_step(self) -> bool:
+        """Serialise one trainer's forward/backward/step transaction.
+
+        Without it, trainer A's optimizer step rewrites parameters in place
+        while trainer B's backward still needs the values its forward saw
+        (autograd version-counter error, or silently stale gradients).  The
+        update order between trainers stays asynchronous and un-averaged."""
+        return self.step_lock.acquire(timeout=RPC_TIMEOUT_S)
+
+    def end_step(self) -> None:
+        if self.step_lock.locked():
+            self.step_lock.release()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.model(x.to(self.device)).cpu()
+
+    def get_dist_gradients(self, cid: int):
+        import torch.distributed.autograd as dist_autograd
+        grads = dist_autograd.get_gradients(cid)
+        return {i: v.detach().cpu() for i, (_, v) in enumerate(grads.items())}
+
+    def get_param_rrefs(self):
+        import torch.distributed.rpc as rpc
+        return [rpc.RRef(p) for p in self.model.parameters()]
+
+    def save(self, path: str, epoch: int, loss: float) -> str:
+        from ..train.checkpoint import save_checkpoint
+        with self.lock:
+            save_checkpoint(Path(path), epoch, self.model, None, loss)
+        return path
+
+    def state_dict(self):
+        return {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+
+
+def get_parameter_network(input_dim, hidden_dim, layer_dim, output_dim, cell="lstm"):
+    """Singleton accessor, called remotely by every trainer (first call builds)."""
+    global _server_model
+    with _server_lock:
+        if _server_model is None:
+            _server_model = ServerModel(input_dim, hidden_dim, layer_dim, output_dim, cell)
+        return _server_model
+
+
+def _rpc_options(address: str, port: str):
+    import torch.distributed.rpc as rpc
+    return rpc.TensorPipeRpcBackendOptions(init_method=f"tcp://{address}:{port}",
+                                           rpc_timeout=RPC_TIMEOUT_S)
+
+
+def run_parameter_server(rank: int, world_size: int, address: str = "127.0.0.1",
+                         port: str = "29500") -> None:
+    import torch.distributed.rpc as rpc
+    if torch.cuda.is_available():
+        torch.cuda.set_device(0)
+    logging.info("PS master initializing RPC")
+    rpc.init_rpc(name=PS_NAME, rank=rank, world_size=world_size,
+                 rpc_backend_options=_rpc_options(address, port))
+    logging.info("RPC initialized! Running parameter server...")
+    rpc.shutdown(graceful=True)  # returns when every trainer has finished
+    logging.info("RPC shutdown on parameter server.")
+
+
+# --------------------------------------------------------------------------- trainer side
+class RemoteModel(nn.Module):
+    """Trainer-side proxy: forward runs on the parameter server."""
+
+    def __init__(self, input_dim, hidden_dim, layer_dim, output_dim, cell="lstm"):
+        super().__init__()
+        import torch.distributed.rpc as rpc
+        self.param_server_rref = rpc.remote(PS_NAME, get_parameter_network,
+                                            args=(input_dim, hidden_dim, layer_dim, output_dim, cell))
+
+    def get_global_param_rrefs(self):
+        return remote_method(ServerModel.get_param_rrefs, self.param_server_rref)
+
+    def forward(self, x, idx=None):
+        if idx is not None:
+            x = x.index_select(0, idx)
+        return remote_method(ServerModel.forward, self.param_server_rref, x)
+
+
+def _make_worker_trainer_cls():
+    from ..data.loader import ShardedSampler
+    from ..train.formatter import TrainingMessageFormatter
+    from ..train.trainer import Trainer
+
+    class ParameterWorkerTrainer(Trainer):
+        def __init__(self, rank, world_size, model, training_set, batch_size, learning_rate,
+                     validation_set=None, test_set=None, checkpoint_dir=None,
+                     legacy_sharding: bool = False, hogwild: bool = False):
+            self.rank = rank
+            self.hogwild = hogwild
+            self._world = world_size
+            if legacy_sharding:
+                sampler = ShardedSampler(len(training_set), num_replicas=world_size, rank=rank)
+            else:
+                sampler = ShardedSampler(len(training_set), num_replicas=world_size - 1, rank=rank - 1)
+            eval_ok = rank == 0
+            super().__init__(model=model, training_set=training_set, batch_size=batch_size,
+                             learning_rate=learning_rate,
+                             validation_set=validation_set if eval_ok else None,
+                             test_set=test_set if eval_ok else None, checkpoint_dir=checkpoint_dir,
+                             sampler=sampler, device=torch.device("cpu"), flatten=False)
+
+        def world_size(self):
+            return self._world
+
+        def _get_formatter(self, epochs):
+            return TrainingMessageFormatter(epochs, self.rank)
+
+        def _get_optimizer(self, model, lr):
+            from torch.distributed.optim import DistributedOptimizer
+            return DistributedOptimizer(torch.optim.Adam, model.get_global_param_rrefs(), lr=lr)
+
+        def _train_step(self, formatter):
+            import torch.distributed.autograd as dist_autograd
+            self.model.train()
+            total_loss, total_correct = 0.0, 0
+            batches = len(self.train_loader)
+            rref = self.model.param_server_rref
+            for batch_idx, (data, target) in enumerate(self.train_loader):
+                if not self.hogwild:
+                    remote_method(ServerModel.begin_step, rref)
+                try:
+                    loss_v, correct = self._one_step(data, target)
+                finally:
+                    if not self.hogwild:
+                        remote_method(ServerModel.end_step, rref)
+                total_loss += loss_v
+                total_correct += correct
+                self.sequences_seen += len(data)
+                logging.info(formatter.train_progress_message(
+                    batch_idx=batch_idx, batches=batches, training_examples=len(data),
+                    correct=correct, loss=loss_v))
+            n = len(self.train_loader.dataset)
+            return total_loss / n, total_correct / n
+
+        def _one_step(self, data, target):
+            import torch.distributed.autograd as dist_autograd
+            if True:
+                with dist_autograd.context() as cid:
+                    output = self.model(data)
+                    target = target.long().reshape(-1)
+                    loss = F.cross_entropy(output, target)
+                    loss_v = loss.item()
+                    correct = int((output.argmax(dim=1) == target).sum())
+                    dist_autograd.backward(cid, [loss])
+                    grads = remote_method(ServerModel.get_dist_gradients, self.model.param_server_rref, cid)
+                    assert grads, "distributed autograd produced no gradients on the server"
+                    self.optimizer.step(cid)
+            return loss_v, correct
+
+        def _save_checkpoint(self, epoch, loss, best=False):
+            return None
+
+    return ParameterWorkerTrainer
+
+
+def run_worker(rank, world_size, epochs, batch_size, learning_rate, input_dim, hidden_dim, layer_dim,
+               output_dim, train_set, validation_set, test_set, address="127.0.0.1", port="29500",
+               legacy_sharding=False, checkpoint_dir: Optional[Path] = None, cell="lstm",
+               hogwild: bool = False):
+    import torch.distributed.rpc as rpc
+    logging.info(f"Worker rank {rank} initializing RPC")
+    rpc.init_rpc(name=f"trainer_{rank}", rank=rank, world_size=world_size,
+                 rpc_backend_options=_rpc_options(address, port))
+    logging.info(f"Worker {rank} done initializing RPC")
+    model = RemoteModel(input_dim, hidden_dim, layer_dim, output_dim, cell)
+    cls = _make_worker_trainer_cls()
+    trainer = cls(rank, world_size, model, train_set, batch_size, learning_rate, validation_set,
+                  test_set, legacy_sharding=legacy_sharding, hogwild=hogwild)
+    result = trainer.train(epochs)
+    if checkpoint_dir is not None and rank == 1:
+        path = Path(checkpoint_dir) / "best-model.pt"
+        remote_method(ServerModel.save, model.param_server_rref, str(path), epochs - 1, float("nan"))
+        logging.info(f"Worker {rank} asked the parameter server to save {path}")
+    rpc.shutdown()
+    return trainer, result
+
+
+# --------------------------------------------------------------------------- CLI
+def add_sub_command(parent_parser):
+    p = parent_parser.add_parser("parameter-server")
+    p.add_argument("--world-size", type=int, required=True,
+                   help="Total number of processes: the server plus every trainer.")
+    p.add_argument("--rank", type=int, required=True, help="Global rank; 0 is the server.")
+    p.add_argument("--master-address", type=str, default="localhost",
+                   help="Address of the server (rank 0).")
+    p.add_argument("--master-port", type=str, default="29500", help="Port of the server.")
+    p.add_argument("--ps-legacy-sharding", action="store_true",
+                   help="shard over all W ranks like the reference (shard 0 never trained)")
+    p.add_argument("--ps-hogwild", action="store_true",
+                   help="let trainers' forward/backward/step interleave on the server (reference "
+                        "behaviour; races on in-place parameter updates)")
+    p.set_defaults(func=execute)
+
+
+def execute(args):
+    logging.getLogger().setLevel(args.log)
+    os.environ["MASTER_ADDR"] = args.master_address
+    os.environ["MASTER_PORT"] = args.master_port
+    address = "127.0.0.1" if args.master_address == "localhost" else args.master_address
+    if args.rank == 0:
+        run_parameter_server(0, args.world_size, address, args.master_port)
+        return None
+    torch.set_num_threads(args.num_threads)
+    from ..cli import _load_datasets
+    from ..data.motion import MotionDataset
+    training_set, validation_set, test_set = _load_datasets(args)
+    return run_worker(args.rank, args.world_size, args.epochs, args.batch_size, args.learning_rate,
+                      training_set.num_features, args.hidden_units, args.stacked_layer,
+                      len(MotionDataset.LABELS), training_set, validation_set, test_set,
+                      address=address, port=args.master_port,
+                      legacy_sharding=args.ps_legacy_sharding,
+                      checkpoint_dir=args.checkpoint_directory if not args.no_validation else None,
+                      cell=getattr(args, "cell", "lstm"), hogwild=args.ps_hogwild)
