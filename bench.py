@@ -1,0 +1,158 @@
+#!/usr/bin/env python
+"""Flagship benchmark: motion-RNN data-parallel training throughput on MI355X.
+
+Measures the reference's headline metric (BASELINE.json): whole-node
+sequences/second of the motion LSTM (2 layers x 32 hidden, 9 inputs x 128
+timesteps, 6 classes, Adam lr 2.5e-3, fp32 -- the reference's precision)
+trained with DDP at a FIXED global batch of 1440 (strong scaling: per-rank
+batch = 1440 / N, exactly like reference src/motion/trainer/distributed.py:48-49).
+Data are synthetic tensors of the UCI-HAR shape ([6912, 128, 9] fp32), weights
+random-init (no network: no dataset or checkpoint download).
+
+Every timed step is the full training step of the CLI's ``distributed``
+trainer (``Trainer.train_batch``): device batch gather, fused LSTM forward,
+fused cross-entropy, fused BPTT backward, native RCCL bucketed all-reduce,
+fused Adam.  ``--warmup`` untimed steps, then ``--steps`` steps bracketed by a
+barrier + device synchronize on both sides; the MAX elapsed time over ranks
+is reported by rank 0 as ONE JSON line.
+
+    python bench.py                       # 1 GPU
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \\
+        --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "sequences/sec (whole node) for motion RNN DDP at 1/2/4/8 MI355X; epoch time"
+# Reference DDP (MPI) seq/s at global batch 1440, 1/2/4/8 nodes (dedup table)
+BASELINE_SEQ_PER_S = {1: 44.8, 2: 85.9, 4: 128.5, 8: 213.3}
+EPOCH_SEQUENCES = 6912
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)))
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--global-batch", type=int, default=1440)
+    ap.add_argument("--hidden", type=int, default=32)
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: global batch fixed (reference); weak: --global-batch per GPU")
+    ap.add_argument("--trainer", choices=("distributed", "horovod"), default="distributed")
+    ap.add_argument("--cell", choices=("lstm", "gru"), default="lstm")
+    ap.add_argument("--seed", type=int, default=123456789)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    logging.basicConfig(level=logging.WARNING)
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_rnn_amd.data.motion import MotionDataset, synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.parallel import env
+    from pytorch_distributed_rnn_amd.train.distributed import DDPTrainer, HorovodTrainer
+
+    torch.manual_seed(args.seed)
+    info = env.init_distributed()
+    world = env.get_world_size()
+    rank = env.get_rank()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but world size is {world}", file=sys.stderr)
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    n_train = max(EPOCH_SEQUENCES, args.global_batch * (world if args.scaling == "weak" else 1))
+    train_set, _, _ = synthetic_motion(n_train=n_train, n_validation=1, n_test=1,
+                                       seq_length=args.seq_len, seed=args.seed)
+    model = MotionModel(train_set.num_features, args.hidden, args.layers,
+                        len(MotionDataset.LABELS), cell=args.cell)
+    cls = DDPTrainer if args.trainer == "distributed" else HorovodTrainer
+    trainer = cls(model=model, training_set=train_set, batch_size=args.global_batch,
+                  learning_rate=0.0025, weak_scaling=args.scaling == "weak", device=dev)
+    per_rank = trainer.train_loader.batch_size
+
+    loader = trainer.train_loader
+
+    def index_stream():
+        epoch = 0
+        while True:
+            trainer.sampler.set_epoch(epoch)
+            for bidx in loader.batch_indices():
+                if bidx.shape[0] == per_rank:  # full batches only: every timed step is global B
+                    yield bidx
+            epoch += 1
+
+    stream = index_stream()
+    trainer.model.train()
+    for _ in range(args.warmup):
+        trainer.train_batch(loader.make_batch(next(stream)))
+    # the sampler's host-side permutations are drawn up front; the batch
+    # assembly (label gather, in-kernel feature gather) is inside the timed loop
+    timed = [next(stream) for _ in range(args.steps)]
+    env.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for bidx in timed:
+        trainer.train_batch(loader.make_batch(bidx))
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    env.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    global_batch = per_rank * world
+    seqs = global_batch * args.steps
+    value = seqs / elapsed
+    ms = elapsed / args.steps * 1e3
+    base = BASELINE_SEQ_PER_S.get(world)
+    # sanity: loss must be finite after training
+    stats, _ = trainer.train_batch(loader.make_batch(timed[0]))
+    loss = float(stats[0])
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "sequences/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": round(value / base, 2) if base else None,
+            "dtype": "fp32",
+            "data": "synthetic (UCI-HAR shape [6912,128,9] fp32, random-init weights)",
+            "config": {
+                "model": f"motion-{args.cell.upper()} {args.layers}x{args.hidden} (9 inputs -> 6 classes)",
+                "global_batch": global_batch,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{world}",
+                "trainer": args.trainer,
+                "per_gpu_batch": per_rank,
+            },
+            "epoch_time_s": round(EPOCH_SEQUENCES / value, 6),
+            "final_loss": round(loss, 6),
+            "baseline_seq_per_s": base,
+        }
+        print(json.dumps(out), flush=True)
+    env.shutdown()
+
+
+if __name__ == "__main__":
+    main()

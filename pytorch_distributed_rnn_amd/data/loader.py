@@ -103,10 +103,12 @@ class DeviceBatchLoader:
         idx = idx.to(self.device, non_blocking=True)
         return list(torch.split(idx, self.batch_size))
 
+    def make_batch(self, bidx: Tensor):
+        y = self.labels.index_select(0, bidx)
+        if self.gather_in_kernel:
+            return self.features, y, bidx
+        return self.features.index_select(0, bidx), y
+
     def __iter__(self):
         for bidx in self.batch_indices():
-            y = self.labels.index_select(0, bidx)
-            if self.gather_in_kernel:
-                yield self.features, y, bidx
-            else:
-                yield self.features.index_select(0, bidx), y
+            yield self.make_batch(bidx)

@@ -23,6 +23,9 @@ from .rnn import GRU, LSTM
 
 
 class MotionModel(nn.Module):
+    # forward(features, idx=...) gathers the batch rows inside the fused kernel
+    supports_index_batches = True
+
     def __init__(self, input_dim: int, hidden_dim: int, layer_dim: int, output_dim: int,
                  cell: str = "lstm", dropout: float = 0.0):
         super().__init__()

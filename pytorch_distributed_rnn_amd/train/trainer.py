@@ -79,7 +79,10 @@ class Trainer:
                          sampler: Optional[ShardedSampler] = None):
         if dataset is None:
             return None
-        return DeviceBatchLoader(dataset, batch_size, sampler=sampler, device=self.device)
+        inner = getattr(self.model, "module", self.model)
+        in_kernel = self.device.type == "cuda" and getattr(inner, "supports_index_batches", False)
+        return DeviceBatchLoader(dataset, batch_size, sampler=sampler, device=self.device,
+                                 gather_in_kernel=in_kernel)
 
     def _get_formatter(self, epochs: int) -> TrainingMessageFormatter:
         return TrainingMessageFormatter(epochs)
