@@ -42,6 +42,10 @@ def main():
                 lstm_forward(x, ws, hidden=a.hidden, num_layers=a.layers, batch_first=True,
                              need_out=False)
 
+        def fused_fwd_save():
+            out, hn, cn = lstm_forward(x, ws, hidden=a.hidden, num_layers=a.layers, batch_first=True)
+            return hn
+
         def fused_fwdbwd():
             out, hn, cn = lstm_forward(x, ws, hidden=a.hidden, num_layers=a.layers, batch_first=True)
             hn[-1].sum().backward()
@@ -54,7 +58,10 @@ def main():
             out, (hn, cn) = ref(x)
             hn[-1].sum().backward()
 
-        r = dict(B=B, fused_fwd_ms=timeit(fused_fwd), fused_train_ms=timeit(fused_fwdbwd),
+        r = dict(B=B, nb_fwd=os.environ.get("PDRNN_LSTM_NB_FWD", "auto"),
+                 nb_bwd=os.environ.get("PDRNN_LSTM_NB_BWD", "auto"),
+                 fused_fwd_ms=timeit(fused_fwd), fused_fwd_save_ms=timeit(fused_fwd_save),
+                 fused_train_ms=timeit(fused_fwdbwd),
                  torch_fwd_ms=timeit(ref_fwd), torch_train_ms=timeit(ref_fwdbwd))
         print(json.dumps(r), flush=True)
         res.append(r)

@@ -13,6 +13,27 @@
 namespace {
 
 using at::Tensor;
+
+// PDRNN_LSTM_STAMPS=1: per-workgroup cycle stamps around the recurrence loop,
+// summarised on stderr (diagnostic builds of the timing, never in benchmarks).
+bool stamps_enabled() {
+  static const bool on = std::getenv("PDRNN_LSTM_STAMPS") != nullptr;
+  return on;
+}
+void report_stamps(const char* what, const Tensor& st, int iters) {
+  auto h = st.cpu();
+  const int64_t g = h.size(0);
+  auto p = h.data_ptr<int64_t>();
+  double cyc = 0, real = 0;
+  for (int64_t i = 0; i < g; ++i) {
+    cyc += (double)(p[i * 4 + 1] - p[i * 4 + 0]);
+    real += (double)(p[i * 4 + 3] - p[i * 4 + 2]);
+  }
+  cyc /= g; real /= g;
+  const double us = real / 100.0;  // s_memrealtime ticks at 100 MHz
+  fprintf(stderr, "[stamps] %s grid=%lld iters=%d loop=%.1f us cycles=%.0f clock=%.2f GHz cyc/iter=%.0f\n", what,
+          (long long)g, iters, us, cyc, cyc / (us * 1e3), cyc / iters);
+}
 using c10::optional;
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
@@ -79,7 +100,7 @@ void check_stack(const std::vector<Tensor>& w, int64_t NL, int64_t H, int64_t I,
 // with idx, x is a [N,T,I] source table and B = len(idx).
 std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx, const std::vector<Tensor>& w,
                                    const optional<Tensor>& h0, const optional<Tensor>& c0, int64_t H, int64_t NL,
-                                   bool batch_first, bool save, bool need_out, int64_t nb) {
+                                   bool batch_first, bool save, bool need_out, int64_t nb, int64_t split) {
   CHECK_HIP_TENSOR(x); CHECK_F32(x);
   TORCH_CHECK(x.dim() == 3, "x must be 3-D");
   TORCH_CHECK(x.stride(2) == 1, "x innermost dim must be contiguous");
@@ -127,7 +148,15 @@ std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx,
   }
   a.hn = hn.data_ptr<float>(); a.cn = cn.data_ptr<float>();
   a.B = (int)B; a.T = (int)T; a.I = (int)I; a.NL = (int)NL;
-  if (B > 0 && T > 0) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&a, (int)H, (int)nb, save ? 1 : 0, cur_stream()));
+  if (split <= 0) split = pdrnn_lstm_small_max_split((int)H, (int)NL, 0);
+  Tensor stamps;
+  if (stamps_enabled()) {
+    stamps = at::zeros({(B + nb - 1) / nb, 4}, opts.dtype(at::kLong));
+    a.stamps = reinterpret_cast<uint64_t*>(stamps.data_ptr<int64_t>());
+  }
+  if (B > 0 && T > 0)
+    HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&a, (int)H, (int)nb, (int)split, save ? 1 : 0, cur_stream()));
+  if (stamps.defined()) report_stamps(save ? "fwd(train)" : "fwd(infer)", stamps, (int)(T + NL - 1));
   return {out, hn, cn, act};
 }
 
@@ -136,7 +165,8 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
                                    const optional<Tensor>& h0, const optional<Tensor>& c0, const Tensor& hseq,
                                    const Tensor& act, const optional<Tensor>& dout, const optional<Tensor>& dhn,
                                    const optional<Tensor>& dcn, int64_t H, int64_t NL, bool batch_first,
-                                   bool need_dx, bool need_dh0, int64_t nb, const optional<Tensor>& grad_accum) {
+                                   bool need_dx, bool need_dh0, int64_t nb, int64_t split,
+                                   const optional<Tensor>& grad_accum) {
   CHECK_HIP_TENSOR(x);
   const c10::DeviceGuard guard(x.device());
   const int64_t I = x.size(2);
@@ -154,7 +184,9 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
   TORCH_CHECK(hseq.is_contiguous() && act.is_contiguous());
   StackLayout L = stack_layout(w, NL, has_bias);
   auto opts = x.options();
-  const int grid = pdrnn_lstm_small_grid((int)H, (int)B, (int)nb);
+  if (split <= 0) split = pdrnn_lstm_small_max_split((int)H, (int)NL, 1);
+  const int grid = pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb, (int)split);
+  TORCH_CHECK(grid > 0, "unsupported backward tile nb=", nb);
   Tensor slab = at::empty({std::max(grid, 1), L.P}, opts);
   Tensor dx, dh0, dc0;
   PdrnnLstmSmallBwdArgs a{};
@@ -204,7 +236,13 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
     dparams = at::empty({L.P}, opts);
   }
   if (B > 0 && T > 0) {
-    HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&a, (int)H, (int)nb, cur_stream()));
+    Tensor stamps;
+    if (stamps_enabled()) {
+      stamps = at::zeros({grid, 4}, opts.dtype(at::kLong));
+      a.stamps = reinterpret_cast<uint64_t*>(stamps.data_ptr<int64_t>());
+    }
+    HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&a, (int)H, (int)nb, (int)split, grid, cur_stream()));
+    if (stamps.defined()) report_stamps("bwd", stamps, (int)(T + NL - 1));
     const int split = std::min<int>(64, std::max<int>(1, grid / 16));
     Tensor work = at::empty({split, L.P}, opts);
     HIP_LAUNCH_CHECK(pdrnn_slab_reduce(slab.data_ptr<float>(), grid, L.P, dparams.data_ptr<float>(), beta,
@@ -213,6 +251,95 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
     dparams.zero_();
   }
   return {dparams, dx, dh0, dc0};
+}
+
+// Fused motion training step on the native path: LSTM stack forward with the
+// classifier head + cross-entropy fused into its epilogue, BPTT backward, and
+// one deterministic reduction that writes every parameter gradient straight
+// into `flat_grad` (the model's flat gradient buffer = the DDP all-reduce
+// bucket, parameter order: lstm.* then head weight, head bias) and the batch
+// statistics [mean loss, n, n_correct] into `stats`.  No autograd graph, no
+// per-op launches: 4 kernels per step, graph-capturable.
+void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Tensor& labels,
+                          const std::vector<Tensor>& w, const Tensor& head_w, const optional<Tensor>& head_b,
+                          Tensor flat_grad, Tensor stats, int64_t H, int64_t NL, int64_t split_fwd,
+                          int64_t split_bwd, int64_t nb_fwd, int64_t nb_bwd) {
+  CHECK_HIP_TENSOR(x); CHECK_F32(x);
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [N, T, I] with contiguous rows");
+  const c10::DeviceGuard guard(x.device());
+  const int64_t I = x.size(2);
+  bool has_bias = false;
+  check_stack(w, NL, H, I, has_bias);
+  TORCH_CHECK(has_bias, "fused train step expects LSTM biases");
+  const bool gathered = idx.has_value() && idx->defined();
+  const int64_t B = gathered ? idx->size(0) : x.size(0);
+  const int64_t T = x.size(1);
+  const int64_t C = head_w.size(0);
+  TORCH_CHECK(head_w.dim() == 2 && head_w.size(1) == H && head_w.is_contiguous() && C <= 16, "head weight [C<=16, H]");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous(), "labels must be int64");
+  StackLayout L = stack_layout(w, NL, true);
+  const int64_t P_params = L.P + C * H + (head_b.has_value() && head_b->defined() ? C : 0);
+  TORCH_CHECK(flat_grad.numel() == P_params && flat_grad.is_contiguous() && flat_grad.scalar_type() == at::kFloat,
+              "flat_grad must be the model's flat fp32 gradient buffer (", P_params, " elements)");
+  TORCH_CHECK(stats.numel() >= 3 && stats.is_contiguous() && stats.scalar_type() == at::kFloat);
+  const int64_t P_head = P_params - L.P;      // head weight (+ bias)
+  const int64_t PH = P_head + 3;              // + [loss, count, correct]
+  auto opts = x.options();
+  Tensor hseq = at::empty({NL, B, T, H}, opts);
+  Tensor act = at::empty({NL, B, T, 5, H}, opts);
+  Tensor hn = at::empty({NL, B, H}, opts), cn = at::empty({NL, B, H}, opts);
+  Tensor dh_top = at::empty({B, H}, opts);
+  Tensor head_slab = at::empty({B, PH}, opts);
+  if (split_fwd <= 0) split_fwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 0);
+  if (split_bwd <= 0) split_bwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 1);
+  TORCH_CHECK(split_fwd == 1 && split_bwd == 1, "fused train step runs on the gate-split / unit-group kernels");
+  if (nb_fwd <= 0) nb_fwd = 1;
+  if (nb_bwd <= 0) nb_bwd = 1;
+  const int gridb = pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb_bwd, (int)split_bwd);
+  TORCH_CHECK(gridb > 0, "unsupported backward tile nb=", nb_bwd);
+  Tensor slab = at::empty({gridb, L.P}, opts);
+
+  PdrnnLstmSmallFwdArgs f{};
+  f.x = x.data_ptr<float>();
+  f.idx = gathered ? idx->data_ptr<int64_t>() : nullptr;
+  f.x_sb = x.stride(0); f.x_st = x.stride(1);
+  for (int64_t l = 0; l < NL; ++l) {
+    f.w_ih[l] = w[l * 4 + 0].data_ptr<float>();
+    f.w_hh[l] = w[l * 4 + 1].data_ptr<float>();
+    f.b_ih[l] = w[l * 4 + 2].data_ptr<float>();
+    f.b_hh[l] = w[l * 4 + 3].data_ptr<float>();
+  }
+  f.hseq = hseq.data_ptr<float>(); f.act = act.data_ptr<float>();
+  f.hn = hn.data_ptr<float>(); f.cn = cn.data_ptr<float>();
+  f.head_w = head_w.data_ptr<float>();
+  f.head_b = (head_b.has_value() && head_b->defined()) ? head_b->data_ptr<float>() : nullptr;
+  f.labels = labels.data_ptr<int64_t>();
+  f.slab = head_slab.data_ptr<float>(); f.dh_top = dh_top.data_ptr<float>();
+  f.slab_P = PH; f.head_off_w = 0; f.head_off_b = C * H; f.stat_off = P_head;
+  f.inv_batch = 1.f / (float)std::max<int64_t>(B, 1);
+  f.C = (int)C;
+  f.B = (int)B; f.T = (int)T; f.I = (int)I; f.NL = (int)NL;
+  hipStream_t st = cur_stream();
+  HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
+
+  PdrnnLstmSmallBwdArgs bk{};
+  bk.x = f.x; bk.idx = f.idx; bk.x_sb = f.x_sb; bk.x_st = f.x_st;
+  for (int64_t l = 0; l < NL; ++l) {
+    bk.w_ih[l] = f.w_ih[l]; bk.w_hh[l] = f.w_hh[l];
+    bk.off_wih[l] = L.off_wih[l]; bk.off_whh[l] = L.off_whh[l];
+    bk.off_bih[l] = L.off_bih[l]; bk.off_bhh[l] = L.off_bhh[l];
+  }
+  bk.hseq = f.hseq; bk.act = f.act;
+  bk.dhn = dh_top.data_ptr<float>(); bk.dhn_top_only = 1;
+  bk.slab = slab.data_ptr<float>(); bk.P = L.P;
+  bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL;
+  HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
+
+  const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, gridb / 16));
+  Tensor work = at::empty({split, L.P + PH}, opts);
+  HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), gridb, L.P, head_slab.data_ptr<float>(), B, PH,
+                                      P_params, flat_grad.data_ptr<float>(), stats.data_ptr<float>(),
+                                      work.data_ptr<float>(), split, st));
 }
 
 std::vector<Tensor> xent_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore_index, bool need_grad) {
@@ -320,9 +447,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "pytorch_distributed_rnn_amd native runtime (gfx950 HIP kernels + RCCL runtime)";
   m.def("lstm_small_fwd", &lstm_small_fwd, "fused small-H LSTM stack forward");
   m.def("lstm_small_bwd", &lstm_small_bwd, "fused small-H LSTM stack BPTT backward");
+  m.def("lstm_small_max_split", [](int64_t H, int64_t NL, bool backward) {
+    return pdrnn_lstm_small_max_split((int)H, (int)NL, backward ? 1 : 0);
+  });
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });
+  m.def("lstm_head_train_step", &lstm_head_train_step, "fused LSTM + head + CE forward/backward -> flat grads");
   m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
   m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer");

@@ -36,6 +36,21 @@ typedef struct {
   int64_t o_sb, o_st;
   float* hn;                 // [NL, B, H]
   float* cn;                 // [NL, B, H]
+  uint64_t* stamps;          // diagnostics: [grid, 4] s_memtime/s_memrealtime around the loop, or NULL
+  // ---- fused classifier head + softmax cross-entropy (train step fusion) ----
+  // When head_w != NULL (requires nb == 1, save == 1): after the last step the
+  // top layer's h_T feeds logits = head_w h_T + head_b, the per-sequence CE
+  // loss against labels[idx[b]] (mean over B: scaled by inv_batch), and
+  // writes into slab row b: dW_head, db_head (cols head_off_w / head_off_b)
+  // and [loss, correct] (cols stat_off); dL/dh_T goes to dh_top [B, H].
+  const float* head_w;       // [C, H]
+  const float* head_b;       // [C] or NULL
+  const int64_t* labels;     // [N] class ids (indexed through idx when given)
+  float* slab;               // [B, P] (shared with the backward's slab)
+  float* dh_top;             // [B, H]
+  int64_t slab_P, head_off_w, head_off_b, stat_off;
+  float inv_batch;
+  int C;
   int B, T, I, NL;
 } PdrnnLstmSmallFwdArgs;
 
@@ -61,20 +76,34 @@ typedef struct {
   int64_t P;
   int64_t off_wih[PDRNN_MAX_LAYERS], off_whh[PDRNN_MAX_LAYERS];
   int64_t off_bih[PDRNN_MAX_LAYERS], off_bhh[PDRNN_MAX_LAYERS];  // -1 = no bias
+  uint64_t* stamps;          // diagnostics (see forward), or NULL
+  int dhn_top_only;          // dhn is [B, H] for the top layer only (fused head path)
   int B, T, I, NL;
 } PdrnnLstmSmallBwdArgs;
 
 // Query the launch geometry chosen for (H, B): returns grid size (number of slab rows).
 int pdrnn_lstm_small_grid(int H, int B, int nb);
 int pdrnn_lstm_small_supported(int H, int I, int NL);
-hipError_t pdrnn_lstm_small_fwd(const PdrnnLstmSmallFwdArgs* a, int H, int nb, int save,
+int pdrnn_lstm_small_max_split(int H, int NL, int backward);
+// split = lanes per hidden unit (forward S in {2,4,8}; backward S2 in {2,4})
+hipError_t pdrnn_lstm_small_fwd(const PdrnnLstmSmallFwdArgs* a, int H, int nb, int split, int save,
                                 hipStream_t stream);
-hipError_t pdrnn_lstm_small_bwd(const PdrnnLstmSmallBwdArgs* a, int H, int nb, hipStream_t stream);
+// grid <= 0: natural grid (persistent for the unit-group map); query with _bwd_grid
+hipError_t pdrnn_lstm_small_bwd(const PdrnnLstmSmallBwdArgs* a, int H, int nb, int split, int grid,
+                                hipStream_t stream);
+int pdrnn_lstm_small_bwd_grid(int H, int NL, int T, int B, int nb, int split);
 
 // Column sums of a [rows, P] fp32 slab into out[P] (out = beta*out + sum).
 // Two deterministic passes through `work` ([split, P] floats, split <= 64).
 hipError_t pdrnn_slab_reduce(const float* slab, int64_t rows, int64_t P, float* out, float beta,
                              float* work, int split, hipStream_t stream);
+// Two slabs reduced side by side (columns of A then of B); the first n_out
+// summed columns go to out, the rest to out_tail.
+hipError_t pdrnn_slab2_reduce(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB, int64_t PB,
+                              int64_t n_out, float* out, float* out_tail, float* work, int split, hipStream_t stream);
+// Same, with columns [P_a, P) written to out_b instead (e.g. loss statistics).
+hipError_t pdrnn_slab_reduce2(const float* slab, int64_t rows, int64_t P, int64_t P_a, float* out_a,
+                              float* out_b, float* work, int split, hipStream_t stream);
 
 // ----------------------------------------------------------------------------
 // Fused cross-entropy (+ accuracy): mean loss over valid rows, dlogits saved.

@@ -70,6 +70,20 @@ PDRNN_DEVICE float tanhf_fast(float x) {
   return copysignf(t, x);
 }
 
+// Workgroup barrier that orders LDS traffic only.  __syncthreads() on gfx950
+// also drains vmcnt (every outstanding global load AND store of the wave)
+// before s_barrier, which in a persistent recurrence serialises each timestep
+// behind the HBM write latency of the previous one.  Cross-wave hand-offs in
+// the recurrent kernels go exclusively through LDS, so waiting for lgkmcnt is
+// sufficient; global prefetches and output stores stay in flight.
+PDRNN_DEVICE void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Diagnostic cycle stamps (shader clock and 100 MHz real-time clock).
+PDRNN_DEVICE uint64_t stamp_cycles() { return __builtin_amdgcn_s_memtime(); }
+PDRNN_DEVICE uint64_t stamp_real() { return __builtin_amdgcn_s_memrealtime(); }
+
 // bf16 <-> f32 (round to nearest even; NaN preserved by the hardware cvt).
 PDRNN_DEVICE float bf16_to_f32(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 PDRNN_DEVICE uint16_t f32_to_bf16(float f) {

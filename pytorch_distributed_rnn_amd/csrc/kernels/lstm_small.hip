@@ -32,12 +32,32 @@
 namespace pdrnn {
 namespace {
 
-template <int H, int S, int NB, bool SAVE>
+// x sequence preloaded into LDS once (zero-padded to H columns) when it fits:
+// layer 0 then reads its input slice straight from LDS every step -- no
+// per-step global load on the recurrence's critical path.
+constexpr int kXldsBytes = 48 * 1024;
+
+template <int H, int NB>
+__device__ __forceinline__ void preload_x(float* xs, const PdrnnLstmSmallFwdArgs& a, const int* bsrc,
+                                          const bool* valid) {
+  const int T = a.T, I = a.I;
+  for (int n = 0; n < NB; ++n) {
+    float* dst = xs + (int64_t)n * T * H;
+    const float* src = a.x + bsrc[n] * a.x_sb;
+    for (int e = threadIdx.x; e < T * H; e += blockDim.x) {
+      const int t = e / H, k = e - t * H;
+      const float v = src[(int64_t)t * a.x_st + min(k, I - 1)];
+      dst[e] = (valid[n] && k < I) ? v : 0.f;
+    }
+  }
+}
+
+template <int H, int S, int NB, bool SAVE, bool XLDS>
 __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   constexpr int K = 2 * H;
   constexpr int KS = K / S;
   constexpr int LANES = H * S;
-  static_assert(KS % 4 == 0, "K slice must be float4 aligned");
+  static_assert(KS % 4 == 0 && H % KS == 0, "K slice must be float4 aligned and not straddle");
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
   const int NL = a.NL, B = a.B, T = a.T, I = a.I;
@@ -46,32 +66,33 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
   const int lg = tid - layer * LANES;
   const int u = lg / S;
   const int s = lg % S;
+  const int k0 = s * KS;  // first column of this lane's K slice
   const int bbase = blockIdx.x * NB;
   const int Iin = layer == 0 ? I : H;
 
-  // vin[n][l][p][k]: k < H layer input, k >= H own hidden state.
+  // LDS: vin[n][l][p][K] (k < H layer input, k >= H own hidden) | xs[n][T][H]
+  float* xs = smem + NB * NL * 2 * K;
   auto vin = [&](int n, int l, int p) -> float* { return smem + ((n * NL + l) * 2 + p) * K; };
 
-  // ---- weights for this lane: rows q*H+u, columns s*KS .. s*KS+KS-1 -------
+  // ---- this lane's rows q*H+u of [W_ih | W_hh], columns k0 .. k0+KS-1 ----
   float w[4][KS];
   float bias[4];
   {
-    const float* Wih = a.w_ih[layer];
-    const float* Whh = a.w_hh[layer];
-    const float* Bih = a.b_ih[layer];
-    const float* Bhh = a.b_hh[layer];
+    const bool in_part = k0 < H;
+    const float* src = in_part ? a.w_ih[layer] : a.w_hh[layer];
+    const int ld = in_part ? Iin : H;
+    const int c0 = in_part ? k0 : k0 - H;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = q * H + u;
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
-        const int k = s * KS + kk;
-        float v;
-        if (k < H) v = k < Iin ? Wih[r * Iin + k] : 0.f;
-        else v = Whh[r * H + (k - H)];
-        w[q][kk] = v;
+        const int c = c0 + kk;
+        const bool live = !in_part || c < Iin;
+        const float v = src[r * ld + (live ? c : 0)];
+        w[q][kk] = live ? v : 0.f;
       }
-      bias[q] = (Bih ? Bih[r] : 0.f) + (Bhh ? Bhh[r] : 0.f);
+      bias[q] = (a.b_ih[layer] ? a.b_ih[layer][r] : 0.f) + (a.b_hh[layer] ? a.b_hh[layer][r] : 0.f);
     }
   }
 
@@ -83,31 +104,39 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
     const int b = bbase + n;
     valid[n] = b < B;
     bsrc[n] = valid[n] ? (a.idx ? (int)a.idx[b] : b) : 0;
-    const float h_init = (a.h0 && valid[n]) ? a.h0[((int64_t)layer * B + b) * H + u] : 0.f;
-    c[n] = (a.c0 && valid[n]) ? a.c0[((int64_t)layer * B + b) * H + u] : 0.f;
+    const int bc = min(b, B - 1);
+    const float h_init = (a.h0 && valid[n]) ? a.h0[((int64_t)layer * B + bc) * H + u] : 0.f;
+    c[n] = (a.c0 && valid[n]) ? a.c0[((int64_t)layer * B + bc) * H + u] : 0.f;
     hl[n] = h_init;
     if (s == 0) vin(n, layer, 0)[H + u] = h_init;
-    if (layer == 0 && lg < H)
+    if (!XLDS && layer == 0 && lg < H)
       vin(n, 0, 0)[lg] = (valid[n] && lg < I) ? a.x[bsrc[n] * a.x_sb + lg] : 0.f;
   }
+  if constexpr (XLDS) preload_x<H, NB>(xs, a, bsrc, valid);
   __syncthreads();
 
+  uint64_t st0 = 0, sr0 = 0;
+  if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
   const int iters = T + NL - 1;
   for (int it = 0; it < iters; ++it) {
     const int t = it - layer;
     if (t >= 0 && t < T) {
       const int p = t & 1;
       float xnext[NB];
-      if (layer == 0 && lg < H) {
+      if (!XLDS && layer == 0 && lg < H) {
+        const int tn = min(t + 1, T - 1);
+        const int kx = min(lg, I - 1);
 #pragma unroll
-        for (int n = 0; n < NB; ++n)
-          xnext[n] = (t + 1 < T && valid[n] && lg < I)
-                         ? a.x[bsrc[n] * a.x_sb + (int64_t)(t + 1) * a.x_st + lg]
-                         : 0.f;
+        for (int n = 0; n < NB; ++n) {
+          const float v = a.x[bsrc[n] * a.x_sb + (int64_t)tn * a.x_st + kx];  // unconditional load
+          xnext[n] = (t + 1 < T && valid[n] && lg < I) ? v : 0.f;
+        }
       }
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
-        const float4* v4 = reinterpret_cast<const float4*>(vin(n, layer, p) + s * KS);
+        const float* src = vin(n, layer, p) + k0;
+        if (XLDS && layer == 0 && k0 < H) src = xs + ((int64_t)n * T + t) * H + k0;
+        const float4* v4 = reinterpret_cast<const float4*>(src);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k4 = 0; k4 < KS / 4; ++k4) {
@@ -147,12 +176,16 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
           }
         }
       }
-      if (layer == 0 && lg < H) {
+      if (!XLDS && layer == 0 && lg < H) {
 #pragma unroll
         for (int n = 0; n < NB; ++n) vin(n, 0, p ^ 1)[lg] = xnext[n];
       }
     }
-    __syncthreads();
+    lds_barrier();
+  }
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
   }
 
 #pragma unroll
@@ -165,14 +198,258 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
   }
 }
 
-template <int H, int S2, int NB>
+// ---------------------------------------------------------------------------
+// Forward, gate-split lane map (default): a layer group is 4H lanes, lane =
+// (unit u, gate q) with the 4 gates of a unit in one DPP quad.  Each lane owns
+// ONE full row of [W_ih | W_hh] (pre-scaled by -log2(e), and by 2 for the g
+// gate so tanh(x) = 2*sigmoid(2x) - 1), computes its dot product with packed
+// fp32 FMAs (v_pk_fma_f32, 2 MACs per instruction), applies ONE transcendental
+// activation, and the quad exchanges the four activated gates with DPP quad
+// broadcasts.  Compared with the K-split map this removes the cross-lane
+// partial-sum tree and three of the four activations from every lane's
+// per-timestep dependency chain (the recurrence is latency-bound: one wave per
+// SIMD at motion batch sizes).
+// ---------------------------------------------------------------------------
+typedef float pdrnn_f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float quad_bcast(float v, int q) {
+  // quad_perm [q,q,q,q]: every lane of the quad reads lane q of the quad
+  switch (q) {
+    case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x00, 0xF, 0xF, false));
+    case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x55, 0xF, 0xF, false));
+    case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xAA, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xFF, 0xF, 0xF, false));
+  }
+}
+
+constexpr float kNegLog2e = -1.4426950408889634f;
+
+template <int H, int NB, bool SAVE, bool XLDS, bool HEAD>
+__global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFwdArgs a) {
+  constexpr int K = 2 * H;
+  constexpr int LANES = 4 * H;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+
+  const int NL = a.NL, B = a.B, T = a.T, I = a.I;
+  const int tid = threadIdx.x;
+  const int layer = __builtin_amdgcn_readfirstlane(tid / LANES);
+  const int lg = tid - layer * LANES;
+  const int u = lg >> 2;
+  const int q = lg & 3;
+  const int r = q * H + u;
+  const int bbase = blockIdx.x * NB;
+  const int Iin = layer == 0 ? I : H;
+
+  float* xs = smem + NB * NL * 2 * K;
+  auto vin = [&](int n, int l, int p) -> float* { return smem + ((n * NL + l) * 2 + p) * K; };
+
+  // activation: sigma(z) with z pre-scaled, then a = sigma * am + ab
+  const float gsc = q == 2 ? 2.f : 1.f;
+  const float am = q == 2 ? 2.f : 1.f;
+  const float ab = q == 2 ? -1.f : 0.f;
+  const float wsc = kNegLog2e * gsc;
+
+  pdrnn_f2 w2[K / 2];
+  float bias;
+  {
+    const float* wih = a.w_ih[layer] + (int64_t)r * Iin;
+    const float* whh = a.w_hh[layer] + (int64_t)r * H;
+#pragma unroll
+    for (int kk = 0; kk < K / 2; ++kk) {
+      float v0, v1;
+      const int k = 2 * kk;
+      if (k < H) {  // compile-time per unrolled kk
+        const float t0 = wih[min(k, Iin - 1)], t1 = wih[min(k + 1, Iin - 1)];
+        v0 = k < Iin ? t0 : 0.f;
+        v1 = k + 1 < Iin ? t1 : 0.f;
+      } else {
+        v0 = whh[k - H];
+        v1 = whh[k + 1 - H];
+      }
+      w2[kk] = pdrnn_f2{v0 * wsc, v1 * wsc};
+    }
+    bias = ((a.b_ih[layer] ? a.b_ih[layer][r] : 0.f) + (a.b_hh[layer] ? a.b_hh[layer][r] : 0.f)) * wsc;
+  }
+
+  int bsrc[NB];
+  bool valid[NB];
+  float c[NB], hl[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const int b = bbase + n;
+    valid[n] = b < B;
+    bsrc[n] = valid[n] ? (a.idx ? (int)a.idx[b] : b) : 0;
+    const int bc = min(b, B - 1);
+    const float h_init = (a.h0 && valid[n]) ? a.h0[((int64_t)layer * B + bc) * H + u] : 0.f;
+    c[n] = (a.c0 && valid[n]) ? a.c0[((int64_t)layer * B + bc) * H + u] : 0.f;
+    hl[n] = h_init;
+    if (q == 0) vin(n, layer, 0)[H + u] = h_init;
+    if (!XLDS && layer == 0 && lg < H)
+      vin(n, 0, 0)[lg] = (valid[n] && lg < I) ? a.x[bsrc[n] * a.x_sb + lg] : 0.f;
+  }
+  if constexpr (XLDS) preload_x<H, NB>(xs, a, bsrc, valid);
+  __syncthreads();
+
+  // per-lane output streams (advanced by one timestep per active iteration)
+  // lane q writes act item q (i,f,g,o); q==0 also writes c_t, q==1 writes h_t
+  float* out1[NB];
+  float* out2[NB];
+  int64_t step1 = 0, step2 = 0;
+  if constexpr (SAVE) {
+    step1 = 5 * H;
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const int bc = min(bbase + n, B - 1);
+      const int64_t row0 = ((int64_t)layer * B + bc) * T;
+      out1[n] = a.act + row0 * 5 * H + q * H + u;
+      out2[n] = q == 0 ? a.act + row0 * 5 * H + 4 * H + u : a.hseq + row0 * H + u;
+    }
+    step2 = q == 0 ? 5 * H : H;
+  } else {
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      out1[n] = a.out ? a.out + (int64_t)min(bbase + n, B - 1) * a.o_sb + u : nullptr;
+      out2[n] = nullptr;
+    }
+    step1 = a.o_st;
+  }
+  const bool write2 = SAVE && q < 2;
+  const bool write1 = SAVE || (a.out != nullptr && layer == NL - 1 && q == 0);
+
+  uint64_t st0 = 0, sr0 = 0;
+  if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
+  const int iters = T + NL - 1;
+  for (int it = 0; it < iters; ++it) {
+    const int t = it - layer;
+    if (t >= 0 && t < T) {
+      const int p = t & 1;
+      float xnext[NB];
+      if (!XLDS && layer == 0 && lg < H) {
+        const int tn = min(t + 1, T - 1);
+        const int kx = min(lg, I - 1);
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          const float v = a.x[bsrc[n] * a.x_sb + (int64_t)tn * a.x_st + kx];
+          xnext[n] = (t + 1 < T && valid[n] && lg < I) ? v : 0.f;
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const float* src_in = vin(n, layer, p);
+        if (XLDS && layer == 0) src_in = xs + ((int64_t)n * T + t) * H;
+        const float* src_h = vin(n, layer, p) + H;
+        pdrnn_f2 acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+        for (int k4 = 0; k4 < K / 4; ++k4) {
+          const float4 v = (4 * k4 < H) ? reinterpret_cast<const float4*>(src_in)[k4]
+                                        : reinterpret_cast<const float4*>(src_h)[k4 - H / 4];
+          acc[(2 * k4) & 3] = __builtin_elementwise_fma(w2[2 * k4], pdrnn_f2{v.x, v.y}, acc[(2 * k4) & 3]);
+          acc[(2 * k4 + 1) & 3] =
+              __builtin_elementwise_fma(w2[2 * k4 + 1], pdrnn_f2{v.z, v.w}, acc[(2 * k4 + 1) & 3]);
+        }
+        const pdrnn_f2 s2 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        const float z = (s2.x + s2.y) + bias;  // = -log2(e) * gsc * preactivation
+        const float sg = fast_rcp(1.f + __builtin_amdgcn_exp2f(z));
+        const float act = fmaf(sg, am, ab);  // sigmoid, or tanh for the g gate
+        const float ig = quad_bcast(act, 0);
+        const float fg = quad_bcast(act, 1);
+        const float gg = quad_bcast(act, 2);
+        const float og = quad_bcast(act, 3);
+        const float cn = fmaf(fg, c[n], ig * gg);
+        const float th = fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(cn * (2.f * kNegLog2e))), 2.f, -1.f);
+        const float h = og * th;
+        c[n] = cn;
+        hl[n] = h;
+        if (q == 0) vin(n, layer, p ^ 1)[H + u] = h;
+        if (q == 1 && layer < NL - 1) vin(n, layer + 1, p)[u] = h;
+        if (valid[n]) {
+          if (write1) out1[n][(int64_t)t * step1] = SAVE ? act : h;
+          if (write2) out2[n][(int64_t)t * step2] = q == 0 ? cn : h;
+        }
+      }
+      if (!XLDS && layer == 0 && lg < H) {
+#pragma unroll
+        for (int n = 0; n < NB; ++n) vin(n, 0, p ^ 1)[lg] = xnext[n];
+      }
+    }
+    lds_barrier();
+  }
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+  }
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const int b = bbase + n;
+    if (valid[n] && q == 0) {
+      a.hn[((int64_t)layer * B + b) * H + u] = hl[n];
+      a.cn[((int64_t)layer * B + b) * H + u] = c[n];
+    }
+  }
+  if constexpr (HEAD) {
+    // Fused classifier head + cross-entropy on the top layer's h_T; wave n
+    // handles sequence n of the tile.  h_T sits in the top layer's
+    // next-parity hidden slot after the loop.
+    static_assert(NB <= 4, "one wave per sequence of the tile");
+    const int n = tid >> 6;
+    const int b = bbase + n;
+    if (n < NB && b < B) {
+      const int lane = tid & 63;
+      const float* hT = vin(n, NL - 1, T & 1) + H;
+      const float hv = lane < H ? hT[lane] : 0.f;
+      const int64_t lab = a.labels[a.idx ? a.idx[b] : b];
+      const int C = a.C;
+      float m = -INFINITY, logit_y = 0.f;
+      int amax = 0;
+      float lg_c[16];
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) {
+        if (cc < C) {
+          const float wv = lane < H ? a.head_w[cc * H + lane] : 0.f;
+          float z = wave_sum(wv * hv) + (a.head_b ? a.head_b[cc] : 0.f);
+          lg_c[cc] = z;
+          if (z > m) { m = z; amax = cc; }
+          if (cc == lab) logit_y = z;
+        }
+      }
+      float se = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc)
+        if (cc < C) se += expf(lg_c[cc] - m);
+      const float lse = m + logf(se);
+      const float inv_se = 1.f / se;
+      float* srow = a.slab + (int64_t)b * a.slab_P;
+      float dh = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) {
+        if (cc < C) {
+          const float d = (expf(lg_c[cc] - m) * inv_se - (cc == lab ? 1.f : 0.f)) * a.inv_batch;
+          if (lane < H) {
+            dh = fmaf(a.head_w[cc * H + lane], d, dh);
+            srow[a.head_off_w + cc * H + lane] = d * hv;
+          }
+          if (lane == 0 && a.head_b) srow[a.head_off_b + cc] = d;
+        }
+      }
+      if (lane < H) a.dh_top[(int64_t)b * H + lane] = dh;
+      if (lane == 0) {  // [mean-loss contribution, count, correct] -> column sums are the batch stats
+        srow[a.stat_off + 0] = (lse - logit_y) * a.inv_batch;
+        srow[a.stat_off + 1] = 1.f;
+        srow[a.stat_off + 2] = amax == lab ? 1.f : 0.f;
+      }
+    }
+  }
+}
+
+template <int H, int S2, int NB, bool XLDS>
 __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
   constexpr int R = 4 * H;        // gate rows
   constexpr int K = 2 * H;        // columns of [W_ih | W_hh] (input padded to H)
   constexpr int RS = R / S2;      // rows per column lane
   constexpr int G = K * S2;       // lanes per layer group
+  constexpr int CH = 4;           // float4 chunks per LDS read burst (bounds VGPRs)
   static_assert(G >= R, "S2 must be >= 2");
-  static_assert(RS % 4 == 0, "row slice must be float4 aligned");
+  static_assert(RS % (4 * CH) == 0, "row slice must be a multiple of the chunk");
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
   const int NL = a.NL, B = a.B, T = a.T, I = a.I;
@@ -182,33 +459,36 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
   const int bbase = blockIdx.x * NB;
   const int Iin = layer == 0 ? I : H;
 
-  // LDS carve: dg[NB][NL][R] | dhrec[NB][NL][H] | dha[NB][NL][H]
+  // LDS carve: dg[NB][NL][R] | dhrec[NB][NL][H] | dha[NB][NL][H] | xs[NB][T][H]
   float* dg_s = smem;
   float* dhrec_s = dg_s + NB * NL * R;
   float* dha_s = dhrec_s + NB * NL * H;
+  float* xs = dha_s + NB * NL * H;
   auto dg = [&](int n, int l) { return dg_s + (n * NL + l) * R; };
   auto dhrec = [&](int n, int l) { return dhrec_s + (n * NL + l) * H; };
   auto dha = [&](int n, int l) { return dha_s + (n * NL + l) * H; };
 
-  // Row role.
+  // Row role (lanes < 4H): gate row r = q*H + u.
   const bool is_row = lg < R;
   const int q = lg / H;
   const int u = lg % H;
-  // Column role.
+  // Column role: column k of [W_ih | W_hh], row slice s2.
   const int k = lg / S2;
   const int s2 = lg % S2;
 
+  // This lane's column: rows s2*RS .. s2*RS+RS-1 at a fixed stride
+  // (branch-free addressing; zero-padded input columns k >= I).
+  const bool col_in = k < H;
+  const bool col_live = !col_in || k < Iin;
+  const int64_t col_stride = col_in ? Iin : H;
+  const int64_t col_off = col_in ? (int64_t)s2 * RS * Iin + k : (int64_t)s2 * RS * H + (k - H);
   float W[RS], dW[RS];
   {
-    const float* Wih = a.w_ih[layer];
-    const float* Whh = a.w_hh[layer];
+    const float* base = (col_in ? a.w_ih[layer] : a.w_hh[layer]) + (col_live ? col_off : 0);
 #pragma unroll
     for (int j = 0; j < RS; ++j) {
-      const int r = s2 * RS + j;
-      float v;
-      if (k < H) v = k < Iin ? Wih[r * Iin + k] : 0.f;
-      else v = Whh[r * H + (k - H)];
-      W[j] = v;
+      const float v = base[j * col_stride];
+      W[j] = col_live ? v : 0.f;
       dW[j] = 0.f;
     }
   }
@@ -221,95 +501,176 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
     const int b = bbase + n;
     valid[n] = b < B;
     bsrc[n] = valid[n] ? (a.idx ? (int)a.idx[b] : b) : 0;
-    dc[n] = (is_row && a.dcn && valid[n]) ? a.dcn[((int64_t)layer * B + b) * H + u] : 0.f;
+    const int bc = min(b, B - 1);
+    dc[n] = (is_row && a.dcn && valid[n]) ? a.dcn[((int64_t)layer * B + bc) * H + u] : 0.f;
     if (lg < H) {
-      dhrec(n, layer)[lg] = (a.dhn && valid[n]) ? a.dhn[((int64_t)layer * B + b) * H + lg] : 0.f;
+      dhrec(n, layer)[lg] = (a.dhn && valid[n]) ? a.dhn[((int64_t)layer * B + bc) * H + lg] : 0.f;
       dha(n, layer)[lg] = 0.f;
     }
   }
+  if constexpr (XLDS) {
+    for (int n = 0; n < NB; ++n) {
+      float* dst = xs + (int64_t)n * T * H;
+      const float* src = a.x + bsrc[n] * a.x_sb;
+      for (int e = tid; e < T * H; e += blockDim.x) {
+        const int t = e / H, kk = e - t * H;
+        const float v = src[(int64_t)t * a.x_st + min(kk, I - 1)];
+        dst[e] = (valid[n] && kk < I) ? v : 0.f;
+      }
+    }
+  }
+
+  // ---- per-timestep operands, prefetched TWO steps ahead (ping-pong sets) --
+  // Loads are unconditional on clamped, always-valid addresses and masked
+  // afterwards: no control flow around them and no register copies between
+  // iterations, so the compiler's waitcnt tracking keeps them in flight
+  // across both barriers of the step in between.
+  // Raw values only: masking happens at the point of use (a select on a
+  // freshly loaded register would force the wait right at the load).
+  struct RowOps { float i, f, g, o, c, cp, dout; };
+  const bool top = layer == NL - 1;
+  auto load_row = [&](int t, int n) {
+    const int b = min(bbase + n, B - 1);
+    const int tc = min(max(t, 0), T - 1);
+    const float* act = a.act + (((int64_t)layer * B + b) * T + tc) * 5 * H + u;
+    RowOps r;
+    r.i = act[0 * H]; r.f = act[1 * H]; r.g = act[2 * H]; r.o = act[3 * H]; r.c = act[4 * H];
+    const float* cpp = tc > 0 ? act - H : (a.c0 ? a.c0 + ((int64_t)layer * B + b) * H + u : act);
+    r.cp = *cpp;
+    const float* dp = (top && a.dout) ? a.dout + b * a.d_sb + (int64_t)tc * a.d_st + u : act;
+    r.dout = *dp;
+    return r;
+  };
+  // global part of the column input (everything except layer-0 x under XLDS)
+  auto load_in = [&](int t, int n) -> float {
+    const int b = min(bbase + n, B - 1);
+    const int tc = min(max(t, 0), T - 1);
+    const float* p;
+    if (k < H) {
+      const float* px = a.x + bsrc[n] * a.x_sb + (int64_t)tc * a.x_st + min(k, I - 1);
+      const float* ph = a.hseq + (((int64_t)(layer > 0 ? layer - 1 : 0) * B + b) * T + tc) * H + k;
+      p = layer == 0 ? px : ph;
+    } else {
+      const int kh = k - H;
+      const float* ph = a.hseq + (((int64_t)layer * B + b) * T + max(tc - 1, 0)) * H + kh;
+      const float* p0 = a.h0 ? a.h0 + ((int64_t)layer * B + b) * H + kh : ph;
+      p = tc > 0 ? ph : p0;
+    }
+    return *p;
+  };
+  // masks, recomputed where the values are consumed
+  auto in_live = [&](int t, int n) -> bool {
+    if (!valid[n] || t < 0 || t >= T) return false;
+    if (k < H) return layer > 0 || k < I;
+    return t > 0 || a.h0 != nullptr;
+  };
+  const bool in_from_lds = XLDS && layer == 0 && k < H;
+
+  const int t_first = T - 1 + (NL - 1 - layer);  // this layer's t at it = 0
+  RowOps ropA[NB], ropB[NB];
+  float inA[NB], inB[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    ropA[n] = load_row(t_first, n);
+    inA[n] = load_in(t_first, n);
+    ropB[n] = load_row(t_first - 1, n);
+    inB[n] = load_in(t_first - 1, n);
+  }
   __syncthreads();
 
-  const int iters = T + NL - 1;
-  for (int it = 0; it < iters; ++it) {
-    const int t = T - 1 - it + (NL - 1 - layer);
+  auto step = [&](int it, RowOps (&rop)[NB], float (&inp)[NB]) {
+    const int t = t_first - it;
     const bool active = t >= 0 && t < T;
     // ---------------- row phase: dgates ----------------
     if (active && is_row) {
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
-        float dgv = 0.f;
-        if (valid[n]) {
-          const int b = bbase + n;
-          const int64_t row = ((int64_t)layer * B + b) * T + t;
-          const float* act = a.act + row * 5 * H;
-          const float ig = act[0 * H + u], fg = act[1 * H + u], gg = act[2 * H + u],
-                      og = act[3 * H + u], ct = act[4 * H + u];
-          float cp;
-          if (t > 0) cp = act[-5 * H + 4 * H + u];
-          else cp = a.c0 ? a.c0[((int64_t)layer * B + b) * H + u] : 0.f;
-          float dh = dhrec(n, layer)[u];
-          if (layer < NL - 1) dh += dha(n, layer)[u];
-          else if (a.dout) dh += a.dout[b * a.d_sb + (int64_t)t * a.d_st + u];
-          const float tc = tanhf_fast(ct);
-          const float dcp = fmaf(dh * og, 1.f - tc * tc, dc[n]);
-          const float d_i = dcp * gg * ig * (1.f - ig);
-          const float d_f = dcp * cp * fg * (1.f - fg);
-          const float d_g = dcp * ig * (1.f - gg * gg);
-          const float d_o = dh * tc * og * (1.f - og);
-          dgv = q == 0 ? d_i : (q == 1 ? d_f : (q == 2 ? d_g : d_o));
-          dc[n] = dcp * fg;
-        }
+        const RowOps& r = rop[n];
+        const float cp = (t > 0 || a.c0) ? r.cp : 0.f;
+        float dh = dhrec(n, layer)[u] + ((top && a.dout) ? r.dout : 0.f);
+        if (layer < NL - 1) dh += dha(n, layer)[u];
+        const float tc = tanhf_fast(r.c);
+        const float dcp = fmaf(dh * r.o, 1.f - tc * tc, dc[n]);
+        const float d_i = dcp * r.g * r.i * (1.f - r.i);
+        const float d_f = dcp * cp * r.f * (1.f - r.f);
+        const float d_g = dcp * r.i * (1.f - r.g * r.g);
+        const float d_o = dh * tc * r.o * (1.f - r.o);
+        float dgv = q == 0 ? d_i : (q == 1 ? d_f : (q == 2 ? d_g : d_o));
+        if (!valid[n]) dgv = 0.f;
+        dc[n] = dcp * r.f;
         dg(n, layer)[lg] = dgv;
         db += dgv;
       }
     }
-    __syncthreads();
+    // refill this set for step t-2 (consumed two iterations from now)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) rop[n] = load_row(t - 2, n);
+    lds_barrier();
     // ---------------- column phase: dh_{t-1}, d(input), dW ----------------
     if (active) {
+      float in_v[NB];
 #pragma unroll
-      for (int n = 0; n < NB; ++n) {
-        const int b = bbase + n;
-        float in = 0.f;
-        if (valid[n]) {
-          if (k < H) {
-            if (layer == 0) {
-              if (k < I) in = a.x[bsrc[n] * a.x_sb + (int64_t)t * a.x_st + k];
-            } else {
-              in = a.hseq[(((int64_t)(layer - 1) * B + b) * T + t) * H + k];
-            }
-          } else {
-            const int kh = k - H;
-            if (t > 0) in = a.hseq[(((int64_t)layer * B + b) * T + (t - 1)) * H + kh];
-            else if (a.h0) in = a.h0[((int64_t)layer * B + b) * H + kh];
+      for (int n = 0; n < NB; ++n)
+        in_v[n] = in_from_lds ? xs[((int64_t)n * T + t) * H + k] : (in_live(t, n) ? inp[n] : 0.f);
+      float ds[NB][4];  // 4 independent chains per sequence (FMA latency)
+#pragma unroll
+      for (int n = 0; n < NB; ++n) ds[n][0] = ds[n][1] = ds[n][2] = ds[n][3] = 0.f;
+#pragma unroll
+      for (int c0 = 0; c0 < RS / 4; c0 += CH) {
+        float4 g[NB][CH];
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          const float4* g4 = reinterpret_cast<const float4*>(dg(n, layer) + s2 * RS);
+#pragma unroll
+          for (int cc = 0; cc < CH; ++cc) g[n][cc] = g4[c0 + cc];
+        }
+#pragma unroll
+        for (int cc = 0; cc < CH; ++cc) {
+          const int j = 4 * (c0 + cc);
+#pragma unroll
+          for (int n = 0; n < NB; ++n) {
+            ds[n][0] = fmaf(W[j + 0], g[n][cc].x, ds[n][0]);
+            ds[n][1] = fmaf(W[j + 1], g[n][cc].y, ds[n][1]);
+            ds[n][2] = fmaf(W[j + 2], g[n][cc].z, ds[n][2]);
+            ds[n][3] = fmaf(W[j + 3], g[n][cc].w, ds[n][3]);
+            dW[j + 0] = fmaf(g[n][cc].x, in_v[n], dW[j + 0]);
+            dW[j + 1] = fmaf(g[n][cc].y, in_v[n], dW[j + 1]);
+            dW[j + 2] = fmaf(g[n][cc].z, in_v[n], dW[j + 2]);
+            dW[j + 3] = fmaf(g[n][cc].w, in_v[n], dW[j + 3]);
           }
         }
-        const float4* g4 = reinterpret_cast<const float4*>(dg(n, layer) + s2 * RS);
-        float ds0 = 0.f, ds1 = 0.f;
+      }
 #pragma unroll
-        for (int j4 = 0; j4 < RS / 4; ++j4) {
-          const float4 g = g4[j4];
-          ds0 = fmaf(W[4 * j4 + 0], g.x, ds0);
-          ds1 = fmaf(W[4 * j4 + 1], g.y, ds1);
-          ds0 = fmaf(W[4 * j4 + 2], g.z, ds0);
-          ds1 = fmaf(W[4 * j4 + 3], g.w, ds1);
-          dW[4 * j4 + 0] = fmaf(g.x, in, dW[4 * j4 + 0]);
-          dW[4 * j4 + 1] = fmaf(g.y, in, dW[4 * j4 + 1]);
-          dW[4 * j4 + 2] = fmaf(g.z, in, dW[4 * j4 + 2]);
-          dW[4 * j4 + 3] = fmaf(g.w, in, dW[4 * j4 + 3]);
-        }
-        const float ds = group_sum<S2>(ds0 + ds1);
+      for (int n = 0; n < NB; ++n) {
+        const float tot = group_sum<S2>((ds[n][0] + ds[n][1]) + (ds[n][2] + ds[n][3]));
         if (s2 == 0) {
           if (k >= H) {
-            dhrec(n, layer)[k - H] = ds;
+            dhrec(n, layer)[k - H] = tot;
           } else if (layer > 0) {
-            dha(n, layer - 1)[k] = ds;
+            dha(n, layer - 1)[k] = tot;
           } else if (a.dx && valid[n] && k < I) {
-            a.dx[b * a.dx_sb + (int64_t)t * a.dx_st + k] = ds;
+            a.dx[(bbase + n) * a.dx_sb + (int64_t)t * a.dx_st + k] = tot;
           }
         }
       }
     }
-    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < NB; ++n) inp[n] = in_from_lds ? 0.f : load_in(t - 2, n);
+    lds_barrier();
+  };
+
+  uint64_t st0 = 0, sr0 = 0;
+  if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
+  const int iters = T + NL - 1;
+  int it = 0;
+  for (; it + 1 < iters; it += 2) {
+    step(it, ropA, inA);
+    step(it + 1, ropB, inB);
+  }
+  if (it < iters) step(it, ropA, inA);
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
   }
 
   // ---------------- epilogue: initial-state grads + partial dW slab --------
@@ -321,18 +682,271 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
     if (a.dc0 && is_row && q == 0) a.dc0[((int64_t)layer * B + b) * H + u] = dc[n];
   }
   float* slab = a.slab + (int64_t)blockIdx.x * a.P;
+  if (col_live) {
+    float* dst = slab + (col_in ? a.off_wih[layer] : a.off_whh[layer]) + col_off;
 #pragma unroll
-  for (int j = 0; j < RS; ++j) {
-    const int r = s2 * RS + j;
-    if (k < H) {
-      if (k < Iin) slab[a.off_wih[layer] + (int64_t)r * Iin + k] = dW[j];
-    } else {
-      slab[a.off_whh[layer] + (int64_t)r * H + (k - H)] = dW[j];
-    }
+    for (int j = 0; j < RS; ++j) dst[j * col_stride] = dW[j];
   }
   if (is_row) {
     if (a.off_bih[layer] >= 0) slab[a.off_bih[layer] + lg] = db;
     if (a.off_bhh[layer] >= 0) slab[a.off_bhh[layer] + lg] = db;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward, unit-group lane map (default): a layer group is H*L lanes, lane =
+// (unit u, j) with the L lanes of a unit adjacent.  Lane j owns the row slice
+// [j*RS, (j+1)*RS) (RS = 4H/L) of COLUMN u of both W_hh and W_ih, and the
+// matching dW accumulators.  Per timestep:
+//   row phase : lanes j<4 compute dgate_j[u] (the quad exchanges the saved
+//               activations with DPP), publish it to LDS (parity buffer);
+//   barrier   : the only one of the step;
+//   col phase : every lane reads its RS dgates, forms partial
+//               dh_{t-1}[u] = sum_r W_hh[r][u] dg[r] and d(input)[u], and
+//               accumulates dW[r][u] += dg[r] * input; an L-lane DPP reduction
+//               gives every lane of the group the full dh_{t-1}[u] -- kept in a
+//               register for the next row phase (no LDS round trip, no second
+//               barrier); d(input) goes to the layer below through a parity
+//               buffer that it reads two iterations later (layer lag 2).
+// Packed fp32 FMAs (v_pk_fma_f32) throughout.
+// ---------------------------------------------------------------------------
+template <int H, int L, int NB, bool XLDS>
+__global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBwdArgs a) {
+  constexpr int R = 4 * H;
+  constexpr int RS = R / L;          // rows per lane
+  constexpr int LANES = H * L;
+  static_assert(L >= 4 && RS % 4 == 0, "need >= 4 lanes per unit, float4 row slices");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+
+  const int NL = a.NL, B = a.B, T = a.T, I = a.I;
+  const int tid = threadIdx.x;
+  const int layer = __builtin_amdgcn_readfirstlane(tid / LANES);
+  const int lg = tid - layer * LANES;
+  const int u = lg / L;
+  const int j = lg % L;
+  const int q = j & 3;
+  const bool rowlane = j < 4;
+  const int Iin = layer == 0 ? I : H;
+  const bool top = layer == NL - 1;
+  const int lag = 2 * (NL - 1 - layer);
+
+  // LDS: dg[NB][NL][2][R] | dha[NB][NL][2][H] | xs[NB][T][H]
+  float* dg_s = smem;
+  float* dha_s = dg_s + NB * NL * 2 * R;
+  float* xs = dha_s + NB * NL * 2 * H;
+  auto dgbuf = [&](int n, int l, int p) { return dg_s + ((n * NL + l) * 2 + p) * R; };
+  auto dhabuf = [&](int n, int l, int p) { return dha_s + ((n * NL + l) * 2 + p) * H; };
+
+  // ---- W columns (u) for rows j*RS.., as float2 pairs along rows ----------
+  // Loaded ONCE and shared by the NB sequences a workgroup interleaves; the
+  // grid is persistent over batch tiles (workgroup g handles tiles g, g+G, ...)
+  // and the dW accumulators run across all of them, so a workgroup writes one
+  // slab row however many sequences it processed.
+  const int r0 = j * RS;
+  const bool ih_live = u < Iin;
+  pdrnn_f2 whh[RS / 2], wih[RS / 2], dwhh[RS / 2], dwih[RS / 2];
+  {
+    const float* ph = a.w_hh[layer] + (int64_t)r0 * H + u;
+    const float* pi = a.w_ih[layer] + (int64_t)r0 * Iin + min(u, Iin - 1);
+#pragma unroll
+    for (int rr = 0; rr < RS / 2; ++rr) {
+      whh[rr] = pdrnn_f2{ph[(2 * rr) * H], ph[(2 * rr + 1) * H]};
+      const float x0 = pi[(int64_t)(2 * rr) * Iin], x1 = pi[(int64_t)(2 * rr + 1) * Iin];
+      wih[rr] = ih_live ? pdrnn_f2{x0, x1} : pdrnn_f2{0.f, 0.f};
+      dwhh[rr] = pdrnn_f2{0.f, 0.f};
+      dwih[rr] = pdrnn_f2{0.f, 0.f};
+    }
+  }
+  float db = 0.f;
+  uint64_t st0 = 0, sr0 = 0;
+  if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
+
+  struct Ops { float aq, ct, cp, dout, hprev, xin; };
+  for (int b0 = blockIdx.x * NB; b0 < B; b0 += gridDim.x * NB) {
+    int bs[NB], bsrc[NB];
+    bool valid[NB];
+    float dh[NB], dc[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      valid[n] = b0 + n < B;
+      bs[n] = min(b0 + n, B - 1);  // invalid slots recompute the last sequence, never store
+      bsrc[n] = a.idx ? (int)a.idx[bs[n]] : bs[n];
+      dh[n] = 0.f;
+      if (a.dhn) {
+        if (a.dhn_top_only) dh[n] = top ? a.dhn[(int64_t)bs[n] * H + u] : 0.f;
+        else dh[n] = a.dhn[((int64_t)layer * B + bs[n]) * H + u];
+      }
+      dc[n] = a.dcn ? a.dcn[((int64_t)layer * B + bs[n]) * H + u] : 0.f;
+      if (lg < H) {
+        dhabuf(n, layer, 0)[lg] = 0.f;
+        dhabuf(n, layer, 1)[lg] = 0.f;
+      }
+    }
+    if constexpr (XLDS) {
+      for (int e = tid; e < NB * T * H; e += blockDim.x) {
+        const int n = e / (T * H);
+        const int rem = e - n * T * H;
+        const int t = rem / H, kk = rem - t * H;
+        const int bn = a.idx ? (int)a.idx[min(b0 + n, B - 1)] : min(b0 + n, B - 1);
+        const float v = a.x[bn * a.x_sb + (int64_t)t * a.x_st + min(kk, I - 1)];
+        xs[e] = kk < I ? v : 0.f;
+      }
+    }
+
+    // ---- raw per-timestep operands (prefetched 2 steps ahead, masked at use)
+    const float* act_base[NB];
+    const float* hs_own[NB];
+    const float* hs_below[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      act_base[n] = a.act + ((int64_t)layer * B + bs[n]) * T * 5 * H;
+      hs_own[n] = a.hseq + ((int64_t)layer * B + bs[n]) * T * H + u;
+      hs_below[n] = a.hseq + ((int64_t)(layer > 0 ? layer - 1 : 0) * B + bs[n]) * T * H + u;
+    }
+    const bool has_dout = top && a.dout;
+    auto load_ops = [&](int n, int t) {
+      const int tc = min(max(t, 0), T - 1);
+      const float* act = act_base[n] + (int64_t)tc * 5 * H + u;
+      Ops o;
+      o.aq = act[q * H];
+      o.ct = act[4 * H];
+      const float* cpp = tc > 0 ? act - H : (a.c0 ? a.c0 + ((int64_t)layer * B + bs[n]) * H + u : act);
+      o.cp = *cpp;
+      o.dout = has_dout ? a.dout[bs[n] * a.d_sb + (int64_t)tc * a.d_st + u] : 0.f;
+      const float* hp = tc > 0 ? hs_own[n] + (int64_t)(tc - 1) * H
+                               : (a.h0 ? a.h0 + ((int64_t)layer * B + bs[n]) * H + u : hs_own[n]);
+      o.hprev = *hp;
+      if (XLDS && layer == 0) {
+        o.xin = 0.f;
+      } else {
+        const float* xp = layer == 0 ? a.x + bsrc[n] * a.x_sb + (int64_t)tc * a.x_st + min(u, I - 1)
+                                     : hs_below[n] + (int64_t)tc * H;
+        o.xin = *xp;
+      }
+      return o;
+    };
+
+    const int t_first = T - 1 + lag;
+    Ops opA[NB], opB[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      opA[n] = load_ops(n, t_first);
+      opB[n] = load_ops(n, t_first - 1);
+    }
+    __syncthreads();
+
+    auto step = [&](int it, Ops* op) {
+      const int t = t_first - it;
+      const bool active = t >= 0 && t < T;
+      const int p = it & 1;
+      // ---------------- row phase ----------------
+      if (active) {
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          const float cp = (t > 0 || a.c0) ? op[n].cp : 0.f;
+          float dht = dh[n] + (has_dout ? op[n].dout : 0.f);
+          if (!top) dht += dhabuf(n, layer, p)[u];  // written by the layer above 2 iterations ago
+          const float ig = quad_bcast(op[n].aq, 0), fg = quad_bcast(op[n].aq, 1);
+          const float gg = quad_bcast(op[n].aq, 2), og = quad_bcast(op[n].aq, 3);
+          const float tc = tanhf_fast(op[n].ct);
+          const float dcp = fmaf(dht * og, 1.f - tc * tc, dc[n]);
+          const float d_i = dcp * gg * ig * (1.f - ig);
+          const float d_f = dcp * cp * fg * (1.f - fg);
+          const float d_g = dcp * ig * (1.f - gg * gg);
+          const float d_o = dht * tc * og * (1.f - og);
+          const float dgv = q == 0 ? d_i : (q == 1 ? d_f : (q == 2 ? d_g : d_o));
+          dc[n] = dcp * fg;
+          if (rowlane) {
+            dgbuf(n, layer, p)[q * H + u] = dgv;
+            if (valid[n]) db += dgv;
+          }
+        }
+      }
+      lds_barrier();
+      // ---------------- column phase ----------------
+      if (active) {
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          const float hprev = (t > 0 || a.h0) ? op[n].hprev : 0.f;
+          float xin;
+          if (XLDS && layer == 0) xin = xs[((int64_t)n * T + t) * H + u];
+          else xin = (layer > 0 || u < I) ? op[n].xin : 0.f;
+          // an invalid slot still runs the recurrence (uniform control flow)
+          // but contributes nothing to dW
+          const float hw = valid[n] ? hprev : 0.f, xw = valid[n] ? xin : 0.f;
+          const float4* g4 = reinterpret_cast<const float4*>(dgbuf(n, layer, p) + r0);
+          pdrnn_f2 sh[2] = {{0.f, 0.f}, {0.f, 0.f}}, sx[2] = {{0.f, 0.f}, {0.f, 0.f}};
+          const pdrnn_f2 hb = {hw, hw}, xb = {xw, xw};
+#pragma unroll
+          for (int r4 = 0; r4 < RS / 4; ++r4) {
+            const float4 g = g4[r4];
+            const pdrnn_f2 g01 = {g.x, g.y}, g23 = {g.z, g.w};
+            sh[0] = __builtin_elementwise_fma(whh[2 * r4], g01, sh[0]);
+            sh[1] = __builtin_elementwise_fma(whh[2 * r4 + 1], g23, sh[1]);
+            sx[0] = __builtin_elementwise_fma(wih[2 * r4], g01, sx[0]);
+            sx[1] = __builtin_elementwise_fma(wih[2 * r4 + 1], g23, sx[1]);
+            dwhh[2 * r4] = __builtin_elementwise_fma(g01, hb, dwhh[2 * r4]);
+            dwhh[2 * r4 + 1] = __builtin_elementwise_fma(g23, hb, dwhh[2 * r4 + 1]);
+            dwih[2 * r4] = __builtin_elementwise_fma(g01, xb, dwih[2 * r4]);
+            dwih[2 * r4 + 1] = __builtin_elementwise_fma(g23, xb, dwih[2 * r4 + 1]);
+          }
+          const pdrnn_f2 shs = sh[0] + sh[1], sxs = sx[0] + sx[1];
+          dh[n] = group_sum<L>(shs.x + shs.y);  // dh_{t-1}[u] on every lane of the unit
+          const float dx = group_sum<L>(sxs.x + sxs.y);
+          if (j == 0) {
+            if (layer > 0) dhabuf(n, layer - 1, p)[u] = dx;  // consumed by layer-1 at it+2 (same parity)
+            else if (a.dx && u < I && valid[n]) a.dx[bs[n] * a.dx_sb + (int64_t)t * a.dx_st + u] = dx;
+          }
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < NB; ++n) op[n] = load_ops(n, t - 2);  // refill for two steps ahead
+    };
+
+    const int iters = T + 2 * (NL - 1);
+    int it = 0;
+    for (; it + 1 < iters; it += 2) {
+      step(it, opA);
+      step(it + 1, opB);
+    }
+    if (it < iters) step(it, opA);
+
+    if (j == 0) {
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        if (!valid[n]) continue;
+        if (a.dh0) a.dh0[((int64_t)layer * B + bs[n]) * H + u] = dh[n];
+        if (a.dc0) a.dc0[((int64_t)layer * B + bs[n]) * H + u] = dc[n];
+      }
+    }
+    __syncthreads();  // LDS is reused by the next tile
+  }
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+  }
+
+  // ---------------- epilogue: this workgroup's partial dW / db ----------
+  float* slab = a.slab + (int64_t)blockIdx.x * a.P;
+  {
+    float* dst = slab + a.off_whh[layer] + (int64_t)r0 * H + u;
+#pragma unroll
+    for (int rr = 0; rr < RS / 2; ++rr) {
+      dst[(2 * rr) * H] = dwhh[rr].x;
+      dst[(2 * rr + 1) * H] = dwhh[rr].y;
+    }
+  }
+  if (ih_live) {
+    float* dst = slab + a.off_wih[layer] + (int64_t)r0 * Iin + u;
+#pragma unroll
+    for (int rr = 0; rr < RS / 2; ++rr) {
+      dst[(int64_t)(2 * rr) * Iin] = dwih[rr].x;
+      dst[(int64_t)(2 * rr + 1) * Iin] = dwih[rr].y;
+    }
+  }
+  if (rowlane) {
+    if (a.off_bih[layer] >= 0) slab[a.off_bih[layer] + q * H + u] = db;
+    if (a.off_bhh[layer] >= 0) slab[a.off_bhh[layer] + q * H + u] = db;
   }
 }
 
@@ -364,13 +978,116 @@ __global__ void slab_reduce_pass2(const float* __restrict__ work, int64_t P, int
   out[p] = beta == 0.f ? acc : fmaf(beta, out[p], acc);
 }
 
+// pass 1 over two slabs side by side: columns [0, PA) from A, [PA, PA+PB) from B
+__global__ void slab2_reduce_pass1(const float* __restrict__ A, int64_t rowsA, int64_t PA,
+                                   const float* __restrict__ Bs, int64_t rowsB, int64_t PB,
+                                   float* __restrict__ work, int split) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int sp = blockIdx.y;
+  const int64_t P = PA + PB;
+  if (p >= P) return;
+  const bool inA = p < PA;
+  const float* src = inA ? A + p : Bs + (p - PA);
+  const int64_t ld = inA ? PA : PB;
+  const int64_t rows = inA ? rowsA : rowsB;
+  const int64_t r0 = rows * sp / split, r1 = rows * (sp + 1) / split;
+  float acc0 = 0.f, acc1 = 0.f;
+  int64_t r = r0;
+  for (; r + 2 <= r1; r += 2) {
+    acc0 += src[r * ld];
+    acc1 += src[(r + 1) * ld];
+  }
+  if (r < r1) acc0 += src[r * ld];
+  work[(int64_t)sp * P + p] = acc0 + acc1;
+}
+
+__global__ void slab_reduce_pass2_split(const float* __restrict__ work, int64_t P, int64_t Pa, int split,
+                                        float* __restrict__ out_a, float* __restrict__ out_b) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  float acc = 0.f;
+  for (int sp = 0; sp < split; ++sp) acc += work[(int64_t)sp * P + p];
+  if (p < Pa) out_a[p] = acc;
+  else out_b[p - Pa] = acc;
+}
+
 template <int H, int S, int NB, bool SAVE>
 hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   constexpr int LANES = H * S;
   const int grid = (a->B + NB - 1) / NB;
   const int block = a->NL * LANES;
   const size_t lds = sizeof(float) * NB * a->NL * 2 * (2 * H);
-  hipLaunchKernelGGL((lstm_small_fwd_kernel<H, S, NB, SAVE>), dim3(grid), dim3(block), lds, st, *a);
+  const size_t xbytes = sizeof(float) * (size_t)NB * a->T * H;
+  if (xbytes <= (size_t)kXldsBytes)
+    hipLaunchKernelGGL((lstm_small_fwd_kernel<H, S, NB, SAVE, true>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  else
+    hipLaunchKernelGGL((lstm_small_fwd_kernel<H, S, NB, SAVE, false>), dim3(grid), dim3(block), lds, st, *a);
+  return hipGetLastError();
+}
+
+template <int H, int NB, bool SAVE>
+hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
+  const int grid = (a->B + NB - 1) / NB;
+  const int block = a->NL * 4 * H;
+  const size_t lds = sizeof(float) * NB * a->NL * 2 * (2 * H);
+  const size_t xbytes = sizeof(float) * (size_t)NB * a->T * H;
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  if constexpr (SAVE) {
+    if (a->head_w) {
+      if (a->C > 16) return hipErrorInvalidValue;
+      if (xl) hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, NB, true, true, true>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+      else hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, NB, true, false, true>), dim3(grid), dim3(block), lds, st, *a);
+      return hipGetLastError();
+    }
+  }
+  if (xl)
+    hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, NB, SAVE, true, false>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  else
+    hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, NB, SAVE, false, false>), dim3(grid), dim3(block), lds, st, *a);
+  return hipGetLastError();
+}
+
+// Persistent grid for the backward: as many workgroups as can be resident
+// (occupancy query x CU count), capped by the number of batch tiles.
+template <int H, int L, int NB, bool XLDS>
+int bwd_gs_resident(int NL, size_t lds) {
+  // one-entry cache per instantiation (the query costs a driver round trip)
+  static thread_local int c_dev = -1, c_nl = -1, c_val = 0;
+  static thread_local size_t c_lds = 0;
+  int per_cu = 0, cus = 0, dev = 0;
+  hipGetDevice(&dev);
+  if (dev == c_dev && NL == c_nl && lds == c_lds) return c_val;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_small_bwd_gs_kernel<H, L, NB, XLDS>, NL * H * L, lds);
+  if (per_cu < 1) per_cu = 1;
+  if (cus < 1) cus = 1;
+  c_dev = dev; c_nl = NL; c_lds = lds; c_val = per_cu * cus;
+  return c_val;
+}
+
+template <int H, int NB>
+size_t bwd_gs_lds(int NL) { return sizeof(float) * NB * NL * 2 * (4 * H + H); }
+template <int H, int NB>
+size_t bwd_gs_xbytes(int T) { return sizeof(float) * (size_t)NB * T * H; }
+
+template <int H, int L, int NB>
+int bwd_gs_grid(const PdrnnLstmSmallBwdArgs* a) {
+  const size_t lds = bwd_gs_lds<H, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
+  const int cap = xbytes <= (size_t)kXldsBytes ? bwd_gs_resident<H, L, NB, true>(a->NL, lds + xbytes)
+                                               : bwd_gs_resident<H, L, NB, false>(a->NL, lds);
+  const int tiles = (a->B + NB - 1) / NB;
+  return tiles < cap ? tiles : cap;
+}
+
+template <int H, int L, int NB>
+hipError_t launch_bwd_gs(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid) {
+  const int block = a->NL * H * L;
+  const size_t lds = bwd_gs_lds<H, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
+  if (grid <= 0) grid = bwd_gs_grid<H, L, NB>(a);
+  if (xbytes <= (size_t)kXldsBytes)
+    hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, NB, true>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  else
+    hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, NB, false>), dim3(grid), dim3(block), lds, st, *a);
   return hipGetLastError();
 }
 
@@ -380,44 +1097,83 @@ hipError_t launch_bwd(const PdrnnLstmSmallBwdArgs* a, hipStream_t st) {
   const int grid = (a->B + NB - 1) / NB;
   const int block = a->NL * G;
   const size_t lds = sizeof(float) * NB * a->NL * (4 * H + 2 * H);
-  hipLaunchKernelGGL((lstm_small_bwd_kernel<H, S2, NB>), dim3(grid), dim3(block), lds, st, *a);
+  const size_t xbytes = sizeof(float) * (size_t)NB * a->T * H;
+  if (xbytes <= (size_t)kXldsBytes)
+    hipLaunchKernelGGL((lstm_small_bwd_kernel<H, S2, NB, true>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  else
+    hipLaunchKernelGGL((lstm_small_bwd_kernel<H, S2, NB, false>), dim3(grid), dim3(block), lds, st, *a);
   return hipGetLastError();
 }
 
-// Forward split S per hidden size: lanes per layer = H*S must be a multiple of
-// 64 and 4*2H/S weight registers must stay <= 128.
-template <int H> struct FwdSplit;
-template <> struct FwdSplit<16> { static constexpr int S = 4; };
-template <> struct FwdSplit<32> { static constexpr int S = 2; };
-template <> struct FwdSplit<64> { static constexpr int S = 4; };
-// Backward split S2: lanes per layer = 2H*S2, rows per column lane 4H/S2.
-template <int H> struct BwdSplit;
-template <> struct BwdSplit<16> { static constexpr int S2 = 2; };
-template <> struct BwdSplit<32> { static constexpr int S2 = 2; };
-template <> struct BwdSplit<64> { static constexpr int S2 = 4; };
+// Valid lane splits.  Forward: lanes per layer H*S (multiple of 64),
+// K slice 2H/S float4-aligned and inside one half of [x | h].  Backward:
+// lanes per layer 2H*S2, row slice 4H/S2 a multiple of 16.  Workgroup size
+// NL * lanes <= 512 (launch bound: keeps 256 VGPRs per lane available).
+constexpr bool fwd_ok(int H, int S) {
+  return (H * S) % 64 == 0 && (2 * H / S) % 4 == 0 && H % (2 * H / S) == 0;
+}
+constexpr bool bwd_ok(int H, int S2) { return S2 >= 2 && (4 * H / S2) % 16 == 0 && (2 * H * S2) % 64 == 0; }
 
-template <int H>
-hipError_t dispatch_fwd(const PdrnnLstmSmallFwdArgs* a, int nb, int save, hipStream_t st) {
-  constexpr int S = FwdSplit<H>::S;
-  if (save) {
-    if (nb == 1) return launch_fwd<H, S, 1, true>(a, st);
-    if (nb == 2) return launch_fwd<H, S, 2, true>(a, st);
-    if (nb == 4) return launch_fwd<H, S, 4, true>(a, st);
+template <int H, int S>
+hipError_t dispatch_fwd_s(const PdrnnLstmSmallFwdArgs* a, int nb, int save, hipStream_t st) {
+  if constexpr (!fwd_ok(H, S)) {
+    return hipErrorInvalidValue;
   } else {
-    if (nb == 1) return launch_fwd<H, S, 1, false>(a, st);
-    if (nb == 2) return launch_fwd<H, S, 2, false>(a, st);
-    if (nb == 4) return launch_fwd<H, S, 4, false>(a, st);
+    if (a->NL * H * S > 512) return hipErrorInvalidConfiguration;
+    if (save) {
+      if (nb == 1) return launch_fwd<H, S, 1, true>(a, st);
+      if (nb == 2) return launch_fwd<H, S, 2, true>(a, st);
+    } else {
+      if (nb == 1) return launch_fwd<H, S, 1, false>(a, st);
+      if (nb == 2) return launch_fwd<H, S, 2, false>(a, st);
+    }
+    return hipErrorInvalidValue;
   }
-  return hipErrorInvalidValue;
 }
 
 template <int H>
-hipError_t dispatch_bwd(const PdrnnLstmSmallBwdArgs* a, int nb, hipStream_t st) {
-  constexpr int S2 = BwdSplit<H>::S2;
-  if (nb == 1) return launch_bwd<H, S2, 1>(a, st);
-  if (nb == 2) return launch_bwd<H, S2, 2>(a, st);
-  if (nb == 4) return launch_bwd<H, S2, 4>(a, st);
-  return hipErrorInvalidValue;
+hipError_t dispatch_fwd(const PdrnnLstmSmallFwdArgs* a, int nb, int split, int save, hipStream_t st) {
+  if (split == 1) {  // gate-split map (4 lanes per unit, one gate each)
+    if (a->NL * 4 * H > 512) return hipErrorInvalidConfiguration;
+    if (save) return nb == 2 ? launch_fwd_gs<H, 2, true>(a, st) : launch_fwd_gs<H, 1, true>(a, st);
+    return nb == 2 ? launch_fwd_gs<H, 2, false>(a, st) : launch_fwd_gs<H, 1, false>(a, st);
+  }
+  switch (split) {
+    case 2: return dispatch_fwd_s<H, 2>(a, nb, save, st);
+    case 4: return dispatch_fwd_s<H, 4>(a, nb, save, st);
+    case 8: return dispatch_fwd_s<H, 8>(a, nb, save, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int H, int S2>
+hipError_t dispatch_bwd_s(const PdrnnLstmSmallBwdArgs* a, int nb, hipStream_t st) {
+  if constexpr (!bwd_ok(H, S2)) {
+    return hipErrorInvalidValue;
+  } else {
+    if (a->NL * 2 * H * S2 > 512) return hipErrorInvalidConfiguration;
+    if (nb == 1) return launch_bwd<H, S2, 1>(a, st);
+    return hipErrorInvalidValue;
+  }
+}
+
+template <int H>
+hipError_t dispatch_bwd(const PdrnnLstmSmallBwdArgs* a, int nb, int split, hipStream_t st, int grid_hint) {
+  if (split == 1) {  // unit-group map, L lanes per unit (row slices of 32)
+    constexpr int L = H >= 64 ? 8 : 4;
+    if (a->NL * H * L > 512) return hipErrorInvalidConfiguration;
+    switch (nb) {
+      case 1: return launch_bwd_gs<H, L, 1>(a, st, grid_hint);
+      case 2: return launch_bwd_gs<H, L, 2>(a, st, grid_hint);
+      case 3: return launch_bwd_gs<H, L, 3>(a, st, grid_hint);
+      default: return hipErrorInvalidConfiguration;
+    }
+  }
+  switch (split) {
+    case 2: return dispatch_bwd_s<H, 2>(a, nb, st);
+    case 4: return dispatch_bwd_s<H, 4>(a, nb, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace
@@ -428,9 +1184,25 @@ extern "C" {
 int pdrnn_lstm_small_supported(int H, int I, int NL) {
   const bool h_ok = H == 16 || H == 32 || H == 64;
   if (!h_ok || I < 1 || I > H || NL < 1 || NL > PDRNN_MAX_LAYERS) return 0;
-  // Workgroup size limit (1024 threads) for the backward: NL * 2H * S2.
-  const int s2 = H == 64 ? 4 : 2;
-  return NL * 2 * H * s2 <= 1024 ? 1 : 0;
+  const int s_min = H == 32 ? 2 : 4;   // smallest valid forward split
+  const int s2_min = H == 64 ? 4 : 2;  // smallest valid backward split
+  return (NL * H * s_min <= 512 && NL * 2 * H * s2_min <= 512) ? 1 : 0;
+}
+
+// Largest split whose workgroup fits: more lanes per unit = shorter
+// per-timestep critical path (latency-bound small batches); the host may
+// request a smaller one for throughput-bound large batches.
+int pdrnn_lstm_small_max_split(int H, int NL, int backward) {
+  if (backward) {
+    if (NL * H * (H >= 64 ? 8 : 4) <= 512) return 1;  // unit-group map
+    for (int s2 = 4; s2 >= 2; s2 /= 2)
+      if (NL * 2 * H * s2 <= 512 && (4 * H / s2) % 16 == 0) return s2;
+    return 0;
+  }
+  if (NL * 4 * H <= 512) return 1;  // gate-split map
+  for (int s = 8; s >= 2; s /= 2)
+    if (NL * H * s <= 512 && (H * s) % 64 == 0 && (2 * H / s) % 4 == 0 && H % (2 * H / s) == 0) return s;
+  return 0;
 }
 
 int pdrnn_lstm_small_grid(int H, int B, int nb) {
@@ -438,23 +1210,45 @@ int pdrnn_lstm_small_grid(int H, int B, int nb) {
   return (B + nb - 1) / nb;
 }
 
-hipError_t pdrnn_lstm_small_fwd(const PdrnnLstmSmallFwdArgs* a, int H, int nb, int save,
+hipError_t pdrnn_lstm_small_fwd(const PdrnnLstmSmallFwdArgs* a, int H, int nb, int split, int save,
                                 hipStream_t stream) {
   switch (H) {
-    case 16: return pdrnn::dispatch_fwd<16>(a, nb, save, stream);
-    case 32: return pdrnn::dispatch_fwd<32>(a, nb, save, stream);
-    case 64: return pdrnn::dispatch_fwd<64>(a, nb, save, stream);
+    case 16: return pdrnn::dispatch_fwd<16>(a, nb, split, save, stream);
+    case 32: return pdrnn::dispatch_fwd<32>(a, nb, split, save, stream);
+    case 64: return pdrnn::dispatch_fwd<64>(a, nb, split, save, stream);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t pdrnn_lstm_small_bwd(const PdrnnLstmSmallBwdArgs* a, int H, int nb, hipStream_t stream) {
+hipError_t pdrnn_lstm_small_bwd(const PdrnnLstmSmallBwdArgs* a, int H, int nb, int split, int grid,
+                                hipStream_t stream) {
   switch (H) {
-    case 16: return pdrnn::dispatch_bwd<16>(a, nb, stream);
-    case 32: return pdrnn::dispatch_bwd<32>(a, nb, stream);
-    case 64: return pdrnn::dispatch_bwd<64>(a, nb, stream);
+    case 16: return pdrnn::dispatch_bwd<16>(a, nb, split, stream, grid);
+    case 32: return pdrnn::dispatch_bwd<32>(a, nb, split, stream, grid);
+    case 64: return pdrnn::dispatch_bwd<64>(a, nb, split, stream, grid);
     default: return hipErrorInvalidValue;
   }
+}
+
+// Slab rows (= grid) the backward will use for (H, NL, T, B, split).
+int pdrnn_lstm_small_bwd_grid(int H, int NL, int T, int B, int nb, int split) {
+  if (split != 1) return (B + nb - 1) / nb;
+  PdrnnLstmSmallBwdArgs a{};
+  a.NL = NL; a.T = T; a.B = B;
+#define PDRNN_BWD_GRID(HH, LL)                                   \
+  switch (nb) {                                                  \
+    case 1: return pdrnn::bwd_gs_grid<HH, LL, 1>(&a);            \
+    case 2: return pdrnn::bwd_gs_grid<HH, LL, 2>(&a);            \
+    case 3: return pdrnn::bwd_gs_grid<HH, LL, 3>(&a);            \
+    default: return -1;                                          \
+  }
+  switch (H) {
+    case 16: PDRNN_BWD_GRID(16, 4)
+    case 32: PDRNN_BWD_GRID(32, 4)
+    case 64: PDRNN_BWD_GRID(64, 8)
+    default: return -1;
+  }
+#undef PDRNN_BWD_GRID
 }
 
 hipError_t pdrnn_slab_reduce(const float* slab, int64_t rows, int64_t P, float* out, float beta,
@@ -468,6 +1262,34 @@ hipError_t pdrnn_slab_reduce(const float* slab, int64_t rows, int64_t P, float* 
   PDRNN_HIP_CHECK(hipGetLastError());
   dim3 g2((unsigned)((P + threads - 1) / threads));
   hipLaunchKernelGGL(pdrnn::slab_reduce_pass2, g2, dim3(threads), 0, stream, work, P, split, out, beta);
+  return hipGetLastError();
+}
+
+hipError_t pdrnn_slab_reduce2(const float* slab, int64_t rows, int64_t P, int64_t P_a, float* out_a,
+                              float* out_b, float* work, int split, hipStream_t stream) {
+  if (split < 1) split = 1;
+  if (split > 64) split = 64;
+  if (split > rows) split = (int)rows > 0 ? (int)rows : 1;
+  const int threads = 256;
+  dim3 g1((unsigned)((P + threads - 1) / threads), (unsigned)split);
+  hipLaunchKernelGGL(pdrnn::slab_reduce_pass1, g1, dim3(threads), 0, stream, slab, rows, P, work, split);
+  PDRNN_HIP_CHECK(hipGetLastError());
+  dim3 g2((unsigned)((P + threads - 1) / threads));
+  hipLaunchKernelGGL(pdrnn::slab_reduce_pass2_split, g2, dim3(threads), 0, stream, work, P, P_a, split, out_a, out_b);
+  return hipGetLastError();
+}
+
+hipError_t pdrnn_slab2_reduce(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB, int64_t PB,
+                              int64_t n_out, float* out, float* out_tail, float* work, int split, hipStream_t stream) {
+  if (split < 1) split = 1;
+  if (split > 64) split = 64;
+  const int64_t P = PA + PB;
+  const int threads = 256;
+  dim3 g1((unsigned)((P + threads - 1) / threads), (unsigned)split);
+  hipLaunchKernelGGL(pdrnn::slab2_reduce_pass1, g1, dim3(threads), 0, stream, A, rowsA, PA, Bs, rowsB, PB, work, split);
+  PDRNN_HIP_CHECK(hipGetLastError());
+  dim3 g2((unsigned)((P + threads - 1) / threads));
+  hipLaunchKernelGGL(pdrnn::slab_reduce_pass2_split, g2, dim3(threads), 0, stream, work, P, n_out, split, out, out_tail);
   return hipGetLastError();
 }
 

@@ -75,8 +75,9 @@ class DeviceBatchLoader:
     ``len(loader)`` is the number of batches and ``loader.dataset`` the
     underlying dataset, like ``torch.utils.data.DataLoader``.  Iteration yields
     ``(x, y)`` already on ``device``.  With ``gather_in_kernel=True`` it yields
-    ``(features, y, idx)`` so models that accept an index (the fused LSTM
-    gathers rows inside the kernel) skip the gather copy."""
+    ``(features, labels, idx)`` -- the full device tables plus the batch's row
+    indices -- so models that accept an index (the fused LSTM gathers rows
+    inside the kernel) skip the gather copy."""
 
     def __init__(self, dataset, batch_size: Optional[int], sampler: Optional[ShardedSampler] = None,
                  device: Optional[torch.device] = None, gather_in_kernel: bool = False):
@@ -104,10 +105,11 @@ class DeviceBatchLoader:
         return list(torch.split(idx, self.batch_size))
 
     def make_batch(self, bidx: Tensor):
-        y = self.labels.index_select(0, bidx)
+        """(x, y) gathered batch, or -- in in-kernel gather mode -- the
+        (features, labels, idx) triple: full device tables + this batch's rows."""
         if self.gather_in_kernel:
-            return self.features, y, bidx
-        return self.features.index_select(0, bidx), y
+            return self.features, self.labels, bidx
+        return self.features.index_select(0, bidx), self.labels.index_select(0, bidx)
 
     def __iter__(self):
         for bidx in self.batch_indices():

@@ -29,19 +29,23 @@ def _env_int(name: str, default: int) -> int:
         return default
 
 
-def small_launch_config(batch: int, hidden: int) -> Tuple[int, int]:
-    """(sequences per workgroup) for forward and backward.
+def small_launch_config(batch: int, hidden: int, num_layers: int = 2) -> Tuple[int, int, int, int]:
+    """(nb_fwd, split_fwd, nb_bwd, split_bwd) for the fused small-H kernels.
 
-    Forward: one sequence per workgroup until the grid already over-fills the
-    chip (256 CUs x ~3 resident workgroups), then two.  Backward keeps one
-    sequence per workgroup (register-bound)."""
+    ``nb``: sequences per workgroup (weights in VGPRs are shared by them);
+    ``split``: lanes per hidden unit (more lanes = shorter per-timestep
+    critical path).  Small batches are latency-bound -> widest split, one
+    sequence per workgroup.  Env overrides (for sweeps): PDRNN_LSTM_NB_FWD,
+    PDRNN_LSTM_SPLIT_FWD, PDRNN_LSTM_NB_BWD, PDRNN_LSTM_SPLIT_BWD."""
     nb_fwd = _env_int("PDRNN_LSTM_NB_FWD", 0)
     nb_bwd = _env_int("PDRNN_LSTM_NB_BWD", 0)
-    if nb_fwd not in (1, 2, 4):
-        nb_fwd = 2 if batch >= 2048 else 1
-    if nb_bwd not in (1, 2, 4):
+    sp_fwd = _env_int("PDRNN_LSTM_SPLIT_FWD", 0)
+    sp_bwd = _env_int("PDRNN_LSTM_SPLIT_BWD", 0)
+    if nb_fwd not in (1, 2):
+        nb_fwd = 1
+    if nb_bwd not in (1, 2, 3):
         nb_bwd = 1
-    return nb_fwd, nb_bwd
+    return nb_fwd, sp_fwd, nb_bwd, sp_bwd  # split 0 = widest valid (chosen natively)
 
 
 def fused_small_supported(x: Tensor, hidden: int, num_layers: int, bidirectional: bool,
@@ -65,13 +69,15 @@ class _FusedSmallLSTM(torch.autograd.Function):
     def forward(ctx, x, idx, h0, c0, cfg, *weights):
         hidden, num_layers, batch_first, need_out = cfg
         mod = _ext.native(x.device)
-        nb_fwd, nb_bwd = small_launch_config(x.shape[0] if batch_first else x.shape[1], hidden)
+        batch = idx.numel() if idx is not None else (x.shape[0] if batch_first else x.shape[1])
+        nb_fwd, sp_fwd, nb_bwd, sp_bwd = small_launch_config(batch, hidden, num_layers)
         h0c = h0.contiguous() if h0 is not None else None
         c0c = c0.contiguous() if c0 is not None else None
         out, hn, cn, act = mod.lstm_small_fwd(
-            x, idx, list(weights), h0c, c0c, hidden, num_layers, batch_first, True, need_out, nb_fwd)
+            x, idx, list(weights), h0c, c0c, hidden, num_layers, batch_first, True, need_out, nb_fwd,
+            sp_fwd)
         ctx.set_materialize_grads(False)
-        ctx.cfg = (hidden, num_layers, batch_first, nb_bwd)
+        ctx.cfg = (hidden, num_layers, batch_first, nb_bwd, sp_bwd)
         ctx.save_for_backward(x, idx, h0c, c0c, out, act, *weights)
         top = out[num_layers - 1]  # [B, T, H]
         if not batch_first:
@@ -81,7 +87,7 @@ class _FusedSmallLSTM(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout, dhn, dcn):
         x, idx, h0, c0, hseq, act, *weights = ctx.saved_tensors
-        hidden, num_layers, batch_first, nb_bwd = ctx.cfg
+        hidden, num_layers, batch_first, nb_bwd, sp_bwd = ctx.cfg
         mod = _ext.native(x.device)
         need_dx = ctx.needs_input_grad[0]
         need_dh0 = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
@@ -91,7 +97,7 @@ class _FusedSmallLSTM(torch.autograd.Function):
         dcn = dcn.contiguous() if dcn is not None else None
         dparams, dx, dh0, dc0 = mod.lstm_small_bwd(
             x, idx, list(weights), h0, c0, hseq, act, dout, dhn, dcn, hidden, num_layers,
-            batch_first, need_dx, need_dh0, nb_bwd, None)
+            batch_first, need_dx, need_dh0, nb_bwd, sp_bwd, None)
         grads = []
         off = 0
         for w in weights:
@@ -154,12 +160,13 @@ def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Te
                 x, idx, h0, c0, (hidden, num_layers, batch_first, need_out), *flat)
             return out, hn, cn
         mod = _ext.native(x.device)
-        nb_fwd, _ = small_launch_config(idx.numel() if idx is not None else
-                                        (x.shape[0] if batch_first else x.shape[1]), hidden)
+        nb_fwd, sp_fwd, _, _ = small_launch_config(
+            idx.numel() if idx is not None else (x.shape[0] if batch_first else x.shape[1]), hidden,
+            num_layers)
         out, hn, cn, _ = mod.lstm_small_fwd(
             x, idx, flat, h0.contiguous() if h0 is not None else None,
             c0.contiguous() if c0 is not None else None, hidden, num_layers, batch_first, False,
-            need_out, nb_fwd)
+            need_out, nb_fwd, sp_fwd)
         return out, hn, cn
     from . import lstm_large
     if lstm_large.supported(x, hidden, num_layers):

@@ -85,6 +85,12 @@ class DDPTrainer(DistributedTrainer):
                          batch_size=batch_size, learning_rate=learning_rate,
                          checkpoint_dir=checkpoint_dir, device=device, **kwargs)
 
+    def _grad_sync(self):
+        reducer = self.model.reducer
+        if self._world_size == 1:
+            return None
+        return reducer.all_reduce_now
+
     @staticmethod
     def _device() -> torch.device:
         if torch.cuda.is_available() and torch.distributed.get_backend() == "nccl":
@@ -112,6 +118,14 @@ class HorovodTrainer(DistributedTrainer):
     def _get_optimizer(self, model: nn.Module, lr: float):
         optimizer = super()._get_optimizer(model, lr)
         return hvd.DistributedOptimizer(optimizer, named_parameters=model.named_parameters())
+
+    def _grad_sync(self):
+        if self._world_size == 1:
+            return None
+        flat = next(iter(getattr(self.model, "_pdrnn_flat").values()))
+        # the fused step bypasses the per-tensor hooks: one fused all-reduce of
+        # the whole flat gradient (= Horovod's fusion buffer holding every tensor)
+        return lambda: hvd.allreduce_(flat.grad, average=True)
 
     def train(self, epochs: int):
         hvd.broadcast_parameters(self.model.state_dict(), root_rank=0)

@@ -24,6 +24,7 @@ MI355X-first differences (all behaviour-preserving):
 from __future__ import annotations
 
 import logging
+import os
 import time
 from pathlib import Path
 from typing import Callable, List, Optional, Tuple
@@ -137,16 +138,39 @@ class Trainer:
 
     def _forward(self, batch) -> Tuple[Tensor, Tensor]:
         if len(batch) == 3:
-            features, labels, idx = batch
-            return self.model(features, idx=idx), labels
+            features, labels_all, idx = batch
+            return self.model(features, idx=idx), labels_all.index_select(0, idx)
         data, labels = batch
         return self.model(data), labels
+
+    # ------------------------------------------------------------ fused step
+    def _grad_sync(self):
+        """Gradient synchronisation used by the fused step (None: local)."""
+        return None
+
+    def _fused_step(self):
+        if getattr(self, "_fused", False) is not False:
+            return self._fused
+        self._fused = None
+        if os.environ.get("PDRNN_FUSED_STEP", "1") != "0":
+            from . import fused_step
+            if fused_step.supported(self.model, self.optimizer, self.device):
+                self._fused = fused_step.MotionTrainStep(self.model, self.optimizer, self._grad_sync())
+        return self._fused
 
     def train_batch(self, batch) -> Tuple[Tensor, int]:
         """One optimizer step on one batch; returns (stats [loss, n, correct], batch size).
 
-        This is the exact step ``bench.py`` times."""
-        labels = batch[1]
+        This is the exact step ``bench.py`` times.  On MI355X the motion model
+        runs the fused whole-step path (train/fused_step.py); otherwise the
+        autograd path below."""
+        fused = self._fused_step()
+        if fused is not None and self.model.training:
+            if len(batch) == 3:
+                features, labels_all, idx = batch
+                return fused(features, labels_all, idx), idx.numel()
+            data, labels = batch
+            return fused(data, labels.reshape(-1).contiguous(), None), labels.shape[0]
         self.optimizer.zero_grad()
         output, labels = self._forward(batch)
         labels = labels.long().reshape(-1)

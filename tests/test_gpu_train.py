@@ -1,0 +1,50 @@
+"""GPU: the fused whole-step path equals the autograd path (same math)."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(model, data, fused: bool):
+    from pytorch_distributed_rnn_amd.train.trainer import Trainer
+    t = Trainer(model, data, batch_size=96, learning_rate=2.5e-3, device=torch.device("cuda"))
+    if not fused:
+        t._fused = None  # force the autograd path
+    return t
+
+
+def test_fused_step_matches_autograd():
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    torch.manual_seed(0)
+    train, _, _ = synthetic_motion(n_train=384, n_validation=2, n_test=2, seed=3)
+    m1 = MotionModel(9, 32, 2, 6)
+    m2 = copy.deepcopy(m1)
+    t1, t2 = _trainer(m1, train, True), _trainer(m2, train, False)
+    assert t1._fused_step() is not None, "fused step not selected on GPU"
+    b1, b2 = list(t1.train_loader), list(t2.train_loader)
+    for x1, x2 in zip(b1, b2):
+        s1, n1 = t1.train_batch(x1)
+        s2, n2 = t2.train_batch(x2)
+        assert n1 == n2
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+        assert int(s1[2]) == int(s2[2])
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
+
+
+def test_local_trainer_epoch_on_gpu(tmp_path):
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.train.trainer import Trainer
+    torch.manual_seed(1)
+    train, val, test = synthetic_motion(n_train=960, n_validation=96, n_test=96, seed=1)
+    t = Trainer(MotionModel(9, 32, 2, 6), train, batch_size=480, learning_rate=2.5e-3,
+                validation_set=val, test_set=test, checkpoint_dir=tmp_path)
+    _, th, vh = t.train(3)
+    assert len(th) == 3 and len(vh) == 3
+    assert (tmp_path / "best-model.pt").exists()
+    ck = torch.load(tmp_path / "best-model.pt", weights_only=True)
+    assert "lstm.weight_ih_l0" in ck["model_state"]
