@@ -80,6 +80,17 @@ PDRNN_DEVICE void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Opaque register copy.  Used to build a genuine {v, v} VGPR pair for a
+// v_pk_fma_f32 broadcast operand: left to itself the compiler encodes the
+// broadcast with op_sel on a register pair whose high half is an unrelated
+// register -- often a prefetch still in flight, which then makes the waitcnt
+// pass stall on that load.
+PDRNN_DEVICE float opaque_copy(float v) {
+  float r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
 // Diagnostic cycle stamps (shader clock and 100 MHz real-time clock).
 PDRNN_DEVICE uint64_t stamp_cycles() { return __builtin_amdgcn_s_memtime(); }
 PDRNN_DEVICE uint64_t stamp_real() { return __builtin_amdgcn_s_memrealtime(); }

@@ -710,7 +710,11 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
 //               buffer that it reads two iterations later (layer lag 2).
 // Packed fp32 FMAs (v_pk_fma_f32) throughout.
 // ---------------------------------------------------------------------------
-template <int H, int L, int NB, bool XLDS>
+// LEAN: the fused training-step configuration (zero initial states, loss only
+// through h_T of the top layer, no dx / dh0 / dc0 outputs) with every optional
+// operand folded away at compile time -- fewer live pointers and no per-step
+// branches on the hot path.
+template <int H, int L, int NB, bool XLDS, bool LEAN>
 __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBwdArgs a) {
   constexpr int R = 4 * H;
   constexpr int RS = R / L;          // rows per lane
@@ -729,6 +733,14 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
   const int Iin = layer == 0 ? I : H;
   const bool top = layer == NL - 1;
   const int lag = 2 * (NL - 1 - layer);
+  const float* const h0p = LEAN ? nullptr : a.h0;
+  const float* const c0p = LEAN ? nullptr : a.c0;
+  const float* const doutp = LEAN ? nullptr : a.dout;
+  const float* const dcnp = LEAN ? nullptr : a.dcn;
+  float* const dxp = LEAN ? nullptr : a.dx;
+  float* const dh0p = LEAN ? nullptr : a.dh0;
+  float* const dc0p = LEAN ? nullptr : a.dc0;
+  const bool top_only = LEAN ? true : a.dhn_top_only;
 
   // LDS: dg[NB][NL][2][R] | dha[NB][NL][2][H] | xs[NB][T][H]
   float* dg_s = smem;
@@ -773,10 +785,10 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       bsrc[n] = a.idx ? (int)a.idx[bs[n]] : bs[n];
       dh[n] = 0.f;
       if (a.dhn) {
-        if (a.dhn_top_only) dh[n] = top ? a.dhn[(int64_t)bs[n] * H + u] : 0.f;
+        if (top_only) dh[n] = top ? a.dhn[(int64_t)bs[n] * H + u] : 0.f;
         else dh[n] = a.dhn[((int64_t)layer * B + bs[n]) * H + u];
       }
-      dc[n] = a.dcn ? a.dcn[((int64_t)layer * B + bs[n]) * H + u] : 0.f;
+      dc[n] = dcnp ? dcnp[((int64_t)layer * B + bs[n]) * H + u] : 0.f;
       if (lg < H) {
         dhabuf(n, layer, 0)[lg] = 0.f;
         dhabuf(n, layer, 1)[lg] = 0.f;
@@ -803,26 +815,27 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       hs_own[n] = a.hseq + ((int64_t)layer * B + bs[n]) * T * H + u;
       hs_below[n] = a.hseq + ((int64_t)(layer > 0 ? layer - 1 : 0) * B + bs[n]) * T * H + u;
     }
-    const bool has_dout = top && a.dout;
+    const bool has_dout = top && doutp != nullptr;
+    // Branch-free: every operand is loaded every step through a selected (always
+    // valid) address and masked at use.  A load under a branch makes the
+    // waitcnt pass fall back to vmcnt(0) at the join, which would wait for the
+    // prefetches issued for later steps as well.
     auto load_ops = [&](int n, int t) {
       const int tc = min(max(t, 0), T - 1);
       const float* act = act_base[n] + (int64_t)tc * 5 * H + u;
       Ops o;
       o.aq = act[q * H];
       o.ct = act[4 * H];
-      const float* cpp = tc > 0 ? act - H : (a.c0 ? a.c0 + ((int64_t)layer * B + bs[n]) * H + u : act);
+      const float* cpp = tc > 0 ? act - H : (c0p ? c0p + ((int64_t)layer * B + bs[n]) * H + u : act);
       o.cp = *cpp;
-      o.dout = has_dout ? a.dout[bs[n] * a.d_sb + (int64_t)tc * a.d_st + u] : 0.f;
+      const float* dp = has_dout ? doutp + bs[n] * a.d_sb + (int64_t)tc * a.d_st + u : act;
+      o.dout = *dp;
       const float* hp = tc > 0 ? hs_own[n] + (int64_t)(tc - 1) * H
-                               : (a.h0 ? a.h0 + ((int64_t)layer * B + bs[n]) * H + u : hs_own[n]);
+                               : (h0p ? h0p + ((int64_t)layer * B + bs[n]) * H + u : hs_own[n]);
       o.hprev = *hp;
-      if (XLDS && layer == 0) {
-        o.xin = 0.f;
-      } else {
-        const float* xp = layer == 0 ? a.x + bsrc[n] * a.x_sb + (int64_t)tc * a.x_st + min(u, I - 1)
-                                     : hs_below[n] + (int64_t)tc * H;
-        o.xin = *xp;
-      }
+      const float* xp = layer > 0 ? hs_below[n] + (int64_t)tc * H
+                                  : (XLDS ? act : a.x + bsrc[n] * a.x_sb + (int64_t)tc * a.x_st + min(u, I - 1));
+      o.xin = *xp;
       return o;
     };
 
@@ -843,7 +856,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       if (active) {
 #pragma unroll
         for (int n = 0; n < NB; ++n) {
-          const float cp = (t > 0 || a.c0) ? op[n].cp : 0.f;
+          const float cp = (t > 0 || c0p) ? op[n].cp : 0.f;
           float dht = dh[n] + (has_dout ? op[n].dout : 0.f);
           if (!top) dht += dhabuf(n, layer, p)[u];  // written by the layer above 2 iterations ago
           const float ig = quad_bcast(op[n].aq, 0), fg = quad_bcast(op[n].aq, 1);
@@ -867,7 +880,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       if (active) {
 #pragma unroll
         for (int n = 0; n < NB; ++n) {
-          const float hprev = (t > 0 || a.h0) ? op[n].hprev : 0.f;
+          const float hprev = (t > 0 || h0p) ? op[n].hprev : 0.f;
           float xin;
           if (XLDS && layer == 0) xin = xs[((int64_t)n * T + t) * H + u];
           else xin = (layer > 0 || u < I) ? op[n].xin : 0.f;
@@ -876,7 +889,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
           const float hw = valid[n] ? hprev : 0.f, xw = valid[n] ? xin : 0.f;
           const float4* g4 = reinterpret_cast<const float4*>(dgbuf(n, layer, p) + r0);
           pdrnn_f2 sh[2] = {{0.f, 0.f}, {0.f, 0.f}}, sx[2] = {{0.f, 0.f}, {0.f, 0.f}};
-          const pdrnn_f2 hb = {hw, hw}, xb = {xw, xw};
+          const pdrnn_f2 hb = {hw, opaque_copy(hw)}, xb = {xw, opaque_copy(xw)};
 #pragma unroll
           for (int r4 = 0; r4 < RS / 4; ++r4) {
             const float4 g = g4[r4];
@@ -895,7 +908,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
           const float dx = group_sum<L>(sxs.x + sxs.y);
           if (j == 0) {
             if (layer > 0) dhabuf(n, layer - 1, p)[u] = dx;  // consumed by layer-1 at it+2 (same parity)
-            else if (a.dx && u < I && valid[n]) a.dx[bs[n] * a.dx_sb + (int64_t)t * a.dx_st + u] = dx;
+            else if (dxp && u < I && valid[n]) dxp[bs[n] * a.dx_sb + (int64_t)t * a.dx_st + u] = dx;
           }
         }
       }
@@ -915,8 +928,8 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         if (!valid[n]) continue;
-        if (a.dh0) a.dh0[((int64_t)layer * B + bs[n]) * H + u] = dh[n];
-        if (a.dc0) a.dc0[((int64_t)layer * B + bs[n]) * H + u] = dc[n];
+        if (dh0p) dh0p[((int64_t)layer * B + bs[n]) * H + u] = dh[n];
+        if (dc0p) dc0p[((int64_t)layer * B + bs[n]) * H + u] = dc[n];
       }
     }
     __syncthreads();  // LDS is reused by the next tile
@@ -1047,9 +1060,23 @@ hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Lanes per hidden unit of the unit-group backward: 8 when the workgroup still
+// fits (NL*H*8 <= 512; shorter per-lane row slices), else 4.
+// PDRNN_LSTM_BWD_L=4|8 overrides (sweeps).
+template <int H>
+int bwd_gs_lanes(int NL) {
+  static const int env = [] {
+    const char* e = getenv("PDRNN_LSTM_BWD_L");
+    return e ? atoi(e) : 0;
+  }();
+  if (H == 64) return 8;
+  if (env == 4 || env == 8) return (env == 8 && NL * H * 8 > 512) ? 4 : env;
+  return 4;
+}
+
 // Persistent grid for the backward: as many workgroups as can be resident
 // (occupancy query x CU count), capped by the number of batch tiles.
-template <int H, int L, int NB, bool XLDS>
+template <int H, int L, int NB, bool XLDS, bool LEAN>
 int bwd_gs_resident(int NL, size_t lds) {
   // one-entry cache per instantiation (the query costs a driver round trip)
   static thread_local int c_dev = -1, c_nl = -1, c_val = 0;
@@ -1058,7 +1085,7 @@ int bwd_gs_resident(int NL, size_t lds) {
   hipGetDevice(&dev);
   if (dev == c_dev && NL == c_nl && lds == c_lds) return c_val;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_small_bwd_gs_kernel<H, L, NB, XLDS>, NL * H * L, lds);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_small_bwd_gs_kernel<H, L, NB, XLDS, LEAN>, NL * H * L, lds);
   if (per_cu < 1) per_cu = 1;
   if (cus < 1) cus = 1;
   c_dev = dev; c_nl = NL; c_lds = lds; c_val = per_cu * cus;
@@ -1070,11 +1097,19 @@ size_t bwd_gs_lds(int NL) { return sizeof(float) * NB * NL * 2 * (4 * H + H); }
 template <int H, int NB>
 size_t bwd_gs_xbytes(int T) { return sizeof(float) * (size_t)NB * T * H; }
 
+inline bool bwd_lean(const PdrnnLstmSmallBwdArgs* a) {
+  return !a->h0 && !a->c0 && !a->dout && !a->dcn && !a->dx && !a->dh0 && !a->dc0 && a->dhn && a->dhn_top_only;
+}
+
 template <int H, int L, int NB>
 int bwd_gs_grid(const PdrnnLstmSmallBwdArgs* a) {
   const size_t lds = bwd_gs_lds<H, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
-  const int cap = xbytes <= (size_t)kXldsBytes ? bwd_gs_resident<H, L, NB, true>(a->NL, lds + xbytes)
-                                               : bwd_gs_resident<H, L, NB, false>(a->NL, lds);
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  int cap;
+  if (bwd_lean(a)) cap = xl ? bwd_gs_resident<H, L, NB, true, true>(a->NL, lds + xbytes)
+                            : bwd_gs_resident<H, L, NB, false, true>(a->NL, lds);
+  else cap = xl ? bwd_gs_resident<H, L, NB, true, false>(a->NL, lds + xbytes)
+                : bwd_gs_resident<H, L, NB, false, false>(a->NL, lds);
   const int tiles = (a->B + NB - 1) / NB;
   return tiles < cap ? tiles : cap;
 }
@@ -1084,10 +1119,14 @@ hipError_t launch_bwd_gs(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int gri
   const int block = a->NL * H * L;
   const size_t lds = bwd_gs_lds<H, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
   if (grid <= 0) grid = bwd_gs_grid<H, L, NB>(a);
-  if (xbytes <= (size_t)kXldsBytes)
-    hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, NB, true>), dim3(grid), dim3(block), lds + xbytes, st, *a);
-  else
-    hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, NB, false>), dim3(grid), dim3(block), lds, st, *a);
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  if (bwd_lean(a)) {
+    if (xl) hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, NB, true, true>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+    else hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, NB, false, true>), dim3(grid), dim3(block), lds, st, *a);
+  } else {
+    if (xl) hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, NB, true, false>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+    else hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, NB, false, false>), dim3(grid), dim3(block), lds, st, *a);
+  }
   return hipGetLastError();
 }
 
@@ -1159,15 +1198,34 @@ hipError_t dispatch_bwd_s(const PdrnnLstmSmallBwdArgs* a, int nb, hipStream_t st
 
 template <int H>
 hipError_t dispatch_bwd(const PdrnnLstmSmallBwdArgs* a, int nb, int split, hipStream_t st, int grid_hint) {
-  if (split == 1) {  // unit-group map, L lanes per unit (row slices of 32)
-    constexpr int L = H >= 64 ? 8 : 4;
-    if (a->NL * H * L > 512) return hipErrorInvalidConfiguration;
-    switch (nb) {
-      case 1: return launch_bwd_gs<H, L, 1>(a, st, grid_hint);
-      case 2: return launch_bwd_gs<H, L, 2>(a, st, grid_hint);
-      case 3: return launch_bwd_gs<H, L, 3>(a, st, grid_hint);
-      default: return hipErrorInvalidConfiguration;
+  if (split == 1) {  // unit-group map, L lanes per unit (row slices of 4H/L)
+    if (bwd_gs_lanes<H>(a->NL) == 8) {
+      if constexpr (H <= 32) {
+        switch (nb) {
+          case 1: return launch_bwd_gs<H, 8, 1>(a, st, grid_hint);
+          case 2: return launch_bwd_gs<H, 8, 2>(a, st, grid_hint);
+          case 3: return launch_bwd_gs<H, 8, 3>(a, st, grid_hint);
+          default: return hipErrorInvalidConfiguration;
+        }
+      }
+      if constexpr (H == 64) {
+        switch (nb) {
+          case 1: return launch_bwd_gs<H, 8, 1>(a, st, grid_hint);
+          default: return hipErrorInvalidConfiguration;
+        }
+      }
     }
+    constexpr int L = 4;
+    if constexpr (H <= 32) {
+      if (a->NL * H * L > 512) return hipErrorInvalidConfiguration;
+      switch (nb) {
+        case 1: return launch_bwd_gs<H, L, 1>(a, st, grid_hint);
+        case 2: return launch_bwd_gs<H, L, 2>(a, st, grid_hint);
+        case 3: return launch_bwd_gs<H, L, 3>(a, st, grid_hint);
+        default: return hipErrorInvalidConfiguration;
+      }
+    }
+    return hipErrorInvalidConfiguration;
   }
   switch (split) {
     case 2: return dispatch_bwd_s<H, 2>(a, nb, st);
@@ -1243,9 +1301,15 @@ int pdrnn_lstm_small_bwd_grid(int H, int NL, int T, int B, int nb, int split) {
     default: return -1;                                          \
   }
   switch (H) {
-    case 16: PDRNN_BWD_GRID(16, 4)
-    case 32: PDRNN_BWD_GRID(32, 4)
-    case 64: PDRNN_BWD_GRID(64, 8)
+    case 16:
+      if (pdrnn::bwd_gs_lanes<16>(NL) == 8) { PDRNN_BWD_GRID(16, 8) }
+      PDRNN_BWD_GRID(16, 4)
+    case 32:
+      if (pdrnn::bwd_gs_lanes<32>(NL) == 8) { PDRNN_BWD_GRID(32, 8) }
+      PDRNN_BWD_GRID(32, 4)
+    case 64:
+      if (nb != 1) return -1;
+      return pdrnn::bwd_gs_grid<64, 8, 1>(&a);
     default: return -1;
   }
 #undef PDRNN_BWD_GRID
