@@ -46,6 +46,12 @@ class _PyComm:
     def all_gather(self, out, inp):
         self._works.append(dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True))
 
+    def send(self, t, peer):
+        self._works.append(dist.isend(t, dist.get_global_rank(self.group, peer), group=self.group))
+
+    def recv(self, t, peer):
+        self._works.append(dist.irecv(t, dist.get_global_rank(self.group, peer), group=self.group))
+
     def wait(self):
         for w in self._works:
             w.wait()
