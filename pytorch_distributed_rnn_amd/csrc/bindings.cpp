@@ -441,6 +441,137 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
   return dw;
 }
 
+
+// ---------------------------------------------------------------------------
+// Large-H LSTM layer (both directions in one launch per step).
+// ---------------------------------------------------------------------------
+int dtype_code(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "16-bit (bf16/fp16) tensor expected");
+  return t.scalar_type() == at::kBFloat16 ? 0 : 1;
+}
+const uint16_t* u16(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* u16m(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const uint16_t* opt_u16(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<const uint16_t*>(t->data_ptr()) : nullptr;
+}
+
+// xp: [T, B, ndir*4H] (16-bit, bias included, gate-interleaved per direction)
+// w:  ndir x [4H, H] gate-interleaved W_hh;  h0: [ndir, B, H] 16-bit;  c0: [ndir, B, H] f32
+// returns hseq [T, B, ndir*H], cseq [ndir, T, B, H] f32, acts [ndir, T, B, 4H]
+std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& w, const optional<Tensor>& h0,
+                                   const optional<Tensor>& c0, int64_t H, int64_t reverse_mask, int64_t tile) {
+  CHECK_HIP_TENSOR(xp);
+  const c10::DeviceGuard guard(xp.device());
+  const int dt = dtype_code(xp);
+  const int ndir = (int)w.size();
+  TORCH_CHECK(ndir == 1 || ndir == 2, "1 or 2 directions");
+  TORCH_CHECK(pdrnn_lstm_large_supported((int)H), "large LSTM path needs H % 64 == 0");
+  TORCH_CHECK(xp.dim() == 3 && xp.size(2) == ndir * 4 * H && xp.stride(2) == 1, "xp must be [T, B, ndir*4H]");
+  const int64_t T = xp.size(0), B = xp.size(1);
+  TORCH_CHECK(xp.stride(1) == ndir * 4 * H && xp.stride(0) == B * ndir * 4 * H, "xp must be contiguous");
+  for (auto& t : w) {
+    TORCH_CHECK(t.is_contiguous() && t.size(0) == 4 * H && t.size(1) == H && dtype_code(t) == dt, "w: [4H, H] contiguous");
+  }
+  auto o16 = xp.options();
+  auto o32 = xp.options().dtype(at::kFloat);
+  Tensor hseq = at::empty({T, B, ndir * H}, o16);
+  Tensor cseq = at::empty({ndir, T, B, H}, o32);
+  Tensor acts = at::empty({ndir, T, B, 4 * H}, o16);
+  const bool has_h0 = h0.has_value() && h0->defined();
+  const bool has_c0 = c0.has_value() && c0->defined();
+  if (has_h0) TORCH_CHECK(h0->is_contiguous() && dtype_code(*h0) == dt && h0->numel() == ndir * B * H, "h0 [ndir,B,H]");
+  if (has_c0) TORCH_CHECK(c0->is_contiguous() && c0->scalar_type() == at::kFloat && c0->numel() == ndir * B * H, "c0");
+  PdrnnLstmLargeStepArgs a{};
+  a.B = (int)B; a.H = (int)H; a.T = (int)T; a.reverse_mask = (int)reverse_mask;
+  for (int d = 0; d < ndir; ++d) {
+    PdrnnLstmLargeDir& dd = a.dir[d];
+    dd.w = u16(w[d]);
+    dd.xp = u16(xp) + d * 4 * H; dd.xp_sb = ndir * 4 * H; dd.xp_st = B * ndir * 4 * H;
+    dd.h0 = has_h0 ? u16(*h0) + d * B * H : nullptr;
+    dd.c0 = has_c0 ? c0->data_ptr<float>() + d * B * H : nullptr;
+    dd.hseq = u16m(hseq) + d * H; dd.hseq_sb = ndir * H; dd.hseq_st = B * ndir * H;
+    dd.cseq = cseq.data_ptr<float>() + d * T * B * H;
+    dd.acts = u16m(acts) + d * T * B * 4 * H;
+  }
+  hipStream_t st = cur_stream();
+  for (int64_t s = 0; s < T; ++s) {
+    a.step = (int)s;
+    HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 0, dt, (int)tile, st));
+  }
+  return {hseq, cseq, acts};
+}
+
+// Backward of one layer: returns dgates [ndir, T, B, 4H] (16-bit), dh0, dc0
+// [ndir, B, H] f32.  wt: ndir x [H, 4H] (transposed gate-interleaved W_hh).
+std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<Tensor>& dhn,
+                                   const optional<Tensor>& dcn, const std::vector<Tensor>& wt, const Tensor& cseq,
+                                   const Tensor& acts, const optional<Tensor>& c0, int64_t H, int64_t reverse_mask,
+                                   int64_t tile) {
+  CHECK_HIP_TENSOR(acts);
+  const c10::DeviceGuard guard(acts.device());
+  const int dt = dtype_code(acts);
+  const int ndir = (int)wt.size();
+  const int64_t T = acts.size(1), B = acts.size(2);
+  TORCH_CHECK(acts.is_contiguous() && acts.size(0) == ndir && acts.size(3) == 4 * H, "acts [ndir, T, B, 4H]");
+  TORCH_CHECK(cseq.is_contiguous() && cseq.scalar_type() == at::kFloat, "cseq f32");
+  for (auto& t : wt) TORCH_CHECK(t.is_contiguous() && t.size(0) == H && t.size(1) == 4 * H && dtype_code(t) == dt, "wt [H, 4H]");
+  const bool has_dout = dout.has_value() && dout->defined();
+  if (has_dout) {
+    TORCH_CHECK(dtype_code(*dout) == dt && dout->dim() == 3 && dout->size(2) == ndir * H && dout->stride(2) == 1,
+                "dout [T, B, ndir*H]");
+  }
+  auto o16 = acts.options();
+  auto o32 = acts.options().dtype(at::kFloat);
+  Tensor dgates = at::empty({ndir, T, B, 4 * H}, o16);
+  Tensor carry = at::empty({ndir, B, H}, o32);
+  Tensor dh0 = at::empty({ndir, B, H}, o32), dc0 = at::empty({ndir, B, H}, o32);
+  auto f32p = [](const optional<Tensor>& t) -> const float* {
+    if (!(t.has_value() && t->defined())) return nullptr;
+    TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kFloat, "f32 contiguous state grad expected");
+    return t->data_ptr<float>();
+  };
+  const float* dhn_p = f32p(dhn);
+  const float* dcn_p = f32p(dcn);
+  const float* c0_p = f32p(c0);
+  PdrnnLstmLargeStepArgs a{};
+  a.B = (int)B; a.H = (int)H; a.T = (int)T; a.reverse_mask = (int)reverse_mask;
+  for (int d = 0; d < ndir; ++d) {
+    PdrnnLstmLargeDir& dd = a.dir[d];
+    dd.wt = u16(wt[d]);
+    dd.c0 = c0_p ? c0_p + d * B * H : nullptr;
+    dd.cseq = cseq.data_ptr<float>() + d * T * B * H;
+    dd.acts = u16m(acts) + d * T * B * 4 * H;
+    dd.dgates = u16m(dgates) + d * T * B * 4 * H;
+    if (has_dout) {
+      dd.dout = u16(*dout) + d * H; dd.dout_sb = dout->stride(1); dd.dout_st = dout->stride(0);
+    }
+    dd.dhn = dhn_p ? dhn_p + d * B * H : nullptr;
+    dd.dcn = dcn_p ? dcn_p + d * B * H : nullptr;
+    dd.dc_carry = carry.data_ptr<float>() + d * B * H;
+    dd.dh0 = dh0.data_ptr<float>() + d * B * H;
+    dd.dc0 = dc0.data_ptr<float>() + d * B * H;
+  }
+  hipStream_t st = cur_stream();
+  HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, ndir, dt, st));
+  for (int64_t s = 0; s < T; ++s) {
+    a.step = (int)s;
+    HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 1, dt, (int)tile, st));
+  }
+  return {dgates, dh0, dc0};
+}
+
+// C[M, N] f32 = A[M, K] Bt[N, K]^T on the MFMA core (tests).
+Tensor gemm_nt(const Tensor& A, const Tensor& Bt) {
+  CHECK_HIP_TENSOR(A);
+  const c10::DeviceGuard guard(A.device());
+  const int dt = dtype_code(A);
+  TORCH_CHECK(A.is_contiguous() && Bt.is_contiguous() && A.size(1) == Bt.size(1) && dtype_code(Bt) == dt);
+  const int64_t M = A.size(0), K = A.size(1), N = Bt.size(0);
+  Tensor C = at::empty({M, N}, A.options().dtype(at::kFloat));
+  HIP_LAUNCH_CHECK(pdrnn_gemm_nt(u16(A), K, u16(Bt), K, C.data_ptr<float>(), N, (int)M, (int)N, (int)K, dt,
+                                 cur_stream()));
+  return C;
+}
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -457,6 +588,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
   m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer");
+  m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
+  m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
+  m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });
+  m.def("gemm_nt", &gemm_nt, "C = A Bt^T (bf16/fp16 in, f32 out) on the MFMA tile core");
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.attr("offload_arch") = "gfx950";

@@ -156,6 +156,45 @@ hipError_t pdrnn_embedding_bwd_csr(const float* dout, const int64_t* perm, const
                                    float* dweight, int64_t num_embeddings, int64_t dim,
                                    int64_t padding_idx, hipStream_t stream);
 
+// ---- large-H LSTM (MFMA per-step kernels, 16-bit storage) -----------------
+// One direction of a layer.  Gate-interleaved layouts: column / row 4u+q is
+// gate q (i, f, g, o) of unit u.
+typedef struct {
+  const uint16_t* w;       // [4H, H] W_hh, gate-interleaved rows (forward GEMM: h Wp^T)
+  const uint16_t* wt;      // [H, 4H] its transpose (backward GEMM: dgates Wp)
+  const uint16_t* xp;      // input projection incl. bias, [t, b, col] at t*xp_st + b*xp_sb + col
+  int64_t xp_sb, xp_st;
+  const uint16_t* h0;      // [B, H] or null
+  const float* c0;         // [B, H] or null
+  uint16_t* hseq;          // outputs h_t at t*hseq_st + b*hseq_sb + u
+  int64_t hseq_sb, hseq_st;
+  float* cseq;             // [T, B, H] fp32 cell states
+  uint16_t* acts;          // [T, B, 4H] activated gates
+  uint16_t* dgates;        // [T, B, 4H] pre-activation gate gradients (backward)
+  const uint16_t* dout;    // grad of hseq (same strides as dout_sb / dout_st) or null
+  int64_t dout_sb, dout_st;
+  const float* dhn;        // [B, H] or null
+  const float* dcn;        // [B, H] or null
+  float* dc_carry;         // [B, H] fp32 scratch
+  float* dh0;              // [B, H] or null
+  float* dc0;              // [B, H] or null
+} PdrnnLstmLargeDir;
+
+typedef struct {
+  PdrnnLstmLargeDir dir[2];
+  int B, H, T;
+  int step;                // processing-order step index (forward) / backward step index
+  int reverse_mask;        // bit d set: direction d runs time-reversed
+} PdrnnLstmLargeStepArgs;
+
+int pdrnn_lstm_large_supported(int H);
+// dtype 0 = bf16, 1 = fp16; tile 0 = auto (32/64/128-row tiles)
+hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
+                                 hipStream_t stream);
+hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir, int dtype, hipStream_t stream);
+hipError_t pdrnn_gemm_nt(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
+                         int M, int N, int K, int dtype, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

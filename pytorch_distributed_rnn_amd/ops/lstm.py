@@ -173,9 +173,12 @@ def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Te
         return out, hn, cn
     from . import lstm_large
     if lstm_large.supported(x, hidden, num_layers):
+        if idx is not None:
+            x = x.index_select(0 if batch_first else 1, idx)
         return lstm_large.lstm_large_forward(x, weights, h0, c0, hidden=hidden,
                                              num_layers=num_layers, batch_first=batch_first,
-                                             bidirectional=bidirectional)
+                                             bidirectional=bidirectional, dropout=dropout,
+                                             training=training)
     if idx is not None:
         x = x.index_select(0, idx)
     return lstm_reference(x, weights, h0, c0, hidden, num_layers, batch_first, dropout, training,
@@ -192,7 +195,7 @@ def lstm_bidirectional_forward(x: Tensor, all_weights: Sequence[Tensor], h0: Opt
     if lstm_large.supported(x, hidden, num_layers, bidirectional=True):
         return lstm_large.lstm_large_forward(x, all_weights, h0, c0, hidden=hidden,
                                              num_layers=num_layers, batch_first=batch_first,
-                                             bidirectional=True)
+                                             bidirectional=True, dropout=dropout, training=training)
     has_bias = len(all_weights) == 8 * num_layers
     ws: List[Optional[Tensor]] = []
     per = 4 if has_bias else 2

@@ -1,10 +1,177 @@
-"""Large-hidden LSTM path (placeholder until the MFMA kernels land)."""
+"""Large-hidden LSTM stack on the MFMA step kernels (csrc/kernels/lstm_large.hip).
+
+Used for 16-bit inputs (bf16 / fp16 compute, fp32 master weights, fp32 cell
+state and weight gradients) when ``H % 64 == 0`` -- the char-LM (H = 1024) and
+stacked bidirectional (H = 4096) configurations.  Per layer:
+
+* input projection for ALL timesteps and both directions in one library GEMM
+  (``Xp = X [W_ih_fwd; W_ih_rev]^T + b``, gate-interleaved columns);
+* T launches of the fused recurrent step (MFMA GEMM ``h_{t-1} W_hh^T`` + LSTM
+  cell epilogue), both directions per launch;
+* backward: one fused first-cell kernel + T launches of the fused BPTT step
+  (MFMA ``dgates_t W_hh`` + cell backward of the previous step), then
+  ``dW_hh``, ``dW_ih``, ``db`` and ``dX`` as library GEMMs over all
+  timesteps with fp32 outputs.
+
+Semantics are torch.nn.LSTM's (gate order i, f, g, o; reference:
+src/motion/model.py:9 builds its model on nn.LSTM); parameters stay in the
+stock nn.LSTM layout -- the gate interleave is a per-call permutation.
+"""
 from __future__ import annotations
 
+import os
+from typing import List, Optional, Sequence, Tuple
 
-def supported(x, hidden, num_layers) -> bool:  # noqa: D401
-    return False
+import torch
+from torch import Tensor
+
+from .. import _ext
+
+_PERM_CACHE = {}
 
 
-def lstm_large_forward(*args, **kwargs):
-    raise NotImplementedError
+def _perm(hidden: int, device) -> Tensor:
+    """perm[4u + q] = q*H + u: torch gate-blocked rows -> gate-interleaved rows."""
+    key = (hidden, str(device))
+    p = _PERM_CACHE.get(key)
+    if p is None:
+        p = torch.arange(4 * hidden, device=device).view(4, hidden).t().reshape(-1)
+        _PERM_CACHE[key] = p
+    return p
+
+
+def _tile() -> int:
+    try:
+        return int(os.environ.get("PDRNN_LSTM_LARGE_TILE", "0"))
+    except ValueError:
+        return 0
+
+
+def supported(x: Tensor, hidden: int, num_layers: int, bidirectional: bool = False) -> bool:
+    if x.dtype not in (torch.bfloat16, torch.float16) or x.device.type != "cuda" or x.dim() != 3:
+        return False
+    mod = _ext.native(x.device)
+    return mod is not None and hasattr(mod, "lstm_large_fwd") and bool(mod.lstm_large_supported(hidden))
+
+
+def _mm_f32(a: Tensor, b: Tensor) -> Tensor:
+    """a @ b with fp32 output from 16-bit inputs (hipBLASLt fp32 accumulate)."""
+    try:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    except (RuntimeError, TypeError):
+        return torch.mm(a.float(), b.float())
+
+
+class _LargeLSTMLayer(torch.autograd.Function):
+    """One layer, 1 or 2 directions.  x: [T, B, I] (compute dtype).
+
+    weights: per direction (w_ih, w_hh, b_ih, b_hh), fp32 master parameters
+    (biases may be None)."""
+
+    @staticmethod
+    def forward(ctx, x, h0, c0, cfg, *weights):
+        hidden, ndir, tile = cfg
+        cdt = x.dtype
+        T, B, I = x.shape
+        H = hidden
+        mod = _ext.native(x.device)
+        perm = _perm(H, x.device)
+        w_ih = [weights[4 * d] for d in range(ndir)]
+        w_hh = [weights[4 * d + 1] for d in range(ndir)]
+        bias = []
+        for d in range(ndir):
+            b_ih, b_hh = weights[4 * d + 2], weights[4 * d + 3]
+            b = torch.zeros(4 * H, device=x.device, dtype=torch.float32)
+            if b_ih is not None:
+                b = b + b_ih.float()
+            if b_hh is not None:
+                b = b + b_hh.float()
+            bias.append(b[perm])
+        wih_p = torch.cat([w[perm] for w in w_ih], 0).to(cdt)                 # [ndir*4H, I]
+        bias_p = torch.cat(bias, 0).to(cdt)
+        xp = torch.addmm(bias_p, x.reshape(T * B, I), wih_p.t()).view(T, B, ndir * 4 * H)
+        whh_p = [w[perm].to(cdt).contiguous() for w in w_hh]
+        h0c = h0.to(cdt).contiguous() if h0 is not None else None
+        c0c = c0.float().contiguous() if c0 is not None else None
+        rev_mask = 2 if ndir == 2 else 0
+        hseq, cseq, acts = mod.lstm_large_fwd(xp, whh_p, h0c, c0c, H, rev_mask, tile)
+        last = [T - 1, 0][:ndir]
+        hn = torch.stack([hseq[last[d], :, d * H:(d + 1) * H] for d in range(ndir)], 0)
+        cn = torch.stack([cseq[d, last[d]] for d in range(ndir)], 0)
+        ctx.save_for_backward(x, hseq, cseq, acts, h0c, c0c, wih_p, *whh_p)
+        ctx.cfg = (H, ndir, tile, rev_mask, [w is not None for w in weights], h0 is not None,
+                   c0 is not None, h0.dtype if h0 is not None else None,
+                   c0.dtype if c0 is not None else None)
+        return hseq, hn, cn.to(cdt)
+
+    @staticmethod
+    def backward(ctx, dhseq, dhn, dcn):
+        x, hseq, cseq, acts, h0c, c0c, wih_p, *whh_p = ctx.saved_tensors
+        H, ndir, tile, rev_mask, has_w, has_h0, has_c0, h0_dtype, c0_dtype = ctx.cfg
+        cdt = x.dtype
+        T, B, I = x.shape
+        mod = _ext.native(x.device)
+        perm = _perm(H, x.device)
+        dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
+        dhn_f = dhn.float().contiguous() if dhn is not None else None
+        dcn_f = dcn.float().contiguous() if dcn is not None else None
+        wt = [w.t().contiguous() for w in whh_p]
+        dgates, dh0, dc0 = mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile)
+        grads: List[Optional[Tensor]] = []
+        dx = None
+        x2 = x.reshape(T * B, I)
+        for d in range(ndir):
+            G = dgates[d].view(T * B, 4 * H)
+            hd = hseq[:, :, d * H:(d + 1) * H]
+            h0d = h0c[d:d + 1] if h0c is not None else torch.zeros(1, B, H, device=x.device, dtype=cdt)
+            hprev = torch.cat([h0d, hd[:-1]], 0) if d == 0 else torch.cat([hd[1:], h0d], 0)
+            dwhh_p = _mm_f32(G.t(), hprev.reshape(T * B, H))
+            dwih_p = _mm_f32(G.t(), x2)
+            db_p = G.float().sum(0)
+            dwih = torch.empty_like(dwih_p)
+            dwih[perm] = dwih_p
+            dwhh = torch.empty_like(dwhh_p)
+            dwhh[perm] = dwhh_p
+            db = torch.empty_like(db_p)
+            db[perm] = db_p
+            part = torch.mm(G, wih_p[d * 4 * H:(d + 1) * 4 * H])
+            dx = part if dx is None else dx + part
+            gb = [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
+            grads += gb
+        dx = dx.view(T, B, I)
+        dh0_out = dh0.to(h0_dtype) if has_h0 else None
+        dc0_out = dc0.to(c0_dtype) if has_c0 else None
+        return (dx, dh0_out, dc0_out, None, *grads)
+
+
+def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor],
+                       c0: Optional[Tensor], *, hidden: int, num_layers: int, batch_first: bool,
+                       bidirectional: bool = False, dropout: float = 0.0,
+                       training: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
+    """Stacked (bi)LSTM on the MFMA step kernels; nn.LSTM-compatible outputs.
+
+    ``weights``: nn.LSTM ``_all_weights`` order (per layer and direction
+    w_ih, w_hh[, b_ih, b_hh])."""
+    ndir = 2 if bidirectional else 1
+    per = len(weights) // (num_layers * ndir)
+    seq = x.transpose(0, 1) if batch_first else x
+    seq = seq.contiguous()
+    B = seq.shape[1]
+    tile = _tile()
+    hns, cns = [], []
+    for l in range(num_layers):
+        ws: List[Optional[Tensor]] = []
+        for d in range(ndir):
+            chunk = list(weights[(l * ndir + d) * per:(l * ndir + d + 1) * per])
+            if per == 2:
+                chunk += [None, None]
+            ws += chunk
+        h0l = h0[l * ndir:(l + 1) * ndir] if h0 is not None else None
+        c0l = c0[l * ndir:(l + 1) * ndir] if c0 is not None else None
+        seq, hn, cn = _LargeLSTMLayer.apply(seq, h0l, c0l, (hidden, ndir, tile), *ws)
+        hns.append(hn)
+        cns.append(cn)
+        if dropout > 0 and training and l < num_layers - 1:
+            seq = torch.nn.functional.dropout(seq, dropout, True)
+    out = seq.transpose(0, 1) if batch_first else seq
+    return out, torch.cat(hns, 0), torch.cat(cns, 0)

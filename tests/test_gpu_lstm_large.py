@@ -1,0 +1,84 @@
+"""Large-H LSTM MFMA path vs the fp32 torch reference on the same 16-bit-rounded
+inputs and weights (numerics tests for csrc/kernels/lstm_large.hip)."""
+import pytest
+import torch
+
+from pytorch_distributed_rnn_amd import _ext
+from pytorch_distributed_rnn_amd.models.rnn import LSTM
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.detach(), b.detach()
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(70, 128, 192), (128, 256, 64), (5, 64, 1024)])
+def test_gemm_nt_core(dt, M, N, K):
+    mod = _ext.require()
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device="cuda").to(dt)
+    b = torch.randn(N, K, device="cuda").to(dt)
+    c = mod.gemm_nt(a, b)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(c, ref, rtol=2e-3, atol=2e-3)
+
+
+def _ref_model(m: LSTM):
+    ref = torch.nn.LSTM(m.input_size, m.hidden_size, m.num_layers, batch_first=m.batch_first,
+                        bidirectional=m.bidirectional).cuda()
+    with torch.no_grad():
+        for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+            q.copy_(p)
+    return ref
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,L,bi,B,T,I", [(64, 1, False, 5, 7, 24), (128, 2, False, 33, 9, 40),
+                                          (64, 2, True, 5, 6, 24), (256, 1, True, 70, 4, 64)])
+def test_large_lstm_matches_torch(dt, H, L, bi, B, T, I):
+    torch.manual_seed(1)
+    m = LSTM(I, H, L, batch_first=True, bidirectional=bi).cuda()
+    # round weights to the compute dtype so both paths see identical values
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(p.to(dt).float())
+    ref = _ref_model(m)
+    x = torch.randn(B, T, I, device="cuda").to(dt)
+    x16 = x.clone().requires_grad_(True)
+    xr = x.float().clone().requires_grad_(True)
+    out, (hn, cn) = m(x16)
+    out_r, (hn_r, cn_r) = ref(xr)
+    assert out.dtype == dt and out.shape == out_r.shape
+    assert _rel(out, out_r) < 2e-2
+    assert _rel(hn, hn_r) < 2e-2
+    assert _rel(cn, cn_r) < 2e-2
+    g = torch.randn_like(out_r)
+    (out.float() * g).sum().backward()
+    (out_r * g).sum().backward()
+    assert _rel(x16.grad, xr.grad) < 4e-2
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert _rel(p.grad, q.grad) < 4e-2, n
+
+
+def test_large_lstm_state_grads():
+    torch.manual_seed(3)
+    dt = torch.bfloat16
+    m = LSTM(32, 64, 1, batch_first=False).cuda()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(p.to(dt).float())
+    ref = _ref_model(m)
+    x = torch.randn(5, 3, 32, device="cuda").to(dt)
+    h0 = torch.randn(1, 3, 64, device="cuda").to(dt)
+    c0 = torch.randn(1, 3, 64, device="cuda")
+    h0a, c0a = h0.clone().requires_grad_(True), c0.clone().requires_grad_(True)
+    h0b, c0b = h0.float().clone().requires_grad_(True), c0.clone().requires_grad_(True)
+    _, (hn, cn) = m(x, (h0a, c0a))
+    _, (hn_r, cn_r) = ref(x.float(), (h0b, c0b))
+    (hn.float().sum() + 0.5 * cn.float().sum()).backward()
+    (hn_r.sum() + 0.5 * cn_r.sum()).backward()
+    assert _rel(h0a.grad, h0b.grad) < 4e-2
+    assert _rel(c0a.grad, c0b.grad) < 4e-2
