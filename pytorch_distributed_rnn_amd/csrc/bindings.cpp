@@ -50,6 +50,16 @@ const float* opt_ptr(const optional<Tensor>& t) {
   return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
 }
 
+int dtype_code(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "16-bit (bf16/fp16) tensor expected");
+  return t.scalar_type() == at::kBFloat16 ? 0 : 1;
+}
+const uint16_t* u16(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* u16m(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const uint16_t* opt_u16(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<const uint16_t*>(t->data_ptr()) : nullptr;
+}
+
 // Parameter layout of one fused LSTM stack, in nn.LSTM parameter order:
 // per layer weight_ih, weight_hh, bias_ih, bias_hh (biases optional).
 struct StackLayout {
@@ -410,7 +420,7 @@ void adam_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_
   HIP_LAUNCH_CHECK(pdrnn_adam_flat(&a, cur_stream()));
 }
 
-Tensor embedding_fwd(const Tensor& weight, const Tensor& idx) {
+Tensor embedding_fwd(const Tensor& weight, const Tensor& idx, optional<at::ScalarType> out_dtype) {
   CHECK_HIP_TENSOR(weight); CHECK_F32(weight);
   TORCH_CHECK(weight.is_contiguous() && weight.dim() == 2);
   TORCH_CHECK(idx.scalar_type() == at::kLong);
@@ -418,9 +428,16 @@ Tensor embedding_fwd(const Tensor& weight, const Tensor& idx) {
   Tensor flat = idx.contiguous().view({-1});
   std::vector<int64_t> shape(idx.sizes().begin(), idx.sizes().end());
   shape.push_back(weight.size(1));
-  Tensor out = at::empty(shape, weight.options());
-  HIP_LAUNCH_CHECK(pdrnn_embedding_fwd(weight.data_ptr<float>(), flat.data_ptr<int64_t>(), out.data_ptr<float>(),
-                                       flat.numel(), weight.size(1), weight.size(0), cur_stream()));
+  const at::ScalarType odt = out_dtype.has_value() ? *out_dtype : at::kFloat;
+  Tensor out = at::empty(shape, weight.options().dtype(odt));
+  if (odt == at::kFloat) {
+    HIP_LAUNCH_CHECK(pdrnn_embedding_fwd(weight.data_ptr<float>(), flat.data_ptr<int64_t>(), out.data_ptr<float>(),
+                                         flat.numel(), weight.size(1), weight.size(0), cur_stream()));
+  } else {
+    HIP_LAUNCH_CHECK(pdrnn_embedding_fwd16(weight.data_ptr<float>(), flat.data_ptr<int64_t>(), u16m(out),
+                                           flat.numel(), weight.size(1), weight.size(0), dtype_code(out),
+                                           cur_stream()));
+  }
   return out;
 }
 
@@ -445,15 +462,6 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 // ---------------------------------------------------------------------------
 // Large-H LSTM layer (both directions in one launch per step).
 // ---------------------------------------------------------------------------
-int dtype_code(const Tensor& t) {
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "16-bit (bf16/fp16) tensor expected");
-  return t.scalar_type() == at::kBFloat16 ? 0 : 1;
-}
-const uint16_t* u16(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
-uint16_t* u16m(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
-const uint16_t* opt_u16(const optional<Tensor>& t) {
-  return (t.has_value() && t->defined()) ? reinterpret_cast<const uint16_t*>(t->data_ptr()) : nullptr;
-}
 
 // xp: [T, B, ndir*4H] (16-bit, bias included, gate-interleaved per direction)
 // w:  ndir x [4H, H] gate-interleaved W_hh;  h0: [ndir, B, H] 16-bit;  c0: [ndir, B, H] f32
@@ -561,7 +569,7 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
 }
 
 // C[M, N] f32 = A[M, K] Bt[N, K]^T on the MFMA core (tests).
-Tensor gemm_nt(const Tensor& A, const Tensor& Bt) {
+Tensor gemm_nt(const Tensor& A, const Tensor& Bt, int64_t tile) {
   CHECK_HIP_TENSOR(A);
   const c10::DeviceGuard guard(A.device());
   const int dt = dtype_code(A);
@@ -569,7 +577,7 @@ Tensor gemm_nt(const Tensor& A, const Tensor& Bt) {
   const int64_t M = A.size(0), K = A.size(1), N = Bt.size(0);
   Tensor C = at::empty({M, N}, A.options().dtype(at::kFloat));
   HIP_LAUNCH_CHECK(pdrnn_gemm_nt(u16(A), K, u16(Bt), K, C.data_ptr<float>(), N, (int)M, (int)N, (int)K, dt,
-                                 cur_stream()));
+                                 (int)tile, cur_stream()));
   return C;
 }
 }  // namespace
@@ -591,8 +599,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
   m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
   m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });
-  m.def("gemm_nt", &gemm_nt, "C = A Bt^T (bf16/fp16 in, f32 out) on the MFMA tile core");
-  m.def("embedding_fwd", &embedding_fwd);
+  m.def("gemm_nt", &gemm_nt, "C = A Bt^T (bf16/fp16 in, f32 out) on the MFMA tile core", py::arg("A"),
+        py::arg("Bt"), py::arg("tile") = -1);
+  m.def("embedding_fwd", &embedding_fwd, py::arg("weight"), py::arg("idx"), py::arg("out_dtype") = py::none());
   m.def("embedding_bwd", &embedding_bwd);
   m.attr("offload_arch") = "gfx950";
   pdrnn::register_runtime(m);

@@ -152,6 +152,8 @@ hipError_t pdrnn_adam_flat(const PdrnnAdamArgs* a, hipStream_t stream);
 // ----------------------------------------------------------------------------
 hipError_t pdrnn_embedding_fwd(const float* weight, const int64_t* idx, float* out, int64_t n_idx,
                                int64_t dim, int64_t num_embeddings, hipStream_t stream);
+hipError_t pdrnn_embedding_fwd16(const float* weight, const int64_t* idx, uint16_t* out, int64_t n_idx, int64_t dim,
+                                 int64_t num_embeddings, int dtype, hipStream_t stream);
 hipError_t pdrnn_embedding_bwd_csr(const float* dout, const int64_t* perm, const int64_t* offsets,
                                    float* dweight, int64_t num_embeddings, int64_t dim,
                                    int64_t padding_idx, hipStream_t stream);
@@ -188,12 +190,13 @@ typedef struct {
 } PdrnnLstmLargeStepArgs;
 
 int pdrnn_lstm_large_supported(int H);
-// dtype 0 = bf16, 1 = fp16; tile 0 = auto (32/64/128-row tiles)
+// dtype 0 = bf16, 1 = fp16; tile -1 = auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
                                  hipStream_t stream);
 hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir, int dtype, hipStream_t stream);
+// tile: -1 auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_gemm_nt(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
-                         int M, int N, int K, int dtype, hipStream_t stream);
+                         int M, int N, int K, int dtype, int tile, hipStream_t stream);
 
 #ifdef __cplusplus
 }

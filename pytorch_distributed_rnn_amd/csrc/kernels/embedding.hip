@@ -34,6 +34,27 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(const float* __restrict__ 
   }
 }
 
+// Gather with the cast to the 16-bit compute dtype fused in (bf16: dtype 0,
+// fp16: dtype 1): the LSTM's input projection consumes it directly.
+template <int DT>
+__global__ void __launch_bounds__(256) emb_fwd16_kernel(const float* __restrict__ w, const int64_t* __restrict__ idx,
+                                                        uint16_t* __restrict__ out, int64_t n, int64_t dim,
+                                                        int64_t V) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wave; r < n; r += nwaves) {
+    int64_t v = idx[r];
+    if (v < 0) v += V;
+    const float* src = w + v * dim;
+    uint16_t* dst = out + r * dim;
+    for (int64_t c = lane; c < dim; c += 64) {
+      const float f = src[c];
+      dst[c] = DT == 0 ? __builtin_bit_cast(uint16_t, (__bf16)f) : __builtin_bit_cast(uint16_t, (_Float16)f);
+    }
+  }
+}
+
 // dweight[v] = sum over j in [off[v], off[v+1]) of dout[perm[j]]; padding row -> 0.
 __global__ void __launch_bounds__(256) emb_bwd_csr_kernel(const float* __restrict__ dout,
                                                           const int64_t* __restrict__ perm,
@@ -72,6 +93,18 @@ hipError_t pdrnn_embedding_fwd(const float* weight, const int64_t* idx, float* o
   if (n_idx <= 0) return hipSuccess;
   hipLaunchKernelGGL(pdrnn::emb_fwd_kernel, dim3(pdrnn::blocks_for(n_idx)), dim3(256), 0, stream, weight, idx, out,
                      n_idx, dim, num_embeddings);
+  return hipGetLastError();
+}
+
+hipError_t pdrnn_embedding_fwd16(const float* weight, const int64_t* idx, uint16_t* out, int64_t n_idx, int64_t dim,
+                                 int64_t num_embeddings, int dtype, hipStream_t stream) {
+  if (n_idx <= 0) return hipSuccess;
+  if (dtype == 0)
+    hipLaunchKernelGGL(pdrnn::emb_fwd16_kernel<0>, dim3(pdrnn::blocks_for(n_idx)), dim3(256), 0, stream, weight, idx,
+                       out, n_idx, dim, num_embeddings);
+  else
+    hipLaunchKernelGGL(pdrnn::emb_fwd16_kernel<1>, dim3(pdrnn::blocks_for(n_idx)), dim3(256), 0, stream, weight, idx,
+                       out, n_idx, dim, num_embeddings);
   return hipGetLastError();
 }
 

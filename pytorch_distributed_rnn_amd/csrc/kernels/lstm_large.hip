@@ -79,101 +79,118 @@ __device__ __forceinline__ float qbcast(float v, int q) {
 // fragment read touches over all bank groups.
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
-// C[M, N] (+)= A[M, K] * Bt[N, K]^T for one BM x BN block tile; 4 waves as
-// 2 x 2, each wave (BM/2) x (BN/2) = MT x NT MFMA 16x16 sub-tiles.  A / Bt are
-// 16-bit, K-contiguous with leading dimensions lda / ldb.  Rows of A beyond M
-// are clamped (their results are discarded by the caller).  K % 64 == 0.
-template <class DT, int BM, int BN>
-struct GemmNT {
-  static constexpr int MT = BM / 32, NT = BN / 32;
-  static constexpr int A_CHUNKS = BM * 8 / 256, B_CHUNKS = BN * 8 / 256;
-  static constexpr int LDS_ELEMS = 2 * (BM + BN) * BK;  // double-buffered A | B
+// C[M, N] = A[M, K] * Bt[N, K]^T for one BM x BN block tile, WM x WN waves,
+// each wave (BM/WM) x (BN/WN) = MT x NT MFMA 16x16x32 sub-tiles.  A / Bt are
+// 16-bit, K-contiguous (lda / ldb).  Rows of A beyond M are clamped (the
+// caller discards their results).  K % 64 == 0.
+//
+// Staging: direct global->LDS DMA (global_load_lds_dwordx4, 1 KiB per wave
+// instruction) into a STAGES-deep ring of [BM+BN][64] tiles, prefetch distance
+// STAGES-1 k-tiles, retired by a counted `s_waitcnt vmcnt` + raw s_barrier so
+// the DMAs stay in flight across barriers (a __syncthreads() would drain
+// them).  The XOR swizzle of the LDS image is applied on the per-lane global
+// SOURCE address (the DMA destination is lane-linear).  All LDS is the one
+// dynamic array (a second __shared__ object makes hipcc drain vmcnt before
+// every ds_read).
+template <class DT, int BM, int BN, int WM, int WN, int STAGES>
+struct GemmPipe {
+  static constexpr int NWAVES = WM * WN, NTHREADS = NWAVES * 64;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int MT = WTM / 16, NT = WTN / 16;
+  static constexpr int ROWS = BM + BN;
+  static constexpr int STAGE_ELEMS = ROWS * BK;
+  static constexpr int GROUPS = ROWS * 8 / 64;  // 1 KiB DMA groups per stage
+  static constexpr int G = GROUPS / NWAVES;     // DMA instructions per wave per stage
+  static constexpr int LDS_ELEMS = STAGES * STAGE_ELEMS;
+  static_assert(GROUPS % NWAVES == 0, "DMA groups must split evenly over the waves");
+  static_assert(MT >= 1 && NT >= 1 && BM % 8 == 0, "tile shape");
+
+  template <int N>
+  __device__ static __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  }
 
   __device__ static void run(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ Bt,
                              int64_t ldb, int M, int K, int m0, int n0, uint16_t* smem, f32x4 (&acc)[MT][NT]) {
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const uint4* ga[A_CHUNKS];
-    const uint4* gb[B_CHUNKS];
-    int la[A_CHUNKS], lb[B_CHUNKS];
+    const uint16_t* src[G];
 #pragma unroll
-    for (int i = 0; i < A_CHUNKS; ++i) {
-      const int id = tid + i * 256, r = id >> 3, c = id & 7;
-      const int gr = min(m0 + r, M - 1);
-      ga[i] = reinterpret_cast<const uint4*>(A + (int64_t)gr * lda + c * 8);
-      la[i] = lds_off(r, c);
+    for (int i = 0; i < G; ++i) {
+      const int cid = (wid * G + i) * 64 + lane;
+      const int row = cid >> 3, slot = cid & 7;
+      const int lc = slot ^ (row & 7);
+      src[i] = row < BM ? A + (int64_t)min(m0 + row, M - 1) * lda + lc * 8
+                        : Bt + (int64_t)(n0 + row - BM) * ldb + lc * 8;
     }
+    auto issue = [&](int kt, int st) {
+      uint16_t* base = smem + st * STAGE_ELEMS + wid * G * 512;
 #pragma unroll
-    for (int i = 0; i < B_CHUNKS; ++i) {
-      const int id = tid + i * 256, r = id >> 3, c = id & 7;
-      gb[i] = reinterpret_cast<const uint4*>(Bt + (int64_t)(n0 + r) * ldb + c * 8);
-      lb[i] = lds_off(r, c);
-    }
-    uint16_t* sA[2] = {smem, smem + (BM + BN) * BK};
-    uint16_t* sB[2] = {smem + BM * BK, smem + (BM + BN) * BK + BM * BK};
-
-    uint4 ra[A_CHUNKS], rb[B_CHUNKS];
+      for (int i = 0; i < G; ++i)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[i] + kt * BK),
+                                         (__attribute__((address_space(3))) void*)(base + i * 512), 16, 0, 0);
+    };
     const int KT = K / BK;
 #pragma unroll
-    for (int i = 0; i < A_CHUNKS; ++i) ra[i] = ga[i][0];
-#pragma unroll
-    for (int i = 0; i < B_CHUNKS; ++i) rb[i] = gb[i][0];
-#pragma unroll
-    for (int i = 0; i < A_CHUNKS; ++i) *reinterpret_cast<uint4*>(sA[0] + la[i]) = ra[i];
-#pragma unroll
-    for (int i = 0; i < B_CHUNKS; ++i) *reinterpret_cast<uint4*>(sB[0] + lb[i]) = rb[i];
-    __syncthreads();
+    for (int p = 0; p < STAGES - 1; ++p)
+      if (p < KT) issue(p, p);
 
     const int fr = lane & 15, fq = lane >> 4;
     for (int kt = 0; kt < KT; ++kt) {
-      const int cur = kt & 1;
-      const bool more = kt + 1 < KT;
-      if (more) {
-        const int koff = (kt + 1) * (BK / 8);  // in uint4 units
-#pragma unroll
-        for (int i = 0; i < A_CHUNKS; ++i) ra[i] = ga[i][koff];
-#pragma unroll
-        for (int i = 0; i < B_CHUNKS; ++i) rb[i] = gb[i][koff];
+      // tiles issued after kt that may stay in flight: min(STAGES-2, KT-1-kt)
+      const int ahead = min(STAGES - 2, KT - 1 - kt);
+      if constexpr (STAGES >= 4) {
+        if (ahead >= 2) wait_vm<2 * G>();
+        else if (ahead == 1) wait_vm<G>();
+        else wait_vm<0>();
+      } else {
+        if (ahead >= 1) wait_vm<G>();
+        else wait_vm<0>();
       }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + STAGES - 1 < KT) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+      const uint16_t* sA = smem + (kt % STAGES) * STAGE_ELEMS;
+      const uint16_t* sB = sA + BM * BK;
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
         uint4 fa[MT], fb[NT];
 #pragma unroll
         for (int i = 0; i < MT; ++i)
-          fa[i] = *reinterpret_cast<const uint4*>(sA[cur] + lds_off(wm * (BM / 2) + i * 16 + fr, ks * 4 + fq));
+          fa[i] = *reinterpret_cast<const uint4*>(sA + lds_off(wm * WTM + i * 16 + fr, ks * 4 + fq));
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          fb[j] = *reinterpret_cast<const uint4*>(sB[cur] + lds_off(wn * (BN / 2) + j * 16 + fr, ks * 4 + fq));
+          fb[j] = *reinterpret_cast<const uint4*>(sB + lds_off(wn * WTN + j * 16 + fr, ks * 4 + fq));
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int j = 0; j < NT; ++j) acc[i][j] = DT::mfma(fa[i], fb[j], acc[i][j]);
       }
-      if (more) {
-        const int nxt = cur ^ 1;
-#pragma unroll
-        for (int i = 0; i < A_CHUNKS; ++i) *reinterpret_cast<uint4*>(sA[nxt] + la[i]) = ra[i];
-#pragma unroll
-        for (int i = 0; i < B_CHUNKS; ++i) *reinterpret_cast<uint4*>(sB[nxt] + lb[i]) = rb[i];
-      }
-      __syncthreads();
     }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 };
+
+// Tile configurations (BM, BN, WM, WN, STAGES)
+#define PDRNN_TILE_CFGS(X)   \
+  X(0, 32, 64, 1, 4, 4)      \
+  X(1, 64, 64, 2, 2, 4)      \
+  X(2, 128, 128, 2, 2, 3)    \
+  X(3, 256, 128, 4, 2, 3)
 
 // ---------------------------------------------------------------------------
 // Forward step: gates = h_{t-1} Wp^T + xp_t  ->  (i, f, g, o), c_t, h_t.
 // Columns are gate-interleaved: col = 4 u + q.
 // ---------------------------------------------------------------------------
-template <class DT, int BM, int BN>
-__global__ void __launch_bounds__(256) lstm_large_fwd_step_kernel(PdrnnLstmLargeStepArgs args) {
-  typedef GemmNT<DT, BM, BN> G;
+template <class DT, int BM, int BN, int WM, int WN, int ST>
+__global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(PdrnnLstmLargeStepArgs args) {
+  typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
   const PdrnnLstmLargeDir& d = args.dir[blockIdx.z];
   const int B = args.B, H = args.H;
@@ -196,7 +213,7 @@ __global__ void __launch_bounds__(256) lstm_large_fwd_step_kernel(PdrnnLstmLarge
   }
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int q = lane & 3;
   const uint16_t* xp = d.xp + (int64_t)t * d.xp_st;
   const float* cprev = first ? d.c0 : d.cseq + (int64_t)tp * B * H;
@@ -205,10 +222,10 @@ __global__ void __launch_bounds__(256) lstm_large_fwd_step_kernel(PdrnnLstmLarge
   uint16_t* acts = d.acts + (int64_t)t * B * 4 * H;
 #pragma unroll
   for (int i = 0; i < G::MT; ++i) {
-    const int rbase = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4;
+    const int rbase = m0 + wm * G::WTM + i * 16 + (lane >> 4) * 4;
 #pragma unroll
     for (int j = 0; j < G::NT; ++j) {
-      const int col = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+      const int col = n0 + wn * G::WTN + j * 16 + (lane & 15);
       const int u = col >> 2;
       float a[4];
 #pragma unroll
@@ -245,9 +262,9 @@ __global__ void __launch_bounds__(256) lstm_large_fwd_step_kernel(PdrnnLstmLarge
 //   dc_carry = dc f
 // With cell == 0 (after the first forward step): dh0 = acc, dc0 = dc_carry.
 // ---------------------------------------------------------------------------
-template <class DT, int BM, int BN>
-__global__ void __launch_bounds__(256) lstm_large_bwd_step_kernel(PdrnnLstmLargeStepArgs args) {
-  typedef GemmNT<DT, BM, BN> G;
+template <class DT, int BM, int BN, int WM, int WN, int ST>
+__global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(PdrnnLstmLargeStepArgs args) {
+  typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
   const PdrnnLstmLargeDir& d = args.dir[blockIdx.z];
   const int B = args.B, H = args.H, T = args.T;
@@ -263,13 +280,13 @@ __global__ void __launch_bounds__(256) lstm_large_bwd_step_kernel(PdrnnLstmLarge
   G::run(d.dgates + (int64_t)t * B * 4 * H, 4 * H, d.wt, 4 * H, B, 4 * H, m0, n0, smem_u16, acc);
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
 #pragma unroll
   for (int i = 0; i < G::MT; ++i) {
-    const int rbase = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4;
+    const int rbase = m0 + wm * G::WTM + i * 16 + (lane >> 4) * 4;
 #pragma unroll
     for (int j = 0; j < G::NT; ++j) {
-      const int u = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+      const int u = n0 + wn * G::WTN + j * 16 + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = rbase + r;
@@ -333,56 +350,85 @@ __global__ void lstm_large_bwd_first_kernel(PdrnnLstmLargeStepArgs args) {
 }
 
 // Plain NT GEMM on the same core (tests / fallbacks): C[M,N] fp32 = A Bt^T.
-template <class DT, int BM, int BN>
-__global__ void __launch_bounds__(256) gemm_nt_kernel(const uint16_t* A, int64_t lda, const uint16_t* Bt,
-                                                      int64_t ldb, float* C, int64_t ldc, int M, int N, int K) {
-  typedef GemmNT<DT, BM, BN> G;
+template <class DT, int BM, int BN, int WM, int WN, int ST>
+__global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(const uint16_t* A, int64_t lda, const uint16_t* Bt,
+                                                               int64_t ldb, float* C, int64_t ldc, int M, int N,
+                                                               int K) {
+  typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   f32x4 acc[G::MT][G::NT];
   G::run(A, lda, Bt, ldb, M, K, m0, n0, smem_u16, acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
 #pragma unroll
   for (int i = 0; i < G::MT; ++i)
 #pragma unroll
     for (int j = 0; j < G::NT; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-        const int col = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        const int row = m0 + wm * G::WTM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn * G::WTN + j * 16 + (lane & 15);
         if (row < M && col < N) C[(int64_t)row * ldc + col] = acc[i][j][r];
       }
 }
 
-template <class DT, int BM, int BN>
+template <class DT, int BM, int BN, int WM, int WN, int ST>
 hipError_t launch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, hipStream_t st) {
+  typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
   const int N = backward ? a->H : 4 * a->H;
+  if (N % BN) return hipErrorInvalidValue;
   dim3 grid(N / BN, (a->B + BM - 1) / BM, ndir);
-  const size_t lds = sizeof(uint16_t) * GemmNT<DT, BM, BN>::LDS_ELEMS;
+  const size_t lds = sizeof(uint16_t) * G::LDS_ELEMS;
   if (backward)
-    hipLaunchKernelGGL((lstm_large_bwd_step_kernel<DT, BM, BN>), grid, dim3(256), lds, st, *a);
+    hipLaunchKernelGGL((lstm_large_bwd_step_kernel<DT, BM, BN, WM, WN, ST>), grid, dim3(G::NTHREADS), lds, st, *a);
   else
-    hipLaunchKernelGGL((lstm_large_fwd_step_kernel<DT, BM, BN>), grid, dim3(256), lds, st, *a);
+    hipLaunchKernelGGL((lstm_large_fwd_step_kernel<DT, BM, BN, WM, WN, ST>), grid, dim3(G::NTHREADS), lds, st, *a);
   return hipGetLastError();
 }
 
-// Tile choice: enough workgroups to cover the CUs (256) at small batch,
-// bigger tiles (more MFMA per LDS byte) once the batch allows.
+// Tile choice: the largest tile that still gives >= 256 workgroups (one per
+// CU) and does not waste more than half of its rows on a small batch.
+inline int pick_tile(int M, int N, int ndir) {
+  const int bm[4] = {32, 64, 128, 256}, bn[4] = {64, 64, 128, 128};
+  for (int c = 3; c >= 0; --c) {
+    if (N % bn[c]) continue;
+    if (c > 0 && M <= bm[c] / 2) continue;
+    const int64_t blocks = (int64_t)(N / bn[c]) * ((M + bm[c] - 1) / bm[c]) * ndir;
+    if (blocks >= 256) return c;
+  }
+  return 0;
+}
+
 template <class DT>
 hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, int tile, hipStream_t st) {
   const int N = backward ? a->H : 4 * a->H;
-  if (tile <= 0) {
-    const int64_t t64 = (int64_t)(N / 64) * ((a->B + 63) / 64) * ndir;
-    const int64_t t128 = (int64_t)(N / 128) * ((a->B + 127) / 128) * ndir;
-    tile = t128 >= 512 ? 128 : (t64 >= 256 ? 64 : 32);
-  }
+  if (tile < 0 || tile > 3) tile = pick_tile(a->B, N, ndir);
   switch (tile) {
-    case 32: return launch_step<DT, 32, 64>(a, ndir, backward, st);
-    case 64: return launch_step<DT, 64, 64>(a, ndir, backward, st);
-    case 128:
-      if (N % 128) return launch_step<DT, 64, 64>(a, ndir, backward, st);
-      return launch_step<DT, 128, 128>(a, ndir, backward, st);
+#define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_) \
+  case ID: return launch_step<DT, BM_, BN_, WM_, WN_, ST_>(a, ndir, backward, st);
+    PDRNN_TILE_CFGS(PDRNN_CASE)
+#undef PDRNN_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <class DT>
+hipError_t gemm_nt_dispatch(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
+                            int M, int N, int K, int tile, hipStream_t st) {
+  if (tile < 0 || tile > 3) tile = pick_tile(M, N, 1);
+  switch (tile) {
+#define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_)                                                      \
+  case ID: {                                                                                        \
+    typedef GemmPipe<DT, BM_, BN_, WM_, WN_, ST_> G;                                                 \
+    if (N % BN_) return hipErrorInvalidValue;                                                        \
+    dim3 grid(N / BN_, (M + BM_ - 1) / BM_);                                                         \
+    hipLaunchKernelGGL((gemm_nt_kernel<DT, BM_, BN_, WM_, WN_, ST_>), grid, dim3(G::NTHREADS),       \
+                       sizeof(uint16_t) * G::LDS_ELEMS, st, A, lda, Bt, ldb, C, ldc, M, N, K);       \
+    return hipGetLastError();                                                                        \
+  }
+    PDRNN_TILE_CFGS(PDRNN_CASE)
+#undef PDRNN_CASE
     default: return hipErrorInvalidValue;
   }
 }
@@ -412,17 +458,10 @@ hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir,
 }
 
 hipError_t pdrnn_gemm_nt(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
-                         int M, int N, int K, int dtype, hipStream_t stream) {
+                         int M, int N, int K, int dtype, int tile, hipStream_t stream) {
   if (K % 64 || N % 64) return hipErrorInvalidValue;
-  dim3 grid(N / 64, (M + 63) / 64);
-  const size_t lds = sizeof(uint16_t) * pdrnn::GemmNT<pdrnn::BF16, 64, 64>::LDS_ELEMS;
-  if (dtype == 0)
-    hipLaunchKernelGGL((pdrnn::gemm_nt_kernel<pdrnn::BF16, 64, 64>), grid, dim3(256), lds, stream, A, lda, Bt, ldb,
-                       C, ldc, M, N, K);
-  else
-    hipLaunchKernelGGL((pdrnn::gemm_nt_kernel<pdrnn::F16, 64, 64>), grid, dim3(256), lds, stream, A, lda, Bt, ldb,
-                       C, ldc, M, N, K);
-  return hipGetLastError();
+  if (dtype == 0) return pdrnn::gemm_nt_dispatch<pdrnn::BF16>(A, lda, Bt, ldb, C, ldc, M, N, K, tile, stream);
+  return pdrnn::gemm_nt_dispatch<pdrnn::F16>(A, lda, Bt, ldb, C, ldc, M, N, K, tile, stream);
 }
 
 }  // extern "C"

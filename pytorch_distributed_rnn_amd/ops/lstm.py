@@ -132,7 +132,11 @@ def lstm_reference(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[
     """Stock ATen LSTM (CPU / MIOpen) -- the torch reference path for tests."""
     dirs = 2 if bidirectional else 1
     has_bias = weights[2] is not None
-    flat = [w for w in weights if w is not None]
+    # mixed precision (16-bit activations, fp32 master weights): compute in the
+    # activation dtype, like torch.autocast does for nn.LSTM
+    flat = [w if w.dtype == x.dtype else w.to(x.dtype) for w in weights if w is not None]
+    if h0 is not None and h0.dtype != x.dtype:
+        h0, c0 = h0.to(x.dtype), c0.to(x.dtype)
     if h0 is None:
         b = x.shape[0] if batch_first else x.shape[1]
         h0 = x.new_zeros(num_layers * dirs, b, hidden)

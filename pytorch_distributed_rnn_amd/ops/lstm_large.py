@@ -42,9 +42,9 @@ def _perm(hidden: int, device) -> Tensor:
 
 def _tile() -> int:
     try:
-        return int(os.environ.get("PDRNN_LSTM_LARGE_TILE", "0"))
+        return int(os.environ.get("PDRNN_LSTM_LARGE_TILE", "-1"))
     except ValueError:
-        return 0
+        return -1
 
 
 def supported(x: Tensor, hidden: int, num_layers: int, bidirectional: bool = False) -> bool:

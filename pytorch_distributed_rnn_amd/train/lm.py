@@ -1,0 +1,96 @@
+"""Language-model trainer: truncated BPTT over token streams, local or
+data-parallel (the framework's DDP: bucketed RCCL all-reduce overlapped with
+the BPTT backward), fused Adam on the flat parameter buffer, flat-buffer
+gradient clipping without a host sync.
+
+The hidden state is carried across consecutive segments of a stream and
+reset at every epoch start -- the working version of the reference's dead
+``_reset_hidden_state`` hook (reference: src/motion/trainer/base.py:161-162,
+src/motion/trainer/ddp.py:35-36).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import time
+from typing import Dict, List, Optional
+
+import torch
+from torch import Tensor, nn
+
+from ..data.charlm import CharCorpus
+from ..ops.adam import FusedAdam
+from ..ops.xent import cross_entropy
+from ..parallel import env
+from ..parallel.ddp import DistributedDataParallel
+from ..utils.flat import flatten_module
+from ..utils.memory import device_peak_mib
+
+
+class LMTrainer:
+    def __init__(self, model: nn.Module, corpus: CharCorpus, global_batch: int, seq_len: int,
+                 learning_rate: float = 2e-3, device: Optional[torch.device] = None,
+                 distributed: bool = False, backend: Optional[str] = None, grad_clip: float = 1.0,
+                 log_interval: int = 50, bucket_cap_mb: Optional[float] = None,
+                 weak_scaling: bool = False):
+        self.rank, self.world = 0, 1
+        if distributed:
+            info = env.init_distributed(backend)
+            self.rank, self.world = env.get_rank(), env.get_world_size()
+            if device is None:
+                device = (env.setup_device(info) if torch.distributed.get_backend() == "nccl"
+                          else torch.device("cpu"))
+        if device is None:
+            device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        self.device = device
+        self.inner = model.to(device)
+        flatten_module(self.inner)
+        self.model = (DistributedDataParallel(self.inner, bucket_cap_mb=bucket_cap_mb)
+                      if distributed and self.world > 1 else self.inner)
+        self.flat = next(iter(self.inner._pdrnn_flat.values()))
+        self.optimizer = FusedAdam(self.inner.parameters(), lr=learning_rate)
+        self.seq_len = seq_len
+        self.grad_clip = grad_clip
+        self.log_interval = log_interval
+        gb = global_batch * self.world if weak_scaling else global_batch
+        self.global_batch = gb
+        self.streams = corpus.streams(gb, self.rank, self.world).to(device)
+        self.vocab = corpus.vocab_size
+
+    def _clip(self) -> None:
+        if self.grad_clip and self.grad_clip > 0:
+            g = self.flat.grad
+            norm = torch.linalg.vector_norm(g)
+            g.mul_(torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0))
+
+    def train_step(self, inp: Tensor, tgt: Tensor) -> Tensor:
+        self.optimizer.zero_grad()
+        logits = self.model(inp, carry=True)                                   # [T, B, V]
+        loss = cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt.t().reshape(-1))
+        loss.backward()
+        self._clip()
+        self.optimizer.step()
+        return loss.detach()
+
+    def train_epoch(self, epoch: int = 0, max_steps: Optional[int] = None) -> Dict[str, float]:
+        self.inner.train()
+        self.inner.reset_hidden_state()
+        losses: List[Tensor] = []
+        tokens = 0
+        t0 = time.perf_counter()
+        for step, (inp, tgt) in enumerate(CharCorpus.segments(self.streams, self.seq_len, max_steps)):
+            losses.append(self.train_step(inp, tgt))
+            tokens += inp.numel()
+            if self.log_interval and (step + 1) % self.log_interval == 0:
+                cur = float(torch.stack(losses[-self.log_interval:]).mean())
+                logging.info(f"Rank: {self.rank:02d}   Epoch {epoch} Step {step + 1}\tLoss: {cur:.6f}"
+                             f"\tbpc: {cur / math.log(2):.4f}")
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dt = time.perf_counter() - t0
+        mean = float(torch.stack(losses).mean()) if losses else float("nan")
+        out = {"loss": mean, "tokens": tokens, "duration": dt, "tokens_per_sec": tokens / dt if dt else 0.0,
+               "steps": len(losses), "device_peak_mib": device_peak_mib(self.device)}
+        logging.info(f"{self.rank}: Epoch {epoch} loss {mean:.6f} tokens/s {out['tokens_per_sec']:.1f} "
+                     f"(x{self.world} ranks) device_peak_mib={out['device_peak_mib']:.1f}")
+        return out

@@ -1,0 +1,66 @@
+"""Char-LM stack on the CPU: corpus layout, TBPTT state carry/reset, and the
+DDP world-size invariance of the per-step loss (gloo, W=2)."""
+import os
+import re
+
+import torch
+
+from _mp import ROOT, run, torchrun
+from pytorch_distributed_rnn_amd.data.charlm import CharCorpus
+from pytorch_distributed_rnn_amd.models.charlm import BiLSTMEncoder, CharLM
+
+_STEP = re.compile(r"Rank: (\d+)\s+Epoch 0 Step (\d+)\tLoss: ([\d.]+)")
+
+
+def test_corpus_streams_and_segments():
+    c = CharCorpus(torch.arange(1000), vocab_size=1000)
+    s = c.streams(4)
+    assert s.shape == (4, 250) and int(s[1, 0]) == 250
+    r1 = c.streams(4, rank=1, world=2)
+    assert torch.equal(r1, s[2:])
+    segs = list(CharCorpus.segments(s, 10, limit=3))
+    assert len(segs) == 3
+    inp, tgt = segs[1]
+    assert torch.equal(tgt[:, :-1], inp[:, 1:]) and int(inp[0, 0]) == 10
+
+
+def test_synthetic_corpus_is_learnable_shape():
+    c = CharCorpus.synthetic(5000, 64, seed=1)
+    assert len(c) == 5000 and int(c.tokens.max()) < 64 and int(c.tokens.min()) >= 0
+    assert (c.tokens == 0).float().mean() > 0.05  # separators present
+
+
+def test_tbptt_carry_and_reset():
+    torch.manual_seed(0)
+    m = CharLM(32, 8, 16, 2)
+    tok = torch.randint(0, 32, (3, 5))
+    a = m(tok, carry=True)
+    b = m(tok, carry=True)          # continues from a's final state
+    m.reset_hidden_state()
+    c = m(tok, carry=True)
+    assert a.shape == (5, 3, 32)
+    assert torch.allclose(a, c) and not torch.allclose(a, b)
+
+
+def test_bilstm_encoder_shape():
+    m = BiLSTMEncoder(6, 8, 2, 3)
+    assert m(torch.randn(7, 2, 6)).shape == (7, 2, 3)
+
+
+def _losses(log):
+    out = {}
+    for m in _STEP.finditer(log):
+        out.setdefault(int(m.group(1)), []).append(float(m.group(3)))
+    return out
+
+
+def test_lm_ddp_invariance(tmp_path):
+    args = ["-m", "pytorch_distributed_rnn_amd.lm_cli", "--hidden", "16", "--embed", "8", "--seq-len", "16",
+            "--batch-size", "8", "--synthetic-tokens", "4000", "--max-steps", "4", "--log-interval", "1",
+            "--device", "cpu", "--vocab", "64"]
+    local = _losses(run(["python"] + args + ["local"], cwd=ROOT))[0]
+    dist = _losses(torchrun(args + ["distributed"], 2, cwd=ROOT))
+    mean = [(a + b) / 2 for a, b in zip(dist[0], dist[1])]
+    assert len(mean) == len(local) == 4
+    for x, y in zip(mean, local):
+        assert abs(x - y) < 5e-5, (mean, local)

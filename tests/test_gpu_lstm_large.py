@@ -15,15 +15,36 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("M,N,K", [(70, 128, 192), (128, 256, 64), (5, 64, 1024)])
-def test_gemm_nt_core(dt, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(70, 128, 192), (128, 256, 64), (5, 128, 1024), (300, 256, 320)])
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3])
+def test_gemm_nt_core(dt, M, N, K, tile):
     mod = _ext.require()
     torch.manual_seed(0)
     a = torch.randn(M, K, device="cuda").to(dt)
     b = torch.randn(N, K, device="cuda").to(dt)
-    c = mod.gemm_nt(a, b)
+    c = mod.gemm_nt(a, b, tile)
     ref = a.float() @ b.float().t()
     torch.testing.assert_close(c, ref, rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+def test_large_lstm_every_tile(tile, monkeypatch):
+    monkeypatch.setenv("PDRNN_LSTM_LARGE_TILE", str(tile))
+    torch.manual_seed(4)
+    m = LSTM(64, 128, 1, batch_first=True, bidirectional=True).cuda()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    ref = _ref_model(m)
+    x = torch.randn(37, 5, 64, device="cuda").to(torch.bfloat16)
+    out, _ = m(x)
+    out_r, _ = ref(x.float())
+    assert _rel(out, out_r) < 2e-2
+    g = torch.randn_like(out_r)
+    (out.float() * g).sum().backward()
+    (out_r * g).sum().backward()
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert _rel(p.grad, q.grad) < 4e-2, n
 
 
 def _ref_model(m: LSTM):
@@ -82,3 +103,16 @@ def test_large_lstm_state_grads():
     (hn_r.sum() + 0.5 * cn_r.sum()).backward()
     assert _rel(h0a.grad, h0b.grad) < 4e-2
     assert _rel(c0a.grad, c0b.grad) < 4e-2
+
+
+def test_charlm_trains_on_large_path():
+    from pytorch_distributed_rnn_amd.data.charlm import CharCorpus
+    from pytorch_distributed_rnn_amd.models.charlm import CharLM
+    from pytorch_distributed_rnn_amd.train.lm import LMTrainer
+    torch.manual_seed(0)
+    corpus = CharCorpus.synthetic(200_000, 64, seed=0)
+    tr = LMTrainer(CharLM(64, 32, 128, 2, 0.0, torch.bfloat16), corpus, 16, 64, 3e-3,
+                   device=torch.device("cuda", 0), log_interval=0)
+    first = tr.train_epoch(0, max_steps=5)["loss"]
+    hist = [tr.train_epoch(e, max_steps=40)["loss"] for e in range(1, 3)]
+    assert hist[-1] < first - 0.5, (first, hist)
