@@ -445,7 +445,11 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
   CHECK_HIP_TENSOR(dout);
   const c10::DeviceGuard guard(dout.device());
   const int64_t dim = dout.size(-1);
-  Tensor g = dout.to(at::kFloat).contiguous().view({-1, dim});
+  Tensor g = dout.contiguous().view({-1, dim});
+  int dt = 2;
+  if (g.scalar_type() == at::kBFloat16) dt = 0;
+  else if (g.scalar_type() == at::kHalf) dt = 1;
+  else g = g.to(at::kFloat);
   Tensor flat = idx.contiguous().view({-1});
   flat = at::where(flat < 0, flat + num_embeddings, flat);
   auto sorted = at::sort(flat, /*stable=*/true, /*dim=*/0, /*descending=*/false);
@@ -453,8 +457,8 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
   Tensor bounds = at::arange(num_embeddings + 1, flat.options());
   Tensor offsets = at::searchsorted(vals, bounds).contiguous();
   Tensor dw = at::empty({num_embeddings, dim}, dout.options().dtype(at::kFloat));
-  HIP_LAUNCH_CHECK(pdrnn_embedding_bwd_csr(g.data_ptr<float>(), perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(),
-                                           dw.data_ptr<float>(), num_embeddings, dim, padding_idx, cur_stream()));
+  HIP_LAUNCH_CHECK(pdrnn_embedding_bwd_csr2(g.data_ptr(), dt, perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(),
+                                            dw.data_ptr<float>(), num_embeddings, dim, padding_idx, cur_stream()));
   return dw;
 }
 

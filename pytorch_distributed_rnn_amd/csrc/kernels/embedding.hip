@@ -76,6 +76,49 @@ __global__ void __launch_bounds__(256) emb_bwd_csr_kernel(const float* __restric
   }
 }
 
+// Same contract, latency-hiding form: one wave per (vocab row, 64-column
+// slice); the contribution list is walked 8 rows at a time (8 independent
+// index loads, then 8 independent row loads, summed in list order -- still
+// bitwise deterministic).  dout may be fp32 / bf16 / fp16 (DT 2 / 0 / 1).
+template <int DT>
+__device__ __forceinline__ float ld_as_f(const void* p, int64_t i) {
+  if constexpr (DT == 2) return reinterpret_cast<const float*>(p)[i];
+  const uint16_t v = reinterpret_cast<const uint16_t*>(p)[i];
+  if constexpr (DT == 0) return __uint_as_float(((uint32_t)v) << 16);
+  return (float)__builtin_bit_cast(_Float16, v);
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) emb_bwd_csr8_kernel(const void* __restrict__ dout,
+                                                           const int64_t* __restrict__ perm,
+                                                           const int64_t* __restrict__ off, float* __restrict__ dw,
+                                                           int64_t V, int64_t dim, int64_t padding_idx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t slices = (dim + 63) / 64;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = wave; w < V * slices; w += nwaves) {
+    const int64_t v = w / slices;
+    const int64_t c = (w - v * slices) * 64 + lane;
+    const int64_t cc = c < dim ? c : dim - 1;
+    const int64_t j0 = off[v], j1 = off[v + 1];
+    float acc = 0.f;
+    if (v != padding_idx) {
+      for (int64_t j = j0; j < j1; j += 8) {
+        int64_t p[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[k] = perm[min(j + k, j1 - 1)];
+        float x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = ld_as_f<DT>(dout, p[k] * dim + cc);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += (j + k < j1) ? x[k] : 0.f;
+      }
+    }
+    if (c < dim) dw[v * dim + c] = acc;
+  }
+}
+
 int blocks_for(int64_t rows) {
   int64_t b = (rows + 3) / 4;  // 4 waves per block, one row per wave
   if (b < 1) b = 1;
@@ -105,6 +148,23 @@ hipError_t pdrnn_embedding_fwd16(const float* weight, const int64_t* idx, uint16
   else
     hipLaunchKernelGGL(pdrnn::emb_fwd16_kernel<1>, dim3(pdrnn::blocks_for(n_idx)), dim3(256), 0, stream, weight, idx,
                        out, n_idx, dim, num_embeddings);
+  return hipGetLastError();
+}
+
+hipError_t pdrnn_embedding_bwd_csr2(const void* dout, int dout_dtype, const int64_t* perm, const int64_t* offsets,
+                                   float* dweight, int64_t num_embeddings, int64_t dim, int64_t padding_idx,
+                                   hipStream_t stream) {
+  const int64_t waves = num_embeddings * ((dim + 63) / 64);
+  const dim3 grid(pdrnn::blocks_for(waves)), block(256);
+  if (dout_dtype == 0)
+    hipLaunchKernelGGL(pdrnn::emb_bwd_csr8_kernel<0>, grid, block, 0, stream, dout, perm, offsets, dweight,
+                       num_embeddings, dim, padding_idx);
+  else if (dout_dtype == 1)
+    hipLaunchKernelGGL(pdrnn::emb_bwd_csr8_kernel<1>, grid, block, 0, stream, dout, perm, offsets, dweight,
+                       num_embeddings, dim, padding_idx);
+  else
+    hipLaunchKernelGGL(pdrnn::emb_bwd_csr8_kernel<2>, grid, block, 0, stream, dout, perm, offsets, dweight,
+                       num_embeddings, dim, padding_idx);
   return hipGetLastError();
 }
 

@@ -182,7 +182,8 @@ struct GemmPipe {
   X(0, 32, 64, 1, 4, 4)      \
   X(1, 64, 64, 2, 2, 4)      \
   X(2, 128, 128, 2, 2, 3)    \
-  X(3, 256, 128, 4, 2, 3)
+  X(3, 256, 128, 4, 2, 3)    \
+  X(4, 32, 32, 2, 2, 4)
 
 // ---------------------------------------------------------------------------
 // Forward step: gates = h_{t-1} Wp^T + xp_t  ->  (i, f, g, o), c_t, h_t.
@@ -212,45 +213,60 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
     G::run(hA, lda, d.w, H, B, H, m0, n0, smem_u16, acc);
   }
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int q = lane & 3;
+  // Epilogue through LDS: the C tile is parked as fp32 [BM][BN+4] in the
+  // (now idle) staging ring, then every thread owns 8 consecutive columns
+  // (= 2 hidden units x 4 gates) of a row: 16-byte loads of xp, 16-byte
+  // stores of the activated gates, 8-byte c and 4-byte h -- instead of
+  // 2-byte scattered accesses straight from the MFMA C layout.
+  constexpr int LDC = BN + 4;
+  static_assert(BM * LDC * 4 <= G::LDS_ELEMS * 2, "C tile must fit in the staging ring");
+  float* cs = reinterpret_cast<float*>(smem_u16);
+  {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+#pragma unroll
+    for (int i = 0; i < G::MT; ++i)
+#pragma unroll
+      for (int j = 0; j < G::NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          cs[(wm * G::WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * G::WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+  }
+  __syncthreads();
   const uint16_t* xp = d.xp + (int64_t)t * d.xp_st;
   const float* cprev = first ? d.c0 : d.cseq + (int64_t)tp * B * H;
   float* cout = d.cseq + (int64_t)t * B * H;
   uint16_t* hout = d.hseq + (int64_t)t * d.hseq_st;
   uint16_t* acts = d.acts + (int64_t)t * B * 4 * H;
+  constexpr int C8 = BN / 8;
+  for (int e = threadIdx.x; e < BM * C8; e += G::NTHREADS) {
+    const int row = e / C8, c8 = e - row * C8;
+    const int b = m0 + row;
+    if (b >= B) continue;
+    const int col = n0 + c8 * 8;
+    const float4 z0 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8);
+    const float4 z1 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8 + 4);
+    const uint4 xv = *reinterpret_cast<const uint4*>(xp + (int64_t)b * d.xp_sb + col);
+    const uint16_t* xh = reinterpret_cast<const uint16_t*>(&xv);
+    const float z[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+    float g[8];
+    uint4 av;
+    uint16_t* ah = reinterpret_cast<uint16_t*>(&av);
 #pragma unroll
-  for (int i = 0; i < G::MT; ++i) {
-    const int rbase = m0 + wm * G::WTM + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int j = 0; j < G::NT; ++j) {
-      const int col = n0 + wn * G::WTN + j * 16 + (lane & 15);
-      const int u = col >> 2;
-      float a[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = min(rbase + r, B - 1);
-        const float z = acc[i][j][r] + DT::to_f(xp[(int64_t)row * d.xp_sb + col]);
-        a[r] = q == 2 ? tanh_(z) : sigm(z);
-        if (rbase + r < B) acts[(int64_t)row * 4 * H + col] = DT::from_f(a[r]);
-      }
-      // lane q of the quad finishes row rbase + q of unit u
-      float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float i_ = qbcast(a[r], 0), f_ = qbcast(a[r], 1), g_ = qbcast(a[r], 2), o_ = qbcast(a[r], 3);
-        if (r == q) { ig = i_; fg = f_; gg = g_; og = o_; }
-      }
-      const int row = rbase + q;
-      if (row < B) {
-        const float cp = cprev ? cprev[(int64_t)row * H + u] : 0.f;
-        const float cn = fmaf(fg, cp, ig * gg);
-        const float h = og * tanh_(cn);
-        cout[(int64_t)row * H + u] = cn;
-        hout[(int64_t)row * d.hseq_sb + u] = DT::from_f(h);
-      }
+    for (int k = 0; k < 8; ++k) {
+      const float zz = z[k] + DT::to_f(xh[k]);
+      g[k] = (k & 3) == 2 ? tanh_(zz) : sigm(zz);
+      ah[k] = DT::from_f(g[k]);
     }
+    *reinterpret_cast<uint4*>(acts + (int64_t)b * 4 * H + col) = av;
+    const int u = col >> 2;
+    float2 cp = make_float2(0.f, 0.f);
+    if (cprev) cp = *reinterpret_cast<const float2*>(cprev + (int64_t)b * H + u);
+    const float c0n = fmaf(g[1], cp.x, g[0] * g[2]);
+    const float c1n = fmaf(g[5], cp.y, g[4] * g[6]);
+    *reinterpret_cast<float2*>(cout + (int64_t)b * H + u) = make_float2(c0n, c1n);
+    const uint32_t hv = (uint32_t)DT::from_f(g[3] * tanh_(c0n)) | ((uint32_t)DT::from_f(g[7] * tanh_(c1n)) << 16);
+    *reinterpret_cast<uint32_t*>(hout + (int64_t)b * d.hseq_sb + u) = hv;
   }
 }
 
@@ -389,6 +405,8 @@ hipError_t launch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward,
 
 // Tile choice: the largest tile that still gives >= 256 workgroups (one per
 // CU) and does not waste more than half of its rows on a small batch.
+// Fallback when no tile reaches one workgroup per CU: the 32x32 tile (most
+// workgroups; the recurrent step is latency-bound there).
 inline int pick_tile(int M, int N, int ndir) {
   const int bm[4] = {32, 64, 128, 256}, bn[4] = {64, 64, 128, 128};
   for (int c = 3; c >= 0; --c) {
@@ -397,13 +415,13 @@ inline int pick_tile(int M, int N, int ndir) {
     const int64_t blocks = (int64_t)(N / bn[c]) * ((M + bm[c] - 1) / bm[c]) * ndir;
     if (blocks >= 256) return c;
   }
-  return 0;
+  return 4;
 }
 
 template <class DT>
 hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, int tile, hipStream_t st) {
   const int N = backward ? a->H : 4 * a->H;
-  if (tile < 0 || tile > 3) tile = pick_tile(a->B, N, ndir);
+  if (tile < 0 || tile > 4) tile = pick_tile(a->B, N, ndir);
   switch (tile) {
 #define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_) \
   case ID: return launch_step<DT, BM_, BN_, WM_, WN_, ST_>(a, ndir, backward, st);
@@ -416,7 +434,7 @@ hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwar
 template <class DT>
 hipError_t gemm_nt_dispatch(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
                             int M, int N, int K, int tile, hipStream_t st) {
-  if (tile < 0 || tile > 3) tile = pick_tile(M, N, 1);
+  if (tile < 0 || tile > 4) tile = pick_tile(M, N, 1);
   switch (tile) {
 #define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_)                                                      \
   case ID: {                                                                                        \
@@ -459,7 +477,7 @@ hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir,
 
 hipError_t pdrnn_gemm_nt(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
                          int M, int N, int K, int dtype, int tile, hipStream_t stream) {
-  if (K % 64 || N % 64) return hipErrorInvalidValue;
+  if (K % 64 || N % 32) return hipErrorInvalidValue;
   if (dtype == 0) return pdrnn::gemm_nt_dispatch<pdrnn::BF16>(A, lda, Bt, ldb, C, ldc, M, N, K, tile, stream);
   return pdrnn::gemm_nt_dispatch<pdrnn::F16>(A, lda, Bt, ldb, C, ldc, M, N, K, tile, stream);
 }

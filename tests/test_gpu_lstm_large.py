@@ -16,7 +16,7 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,N,K", [(70, 128, 192), (128, 256, 64), (5, 128, 1024), (300, 256, 320)])
-@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3, 4])
 def test_gemm_nt_core(dt, M, N, K, tile):
     mod = _ext.require()
     torch.manual_seed(0)
@@ -27,7 +27,7 @@ def test_gemm_nt_core(dt, M, N, K, tile):
     torch.testing.assert_close(c, ref, rtol=2e-3, atol=2e-3)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
 def test_large_lstm_every_tile(tile, monkeypatch):
     monkeypatch.setenv("PDRNN_LSTM_LARGE_TILE", str(tile))
     torch.manual_seed(4)
@@ -116,3 +116,23 @@ def test_charlm_trains_on_large_path():
     first = tr.train_epoch(0, max_steps=5)["loss"]
     hist = [tr.train_epoch(e, max_steps=40)["loss"] for e in range(1, 3)]
     assert hist[-1] < first - 0.5, (first, hist)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_embedding_bwd_csr8(dt):
+    mod = _ext.require()
+    torch.manual_seed(5)
+    V, D, N = 300, 200, 5000
+    idx = torch.randint(0, V, (N,), device="cuda")
+    idx[:7] = 3  # a hot row
+    g = torch.randn(N, D, device="cuda").to(dt)
+    dw = mod.embedding_bwd(g, idx, V, 5)
+    ref = torch.zeros(V, D, device="cuda").index_add_(0, idx, g.float())
+    ref[5] = 0
+    torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-4)
+    # bitwise deterministic
+    assert torch.equal(dw, mod.embedding_bwd(g, idx, V, 5))
+    # fused 16-bit gather
+    w = torch.randn(V, D, device="cuda")
+    out = mod.embedding_fwd(w, idx, torch.bfloat16)
+    assert out.dtype == torch.bfloat16 and torch.equal(out, w[idx].to(torch.bfloat16))
