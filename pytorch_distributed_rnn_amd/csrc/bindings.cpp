@@ -110,7 +110,8 @@ void check_stack(const std::vector<Tensor>& w, int64_t NL, int64_t H, int64_t I,
 // with idx, x is a [N,T,I] source table and B = len(idx).
 std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx, const std::vector<Tensor>& w,
                                    const optional<Tensor>& h0, const optional<Tensor>& c0, int64_t H, int64_t NL,
-                                   bool batch_first, bool save, bool need_out, int64_t nb, int64_t split) {
+                                   bool batch_first, bool save, bool need_out, int64_t nb, int64_t split,
+                                   int64_t cell) {
   CHECK_HIP_TENSOR(x); CHECK_F32(x);
   TORCH_CHECK(x.dim() == 3, "x must be 3-D");
   TORCH_CHECK(x.stride(2) == 1, "x innermost dim must be contiguous");
@@ -157,7 +158,7 @@ std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx,
     a.o_st = batch_first ? H : B * H;
   }
   a.hn = hn.data_ptr<float>(); a.cn = cn.data_ptr<float>();
-  a.B = (int)B; a.T = (int)T; a.I = (int)I; a.NL = (int)NL;
+  a.B = (int)B; a.T = (int)T; a.I = (int)I; a.NL = (int)NL; a.cell = (int)cell;
   if (split <= 0) split = pdrnn_lstm_small_max_split((int)H, (int)NL, 0);
   Tensor stamps;
   if (stamps_enabled()) {
@@ -176,7 +177,7 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
                                    const Tensor& act, const optional<Tensor>& dout, const optional<Tensor>& dhn,
                                    const optional<Tensor>& dcn, int64_t H, int64_t NL, bool batch_first,
                                    bool need_dx, bool need_dh0, int64_t nb, int64_t split,
-                                   const optional<Tensor>& grad_accum) {
+                                   const optional<Tensor>& grad_accum, int64_t cell) {
   CHECK_HIP_TENSOR(x);
   const c10::DeviceGuard guard(x.device());
   const int64_t I = x.size(2);
@@ -235,7 +236,7 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
   }
   a.slab = slab.data_ptr<float>();
   a.P = L.P;
-  a.B = (int)B; a.T = (int)T; a.I = (int)I; a.NL = (int)NL;
+  a.B = (int)B; a.T = (int)T; a.I = (int)I; a.NL = (int)NL; a.cell = (int)cell;
   Tensor dparams;
   float beta = 0.f;
   if (grad_accum.has_value() && grad_accum->defined()) {
@@ -588,8 +589,13 @@ Tensor gemm_nt(const Tensor& A, const Tensor& Bt, int64_t tile) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "pytorch_distributed_rnn_amd native runtime (gfx950 HIP kernels + RCCL runtime)";
-  m.def("lstm_small_fwd", &lstm_small_fwd, "fused small-H LSTM stack forward");
-  m.def("lstm_small_bwd", &lstm_small_bwd, "fused small-H LSTM stack BPTT backward");
+  m.def("lstm_small_fwd", &lstm_small_fwd, "fused small-H LSTM / GRU stack forward", py::arg("x"), py::arg("idx"),
+        py::arg("w"), py::arg("h0"), py::arg("c0"), py::arg("H"), py::arg("NL"), py::arg("batch_first"),
+        py::arg("save"), py::arg("need_out"), py::arg("nb"), py::arg("split"), py::arg("cell") = 0);
+  m.def("lstm_small_bwd", &lstm_small_bwd, "fused small-H LSTM / GRU stack BPTT backward", py::arg("x"),
+        py::arg("idx"), py::arg("w"), py::arg("h0"), py::arg("c0"), py::arg("hseq"), py::arg("act"), py::arg("dout"),
+        py::arg("dhn"), py::arg("dcn"), py::arg("H"), py::arg("NL"), py::arg("batch_first"), py::arg("need_dx"),
+        py::arg("need_dh0"), py::arg("nb"), py::arg("split"), py::arg("grad_accum"), py::arg("cell") = 0);
   m.def("lstm_small_max_split", [](int64_t H, int64_t NL, bool backward) {
     return pdrnn_lstm_small_max_split((int)H, (int)NL, backward ? 1 : 0);
   });

@@ -52,6 +52,7 @@ typedef struct {
   float inv_batch;
   int C;
   int B, T, I, NL;
+  int cell;                  // 0 = LSTM, 1 = GRU (packed as a 4-row-block stack, see ops/gru.py)
 } PdrnnLstmSmallFwdArgs;
 
 typedef struct {
@@ -79,6 +80,7 @@ typedef struct {
   uint64_t* stamps;          // diagnostics (see forward), or NULL
   int dhn_top_only;          // dhn is [B, H] for the top layer only (fused head path)
   int B, T, I, NL;
+  int cell;                  // 0 = LSTM, 1 = GRU (packed as a 4-row-block stack, see ops/gru.py)
 } PdrnnLstmSmallBwdArgs;
 
 // Query the launch geometry chosen for (H, B): returns grid size (number of slab rows).

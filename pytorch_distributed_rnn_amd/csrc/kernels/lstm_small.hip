@@ -224,7 +224,12 @@ __device__ __forceinline__ float quad_bcast(float v, int q) {
 
 constexpr float kNegLog2e = -1.4426950408889634f;
 
-template <int H, int NB, bool SAVE, bool XLDS, bool HEAD>
+// CELL 1 = GRU on the same lane map: the quad's four rows are [r | z | n_x |
+// n_h] (n_x = W_in x + b_in and n_h = W_hn h + b_hn kept linear), packed by the
+// host as a 4-block stack with zero blocks (W_ih: [W_ir; W_iz; W_in; 0], W_hh:
+// [W_hr; W_hz; 0; W_hn]); n = tanh(n_x + r n_h), h = n + z (h_prev - n).  The
+// saved activation slots hold r, z, n_x, n_h and n (in the cell-state slot).
+template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
 __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFwdArgs a) {
   constexpr int K = 2 * H;
   constexpr int LANES = 4 * H;
@@ -244,10 +249,12 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
   auto vin = [&](int n, int l, int p) -> float* { return smem + ((n * NL + l) * 2 + p) * K; };
 
   // activation: sigma(z) with z pre-scaled, then a = sigma * am + ab
-  const float gsc = q == 2 ? 2.f : 1.f;
-  const float am = q == 2 ? 2.f : 1.f;
-  const float ab = q == 2 ? -1.f : 0.f;
-  const float wsc = kNegLog2e * gsc;
+  // (GRU n_x / n_h rows stay linear: unscaled weights, activation skipped)
+  const bool lin = CELL == 1 && q >= 2;
+  const float gsc = (CELL == 0 && q == 2) ? 2.f : 1.f;
+  const float am = gsc;
+  const float ab = (CELL == 0 && q == 2) ? -1.f : 0.f;
+  const float wsc = lin ? 1.f : kNegLog2e * gsc;
 
   pdrnn_f2 w2[K / 2];
   float bias;
@@ -350,14 +357,21 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
         const pdrnn_f2 s2 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         const float z = (s2.x + s2.y) + bias;  // = -log2(e) * gsc * preactivation
         const float sg = fast_rcp(1.f + __builtin_amdgcn_exp2f(z));
-        const float act = fmaf(sg, am, ab);  // sigmoid, or tanh for the g gate
+        const float act = lin ? z : fmaf(sg, am, ab);  // sigmoid, or tanh for the g gate
         const float ig = quad_bcast(act, 0);
         const float fg = quad_bcast(act, 1);
         const float gg = quad_bcast(act, 2);
         const float og = quad_bcast(act, 3);
-        const float cn = fmaf(fg, c[n], ig * gg);
-        const float th = fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(cn * (2.f * kNegLog2e))), 2.f, -1.f);
-        const float h = og * th;
+        float cn, h;
+        if constexpr (CELL == 0) {
+          cn = fmaf(fg, c[n], ig * gg);
+          const float th = fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(cn * (2.f * kNegLog2e))), 2.f, -1.f);
+          h = og * th;
+        } else {  // GRU: ig = r, fg = z, gg = n_x, og = n_h; cn carries n
+          const float pre = fmaf(ig, og, gg);
+          cn = fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(pre * (2.f * kNegLog2e))), 2.f, -1.f);
+          h = fmaf(fg, hl[n] - cn, cn);
+        }
         c[n] = cn;
         hl[n] = h;
         if (q == 0) vin(n, layer, p ^ 1)[H + u] = h;
@@ -383,7 +397,7 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
     const int b = bbase + n;
     if (valid[n] && q == 0) {
       a.hn[((int64_t)layer * B + b) * H + u] = hl[n];
-      a.cn[((int64_t)layer * B + b) * H + u] = c[n];
+      if (CELL == 0) a.cn[((int64_t)layer * B + b) * H + u] = c[n];
     }
   }
   if constexpr (HEAD) {
@@ -714,7 +728,11 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
 // through h_T of the top layer, no dx / dh0 / dc0 outputs) with every optional
 // operand folded away at compile time -- fewer live pointers and no per-step
 // branches on the hot path.
-template <int H, int L, int NB, bool XLDS, bool LEAN>
+// CELL 1 = GRU (packing as in the forward): the gate-gradient vector is
+// [dr*r(1-r) | dz*z(1-z) | dpre_n | dpre_n*r] with dpre_n = dh (1-z) (1-n^2),
+// so the column phase (W^T g, dW += g h^T / g x^T) is the LSTM's unchanged;
+// the direct path dh_{t-1} += dh_t z rides in the dc register.
+template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0>
 __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBwdArgs a) {
   constexpr int R = 4 * H;
   constexpr int RS = R / L;          // rows per lane
@@ -856,19 +874,30 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       if (active) {
 #pragma unroll
         for (int n = 0; n < NB; ++n) {
-          const float cp = (t > 0 || c0p) ? op[n].cp : 0.f;
           float dht = dh[n] + (has_dout ? op[n].dout : 0.f);
           if (!top) dht += dhabuf(n, layer, p)[u];  // written by the layer above 2 iterations ago
           const float ig = quad_bcast(op[n].aq, 0), fg = quad_bcast(op[n].aq, 1);
           const float gg = quad_bcast(op[n].aq, 2), og = quad_bcast(op[n].aq, 3);
-          const float tc = tanhf_fast(op[n].ct);
-          const float dcp = fmaf(dht * og, 1.f - tc * tc, dc[n]);
-          const float d_i = dcp * gg * ig * (1.f - ig);
-          const float d_f = dcp * cp * fg * (1.f - fg);
-          const float d_g = dcp * ig * (1.f - gg * gg);
-          const float d_o = dht * tc * og * (1.f - og);
-          const float dgv = q == 0 ? d_i : (q == 1 ? d_f : (q == 2 ? d_g : d_o));
-          dc[n] = dcp * fg;
+          float dgv;
+          if constexpr (CELL == 0) {
+            const float cp = (t > 0 || c0p) ? op[n].cp : 0.f;
+            const float tc = tanhf_fast(op[n].ct);
+            const float dcp = fmaf(dht * og, 1.f - tc * tc, dc[n]);
+            const float d_i = dcp * gg * ig * (1.f - ig);
+            const float d_f = dcp * cp * fg * (1.f - fg);
+            const float d_g = dcp * ig * (1.f - gg * gg);
+            const float d_o = dht * tc * og * (1.f - og);
+            dgv = q == 0 ? d_i : (q == 1 ? d_f : (q == 2 ? d_g : d_o));
+            dc[n] = dcp * fg;
+          } else {  // GRU: ig = r, fg = z, og = n_h, ct = n
+            const float hp = (t > 0 || h0p) ? op[n].hprev : 0.f;
+            const float nn = op[n].ct;
+            const float dpn = dht * (1.f - fg) * (1.f - nn * nn);
+            const float d_r = dpn * og * ig * (1.f - ig);
+            const float d_z = dht * (hp - nn) * fg * (1.f - fg);
+            dgv = q == 0 ? d_r : (q == 1 ? d_z : (q == 2 ? dpn : dpn * ig));
+            dc[n] = dht * fg;  // direct path into dh_{t-1}
+          }
           if (rowlane) {
             dgbuf(n, layer, p)[q * H + u] = dgv;
             if (valid[n]) db += dgv;
@@ -905,6 +934,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
           }
           const pdrnn_f2 shs = sh[0] + sh[1], sxs = sx[0] + sx[1];
           dh[n] = group_sum<L>(shs.x + shs.y);  // dh_{t-1}[u] on every lane of the unit
+          if constexpr (CELL == 1) dh[n] += dc[n];
           const float dx = group_sum<L>(sxs.x + sxs.y);
           if (j == 0) {
             if (layer > 0) dhabuf(n, layer - 1, p)[u] = dx;  // consumed by layer-1 at it+2 (same parity)
@@ -929,7 +959,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       for (int n = 0; n < NB; ++n) {
         if (!valid[n]) continue;
         if (dh0p) dh0p[((int64_t)layer * B + bs[n]) * H + u] = dh[n];
-        if (dc0p) dc0p[((int64_t)layer * B + bs[n]) * H + u] = dc[n];
+        if (CELL == 0 && dc0p) dc0p[((int64_t)layer * B + bs[n]) * H + u] = dc[n];
       }
     }
     __syncthreads();  // LDS is reused by the next tile
@@ -1039,6 +1069,24 @@ hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
 }
 
 template <int H, int NB, bool SAVE>
+hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st);
+
+// GRU forward: one sequence per workgroup, no fused head.
+template <int H, bool SAVE>
+hipError_t launch_fwd_gs_gru(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
+  const int grid = a->B;
+  const int block = a->NL * 4 * H;
+  const size_t lds = sizeof(float) * a->NL * 2 * (2 * H);
+  const size_t xbytes = sizeof(float) * (size_t)a->T * H;
+  if (a->head_w) return hipErrorInvalidValue;
+  if (xbytes <= (size_t)kXldsBytes)
+    hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, 1, SAVE, true, false, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  else
+    hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, 1, SAVE, false, false, 1>), dim3(grid), dim3(block), lds, st, *a);
+  return hipGetLastError();
+}
+
+template <int H, int NB, bool SAVE>
 hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   const int grid = (a->B + NB - 1) / NB;
   const int block = a->NL * 4 * H;
@@ -1114,6 +1162,18 @@ int bwd_gs_grid(const PdrnnLstmSmallBwdArgs* a) {
   return tiles < cap ? tiles : cap;
 }
 
+template <int H, int L>
+hipError_t launch_bwd_gs_gru(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid) {
+  const int block = a->NL * H * L;
+  const size_t lds = bwd_gs_lds<H, 1>(a->NL), xbytes = bwd_gs_xbytes<H, 1>(a->T);
+  if (grid <= 0) grid = bwd_gs_grid<H, L, 1>(a);
+  if (xbytes <= (size_t)kXldsBytes)
+    hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, 1, true, false, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  else
+    hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, 1, false, false, 1>), dim3(grid), dim3(block), lds, st, *a);
+  return hipGetLastError();
+}
+
 template <int H, int L, int NB>
 hipError_t launch_bwd_gs(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid) {
   const int block = a->NL * H * L;
@@ -1172,8 +1232,10 @@ hipError_t dispatch_fwd_s(const PdrnnLstmSmallFwdArgs* a, int nb, int save, hipS
 
 template <int H>
 hipError_t dispatch_fwd(const PdrnnLstmSmallFwdArgs* a, int nb, int split, int save, hipStream_t st) {
+  if (a->cell == 1 && split != 1) return hipErrorInvalidConfiguration;  // GRU: gate-split map only
   if (split == 1) {  // gate-split map (4 lanes per unit, one gate each)
     if (a->NL * 4 * H > 512) return hipErrorInvalidConfiguration;
+    if (a->cell == 1) return save ? launch_fwd_gs_gru<H, true>(a, st) : launch_fwd_gs_gru<H, false>(a, st);
     if (save) return nb == 2 ? launch_fwd_gs<H, 2, true>(a, st) : launch_fwd_gs<H, 1, true>(a, st);
     return nb == 2 ? launch_fwd_gs<H, 2, false>(a, st) : launch_fwd_gs<H, 1, false>(a, st);
   }
@@ -1198,7 +1260,13 @@ hipError_t dispatch_bwd_s(const PdrnnLstmSmallBwdArgs* a, int nb, hipStream_t st
 
 template <int H>
 hipError_t dispatch_bwd(const PdrnnLstmSmallBwdArgs* a, int nb, int split, hipStream_t st, int grid_hint) {
+  if (a->cell == 1 && (split != 1 || nb != 1)) return hipErrorInvalidConfiguration;
   if (split == 1) {  // unit-group map, L lanes per unit (row slices of 4H/L)
+    if (a->cell == 1) {
+      if (a->NL * H * (H >= 64 ? 8 : 4) > 512) return hipErrorInvalidConfiguration;
+      if constexpr (H >= 64) return launch_bwd_gs_gru<H, 8>(a, st, grid_hint);
+      else return launch_bwd_gs_gru<H, 4>(a, st, grid_hint);
+    }
     if (bwd_gs_lanes<H>(a->NL) == 8) {
       if constexpr (H <= 32) {
         switch (nb) {

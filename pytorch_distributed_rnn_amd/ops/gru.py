@@ -27,12 +27,8 @@ def gru_reference(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[T
 
 
 def fused_small_supported(x: Tensor, hidden: int, num_layers: int) -> bool:
-    if x.dtype != torch.float32 or x.dim() != 3:
-        return False
-    mod = _ext.native(x.device)
-    if mod is None or not hasattr(mod, "gru_small_supported"):
-        return False
-    return bool(mod.gru_small_supported(hidden, x.shape[-1], num_layers))
+    from . import gru_fused
+    return gru_fused.supported(x, hidden, num_layers)
 
 
 def gru_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor] = None, *,
