@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--trainer", choices=("distributed", "horovod"), default="distributed")
     ap.add_argument("--cell", choices=("lstm", "gru"), default="lstm")
     ap.add_argument("--seed", type=int, default=123456789)
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="bf16: BASELINE config 2 (bf16 inputs/weights, fp32 accumulate)")
     return ap.parse_args(argv)
 
 
@@ -78,7 +80,8 @@ def main(argv=None):
     train_set, _, _ = synthetic_motion(n_train=n_train, n_validation=1, n_test=1,
                                        seq_length=args.seq_len, seed=args.seed)
     model = MotionModel(train_set.num_features, args.hidden, args.layers,
-                        len(MotionDataset.LABELS), cell=args.cell)
+                        len(MotionDataset.LABELS), cell=args.cell,
+                        compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     cls = DDPTrainer if args.trainer == "distributed" else HorovodTrainer
     trainer = cls(model=model, training_set=train_set, batch_size=args.global_batch,
                   learning_rate=0.0025, weak_scaling=args.scaling == "weak", device=dev)
@@ -136,7 +139,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": round(value / base, 2) if base else None,
-            "dtype": "fp32",
+            "dtype": args.dtype,
             "data": "synthetic (UCI-HAR shape [6912,128,9] fp32, random-init weights)",
             "config": {
                 "model": f"motion-{args.cell.upper()} {args.layers}x{args.hidden} (9 inputs -> 6 classes)",

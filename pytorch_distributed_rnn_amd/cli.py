@@ -57,6 +57,8 @@ def build_parser(script_dir: Optional[Path] = None) -> argparse.ArgumentParser:
                    help="train on generated UCI-HAR-shaped data (also used when no data is found)")
     p.add_argument("--synthetic-size", default=6912, type=int)
     p.add_argument("--cell", choices=("lstm", "gru"), default="lstm")
+    p.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                   help="bf16: bf16 inputs and recurrent weights, fp32 accumulation / masters")
     p.add_argument("--backend", default=None, help="nccl|rccl|gloo|mpi (default: RCCL on GPU, gloo on CPU)")
     p.add_argument("--bucket-mb", default=None, type=float)
     p.add_argument("--kernel", choices=("hip", "torch"), default="hip")
@@ -125,7 +127,8 @@ def train(args, name: str):
     from .models.motion import MotionModel
     model = MotionModel(input_dim=training_set.num_features, hidden_dim=args.hidden_units,
                         layer_dim=args.stacked_layer, output_dim=len(MotionDataset.LABELS),
-                        cell=args.cell)
+                        cell=args.cell,
+                        compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     trainer_cls = _trainer_class(name)
     kw = dict(model=model, training_set=training_set, validation_set=validation_set,
               test_set=test_set, batch_size=args.batch_size, learning_rate=args.learning_rate,

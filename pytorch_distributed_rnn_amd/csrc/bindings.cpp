@@ -112,7 +112,8 @@ std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx,
                                    const optional<Tensor>& h0, const optional<Tensor>& c0, int64_t H, int64_t NL,
                                    bool batch_first, bool save, bool need_out, int64_t nb, int64_t split,
                                    int64_t cell) {
-  CHECK_HIP_TENSOR(x); CHECK_F32(x);
+  CHECK_HIP_TENSOR(x);
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be float32 or bfloat16");
   TORCH_CHECK(x.dim() == 3, "x must be 3-D");
   TORCH_CHECK(x.stride(2) == 1, "x innermost dim must be contiguous");
   const c10::DeviceGuard guard(x.device());
@@ -129,11 +130,12 @@ std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx,
   } else {
     T = x.size(0); B = x.size(1); x_sb = x.stride(1); x_st = x.stride(0);
   }
-  auto opts = x.options();
+  auto opts = x.options().dtype(at::kFloat);
   Tensor hn = at::empty({NL, B, H}, opts), cn = at::empty({NL, B, H}, opts);
   Tensor hseq, act, out;
   PdrnnLstmSmallFwdArgs a{};
-  a.x = x.data_ptr<float>();
+  a.x = reinterpret_cast<const float*>(x.data_ptr());
+  a.x_bf16 = x.scalar_type() == at::kBFloat16;
   a.idx = (idx.has_value() && idx->defined()) ? idx->data_ptr<int64_t>() : nullptr;
   a.x_sb = x_sb; a.x_st = x_st;
   for (int64_t l = 0; l < NL; ++l) {
@@ -194,14 +196,15 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
   }
   TORCH_CHECK(hseq.is_contiguous() && act.is_contiguous());
   StackLayout L = stack_layout(w, NL, has_bias);
-  auto opts = x.options();
+  auto opts = x.options().dtype(at::kFloat);
   if (split <= 0) split = pdrnn_lstm_small_max_split((int)H, (int)NL, 1);
   const int grid = pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb, (int)split);
   TORCH_CHECK(grid > 0, "unsupported backward tile nb=", nb);
   Tensor slab = at::empty({std::max(grid, 1), L.P}, opts);
   Tensor dx, dh0, dc0;
   PdrnnLstmSmallBwdArgs a{};
-  a.x = x.data_ptr<float>();
+  a.x = reinterpret_cast<const float*>(x.data_ptr());
+  a.x_bf16 = x.scalar_type() == at::kBFloat16;
   a.idx = gathered ? idx->data_ptr<int64_t>() : nullptr;
   a.x_sb = x_sb; a.x_st = x_st;
   for (int64_t l = 0; l < NL; ++l) {
@@ -224,7 +227,7 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
   a.dhn = opt_ptr(dhn); a.dcn = opt_ptr(dcn);
   if (need_dx) {
     TORCH_CHECK(!gathered, "input gradient of a gathered batch is not supported");
-    dx = at::zeros_like(x);
+    dx = at::zeros(x.sizes(), x.options().dtype(at::kFloat));
     a.dx = dx.data_ptr<float>();
     a.dx_sb = batch_first ? dx.stride(0) : dx.stride(1);
     a.dx_st = batch_first ? dx.stride(1) : dx.stride(0);
@@ -275,7 +278,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
                           const std::vector<Tensor>& w, const Tensor& head_w, const optional<Tensor>& head_b,
                           Tensor flat_grad, Tensor stats, int64_t H, int64_t NL, int64_t split_fwd,
                           int64_t split_bwd, int64_t nb_fwd, int64_t nb_bwd) {
-  CHECK_HIP_TENSOR(x); CHECK_F32(x);
+  CHECK_HIP_TENSOR(x);
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be float32 or bfloat16");
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [N, T, I] with contiguous rows");
   const c10::DeviceGuard guard(x.device());
   const int64_t I = x.size(2);
@@ -295,7 +299,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   TORCH_CHECK(stats.numel() >= 3 && stats.is_contiguous() && stats.scalar_type() == at::kFloat);
   const int64_t P_head = P_params - L.P;      // head weight (+ bias)
   const int64_t PH = P_head + 3;              // + [loss, count, correct]
-  auto opts = x.options();
+  auto opts = x.options().dtype(at::kFloat);
   Tensor hseq = at::empty({NL, B, T, H}, opts);
   Tensor act = at::empty({NL, B, T, 5, H}, opts);
   Tensor hn = at::empty({NL, B, H}, opts), cn = at::empty({NL, B, H}, opts);
@@ -311,7 +315,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   Tensor slab = at::empty({gridb, L.P}, opts);
 
   PdrnnLstmSmallFwdArgs f{};
-  f.x = x.data_ptr<float>();
+  f.x = reinterpret_cast<const float*>(x.data_ptr());
+  f.x_bf16 = x.scalar_type() == at::kBFloat16;
   f.idx = gathered ? idx->data_ptr<int64_t>() : nullptr;
   f.x_sb = x.stride(0); f.x_st = x.stride(1);
   for (int64_t l = 0; l < NL; ++l) {
@@ -334,7 +339,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
 
   PdrnnLstmSmallBwdArgs bk{};
-  bk.x = f.x; bk.idx = f.idx; bk.x_sb = f.x_sb; bk.x_st = f.x_st;
+  bk.x = f.x; bk.x_bf16 = f.x_bf16; bk.idx = f.idx; bk.x_sb = f.x_sb; bk.x_st = f.x_st;
   for (int64_t l = 0; l < NL; ++l) {
     bk.w_ih[l] = f.w_ih[l]; bk.w_hh[l] = f.w_hh[l];
     bk.off_wih[l] = L.off_wih[l]; bk.off_whh[l] = L.off_whh[l];

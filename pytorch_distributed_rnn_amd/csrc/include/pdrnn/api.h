@@ -53,6 +53,7 @@ typedef struct {
   int C;
   int B, T, I, NL;
   int cell;                  // 0 = LSTM, 1 = GRU (packed as a 4-row-block stack, see ops/gru.py)
+  int x_bf16;                // x holds bf16 values (read once into LDS; requires the LDS-resident x path)
 } PdrnnLstmSmallFwdArgs;
 
 typedef struct {
@@ -81,6 +82,7 @@ typedef struct {
   int dhn_top_only;          // dhn is [B, H] for the top layer only (fused head path)
   int B, T, I, NL;
   int cell;                  // 0 = LSTM, 1 = GRU (packed as a 4-row-block stack, see ops/gru.py)
+  int x_bf16;                // x holds bf16 values (read once into LDS; requires the LDS-resident x path)
 } PdrnnLstmSmallBwdArgs;
 
 // Query the launch geometry chosen for (H, B): returns grid size (number of slab rows).

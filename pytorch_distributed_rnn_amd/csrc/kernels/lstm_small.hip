@@ -37,16 +37,22 @@ namespace {
 // per-step global load on the recurrence's critical path.
 constexpr int kXldsBytes = 48 * 1024;
 
+// x element i as fp32 (x may be stored in bf16: mixed-precision inputs are
+// widened once, while staging into LDS)
+__device__ __forceinline__ float ldx(const float* x, int64_t i, int bf) {
+  return bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(x)[i]) : x[i];
+}
+
 template <int H, int NB>
 __device__ __forceinline__ void preload_x(float* xs, const PdrnnLstmSmallFwdArgs& a, const int* bsrc,
                                           const bool* valid) {
   const int T = a.T, I = a.I;
   for (int n = 0; n < NB; ++n) {
     float* dst = xs + (int64_t)n * T * H;
-    const float* src = a.x + bsrc[n] * a.x_sb;
+    const int64_t base = (int64_t)bsrc[n] * a.x_sb;
     for (int e = threadIdx.x; e < T * H; e += blockDim.x) {
       const int t = e / H, k = e - t * H;
-      const float v = src[(int64_t)t * a.x_st + min(k, I - 1)];
+      const float v = ldx(a.x, base + (int64_t)t * a.x_st + min(k, I - 1), a.x_bf16);
       dst[e] = (valid[n] && k < I) ? v : 0.f;
     }
   }
@@ -525,10 +531,10 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
   if constexpr (XLDS) {
     for (int n = 0; n < NB; ++n) {
       float* dst = xs + (int64_t)n * T * H;
-      const float* src = a.x + bsrc[n] * a.x_sb;
+      const int64_t base = (int64_t)bsrc[n] * a.x_sb;
       for (int e = tid; e < T * H; e += blockDim.x) {
         const int t = e / H, kk = e - t * H;
-        const float v = src[(int64_t)t * a.x_st + min(kk, I - 1)];
+        const float v = ldx(a.x, base + (int64_t)t * a.x_st + min(kk, I - 1), a.x_bf16);
         dst[e] = (valid[n] && kk < I) ? v : 0.f;
       }
     }
@@ -818,7 +824,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
         const int rem = e - n * T * H;
         const int t = rem / H, kk = rem - t * H;
         const int bn = a.idx ? (int)a.idx[min(b0 + n, B - 1)] : min(b0 + n, B - 1);
-        const float v = a.x[bn * a.x_sb + (int64_t)t * a.x_st + min(kk, I - 1)];
+        const float v = ldx(a.x, (int64_t)bn * a.x_sb + (int64_t)t * a.x_st + min(kk, I - 1), a.x_bf16);
         xs[e] = kk < I ? v : 0.f;
       }
     }
@@ -1338,6 +1344,9 @@ int pdrnn_lstm_small_grid(int H, int B, int nb) {
 
 hipError_t pdrnn_lstm_small_fwd(const PdrnnLstmSmallFwdArgs* a, int H, int nb, int split, int save,
                                 hipStream_t stream) {
+  // bf16 inputs are widened while staging x into LDS: needs the LDS-resident x path
+  if (a->x_bf16 && (size_t)a->T * H * sizeof(float) * (nb > 1 ? nb : 1) > (size_t)pdrnn::kXldsBytes)
+    return hipErrorInvalidConfiguration;
   switch (H) {
     case 16: return pdrnn::dispatch_fwd<16>(a, nb, split, save, stream);
     case 32: return pdrnn::dispatch_fwd<32>(a, nb, split, save, stream);
@@ -1348,6 +1357,8 @@ hipError_t pdrnn_lstm_small_fwd(const PdrnnLstmSmallFwdArgs* a, int H, int nb, i
 
 hipError_t pdrnn_lstm_small_bwd(const PdrnnLstmSmallBwdArgs* a, int H, int nb, int split, int grid,
                                 hipStream_t stream) {
+  if (a->x_bf16 && (split != 1 || (size_t)a->T * H * sizeof(float) * (nb > 1 ? nb : 1) > (size_t)pdrnn::kXldsBytes))
+    return hipErrorInvalidConfiguration;
   switch (H) {
     case 16: return pdrnn::dispatch_bwd<16>(a, nb, split, stream, grid);
     case 32: return pdrnn::dispatch_bwd<32>(a, nb, split, stream, grid);

@@ -80,10 +80,11 @@ class DeviceBatchLoader:
     inside the kernel) skip the gather copy."""
 
     def __init__(self, dataset, batch_size: Optional[int], sampler: Optional[ShardedSampler] = None,
-                 device: Optional[torch.device] = None, gather_in_kernel: bool = False):
+                 device: Optional[torch.device] = None, gather_in_kernel: bool = False,
+                 feature_dtype: Optional[torch.dtype] = None):
         self.dataset = dataset
         self.device = torch.device(device) if device is not None else dataset.features.device
-        self.features = dataset.features.to(self.device)
+        self.features = dataset.features.to(self.device, dtype=feature_dtype)
         self.labels = dataset.labels.to(self.device)
         self.sampler = sampler
         n = len(sampler) if sampler is not None else len(dataset)

@@ -27,8 +27,11 @@ class MotionModel(nn.Module):
     supports_index_batches = True
 
     def __init__(self, input_dim: int, hidden_dim: int, layer_dim: int, output_dim: int,
-                 cell: str = "lstm", dropout: float = 0.0):
+                 cell: str = "lstm", dropout: float = 0.0, compute_dtype: torch.dtype = torch.float32):
         super().__init__()
+        # bf16: inputs and recurrent weights in bf16 storage, fp32 accumulation,
+        # cell state and master weights (BASELINE config 2)
+        self.compute_dtype = compute_dtype
         self.hidden_dim = hidden_dim
         self.layer_dim = layer_dim
         self.cell = cell
@@ -38,10 +41,13 @@ class MotionModel(nn.Module):
         self.fc = nn.Linear(hidden_dim, output_dim)
 
     def forward(self, x: Tensor, idx: Optional[Tensor] = None) -> Tensor:
+        if self.compute_dtype != torch.float32 and x.dtype != self.compute_dtype:
+            x = x.to(self.compute_dtype)
         if self.cell == "lstm":
             _, (hn, _) = self.lstm(x, need_out=False, idx=idx)
         else:
             if idx is not None:
                 x = x.index_select(0, idx)
             _, hn = self.lstm(x)
-        return self.fc(hn[-1])
+        h = hn[-1]
+        return self.fc(h if h.dtype == self.fc.weight.dtype else h.to(self.fc.weight.dtype))

@@ -52,11 +52,16 @@ def small_launch_config(batch: int, hidden: int, num_layers: int = 2) -> Tuple[i
 
 
 def fused_small_supported(x: Tensor, hidden: int, num_layers: int, bidirectional: bool,
-                          proj_size: int = 0) -> bool:
+                          proj_size: int = 0, batch_first: bool = True) -> bool:
     if bidirectional or proj_size:
         return False
-    if x.dtype != torch.float32 or x.dim() != 3:
+    if x.dtype not in (torch.float32, torch.bfloat16) or x.dim() != 3:
         return False
+    if x.dtype == torch.bfloat16:
+        if x.shape[1 if batch_first else 0] * hidden * 4 > 48 * 1024:
+            return False  # bf16 x is widened while staging into LDS: sequence must fit there
+        if hidden >= 128:
+            return False  # the MFMA large-H path serves 16-bit models from H = 128 up
     mod = _ext.native(x.device)
     if mod is None:
         return False
@@ -72,6 +77,10 @@ class _FusedSmallLSTM(torch.autograd.Function):
     def forward(ctx, x, idx, h0, c0, cfg, *weights):
         hidden, num_layers, batch_first, need_out = cfg
         mod = _ext.native(x.device)
+        if x.dtype == torch.bfloat16:
+            # bf16 model: recurrent weights rounded to bf16 (fp32 masters keep
+            # the update; gradients pass straight through), fp32 accumulation
+            weights = tuple(w.to(torch.bfloat16).float() for w in weights)
         batch = idx.numel() if idx is not None else (x.shape[0] if batch_first else x.shape[1])
         nb_fwd, sp_fwd, nb_bwd, sp_bwd = small_launch_config(batch, hidden, num_layers)
         h0c = h0.contiguous() if h0 is not None else None
@@ -157,7 +166,7 @@ def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Te
     inside the kernel; ``need_out=False`` lets inference skip the per-timestep
     output stream when only h_n is consumed."""
     if (not bidirectional and dropout == 0.0
-            and fused_small_supported(x, hidden, num_layers, bidirectional)):
+            and fused_small_supported(x, hidden, num_layers, bidirectional, batch_first=batch_first)):
         flat = _flat_weights(weights, num_layers, hidden, x)
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or any(w.requires_grad for w in flat)

@@ -57,6 +57,8 @@ def supported(model: nn.Module, optimizer, device: torch.device) -> bool:
     params = list(m.parameters())
     if any(p.dtype != torch.float32 for p in params):
         return False
+    if getattr(m, "compute_dtype", torch.float32) not in (torch.float32, torch.bfloat16):
+        return False
     return contiguous_span([p.data for p in params]) is not None
 
 
@@ -80,15 +82,30 @@ class MotionTrainStep:
             raise RuntimeError("fused step needs the model's flat parameter storage")
         self.flat = next(iter(flat.values()))
         self.stats = torch.zeros(3, dtype=torch.float32, device=self.flat.grad.device)
+        # bf16 model: recurrent weights used rounded to bf16 (one cast of the
+        # flat master buffer per step); gradients land on the fp32 masters
+        self.bf16 = getattr(self.m, "compute_dtype", torch.float32) == torch.bfloat16
+        base = self.flat.data.data_ptr()
+        self._offs = [((w.data_ptr() - base) // 4, w.shape) for w in self.weights]
+
+    def _rounded(self):
+        r = self.flat.data.to(torch.bfloat16).float()
+        return [r[o:o + int(torch.Size(s).numel())].view(s) for o, s in self._offs]
 
     def __call__(self, features: Tensor, labels: Tensor, idx: Optional[Tensor]) -> Tensor:
         from ..ops.lstm import small_launch_config
         self.flat.attach_grads()
         batch = idx.numel() if idx is not None else features.shape[0]
         nb_fwd, _, nb_bwd, _ = small_launch_config(batch, self.H, self.NL)
+        hw, hb = self.m.fc.weight, self.m.fc.bias  # the classifier head stays fp32
+        if self.bf16:
+            ws = self._rounded()
+            if features.dtype != torch.bfloat16:
+                features = features.to(torch.bfloat16)
+        else:
+            ws = self.weights
         self.mod.lstm_head_train_step(
-            features, idx, labels, self.weights, self.m.fc.weight, self.m.fc.bias,
-            self.flat.grad, self.stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd)
+            features, idx, labels, ws, hw, hb, self.flat.grad, self.stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd)
         if self.grad_sync is not None:
             self.grad_sync()
         self.optimizer.step()

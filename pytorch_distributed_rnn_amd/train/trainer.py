@@ -82,8 +82,10 @@ class Trainer:
             return None
         inner = getattr(self.model, "module", self.model)
         in_kernel = self.device.type == "cuda" and getattr(inner, "supports_index_batches", False)
+        cdt = getattr(inner, "compute_dtype", torch.float32)
         return DeviceBatchLoader(dataset, batch_size, sampler=sampler, device=self.device,
-                                 gather_in_kernel=in_kernel)
+                                 gather_in_kernel=in_kernel,
+                                 feature_dtype=cdt if self.device.type == "cuda" else None)
 
     def _get_formatter(self, epochs: int) -> TrainingMessageFormatter:
         return TrainingMessageFormatter(epochs)

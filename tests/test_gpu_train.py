@@ -48,3 +48,37 @@ def test_local_trainer_epoch_on_gpu(tmp_path):
     assert (tmp_path / "best-model.pt").exists()
     ck = torch.load(tmp_path / "best-model.pt", weights_only=True)
     assert "lstm.weight_ih_l0" in ck["model_state"]
+
+
+def test_bf16_fused_step_matches_autograd():
+    """BASELINE config 2: single-layer motion model, bf16 inputs/recurrent
+    weights, fused whole-step path == autograd path."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    torch.manual_seed(0)
+    train, _, _ = synthetic_motion(n_train=384, n_validation=2, n_test=2, seed=3)
+    m1 = MotionModel(9, 32, 1, 6, compute_dtype=torch.bfloat16)
+    m2 = copy.deepcopy(m1)
+    t1, t2 = _trainer(m1, train, True), _trainer(m2, train, False)
+    assert t1._fused_step() is not None and t1.train_loader.features.dtype == torch.bfloat16
+    for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
+        s1, _ = t1.train_batch(x1)
+        s2, _ = t2.train_batch(x2)
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
+
+
+def test_bf16_lstm_matches_rounded_fp64_reference():
+    from pytorch_distributed_rnn_amd.models.rnn import LSTM
+    torch.manual_seed(2)
+    m = LSTM(9, 32, 1, batch_first=True).cuda()
+    ref = torch.nn.LSTM(9, 32, 1, batch_first=True).cuda().double()
+    with torch.no_grad():
+        for p, q in zip(m.parameters(), ref.parameters()):
+            q.copy_(p.to(torch.bfloat16).double())
+    x = torch.randn(20, 128, 9, device="cuda").to(torch.bfloat16)
+    out, (hn, _) = m(x)
+    out_r, (hn_r, _) = ref(x.double())
+    torch.testing.assert_close(out.double(), out_r, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(hn.double(), hn_r, rtol=1e-4, atol=1e-5)
