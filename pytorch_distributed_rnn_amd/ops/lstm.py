@@ -83,8 +83,9 @@ class _FusedSmallLSTM(torch.autograd.Function):
             weights = tuple(w.to(torch.bfloat16).float() for w in weights)
         batch = idx.numel() if idx is not None else (x.shape[0] if batch_first else x.shape[1])
         nb_fwd, sp_fwd, nb_bwd, sp_bwd = small_launch_config(batch, hidden, num_layers)
-        h0c = h0.contiguous() if h0 is not None else None
-        c0c = c0.contiguous() if c0 is not None else None
+        h0c = h0.float().contiguous() if h0 is not None else None
+        c0c = c0.float().contiguous() if c0 is not None else None
+        ctx.state_dtypes = (h0.dtype if h0 is not None else None, c0.dtype if c0 is not None else None)
         out, hn, cn, act = mod.lstm_small_fwd(
             x, idx, list(weights), h0c, c0c, hidden, num_layers, batch_first, True, need_out, nb_fwd,
             sp_fwd)
@@ -116,9 +117,12 @@ class _FusedSmallLSTM(torch.autograd.Function):
             n = w.numel()
             grads.append(dparams[off:off + n].view_as(w))
             off += n
+        hdt, cdt = ctx.state_dtypes
+        if dx is not None and dx.dtype != x.dtype:
+            dx = dx.to(x.dtype)
         return (dx if need_dx else None, None,
-                dh0 if ctx.needs_input_grad[2] else None,
-                dc0 if ctx.needs_input_grad[3] else None, None, *grads)
+                dh0.to(hdt) if ctx.needs_input_grad[2] else None,
+                dc0.to(cdt) if ctx.needs_input_grad[3] else None, None, *grads)
 
 
 def _flat_weights(weights: Sequence[Optional[Tensor]], num_layers: int, hidden: int,

@@ -84,17 +84,18 @@ def test_large_lstm_matches_torch(dt, H, L, bi, B, T, I):
         assert _rel(p.grad, q.grad) < 4e-2, n
 
 
-def test_large_lstm_state_grads():
+@pytest.mark.parametrize("H", [64, 128])  # 64: small fused path with bf16 inputs, 128: MFMA path
+def test_large_lstm_state_grads(H):
     torch.manual_seed(3)
     dt = torch.bfloat16
-    m = LSTM(32, 64, 1, batch_first=False).cuda()
+    m = LSTM(32, H, 1, batch_first=False).cuda()
     with torch.no_grad():
         for p in m.parameters():
             p.copy_(p.to(dt).float())
     ref = _ref_model(m)
     x = torch.randn(5, 3, 32, device="cuda").to(dt)
-    h0 = torch.randn(1, 3, 64, device="cuda").to(dt)
-    c0 = torch.randn(1, 3, 64, device="cuda")
+    h0 = torch.randn(1, 3, H, device="cuda").to(dt)
+    c0 = torch.randn(1, 3, H, device="cuda")
     h0a, c0a = h0.clone().requires_grad_(True), c0.clone().requires_grad_(True)
     h0b, c0b = h0.float().clone().requires_grad_(True), c0.clone().requires_grad_(True)
     _, (hn, cn) = m(x, (h0a, c0a))
