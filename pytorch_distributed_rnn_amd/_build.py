@@ -103,6 +103,8 @@ def build(verbose: bool = False, clean: bool = False, jobs: int | None = None) -
     hip_flags = [
         "-c", "-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
         "-munsafe-fp-atomics", "-Wno-unused-result", *common_inc,
+        # diagnostics only (e.g. -DPDRNN_ABLATE=N timing ablations); part of the build signature
+        *os.environ.get("PDRNN_HIP_EXTRA_FLAGS", "").split(),
     ]
     host_flags = [
         "-c", "-O2", "-fPIC", "-fvisibility=hidden", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",

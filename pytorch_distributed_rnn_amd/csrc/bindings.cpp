@@ -336,6 +336,12 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   f.C = (int)C;
   f.B = (int)B; f.T = (int)T; f.I = (int)I; f.NL = (int)NL;
   hipStream_t st = cur_stream();
+  Tensor st_f, st_b;
+  if (stamps_enabled()) {
+    st_f = at::zeros({(B + nb_fwd - 1) / nb_fwd, 4}, opts.dtype(at::kLong));
+    st_b = at::zeros({gridb, 4}, opts.dtype(at::kLong));
+    f.stamps = reinterpret_cast<uint64_t*>(st_f.data_ptr<int64_t>());
+  }
   HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
 
   PdrnnLstmSmallBwdArgs bk{};
@@ -349,7 +355,12 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.dhn = dh_top.data_ptr<float>(); bk.dhn_top_only = 1;
   bk.slab = slab.data_ptr<float>(); bk.P = L.P;
   bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL;
+  if (st_b.defined()) bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
   HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
+  if (st_f.defined()) {
+    report_stamps("fwd(head step)", st_f, (int)(T + NL - 1));
+    report_stamps("bwd(head step, lean)", st_b, (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)gridb * nb_bwd - 1) / ((int64_t)gridb * nb_bwd)));
+  }
 
   const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, gridb / 16));
   Tensor work = at::empty({split, L.P + PH}, opts);

@@ -37,6 +37,28 @@ namespace {
 // per-step global load on the recurrence's critical path.
 constexpr int kXldsBytes = 48 * 1024;
 
+// Timing ablations (diagnostic builds only, -DPDRNN_ABLATE=bits; results are
+// wrong): 1 no dW FMAs, 2 no W^T g FMAs, 4 no per-step operand loads (bwd),
+// 8 no bwd barrier, 16 no bwd tanh, 32 no fwd LDS operand reads, 64 no fwd
+// barrier, 128 no fwd transcendentals.
+#ifndef PDRNN_ABLATE
+#define PDRNN_ABLATE 0
+#endif
+
+// Buffer descriptor for a wave-uniform base pointer: the halves go through
+// readfirstlane so the compiler can keep the descriptor in SGPRs (no
+// waterfall loop around each buffer op).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  void* up = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(up, 0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff_bytes, uint32_t soff_bytes) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff_bytes, soff_bytes, 0));
+}
+
 // x element i as fp32 (x may be stored in bf16: mixed-precision inputs are
 // widened once, while staging into LDS)
 __device__ __forceinline__ float ldx(const float* x, int64_t i, int bf) {
@@ -354,15 +376,16 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
         pdrnn_f2 acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
         for (int k4 = 0; k4 < K / 4; ++k4) {
-          const float4 v = (4 * k4 < H) ? reinterpret_cast<const float4*>(src_in)[k4]
-                                        : reinterpret_cast<const float4*>(src_h)[k4 - H / 4];
+          const float4 v = (PDRNN_ABLATE & 32) ? make_float4(hl[n], c[n], hl[n], c[n])
+                           : (4 * k4 < H) ? reinterpret_cast<const float4*>(src_in)[k4]
+                                          : reinterpret_cast<const float4*>(src_h)[k4 - H / 4];
           acc[(2 * k4) & 3] = __builtin_elementwise_fma(w2[2 * k4], pdrnn_f2{v.x, v.y}, acc[(2 * k4) & 3]);
           acc[(2 * k4 + 1) & 3] =
               __builtin_elementwise_fma(w2[2 * k4 + 1], pdrnn_f2{v.z, v.w}, acc[(2 * k4 + 1) & 3]);
         }
         const pdrnn_f2 s2 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         const float z = (s2.x + s2.y) + bias;  // = -log2(e) * gsc * preactivation
-        const float sg = fast_rcp(1.f + __builtin_amdgcn_exp2f(z));
+        const float sg = (PDRNN_ABLATE & 128) ? z : fast_rcp(1.f + __builtin_amdgcn_exp2f(z));
         const float act = lin ? z : fmaf(sg, am, ab);  // sigmoid, or tanh for the g gate
         const float ig = quad_bcast(act, 0);
         const float fg = quad_bcast(act, 1);
@@ -371,7 +394,7 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
         float cn, h;
         if constexpr (CELL == 0) {
           cn = fmaf(fg, c[n], ig * gg);
-          const float th = fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(cn * (2.f * kNegLog2e))), 2.f, -1.f);
+          const float th = (PDRNN_ABLATE & 128) ? cn : fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(cn * (2.f * kNegLog2e))), 2.f, -1.f);
           h = og * th;
         } else {  // GRU: ig = r, fg = z, gg = n_x, og = n_h; cn carries n
           const float pre = fmaf(ig, og, gg);
@@ -392,7 +415,8 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
         for (int n = 0; n < NB; ++n) vin(n, 0, p ^ 1)[lg] = xnext[n];
       }
     }
-    lds_barrier();
+    if constexpr (PDRNN_ABLATE & 64) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else lds_barrier();
   }
   if (a.stamps && tid == 0) {
     uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
@@ -801,13 +825,14 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
   for (int b0 = blockIdx.x * NB; b0 < B; b0 += gridDim.x * NB) {
     int bs[NB], bsrc[NB];
     bool valid[NB];
-    float dh[NB], dc[NB];
+    float dh[NB], dc[NB], dha_r[NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
       valid[n] = b0 + n < B;
       bs[n] = min(b0 + n, B - 1);  // invalid slots recompute the last sequence, never store
       bsrc[n] = a.idx ? (int)a.idx[bs[n]] : bs[n];
       dh[n] = 0.f;
+      dha_r[n] = 0.f;
       if (a.dhn) {
         if (top_only) dh[n] = top ? a.dhn[(int64_t)bs[n] * H + u] : 0.f;
         else dh[n] = a.dhn[((int64_t)layer * B + bs[n]) * H + u];
@@ -830,126 +855,176 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
     }
 
     // ---- raw per-timestep operands (prefetched 2 steps ahead, masked at use)
-    const float* act_base[NB];
-    const float* hs_own[NB];
-    const float* hs_below[NB];
+    // Every stream is a buffer descriptor on a wave-uniform base (SGPRs), a
+    // per-lane byte offset fixed for the whole loop (VGPR) and a per-step
+    // scalar offset: one buffer_load per operand, no per-step VALU address
+    // arithmetic.  Out-of-range steps are clamped, the values masked at use.
+    __amdgpu_buffer_rsrc_t r_act[NB], r_own[NB], r_in[NB];
+    const int x_layer0 = layer == 0 && !XLDS;
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
-      act_base[n] = a.act + ((int64_t)layer * B + bs[n]) * T * 5 * H;
-      hs_own[n] = a.hseq + ((int64_t)layer * B + bs[n]) * T * H + u;
-      hs_below[n] = a.hseq + ((int64_t)(layer > 0 ? layer - 1 : 0) * B + bs[n]) * T * H + u;
+      const int64_t lb = (int64_t)layer * B + bs[n];
+      r_act[n] = uniform_rsrc(a.act + lb * T * 5 * H);
+      r_own[n] = uniform_rsrc(a.hseq + lb * T * H);
+      r_in[n] = uniform_rsrc(x_layer0 ? a.x + (int64_t)bsrc[n] * a.x_sb
+                                      : a.hseq + ((int64_t)(layer > 0 ? layer - 1 : 0) * B + bs[n]) * T * H);
     }
     const bool has_dout = top && doutp != nullptr;
-    // Branch-free: every operand is loaded every step through a selected (always
-    // valid) address and masked at use.  A load under a branch makes the
-    // waitcnt pass fall back to vmcnt(0) at the join, which would wait for the
-    // prefetches issued for later steps as well.
+    const uint32_t vo_q = (q * H + u) * 4, vo_c = (4 * H + u) * 4, vo_u = u * 4;
+    const uint32_t vo_x = (x_layer0 ? min(u, I - 1) : u) * 4;
+    const uint32_t st_act = 5 * H * 4, st_h = H * 4;
+    const uint32_t st_x = x_layer0 ? (uint32_t)a.x_st * 4 : st_h;
+    // Branch-free: every operand is loaded every step and masked at use.  A
+    // load under a branch makes the waitcnt pass fall back to vmcnt(0) at the
+    // join, which would wait for the prefetches issued for later steps too.
     auto load_ops = [&](int n, int t) {
-      const int tc = min(max(t, 0), T - 1);
-      const float* act = act_base[n] + (int64_t)tc * 5 * H + u;
+      // scalar offsets (readfirstlane: provably uniform -> SGPR soffset, no waterfall)
+      const uint32_t tc = __builtin_amdgcn_readfirstlane((uint32_t)min(max(t, 0), T - 1));
+      const uint32_t tp = tc > 0 ? tc - 1 : 0;
+      const uint32_t so_a = __builtin_amdgcn_readfirstlane(tc * st_act);
+      const uint32_t so_ap = __builtin_amdgcn_readfirstlane(tp * st_act);
+      const uint32_t so_h = __builtin_amdgcn_readfirstlane(tp * st_h);
+      const uint32_t so_x = __builtin_amdgcn_readfirstlane(tc * st_x);
       Ops o;
-      o.aq = act[q * H];
-      o.ct = act[4 * H];
-      const float* cpp = tc > 0 ? act - H : (c0p ? c0p + ((int64_t)layer * B + bs[n]) * H + u : act);
-      o.cp = *cpp;
-      const float* dp = has_dout ? doutp + bs[n] * a.d_sb + (int64_t)tc * a.d_st + u : act;
-      o.dout = *dp;
-      const float* hp = tc > 0 ? hs_own[n] + (int64_t)(tc - 1) * H
-                               : (h0p ? h0p + ((int64_t)layer * B + bs[n]) * H + u : hs_own[n]);
-      o.hprev = *hp;
-      const float* xp = layer > 0 ? hs_below[n] + (int64_t)tc * H
-                                  : (XLDS ? act : a.x + bsrc[n] * a.x_sb + (int64_t)tc * a.x_st + min(u, I - 1));
-      o.xin = *xp;
+      o.aq = bload(r_act[n], vo_q, so_a);
+      o.ct = bload(r_act[n], vo_c, so_a);
+      o.cp = bload(r_act[n], vo_c, so_ap);
+      // optional operands (generic kernel only): descriptors built on demand
+      // to keep the SGPR budget of the hot loop
+      const int64_t lb = (int64_t)layer * B + bs[n];
+      if (c0p && tc == 0) o.cp = bload(uniform_rsrc(c0p + lb * H), vo_u, 0);
+      o.dout = has_dout ? bload(uniform_rsrc(doutp + bs[n] * a.d_sb), vo_u,
+                                __builtin_amdgcn_readfirstlane(tc * (uint32_t)a.d_st * 4))
+                        : 0.f;
+      o.hprev = bload(r_own[n], vo_u, so_h);
+      if (h0p && tc == 0) o.hprev = bload(uniform_rsrc(h0p + lb * H), vo_u, 0);
+      o.xin = bload(r_in[n], vo_x, so_x);
       return o;
     };
 
     const int t_first = T - 1 + lag;
     Ops opA[NB], opB[NB];
+    // issue order pinned (A's loads, then B's): the loop's counted vmcnt waits
+    // are the max over its entry edges, so a reordered prologue would make
+    // every in-loop wait conservative
 #pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      opA[n] = load_ops(n, t_first);
-      opB[n] = load_ops(n, t_first - 1);
-    }
+    for (int n = 0; n < NB; ++n) opA[n] = load_ops(n, t_first);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) opB[n] = load_ops(n, t_first - 1);
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
 
+    // The step body is branch-free (inactive steps compute and mask): a branch
+    // join makes the waitcnt pass conservative, and every conservative
+    // vmcnt here would wait for the prefetches of the next two steps.
+    const int dha_tgt = layer > 0 ? layer - 1 : NL - 1;  // top layer's dha slots are never read
     auto step = [&](int it, Ops* op) {
       const int t = t_first - it;
       const bool active = t >= 0 && t < T;
       const int p = it & 1;
       // ---------------- row phase ----------------
-      if (active) {
 #pragma unroll
-        for (int n = 0; n < NB; ++n) {
-          float dht = dh[n] + (has_dout ? op[n].dout : 0.f);
-          if (!top) dht += dhabuf(n, layer, p)[u];  // written by the layer above 2 iterations ago
-          const float ig = quad_bcast(op[n].aq, 0), fg = quad_bcast(op[n].aq, 1);
-          const float gg = quad_bcast(op[n].aq, 2), og = quad_bcast(op[n].aq, 3);
-          float dgv;
-          if constexpr (CELL == 0) {
-            const float cp = (t > 0 || c0p) ? op[n].cp : 0.f;
-            const float tc = tanhf_fast(op[n].ct);
-            const float dcp = fmaf(dht * og, 1.f - tc * tc, dc[n]);
-            const float d_i = dcp * gg * ig * (1.f - ig);
-            const float d_f = dcp * cp * fg * (1.f - fg);
-            const float d_g = dcp * ig * (1.f - gg * gg);
-            const float d_o = dht * tc * og * (1.f - og);
-            dgv = q == 0 ? d_i : (q == 1 ? d_f : (q == 2 ? d_g : d_o));
-            dc[n] = dcp * fg;
-          } else {  // GRU: ig = r, fg = z, og = n_h, ct = n
-            const float hp = (t > 0 || h0p) ? op[n].hprev : 0.f;
-            const float nn = op[n].ct;
-            const float dpn = dht * (1.f - fg) * (1.f - nn * nn);
-            const float d_r = dpn * og * ig * (1.f - ig);
-            const float d_z = dht * (hp - nn) * fg * (1.f - fg);
-            dgv = q == 0 ? d_r : (q == 1 ? d_z : (q == 2 ? dpn : dpn * ig));
-            dc[n] = dht * fg;  // direct path into dh_{t-1}
-          }
-          if (rowlane) {
-            dgbuf(n, layer, p)[q * H + u] = dgv;
-            if (valid[n]) db += dgv;
-          }
+      for (int n = 0; n < NB; ++n) {
+        float dht = dh[n] + (has_dout ? op[n].dout : 0.f);
+        if (!top) dht += dha_r[n];  // dh from the layer above (prefetched, see the column phase)
+        const float ig = quad_bcast(op[n].aq, 0), fg = quad_bcast(op[n].aq, 1);
+        const float gg = quad_bcast(op[n].aq, 2), og = quad_bcast(op[n].aq, 3);
+        float dgv, dcn;
+        if constexpr (CELL == 0) {
+          const float cp = (t > 0 || c0p) ? op[n].cp : 0.f;
+          const float tc = (PDRNN_ABLATE & 16) ? op[n].ct : tanhf_fast(op[n].ct);
+          const float dcp = fmaf(dht * og, 1.f - tc * tc, dc[n]);
+          const float d_i = dcp * gg * ig * (1.f - ig);
+          const float d_f = dcp * cp * fg * (1.f - fg);
+          const float d_g = dcp * ig * (1.f - gg * gg);
+          const float d_o = dht * tc * og * (1.f - og);
+          dgv = q == 0 ? d_i : (q == 1 ? d_f : (q == 2 ? d_g : d_o));
+          dcn = dcp * fg;
+        } else {  // GRU: ig = r, fg = z, og = n_h, ct = n
+          const float hp = (t > 0 || h0p) ? op[n].hprev : 0.f;
+          const float nn = op[n].ct;
+          const float dpn = dht * (1.f - fg) * (1.f - nn * nn);
+          const float d_r = dpn * og * ig * (1.f - ig);
+          const float d_z = dht * (hp - nn) * fg * (1.f - fg);
+          dgv = q == 0 ? d_r : (q == 1 ? d_z : (q == 2 ? dpn : dpn * ig));
+          dcn = dht * fg;  // direct path into dh_{t-1}
+        }
+        dgv = active ? dgv : 0.f;  // inactive: zero gate gradients (dW, db, dh unaffected)
+        dc[n] = active ? dcn : dc[n];
+        if (L == 4 || rowlane) {
+          dgbuf(n, layer, p)[q * H + u] = dgv;
+          db += valid[n] ? dgv : 0.f;
         }
       }
-      lds_barrier();
+      if constexpr (PDRNN_ABLATE & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else lds_barrier();
       // ---------------- column phase ----------------
-      if (active) {
 #pragma unroll
-        for (int n = 0; n < NB; ++n) {
-          const float hprev = (t > 0 || h0p) ? op[n].hprev : 0.f;
-          float xin;
-          if (XLDS && layer == 0) xin = xs[((int64_t)n * T + t) * H + u];
-          else xin = (layer > 0 || u < I) ? op[n].xin : 0.f;
-          // an invalid slot still runs the recurrence (uniform control flow)
-          // but contributes nothing to dW
-          const float hw = valid[n] ? hprev : 0.f, xw = valid[n] ? xin : 0.f;
-          const float4* g4 = reinterpret_cast<const float4*>(dgbuf(n, layer, p) + r0);
-          pdrnn_f2 sh[2] = {{0.f, 0.f}, {0.f, 0.f}}, sx[2] = {{0.f, 0.f}, {0.f, 0.f}};
-          const pdrnn_f2 hb = {hw, opaque_copy(hw)}, xb = {xw, opaque_copy(xw)};
+      for (int n = 0; n < NB; ++n) {
+        const float hprev = (t > 0 || h0p) ? op[n].hprev : 0.f;
+        // both candidates live at once (a select, not a branch): otherwise the
+        // LDS read reuses the prefetch register and waits on in-flight loads
+        const int tcl = min(max(t, 0), T - 1);
+        const float xsv = XLDS ? xs[((int64_t)n * T + tcl) * H + u] : 0.f;
+        const float xgv = (layer > 0 || u < I) ? op[n].xin : 0.f;
+        const float xin = (XLDS && layer == 0) ? xsv : xgv;
+        // an invalid slot still runs the recurrence but contributes nothing to dW
+        const float hw = valid[n] ? hprev : 0.f, xw = valid[n] ? xin : 0.f;
+        const float4* g4 = reinterpret_cast<const float4*>(dgbuf(n, layer, p) + r0);
+        // all of this lane's gate-gradient slice in flight at once: one
+        // LDS latency per step instead of one per read batch
+        float4 gv[RS / 4];
 #pragma unroll
-          for (int r4 = 0; r4 < RS / 4; ++r4) {
-            const float4 g = g4[r4];
-            const pdrnn_f2 g01 = {g.x, g.y}, g23 = {g.z, g.w};
+        for (int r4 = 0; r4 < RS / 4; ++r4) gv[r4] = g4[r4];
+        __builtin_amdgcn_sched_barrier(0);
+        pdrnn_f2 sh[2] = {{0.f, 0.f}, {0.f, 0.f}}, sx[2] = {{0.f, 0.f}, {0.f, 0.f}};
+        const pdrnn_f2 hb = {hw, opaque_copy(hw)}, xb = {xw, opaque_copy(xw)};
+#pragma unroll
+        for (int r4 = 0; r4 < RS / 4; ++r4) {
+          const float4 g = gv[r4];
+          const pdrnn_f2 g01 = {g.x, g.y}, g23 = {g.z, g.w};
+          if constexpr (!(PDRNN_ABLATE & 2)) {
             sh[0] = __builtin_elementwise_fma(whh[2 * r4], g01, sh[0]);
             sh[1] = __builtin_elementwise_fma(whh[2 * r4 + 1], g23, sh[1]);
             sx[0] = __builtin_elementwise_fma(wih[2 * r4], g01, sx[0]);
             sx[1] = __builtin_elementwise_fma(wih[2 * r4 + 1], g23, sx[1]);
+          } else {
+            sh[0] += g01; sx[1] += g23;
+          }
+          if constexpr (!(PDRNN_ABLATE & 1)) {
             dwhh[2 * r4] = __builtin_elementwise_fma(g01, hb, dwhh[2 * r4]);
             dwhh[2 * r4 + 1] = __builtin_elementwise_fma(g23, hb, dwhh[2 * r4 + 1]);
             dwih[2 * r4] = __builtin_elementwise_fma(g01, xb, dwih[2 * r4]);
             dwih[2 * r4 + 1] = __builtin_elementwise_fma(g23, xb, dwih[2 * r4 + 1]);
           }
-          const pdrnn_f2 shs = sh[0] + sh[1], sxs = sx[0] + sx[1];
-          dh[n] = group_sum<L>(shs.x + shs.y);  // dh_{t-1}[u] on every lane of the unit
-          if constexpr (CELL == 1) dh[n] += dc[n];
-          const float dx = group_sum<L>(sxs.x + sxs.y);
-          if (j == 0) {
-            if (layer > 0) dhabuf(n, layer - 1, p)[u] = dx;  // consumed by layer-1 at it+2 (same parity)
-            else if (dxp && u < I && valid[n]) dxp[bs[n] * a.dx_sb + (int64_t)t * a.dx_st + u] = dx;
-          }
         }
+        const pdrnn_f2 shs = sh[0] + sh[1], sxs = sx[0] + sx[1];
+        float dhn_ = group_sum<L>(shs.x + shs.y);  // dh_{t-1}[u] on every lane of the unit
+        if constexpr (CELL == 1) dhn_ += dc[n];
+        dh[n] = active ? dhn_ : dh[n];
+        const float dx = group_sum<L>(sxs.x + sxs.y);
+        // every lane of the unit holds dx: all write the same value (no branch);
+        // consumed by layer-1 at it+2 (same parity)
+        dhabuf(n, dha_tgt, p)[u] = dx;
+        if (!LEAN && layer == 0 && dxp && active && j == 0 && u < I && valid[n])
+          dxp[bs[n] * a.dx_sb + (int64_t)t * a.dx_st + u] = dx;
+      }
+      // dh the layer above wrote for the NEXT iteration (its column phase of
+      // it-1, published by this iteration's barrier): read now, off the next
+      // row phase's critical path.  Its next overwrite is after the next barrier.
+      if (!top) {
+#pragma unroll
+        for (int n = 0; n < NB; ++n) dha_r[n] = dhabuf(n, layer, (it + 1) & 1)[u];
       }
 #pragma unroll
-      for (int n = 0; n < NB; ++n) op[n] = load_ops(n, t - 2);  // refill for two steps ahead
+      for (int n = 0; n < NB; ++n) {
+        if constexpr (PDRNN_ABLATE & 4) {
+          op[n].aq += 1e-3f; op[n].ct += 1e-3f; op[n].hprev += 1e-3f; op[n].xin += 1e-3f;
+        } else {
+          op[n] = load_ops(n, t - 2);  // refill for two steps ahead
+        }
+      }
     };
 
     const int iters = T + 2 * (NL - 1);
