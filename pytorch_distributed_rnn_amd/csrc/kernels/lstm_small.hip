@@ -44,6 +44,10 @@ constexpr int kXldsBytes = 48 * 1024;
 #ifndef PDRNN_ABLATE
 #define PDRNN_ABLATE 0
 #endif
+#ifndef PDRNN_FWD_BULK_LDS
+#define PDRNN_FWD_BULK_LDS 1
+#endif
+constexpr bool kFwdBulkLds = PDRNN_FWD_BULK_LDS;
 
 // Buffer descriptor for a wave-uniform base pointer: the halves go through
 // readfirstlane so the compiler can keep the descriptor in SGPRs (no
@@ -374,11 +378,19 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
         if (XLDS && layer == 0) src_in = xs + ((int64_t)n * T + t) * H;
         const float* src_h = vin(n, layer, p) + H;
         pdrnn_f2 acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+        // the whole [x_t; h_{t-1}] operand vector in flight at once (one LDS
+        // latency per step; left to itself the scheduler keeps 2-3 reads in
+        // flight to save VGPRs and exposes the latency ~6 times per step)
+        float4 vin4[K / 4];
+#pragma unroll
+        for (int k4 = 0; k4 < K / 4; ++k4)
+          vin4[k4] = (PDRNN_ABLATE & 32) ? make_float4(hl[n], c[n], hl[n], c[n])
+                     : (4 * k4 < H) ? reinterpret_cast<const float4*>(src_in)[k4]
+                                    : reinterpret_cast<const float4*>(src_h)[k4 - H / 4];
+        if constexpr (kFwdBulkLds) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k4 = 0; k4 < K / 4; ++k4) {
-          const float4 v = (PDRNN_ABLATE & 32) ? make_float4(hl[n], c[n], hl[n], c[n])
-                           : (4 * k4 < H) ? reinterpret_cast<const float4*>(src_in)[k4]
-                                          : reinterpret_cast<const float4*>(src_h)[k4 - H / 4];
+          const float4 v = vin4[k4];
           acc[(2 * k4) & 3] = __builtin_elementwise_fma(w2[2 * k4], pdrnn_f2{v.x, v.y}, acc[(2 * k4) & 3]);
           acc[(2 * k4 + 1) & 3] =
               __builtin_elementwise_fma(w2[2 * k4 + 1], pdrnn_f2{v.z, v.w}, acc[(2 * k4 + 1) & 3]);
