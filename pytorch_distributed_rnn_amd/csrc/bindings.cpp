@@ -277,7 +277,9 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
 void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Tensor& labels,
                           const std::vector<Tensor>& w, const Tensor& head_w, const optional<Tensor>& head_b,
                           Tensor flat_grad, Tensor stats, int64_t H, int64_t NL, int64_t split_fwd,
-                          int64_t split_bwd, int64_t nb_fwd, int64_t nb_bwd) {
+                          int64_t split_bwd, int64_t nb_fwd, int64_t nb_bwd,
+                          const optional<std::vector<Tensor>>& adam_state,
+                          const optional<std::vector<double>>& adam_hp) {
   CHECK_HIP_TENSOR(x);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be float32 or bfloat16");
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [N, T, I] with contiguous rows");
@@ -364,6 +366,27 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
 
   const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, gridb / 16));
   Tensor work = at::empty({split, L.P + PH}, opts);
+  if (adam_state.has_value() && adam_hp.has_value()) {
+    // single-process step: the second reduction pass runs inside Adam
+    const auto& as = *adam_state;
+    const auto& hp = *adam_hp;  // lr, beta1, beta2, eps, weight_decay, step, decoupled
+    TORCH_CHECK(as.size() == 3 && hp.size() == 7, "adam_state = [param, exp_avg, exp_avg_sq], 7 hyper-parameters");
+    for (const auto& t : as)
+      TORCH_CHECK(t.is_contiguous() && t.numel() == P_params && t.scalar_type() == at::kFloat, "flat fp32 Adam buffers");
+    HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), gridb, L.P, head_slab.data_ptr<float>(), B, PH,
+                                              work.data_ptr<float>(), split, st));
+    PdrnnAdamArgs ad{};
+    ad.param = as[0].data_ptr<float>(); ad.exp_avg = as[1].data_ptr<float>(); ad.exp_avg_sq = as[2].data_ptr<float>();
+    ad.n = P_params;
+    ad.lr = (float)hp[0]; ad.beta1 = (float)hp[1]; ad.beta2 = (float)hp[2]; ad.eps = (float)hp[3];
+    ad.weight_decay = (float)hp[4];
+    ad.bias_correction1 = (float)(1.0 - std::pow(hp[1], hp[5]));
+    ad.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(hp[2], hp[5]));
+    ad.grad_scale = 1.f; ad.decoupled = hp[6] != 0.0 ? 1 : 0; ad.maximize = 0;
+    HIP_LAUNCH_CHECK(pdrnn_adam_partials(&ad, work.data_ptr<float>(), split, L.P + PH, flat_grad.data_ptr<float>(),
+                                         stats.data_ptr<float>(), 3, st));
+    return;
+  }
   HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), gridb, L.P, head_slab.data_ptr<float>(), B, PH,
                                       P_params, flat_grad.data_ptr<float>(), stats.data_ptr<float>(),
                                       work.data_ptr<float>(), split, st));
@@ -618,7 +641,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });
-  m.def("lstm_head_train_step", &lstm_head_train_step, "fused LSTM + head + CE forward/backward -> flat grads");
+  m.def("lstm_head_train_step", &lstm_head_train_step, "fused LSTM + head + CE forward/backward -> flat grads",
+        py::arg("x"), py::arg("idx"), py::arg("labels"), py::arg("w"), py::arg("head_w"), py::arg("head_b"),
+        py::arg("flat_grad"), py::arg("stats"), py::arg("H"), py::arg("NL"), py::arg("split_fwd"),
+        py::arg("split_bwd"), py::arg("nb_fwd"), py::arg("nb_bwd"), py::arg("adam_state") = py::none(),
+        py::arg("adam_hp") = py::none());
   m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
   m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer");

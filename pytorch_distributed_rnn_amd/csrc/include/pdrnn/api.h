@@ -105,6 +105,10 @@ hipError_t pdrnn_slab_reduce(const float* slab, int64_t rows, int64_t P, float* 
 // summed columns go to out, the rest to out_tail.
 hipError_t pdrnn_slab2_reduce(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB, int64_t PB,
                               int64_t n_out, float* out, float* out_tail, float* work, int split, hipStream_t stream);
+// First pass only (work[split][PA+PB] partial column sums); the second pass
+// can be fused into its consumer (pdrnn_adam_partials).
+hipError_t pdrnn_slab2_reduce_pass1(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB,
+                                   int64_t PB, float* work, int split, hipStream_t stream);
 // Same, with columns [P_a, P) written to out_b instead (e.g. loss statistics).
 hipError_t pdrnn_slab_reduce2(const float* slab, int64_t rows, int64_t P, int64_t P_a, float* out_a,
                               float* out_b, float* work, int split, hipStream_t stream);
@@ -205,6 +209,11 @@ hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir,
 // tile: -1 auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_gemm_nt(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
                          int M, int N, int K, int dtype, int tile, hipStream_t stream);
+
+// Adam whose gradient is the fixed-order sum of `split` rows of work[split][P_total]
+// (columns [0, a->n)); grad_out receives it, columns [n, n + n_stats) -> stats_out.
+hipError_t pdrnn_adam_partials(const PdrnnAdamArgs* a, const float* work, int split, int64_t P_total,
+                               float* grad_out, float* stats_out, int n_stats, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -85,8 +85,49 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(PdrnnAdamArgs a) {
   }
 }
 
+// Adam fused with the last reduction pass of the fused training step: the
+// gradient of element i is the fixed-order sum of `split` partial rows
+// (work[s][i], exactly the second pass of the deterministic slab reduction),
+// written to grad_out and consumed in registers; the trailing n_stats
+// columns are the batch statistics.  One launch instead of two, no
+// gradient re-read.
+__global__ void __launch_bounds__(256) adam_partials_kernel(PdrnnAdamArgs a, const float* __restrict__ work,
+                                                            int split, int64_t P_total, float* __restrict__ grad_out,
+                                                            float* __restrict__ stats_out, int n_stats) {
+  AdamScalars s;
+  s.lr = a.lr; s.b1 = a.beta1; s.b2 = a.beta2; s.eps = a.eps; s.wd = a.weight_decay;
+  s.bc1 = a.bias_correction1; s.bc2_sqrt = a.bias_correction2_sqrt;
+  s.gscale = a.grad_scale; s.decoupled = a.decoupled; s.maximize = a.maximize;
+  s.amsgrad = 0;
+  const int64_t n = a.n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + n_stats; i += stride) {
+    float g = 0.f;
+    for (int sp = 0; sp < split; ++sp) g += work[(int64_t)sp * P_total + i];
+    if (i < n) {
+      grad_out[i] = g;
+      float p = a.param[i], m = a.exp_avg[i], v = a.exp_avg_sq[i];
+      adam_elem(p, g, m, v, nullptr, s);
+      a.param[i] = p; a.exp_avg[i] = m; a.exp_avg_sq[i] = v;
+    } else {
+      stats_out[i - n] = g;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace pdrnn
+
+extern "C" hipError_t pdrnn_adam_partials(const PdrnnAdamArgs* a, const float* work, int split, int64_t P_total,
+                                          float* grad_out, float* stats_out, int n_stats, hipStream_t stream) {
+  const int64_t total = a->n + n_stats;
+  if (total <= 0) return hipSuccess;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pdrnn::adam_partials_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, *a, work, split,
+                     P_total, grad_out, stats_out, n_stats);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t pdrnn_adam_flat(const PdrnnAdamArgs* a, hipStream_t stream) {
   if (a->n <= 0) return hipSuccess;

@@ -69,19 +69,44 @@ __device__ __forceinline__ float ldx(const float* x, int64_t i, int bf) {
   return bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(x)[i]) : x[i];
 }
 
+// Stage one sequence's inputs x[t][0..I) into the LDS image xs[t][0..H)
+// (columns >= I zero): only the I real columns are loaded (not H), 4 loads
+// in flight per thread, so the prologue is one memory round trip instead of
+// T*H/blockDim dependent ones.
+template <int H>
+__device__ __forceinline__ void stage_x(float* dst, const float* x, int64_t base, int64_t x_st, int T, int I,
+                                        int bf, bool valid) {
+  const int nthr = blockDim.x;
+  for (int e = threadIdx.x; e < T * H; e += nthr) {
+    const int k = e % H;
+    if (k >= I || !valid) dst[e] = 0.f;
+  }
+  if (!valid) return;
+  const int n = T * I;
+  for (int e0 = threadIdx.x; e0 < n; e0 += 4 * nthr) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = min(e0 + r * nthr, n - 1);
+      const int t = e / I, k = e - t * I;
+      v[r] = ldx(x, base + (int64_t)t * x_st + k, bf);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = e0 + r * nthr;
+      if (e < n) {
+        const int t = e / I, k = e - t * I;
+        dst[t * H + k] = v[r];
+      }
+    }
+  }
+}
+
 template <int H, int NB>
 __device__ __forceinline__ void preload_x(float* xs, const PdrnnLstmSmallFwdArgs& a, const int* bsrc,
                                           const bool* valid) {
-  const int T = a.T, I = a.I;
-  for (int n = 0; n < NB; ++n) {
-    float* dst = xs + (int64_t)n * T * H;
-    const int64_t base = (int64_t)bsrc[n] * a.x_sb;
-    for (int e = threadIdx.x; e < T * H; e += blockDim.x) {
-      const int t = e / H, k = e - t * H;
-      const float v = ldx(a.x, base + (int64_t)t * a.x_st + min(k, I - 1), a.x_bf16);
-      dst[e] = (valid[n] && k < I) ? v : 0.f;
-    }
-  }
+  for (int n = 0; n < NB; ++n)
+    stage_x<H>(xs + (int64_t)n * a.T * H, a.x, (int64_t)bsrc[n] * a.x_sb, a.x_st, a.T, a.I, a.x_bf16, valid[n]);
 }
 
 template <int H, int S, int NB, bool SAVE, bool XLDS>
@@ -856,14 +881,9 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       }
     }
     if constexpr (XLDS) {
-      for (int e = tid; e < NB * T * H; e += blockDim.x) {
-        const int n = e / (T * H);
-        const int rem = e - n * T * H;
-        const int t = rem / H, kk = rem - t * H;
-        const int bn = a.idx ? (int)a.idx[min(b0 + n, B - 1)] : min(b0 + n, B - 1);
-        const float v = ldx(a.x, (int64_t)bn * a.x_sb + (int64_t)t * a.x_st + min(kk, I - 1), a.x_bf16);
-        xs[e] = kk < I ? v : 0.f;
-      }
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+        stage_x<H>(xs + (int64_t)n * T * H, a.x, (int64_t)bsrc[n] * a.x_sb, a.x_st, T, I, a.x_bf16, true);
     }
 
     // ---- raw per-timestep operands (prefetched 2 steps ahead, masked at use)
@@ -1506,6 +1526,17 @@ hipError_t pdrnn_slab_reduce2(const float* slab, int64_t rows, int64_t P, int64_
   PDRNN_HIP_CHECK(hipGetLastError());
   dim3 g2((unsigned)((P + threads - 1) / threads));
   hipLaunchKernelGGL(pdrnn::slab_reduce_pass2_split, g2, dim3(threads), 0, stream, work, P, P_a, split, out_a, out_b);
+  return hipGetLastError();
+}
+
+hipError_t pdrnn_slab2_reduce_pass1(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB,
+                                   int64_t PB, float* work, int split, hipStream_t stream) {
+  if (split < 1) split = 1;
+  if (split > 64) split = 64;
+  const int64_t P = PA + PB;
+  const int threads = 256;
+  dim3 g1((unsigned)((P + threads - 1) / threads), (unsigned)split);
+  hipLaunchKernelGGL(pdrnn::slab2_reduce_pass1, g1, dim3(threads), 0, stream, A, rowsA, PA, Bs, rowsB, PB, work, split);
   return hipGetLastError();
 }
 

@@ -63,7 +63,14 @@ def supported(model: nn.Module, optimizer, device: torch.device) -> bool:
 
 
 class MotionTrainStep:
-    """Callable running one fused training step; returns [loss, n, correct]."""
+    """Callable running one fused training step; returns [loss, n, correct].
+
+    Single process (no gradient sync): the optimizer step is fused into the
+    tail of the gradient reduction (``adam_partials`` kernel), so one step
+    is four launches: forward+head+CE, BPTT, reduction pass 1, reduction
+    pass 2 + Adam."""
+
+    RING = 16384
 
     def __init__(self, model: nn.Module, optimizer, grad_sync: Optional[Callable[[], None]] = None):
         self.model = model
@@ -81,7 +88,10 @@ class MotionTrainStep:
         if not flat or len(flat) != 1:
             raise RuntimeError("fused step needs the model's flat parameter storage")
         self.flat = next(iter(flat.values()))
-        self.stats = torch.zeros(3, dtype=torch.float32, device=self.flat.grad.device)
+        # batch statistics land in a ring of rows (returned as views, no copy
+        # kernel per step); a row is reused after RING steps
+        self.ring = torch.zeros(self.RING, 3, dtype=torch.float32, device=self.flat.grad.device)
+        self._slot = 0
         # bf16 model: recurrent weights used rounded to bf16 (one cast of the
         # flat master buffer per step); gradients land on the fp32 masters
         self.bf16 = getattr(self.m, "compute_dtype", torch.float32) == torch.bfloat16
@@ -91,6 +101,25 @@ class MotionTrainStep:
     def _rounded(self):
         r = self.flat.data.to(torch.bfloat16).float()
         return [r[o:o + int(torch.Size(s).numel())].view(s) for o, s in self._offs]
+
+    def _fused_adam(self):
+        """(state, hyper-parameters) when Adam can run inside the reduction tail."""
+        from ..ops.adam import FusedAdam
+        opt = self.optimizer
+        if self.grad_sync is not None or type(opt) is not FusedAdam or len(opt.param_groups) != 1:
+            return None
+        g = opt.param_groups[0]
+        if g.get("amsgrad") or g.get("maximize") or opt._pdrnn_grad_scale != 1.0:
+            return None
+        fs = opt._group_flat(0, g)
+        if fs is None or fs["flat_p"].data_ptr() != self.flat.data.data_ptr() or \
+                fs["flat_p"].numel() != self.flat.data.numel():
+            return None
+        fs["step"] += 1.0
+        b1, b2 = g["betas"]
+        hp = [float(g["lr"]), b1, b2, g["eps"], g["weight_decay"], float(fs["step"]),
+              1.0 if g.get("decoupled_weight_decay", False) else 0.0]
+        return [fs["flat_p"], fs["exp_avg"], fs["exp_avg_sq"]], hp
 
     def __call__(self, features: Tensor, labels: Tensor, idx: Optional[Tensor]) -> Tensor:
         from ..ops.lstm import small_launch_config
@@ -104,9 +133,16 @@ class MotionTrainStep:
                 features = features.to(torch.bfloat16)
         else:
             ws = self.weights
+        stats = self.ring[self._slot]
+        self._slot = (self._slot + 1) % self.RING
+        fused = self._fused_adam()
+        if fused is not None:
+            self.mod.lstm_head_train_step(features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H,
+                                          self.NL, 0, 0, nb_fwd, nb_bwd, fused[0], fused[1])
+            return stats
         self.mod.lstm_head_train_step(
-            features, idx, labels, ws, hw, hb, self.flat.grad, self.stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd)
+            features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd)
         if self.grad_sync is not None:
             self.grad_sync()
         self.optimizer.step()
-        return self.stats.clone()
+        return stats
