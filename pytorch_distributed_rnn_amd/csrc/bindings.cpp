@@ -603,6 +603,16 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
     dd.dh0 = dh0.data_ptr<float>() + d * B * H;
     dd.dc0 = dc0.data_ptr<float>() + d * B * H;
   }
+  static const int env_splitk = [] {
+    const char* e = std::getenv("PDRNN_LSTM_LARGE_SPLITK");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.splitk = env_splitk > 0 ? env_splitk : pdrnn_lstm_large_bwd_splitk((int)B, (int)H, ndir);
+  Tensor ws;
+  if (a.splitk > 1) {
+    ws = at::empty({a.splitk, 2, B, H}, o32);
+    a.ws = ws.data_ptr<float>();
+  }
   hipStream_t st = cur_stream();
   HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, ndir, dt, st));
   for (int64_t s = 0; s < T; ++s) {

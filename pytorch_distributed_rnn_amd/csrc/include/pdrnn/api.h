@@ -199,9 +199,12 @@ typedef struct {
   int B, H, T;
   int step;                // processing-order step index (forward) / backward step index
   int reverse_mask;        // bit d set: direction d runs time-reversed
+  int splitk;              // backward: K slices (> 1 needs ws)
+  float* ws;               // backward split-K partials [splitk][2][B][H] fp32
 } PdrnnLstmLargeStepArgs;
 
 int pdrnn_lstm_large_supported(int H);
+int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir);
 // dtype 0 = bf16, 1 = fp16; tile -1 = auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
                                  hipStream_t stream);

@@ -270,6 +270,36 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
   }
 }
 
+// Cell backward of step tn for one (b, u), given the recurrent dh from the
+// step GEMM: dgates_tn and the dc carry; after the first forward step
+// (cell == false) it emits dh0 / dc0 instead.
+template <class DT>
+__device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B, int H, int T, bool rev, int tn,
+                                              bool cell, int b, int u, float dh) {
+  const int64_t bu = (int64_t)b * H + u;
+  if (!cell) {
+    if (d.dh0) d.dh0[bu] = dh;
+    if (d.dc0) d.dc0[bu] = d.dc_carry[bu];
+    return;
+  }
+  if (d.dout) dh += DT::to_f(d.dout[(int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u]);
+  const u16x4 av = *reinterpret_cast<const u16x4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u);
+  const float ig = DT::to_f(av.x), fg = DT::to_f(av.y), gg = DT::to_f(av.z), og = DT::to_f(av.w);
+  const float c = d.cseq[(int64_t)tn * B * H + bu];
+  const int tpp = rev ? tn + 1 : tn - 1;
+  const bool has_prev = rev ? tpp < T : tpp >= 0;
+  const float cp = has_prev ? d.cseq[(int64_t)tpp * B * H + bu] : (d.c0 ? d.c0[bu] : 0.f);
+  const float tc = tanh_(c);
+  const float dc = fmaf(dh * og, 1.f - tc * tc, d.dc_carry[bu]);
+  u16x4 dg;
+  dg.x = DT::from_f(dc * gg * ig * (1.f - ig));
+  dg.y = DT::from_f(dc * cp * fg * (1.f - fg));
+  dg.z = DT::from_f(dc * ig * (1.f - gg * gg));
+  dg.w = DT::from_f(dh * tc * og * (1.f - og));
+  *reinterpret_cast<u16x4*>(d.dgates + ((int64_t)tn * B + b) * 4 * H + 4 * u) = dg;
+  d.dc_carry[bu] = dc * fg;
+}
+
 // ---------------------------------------------------------------------------
 // Backward step: dh_{t'} = dgates_t Wp  (t' = the step processed before t in
 // forward order) fused with the cell backward of step t':
@@ -306,33 +336,60 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(Pdrnn
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = rbase + r;
-        if (b >= B) continue;
-        const int64_t bu = (int64_t)b * H + u;
-        float dh = acc[i][j][r];
-        if (!cell) {
-          if (d.dh0) d.dh0[bu] = dh;
-          if (d.dc0) d.dc0[bu] = d.dc_carry[bu];
-          continue;
-        }
-        if (d.dout) dh += DT::to_f(d.dout[(int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u]);
-        const u16x4 av = *reinterpret_cast<const u16x4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u);
-        const float ig = DT::to_f(av.x), fg = DT::to_f(av.y), gg = DT::to_f(av.z), og = DT::to_f(av.w);
-        const float c = d.cseq[(int64_t)tn * B * H + bu];
-        const int tpp = rev ? tn + 1 : tn - 1;
-        const bool has_prev = rev ? tpp < T : tpp >= 0;
-        const float cp = has_prev ? d.cseq[(int64_t)tpp * B * H + bu] : (d.c0 ? d.c0[bu] : 0.f);
-        const float tc = tanh_(c);
-        const float dc = fmaf(dh * og, 1.f - tc * tc, d.dc_carry[bu]);
-        u16x4 dg;
-        dg.x = DT::from_f(dc * gg * ig * (1.f - ig));
-        dg.y = DT::from_f(dc * cp * fg * (1.f - fg));
-        dg.z = DT::from_f(dc * ig * (1.f - gg * gg));
-        dg.w = DT::from_f(dh * tc * og * (1.f - og));
-        *reinterpret_cast<u16x4*>(d.dgates + ((int64_t)tn * B + b) * 4 * H + 4 * u) = dg;
-        d.dc_carry[bu] = dc * fg;
+        if (b < B) cell_bwd_elem<DT>(d, B, H, T, rev, tn, cell, b, u, acc[i][j][r]);
       }
     }
   }
+}
+
+// Split-K form of the backward step for small batches (few output tiles, long
+// K = 4H): blockIdx.z = direction * S + slice; each workgroup writes its fp32
+// partial tile to ws[slice][dir][B][H]; the cell kernel sums the S partials
+// in fixed order (deterministic) and runs the cell backward.
+template <class DT, int BM, int BN, int WM, int WN, int ST>
+__global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_splitk_kernel(PdrnnLstmLargeStepArgs args) {
+  typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
+  const int S = args.splitk;
+  const int dir = blockIdx.z / S, sl = blockIdx.z - dir * S;
+  const PdrnnLstmLargeDir& d = args.dir[dir];
+  const int B = args.B, H = args.H, T = args.T;
+  const bool rev = args.reverse_mask & (1 << dir);
+  const int t = rev ? args.step : T - 1 - args.step;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int Ks = 4 * H / S, k0 = sl * Ks;
+  f32x4 acc[G::MT][G::NT];
+  G::run(d.dgates + (int64_t)t * B * 4 * H + k0, 4 * H, d.wt + k0, 4 * H, B, Ks, m0, n0, smem_u16, acc);
+  float* ws = args.ws + ((int64_t)sl * 2 + dir) * B * H;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+#pragma unroll
+  for (int i = 0; i < G::MT; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = m0 + wm * G::WTM + i * 16 + (lane >> 4) * 4 + r;
+        const int u = n0 + wn * G::WTN + j * 16 + (lane & 15);
+        if (b < B) ws[(int64_t)b * H + u] = acc[i][j][r];
+      }
+}
+
+template <class DT>
+__global__ void lstm_large_bwd_cell_kernel(PdrnnLstmLargeStepArgs args) {
+  const int dir = blockIdx.z;
+  const PdrnnLstmLargeDir& d = args.dir[dir];
+  const int B = args.B, H = args.H, T = args.T, S = args.splitk;
+  const bool rev = args.reverse_mask & (1 << dir);
+  const int t = rev ? args.step : T - 1 - args.step;
+  const int tn = rev ? t + 1 : t - 1;
+  const bool cell = rev ? tn < T : tn >= 0;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)B * H) return;
+  float dh = 0.f;
+  for (int sl = 0; sl < S; ++sl) dh += args.ws[((int64_t)sl * 2 + dir) * B * H + e];
+  const int b = (int)(e / H), u = (int)(e - (int64_t)b * H);
+  cell_bwd_elem<DT>(d, B, H, T, rev, tn, cell, b, u, dh);
 }
 
 // Cell backward of the LAST forward step (no recurrent dh yet):
@@ -421,6 +478,19 @@ inline int pick_tile(int M, int N, int ndir) {
 template <class DT>
 hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, int tile, hipStream_t st) {
   const int N = backward ? a->H : 4 * a->H;
+  if (backward && a->splitk > 1 && a->ws) {
+    // 32x32 tiles, S K-slices, then the fixed-order sum + cell backward
+    typedef GemmPipe<DT, 32, 32, 2, 2, 4> G;
+    if (N % 32 || (4 * a->H) % (64 * a->splitk)) return hipErrorInvalidValue;
+    dim3 grid(N / 32, (a->B + 31) / 32, ndir * a->splitk);
+    hipLaunchKernelGGL((lstm_large_bwd_splitk_kernel<DT, 32, 32, 2, 2, 4>), grid, dim3(G::NTHREADS),
+                       sizeof(uint16_t) * G::LDS_ELEMS, st, *a);
+    PDRNN_HIP_CHECK(hipGetLastError());
+    const int64_t n = (int64_t)a->B * a->H;
+    hipLaunchKernelGGL(lstm_large_bwd_cell_kernel<DT>, dim3((unsigned)((n + 255) / 256), 1, ndir), dim3(256), 0, st,
+                       *a);
+    return hipGetLastError();
+  }
   if (tile < 0 || tile > 4) tile = pick_tile(a->B, N, ndir);
   switch (tile) {
 #define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_) \
@@ -457,6 +527,16 @@ hipError_t gemm_nt_dispatch(const uint16_t* A, int64_t lda, const uint16_t* Bt, 
 extern "C" {
 
 int pdrnn_lstm_large_supported(int H) { return H >= 64 && H % 64 == 0; }
+
+// K-slices for the backward step GEMM (1 = no split): split while the 32x32
+// tiling leaves fewer than 256 workgroups and each slice keeps >= 8 k-tiles.
+int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir) {
+  const int64_t tiles = (int64_t)(H / 32) * ((B + 31) / 32) * ndir;
+  int s = 1;
+  while (tiles * s * 2 <= 512 && (4 * H) / (64 * s * 2) >= 8) s *= 2;
+  if (tiles >= 256) s = 1;
+  return s;
+}
 
 hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
                                  hipStream_t stream) {

@@ -48,6 +48,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--log-interval", type=int, default=50)
     p.add_argument("--device", default=None)
     p.add_argument("--history-file", default=None)
+    p.add_argument("--checkpoint-directory", default=None, help="save <dir>/charlm-epoch<k>.pt after every epoch")
+    p.add_argument("--resume", default=None, help="checkpoint to continue from")
     p.add_argument("mode", choices=("local", "distributed"))
     return p
 
@@ -64,7 +66,14 @@ def main(argv=None):
                         distributed=args.mode == "distributed", backend=args.backend,
                         grad_clip=args.grad_clip, log_interval=args.log_interval,
                         bucket_cap_mb=args.bucket_mb, weak_scaling=args.weak_scaling)
-    history = [trainer.train_epoch(e, args.max_steps) for e in range(args.epochs)]
+    start = trainer.resume(args.resume) if args.resume else 0
+    history = []
+    for e in range(start, start + args.epochs):
+        h = trainer.train_epoch(e, args.max_steps)
+        history.append(h)
+        if args.checkpoint_directory:
+            from pathlib import Path
+            trainer.save(Path(args.checkpoint_directory) / f"charlm-epoch{e}.pt", e, h["loss"])
     if trainer.rank == 0 and args.history_file:
         with open(args.history_file, "w") as f:
             json.dump(history, f)

@@ -19,6 +19,7 @@ import torch
 from torch import Tensor, nn
 
 from ..data.charlm import CharCorpus
+from .checkpoint import adapt_state_dict_keys, save_checkpoint
 from ..ops.adam import FusedAdam
 from ..ops.xent import cross_entropy
 from ..parallel import env
@@ -94,3 +95,19 @@ class LMTrainer:
         logging.info(f"{self.rank}: Epoch {epoch} loss {mean:.6f} tokens/s {out['tokens_per_sec']:.1f} "
                      f"(x{self.world} ranks) device_peak_mib={out['device_peak_mib']:.1f}")
         return out
+
+    # ------------------------------------------------------------ checkpoints
+    def save(self, path, epoch: int, loss: float):
+        """Rank 0 writes the reference checkpoint layout (epoch, model_state,
+        optimizer_state, loss); returns the path or None on other ranks."""
+        if self.rank != 0:
+            return None
+        return save_checkpoint(path, epoch, self.model, self.optimizer, loss)
+
+    def resume(self, path) -> int:
+        """Load a checkpoint (weights_only); returns the next epoch index."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        self.model.load_state_dict(adapt_state_dict_keys(ck["model_state"], self.model))
+        if ck.get("optimizer_state") is not None:
+            self.optimizer.load_state_dict(ck["optimizer_state"])
+        return int(ck.get("epoch", 0))

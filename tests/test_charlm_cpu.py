@@ -64,3 +64,16 @@ def test_lm_ddp_invariance(tmp_path):
     assert len(mean) == len(local) == 4
     for x, y in zip(mean, local):
         assert abs(x - y) < 5e-5, (mean, local)
+
+
+def test_lm_checkpoint_resume(tmp_path):
+    args = ["python", "-m", "pytorch_distributed_rnn_amd.lm_cli", "--hidden", "16", "--embed", "8", "--seq-len", "16",
+            "--batch-size", "4", "--synthetic-tokens", "3000", "--max-steps", "3", "--log-interval", "0",
+            "--device", "cpu", "--vocab", "64", "--checkpoint-directory", str(tmp_path)]
+    run(args + ["local"], cwd=ROOT)
+    ck = tmp_path / "charlm-epoch0.pt"
+    assert ck.exists()
+    state = torch.load(ck, weights_only=True)
+    assert state["epoch"] == 1 and "embedding.weight" in state["model_state"]
+    run(args + ["--resume", str(ck), "local"], cwd=ROOT)
+    assert (tmp_path / "charlm-epoch1.pt").exists()

@@ -58,6 +58,7 @@ def _ref_model(m: LSTM):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("H,L,bi,B,T,I", [(128, 1, False, 5, 7, 24), (128, 2, False, 33, 9, 40),
+                                          (1024, 1, False, 16, 3, 32),  # split-K backward (8 slices)
                                           (64, 2, True, 5, 6, 24), (256, 1, True, 70, 4, 64)])
 def test_large_lstm_matches_torch(dt, H, L, bi, B, T, I):
     torch.manual_seed(1)
