@@ -607,7 +607,10 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
     const char* e = std::getenv("PDRNN_LSTM_LARGE_SPLITK");
     return e ? std::atoi(e) : 0;
   }();
-  a.splitk = env_splitk > 0 ? env_splitk : pdrnn_lstm_large_bwd_splitk((int)B, (int)H, ndir);
+  int big = 0;
+  const int auto_splitk = pdrnn_lstm_large_bwd_splitk((int)B, (int)H, ndir, &big);
+  a.splitk = env_splitk > 0 ? env_splitk : auto_splitk;
+  a.splitk_big = env_splitk > 0 ? (B >= 128 && H % 128 == 0) : big;
   Tensor ws;
   if (a.splitk > 1) {
     ws = at::empty({a.splitk, 2, B, H}, o32);

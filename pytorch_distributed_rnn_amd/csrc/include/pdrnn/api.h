@@ -200,11 +200,12 @@ typedef struct {
   int step;                // processing-order step index (forward) / backward step index
   int reverse_mask;        // bit d set: direction d runs time-reversed
   int splitk;              // backward: K slices (> 1 needs ws)
+  int splitk_big;          // split-K tile: 0 = 32x32, 1 = 128x128
   float* ws;               // backward split-K partials [splitk][2][B][H] fp32
 } PdrnnLstmLargeStepArgs;
 
 int pdrnn_lstm_large_supported(int H);
-int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir);
+int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir, int* big);
 // dtype 0 = bf16, 1 = fp16; tile -1 = auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
                                  hipStream_t stream);

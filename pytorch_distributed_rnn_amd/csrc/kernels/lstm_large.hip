@@ -479,12 +479,21 @@ template <class DT>
 hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, int tile, hipStream_t st) {
   const int N = backward ? a->H : 4 * a->H;
   if (backward && a->splitk > 1 && a->ws) {
-    // 32x32 tiles, S K-slices, then the fixed-order sum + cell backward
-    typedef GemmPipe<DT, 32, 32, 2, 2, 4> G;
-    if (N % 32 || (4 * a->H) % (64 * a->splitk)) return hipErrorInvalidValue;
-    dim3 grid(N / 32, (a->B + 31) / 32, ndir * a->splitk);
-    hipLaunchKernelGGL((lstm_large_bwd_splitk_kernel<DT, 32, 32, 2, 2, 4>), grid, dim3(G::NTHREADS),
-                       sizeof(uint16_t) * G::LDS_ELEMS, st, *a);
+    // S K-slices (32x32 tiles for small batches, 128x128 once the batch fills
+    // them), then the fixed-order sum + cell backward
+    if ((4 * a->H) % (64 * a->splitk)) return hipErrorInvalidValue;
+    if (a->splitk_big && N % 128 == 0) {
+      typedef GemmPipe<DT, 128, 128, 2, 2, 3> G;
+      dim3 grid(N / 128, (a->B + 127) / 128, ndir * a->splitk);
+      hipLaunchKernelGGL((lstm_large_bwd_splitk_kernel<DT, 128, 128, 2, 2, 3>), grid, dim3(G::NTHREADS),
+                         sizeof(uint16_t) * G::LDS_ELEMS, st, *a);
+    } else {
+      typedef GemmPipe<DT, 32, 32, 2, 2, 4> G;
+      if (N % 32) return hipErrorInvalidValue;
+      dim3 grid(N / 32, (a->B + 31) / 32, ndir * a->splitk);
+      hipLaunchKernelGGL((lstm_large_bwd_splitk_kernel<DT, 32, 32, 2, 2, 4>), grid, dim3(G::NTHREADS),
+                         sizeof(uint16_t) * G::LDS_ELEMS, st, *a);
+    }
     PDRNN_HIP_CHECK(hipGetLastError());
     const int64_t n = (int64_t)a->B * a->H;
     hipLaunchKernelGGL(lstm_large_bwd_cell_kernel<DT>, dim3((unsigned)((n + 255) / 256), 1, ndir), dim3(256), 0, st,
@@ -528,13 +537,24 @@ extern "C" {
 
 int pdrnn_lstm_large_supported(int H) { return H >= 64 && H % 64 == 0; }
 
-// K-slices for the backward step GEMM (1 = no split): split while the 32x32
-// tiling leaves fewer than 256 workgroups and each slice keeps >= 8 k-tiles.
-int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir) {
+// K-slices for the backward step GEMM (1 = no split) and their tile
+// (*big: 128x128 instead of 32x32).  Large batches: 128x128 tiles with the
+// fewest slices reaching one workgroup per CU (bi-LSTM h4096 B256: 2 slices,
+// -6 % step time); small batches: 32x32 tiles, slices while < 512 workgroups
+// and each slice keeps >= 8 k-tiles (char-LM h1024 B128: 4 slices).
+int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir, int* big) {
+  *big = 0;
+  const int kt = 4 * H / 64;
+  if (B >= 128 && H % 128 == 0) {
+    const int64_t t128 = (int64_t)(H / 128) * ((B + 127) / 128) * ndir;
+    if (t128 >= 256) return 1;
+    for (int s = 2; s <= 4; s *= 2)
+      if (t128 * s >= 256 && kt / s >= 8) { *big = 1; return s; }
+  }
   const int64_t tiles = (int64_t)(H / 32) * ((B + 31) / 32) * ndir;
+  if (tiles >= 256) return 1;
   int s = 1;
-  while (tiles * s * 2 <= 512 && (4 * H) / (64 * s * 2) >= 8) s *= 2;
-  if (tiles >= 256) s = 1;
+  while (tiles * s * 2 <= 512 && kt / (s * 2) >= 8) s *= 2;
   return s;
 }
 
