@@ -175,7 +175,7 @@ hipError_t pdrnn_embedding_bwd_csr(const float* dout, const int64_t* perm, const
 // gate q (i, f, g, o) of unit u.
 typedef struct {
   const uint16_t* w;       // [4H, H] W_hh, gate-interleaved rows (forward GEMM: h Wp^T)
-  const uint16_t* wt;      // [H, 4H] its transpose (backward GEMM: dgates Wp)
+  const uint16_t* wt;      // [H, 4H] W_hh^T, torch gate-blocked order (backward GEMM: dgates W_hh)
   const uint16_t* xp;      // input projection incl. bias, [t, b, col] at t*xp_st + b*xp_sb + col
   int64_t xp_sb, xp_st;
   const uint16_t* h0;      // [B, H] or null
@@ -184,7 +184,7 @@ typedef struct {
   int64_t hseq_sb, hseq_st;
   float* cseq;             // [T, B, H] fp32 cell states
   uint16_t* acts;          // [T, B, 4H] activated gates
-  uint16_t* dgates;        // [T, B, 4H] pre-activation gate gradients (backward)
+  uint16_t* dgates;        // [T, B, 4H] pre-activation gate gradients, gate-blocked (i|f|g|o)
   const uint16_t* dout;    // grad of hseq (same strides as dout_sb / dout_st) or null
   int64_t dout_sb, dout_st;
   const float* dhn;        // [B, H] or null

@@ -296,7 +296,11 @@ __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B,
   dg.y = DT::from_f(dc * cp * fg * (1.f - fg));
   dg.z = DT::from_f(dc * ig * (1.f - gg * gg));
   dg.w = DT::from_f(dh * tc * og * (1.f - og));
-  *reinterpret_cast<u16x4*>(d.dgates + ((int64_t)tn * B + b) * 4 * H + 4 * u) = dg;
+  // gate-BLOCKED layout (torch's i|f|g|o row order): the next step GEMM pairs
+  // it with W_hh^T as stored, and the weight-gradient GEMMs land directly in
+  // the parameters' layout (no permutation copies)
+  uint16_t* dgp = d.dgates + ((int64_t)tn * B + b) * 4 * H + u;
+  dgp[0] = dg.x; dgp[H] = dg.y; dgp[2 * H] = dg.z; dgp[3 * H] = dg.w;
   d.dc_carry[bu] = dc * fg;
 }
 
@@ -418,7 +422,11 @@ __global__ void lstm_large_bwd_first_kernel(PdrnnLstmLargeStepArgs args) {
   dg.y = DT::from_f(dc * cp * fg * (1.f - fg));
   dg.z = DT::from_f(dc * ig * (1.f - gg * gg));
   dg.w = DT::from_f(dh * tc * og * (1.f - og));
-  *reinterpret_cast<u16x4*>(d.dgates + ((int64_t)tn * B + b) * 4 * H + 4 * u) = dg;
+  // gate-BLOCKED layout (torch's i|f|g|o row order): the next step GEMM pairs
+  // it with W_hh^T as stored, and the weight-gradient GEMMs land directly in
+  // the parameters' layout (no permutation copies)
+  uint16_t* dgp = d.dgates + ((int64_t)tn * B + b) * 4 * H + u;
+  dgp[0] = dg.x; dgp[H] = dg.y; dgp[2 * H] = dg.z; dgp[3 * H] = dg.w;
   d.dc_carry[e] = dc * fg;
 }
 

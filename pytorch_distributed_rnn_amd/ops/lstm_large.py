@@ -40,6 +40,12 @@ def _perm(hidden: int, device) -> Tensor:
     return p
 
 
+def _interleave(w: Tensor, hidden: int) -> Tensor:
+    """Rows q*H+u (torch gate-blocked) -> rows 4u+q (gate-interleaved), one
+    transpose copy (cheaper than an index gather)."""
+    return w.reshape(4, hidden, -1).transpose(0, 1).reshape(4 * hidden, -1)
+
+
 def _tile() -> int:
     try:
         return int(os.environ.get("PDRNN_LSTM_LARGE_TILE", "-1"))
@@ -87,10 +93,10 @@ class _LargeLSTMLayer(torch.autograd.Function):
             if b_hh is not None:
                 b = b + b_hh.float()
             bias.append(b[perm])
-        wih_p = torch.cat([w[perm] for w in w_ih], 0).to(cdt)                 # [ndir*4H, I]
+        wih_p = torch.cat([_interleave(w.to(cdt), H) for w in w_ih], 0)     # [ndir*4H, I]
         bias_p = torch.cat(bias, 0).to(cdt)
         xp = torch.addmm(bias_p, x.reshape(T * B, I), wih_p.t()).view(T, B, ndir * 4 * H)
-        whh_p = [w[perm].to(cdt).contiguous() for w in w_hh]
+        whh_p = [_interleave(w.to(cdt), H).contiguous() for w in w_hh]
         h0c = h0.to(cdt).contiguous() if h0 is not None else None
         c0c = c0.float().contiguous() if c0 is not None else None
         rev_mask = 2 if ndir == 2 else 0
@@ -98,7 +104,9 @@ class _LargeLSTMLayer(torch.autograd.Function):
         last = [T - 1, 0][:ndir]
         hn = torch.stack([hseq[last[d], :, d * H:(d + 1) * H] for d in range(ndir)], 0)
         cn = torch.stack([cseq[d, last[d]] for d in range(ndir)], 0)
-        ctx.save_for_backward(x, hseq, cseq, acts, h0c, c0c, wih_p, *whh_p)
+        # backward works in torch's gate-blocked order: weights as stored (cast)
+        ctx.save_for_backward(x, hseq, cseq, acts, h0c, c0c, *[w.to(cdt) for w in w_ih],
+                              *[w.to(cdt) for w in w_hh])
         ctx.cfg = (H, ndir, tile, rev_mask, [w is not None for w in weights], h0 is not None,
                    c0 is not None, h0.dtype if h0 is not None else None,
                    c0.dtype if c0 is not None else None)
@@ -106,38 +114,31 @@ class _LargeLSTMLayer(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dhseq, dhn, dcn):
-        x, hseq, cseq, acts, h0c, c0c, wih_p, *whh_p = ctx.saved_tensors
         H, ndir, tile, rev_mask, has_w, has_h0, has_c0, h0_dtype, c0_dtype = ctx.cfg
+        x, hseq, cseq, acts, h0c, c0c, *ws = ctx.saved_tensors
+        wih, whh = ws[:ndir], ws[ndir:]
         cdt = x.dtype
         T, B, I = x.shape
         mod = _ext.native(x.device)
-        perm = _perm(H, x.device)
         dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
         dhn_f = dhn.float().contiguous() if dhn is not None else None
         dcn_f = dcn.float().contiguous() if dcn is not None else None
-        wt = [w.t().contiguous() for w in whh_p]
+        wt = [w.t().contiguous() for w in whh]                      # [H, 4H], gate-blocked
         dgates, dh0, dc0 = mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile)
         grads: List[Optional[Tensor]] = []
         dx = None
         x2 = x.reshape(T * B, I)
         for d in range(ndir):
-            G = dgates[d].view(T * B, 4 * H)
+            G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
             hd = hseq[:, :, d * H:(d + 1) * H]
             h0d = h0c[d:d + 1] if h0c is not None else torch.zeros(1, B, H, device=x.device, dtype=cdt)
             hprev = torch.cat([h0d, hd[:-1]], 0) if d == 0 else torch.cat([hd[1:], h0d], 0)
-            dwhh_p = _mm_f32(G.t(), hprev.reshape(T * B, H))
-            dwih_p = _mm_f32(G.t(), x2)
-            db_p = G.float().sum(0)
-            dwih = torch.empty_like(dwih_p)
-            dwih[perm] = dwih_p
-            dwhh = torch.empty_like(dwhh_p)
-            dwhh[perm] = dwhh_p
-            db = torch.empty_like(db_p)
-            db[perm] = db_p
-            part = torch.mm(G, wih_p[d * 4 * H:(d + 1) * 4 * H])
+            dwhh = _mm_f32(G.t(), hprev.reshape(T * B, H))
+            dwih = _mm_f32(G.t(), x2)
+            db = G.float().sum(0)
+            part = torch.mm(G, wih[d])
             dx = part if dx is None else dx + part
-            gb = [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
-            grads += gb
+            grads += [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
         dx = dx.view(T, B, I)
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         dc0_out = dc0.to(c0_dtype) if has_c0 else None
