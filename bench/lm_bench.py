@@ -69,7 +69,9 @@ def main(argv=None):
         dtype, model_name = "bf16", f"char-LM LSTM {a.layers}x{H} (vocab 256, embed 256)"
         metric = "tokens/sec (whole node) char-LM 2-layer LSTM h1024 seq512 bf16 DDP"
     else:
-        B, T, H = a.batch or 256, a.seq_len or 64, a.hidden or 4096
+        # batch sized for HBM: B=4096 x T=64 holds ~115 GB of activations on one
+        # 288 GB MI355X (B sweep 256/512/1024/2048/4096: 239k/265k/307k/313k/323k tok/s)
+        B, T, H = a.batch or 4096, a.seq_len or 64, a.hidden or 4096
         model = BiLSTMEncoder(a.input_dim, H, a.layers, 32, torch.float16).to(dev)
         flatten_module(model)
         net = DistributedDataParallel(model) if world > 1 else model

@@ -510,8 +510,11 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 // xp: [T, B, ndir*4H] (16-bit, bias included, gate-interleaved per direction)
 // w:  ndir x [4H, H] gate-interleaved W_hh;  h0: [ndir, B, H] 16-bit;  c0: [ndir, B, H] f32
 // returns hseq [T, B, ndir*H], cseq [ndir, T, B, H] f32, acts [ndir, T, B, 4H]
+// cell 1 = GRU packed as [r|z|n_x|n_h] (ops/gru_large.py): c0 is the fp32
+// initial hidden state and cseq the fp32 hidden states.
 std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& w, const optional<Tensor>& h0,
-                                   const optional<Tensor>& c0, int64_t H, int64_t reverse_mask, int64_t tile) {
+                                   const optional<Tensor>& c0, int64_t H, int64_t reverse_mask, int64_t tile,
+                                   int64_t cell) {
   CHECK_HIP_TENSOR(xp);
   const c10::DeviceGuard guard(xp.device());
   const int dt = dtype_code(xp);
@@ -535,6 +538,8 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
   if (has_c0) TORCH_CHECK(c0->is_contiguous() && c0->scalar_type() == at::kFloat && c0->numel() == ndir * B * H, "c0");
   PdrnnLstmLargeStepArgs a{};
   a.B = (int)B; a.H = (int)H; a.T = (int)T; a.reverse_mask = (int)reverse_mask;
+  TORCH_CHECK(cell == 0 || cell == 1, "cell: 0 = LSTM, 1 = GRU");
+  a.cell = (int)cell;
   for (int d = 0; d < ndir; ++d) {
     PdrnnLstmLargeDir& dd = a.dir[d];
     dd.w = u16(w[d]);
@@ -558,7 +563,7 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
 std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<Tensor>& dhn,
                                    const optional<Tensor>& dcn, const std::vector<Tensor>& wt, const Tensor& cseq,
                                    const Tensor& acts, const optional<Tensor>& c0, int64_t H, int64_t reverse_mask,
-                                   int64_t tile) {
+                                   int64_t tile, int64_t cell) {
   CHECK_HIP_TENSOR(acts);
   const c10::DeviceGuard guard(acts.device());
   const int dt = dtype_code(acts);
@@ -587,6 +592,8 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   const float* c0_p = f32p(c0);
   PdrnnLstmLargeStepArgs a{};
   a.B = (int)B; a.H = (int)H; a.T = (int)T; a.reverse_mask = (int)reverse_mask;
+  TORCH_CHECK(cell == 0 || cell == 1, "cell: 0 = LSTM, 1 = GRU");
+  a.cell = (int)cell;
   for (int d = 0; d < ndir; ++d) {
     PdrnnLstmLargeDir& dd = a.dir[d];
     dd.wt = u16(wt[d]);

@@ -201,6 +201,7 @@ typedef struct {
   int reverse_mask;        // bit d set: direction d runs time-reversed
   int splitk;              // backward: K slices (> 1 needs ws)
   int splitk_big;          // split-K tile: 0 = 32x32, 1 = 128x128
+  int cell;                // 0 = LSTM; 1 = GRU packed as [r|z|n_x|n_h] (cseq = fp32 h, acts = r,z,n,n_h)
   float* ws;               // backward split-K partials [splitk][2][B][H] fp32
 } PdrnnLstmLargeStepArgs;
 

@@ -16,6 +16,8 @@
 //     weight gradients are then library GEMMs over all timesteps.
 // Both directions of a bidirectional layer run in the same launch
 // (blockIdx.z = direction), doubling the workgroups per step.
+// The same kernels serve the large-H GRU (CELL = 1, ops/gru_large.py): its
+// gates ride on the LSTM quad as [r | z | n_x | n_h] with zero weight blocks.
 //
 // Reference semantics: torch.nn.LSTM (gate order i, f, g, o), the op the
 // reference's MotionModel uses (reference: src/motion/model.py:9,14).
@@ -189,7 +191,11 @@ struct GemmPipe {
 // Forward step: gates = h_{t-1} Wp^T + xp_t  ->  (i, f, g, o), c_t, h_t.
 // Columns are gate-interleaved: col = 4 u + q.
 // ---------------------------------------------------------------------------
-template <class DT, int BM, int BN, int WM, int WN, int ST>
+// CELL 1 = GRU on the same quad (host packing in ops/gru_large.py): the four
+// columns of a unit are [r | z | n_x | n_h] (n_x = W_in x + b_in from xp,
+// n_h = W_hn h + b_hn), cseq holds the fp32 hidden state h_t, and the saved
+// quad is (r, z, n, n_h).
+template <class DT, int BM, int BN, int WM, int WN, int ST, int CELL>
 __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(PdrnnLstmLargeStepArgs args) {
   typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
@@ -250,58 +256,89 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
     const uint16_t* xh = reinterpret_cast<const uint16_t*>(&xv);
     const float z[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
     float g[8];
-    uint4 av;
-    uint16_t* ah = reinterpret_cast<uint16_t*>(&av);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float zz = z[k] + DT::to_f(xh[k]);
-      g[k] = (k & 3) == 2 ? tanh_(zz) : sigm(zz);
-      ah[k] = DT::from_f(g[k]);
+      if constexpr (CELL == 0) g[k] = (k & 3) == 2 ? tanh_(zz) : sigm(zz);
+      else g[k] = (k & 3) < 2 ? sigm(zz) : zz;  // GRU: r, z activated; n_x, n_h linear
     }
-    *reinterpret_cast<uint4*>(acts + (int64_t)b * 4 * H + col) = av;
     const int u = col >> 2;
     float2 cp = make_float2(0.f, 0.f);
     if (cprev) cp = *reinterpret_cast<const float2*>(cprev + (int64_t)b * H + u);
-    const float c0n = fmaf(g[1], cp.x, g[0] * g[2]);
-    const float c1n = fmaf(g[5], cp.y, g[4] * g[6]);
-    *reinterpret_cast<float2*>(cout + (int64_t)b * H + u) = make_float2(c0n, c1n);
-    const uint32_t hv = (uint32_t)DT::from_f(g[3] * tanh_(c0n)) | ((uint32_t)DT::from_f(g[7] * tanh_(c1n)) << 16);
+    float s0, s1, h0v, h1v;
+    if constexpr (CELL == 0) {
+      s0 = fmaf(g[1], cp.x, g[0] * g[2]);
+      s1 = fmaf(g[5], cp.y, g[4] * g[6]);
+      h0v = g[3] * tanh_(s0);
+      h1v = g[7] * tanh_(s1);
+    } else {
+      // n = tanh(n_x + r n_h) takes n_x's slot in the saved quad;
+      // h = n + z (h_prev - n) with the fp32 h_prev
+      g[2] = tanh_(fmaf(g[0], g[3], g[2]));
+      g[6] = tanh_(fmaf(g[4], g[7], g[6]));
+      s0 = h0v = fmaf(g[1], cp.x - g[2], g[2]);
+      s1 = h1v = fmaf(g[5], cp.y - g[6], g[6]);
+    }
+    uint4 av;
+    uint16_t* ah = reinterpret_cast<uint16_t*>(&av);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ah[k] = DT::from_f(g[k]);
+    *reinterpret_cast<uint4*>(acts + (int64_t)b * 4 * H + col) = av;
+    *reinterpret_cast<float2*>(cout + (int64_t)b * H + u) = make_float2(s0, s1);
+    const uint32_t hv = (uint32_t)DT::from_f(h0v) | ((uint32_t)DT::from_f(h1v) << 16);
     *reinterpret_cast<uint32_t*>(hout + (int64_t)b * d.hseq_sb + u) = hv;
   }
 }
 
 // Cell backward of step tn for one (b, u), given the recurrent dh from the
-// step GEMM: dgates_tn and the dc carry; after the first forward step
-// (cell == false) it emits dh0 / dc0 instead.
-template <class DT>
+// step GEMM and the carry of the step after tn (LSTM: dc; GRU: the direct
+// path dh_{tn+1} z_{tn+1}): emits dgates_tn and the new carry; after the
+// first forward step (cell == false) it emits dh0 / dc0 instead.
+template <class DT, int CELL>
 __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B, int H, int T, bool rev, int tn,
-                                              bool cell, int b, int u, float dh) {
+                                              bool cell, int b, int u, float dh, float carry) {
   const int64_t bu = (int64_t)b * H + u;
+  if constexpr (CELL == 1) dh += carry;
   if (!cell) {
     if (d.dh0) d.dh0[bu] = dh;
-    if (d.dc0) d.dc0[bu] = d.dc_carry[bu];
+    if (CELL == 0 && d.dc0) d.dc0[bu] = carry;
     return;
   }
   if (d.dout) dh += DT::to_f(d.dout[(int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u]);
   const u16x4 av = *reinterpret_cast<const u16x4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u);
-  const float ig = DT::to_f(av.x), fg = DT::to_f(av.y), gg = DT::to_f(av.z), og = DT::to_f(av.w);
-  const float c = d.cseq[(int64_t)tn * B * H + bu];
+  const float a0 = DT::to_f(av.x), a1 = DT::to_f(av.y), a2 = DT::to_f(av.z), a3 = DT::to_f(av.w);
   const int tpp = rev ? tn + 1 : tn - 1;
   const bool has_prev = rev ? tpp < T : tpp >= 0;
-  const float cp = has_prev ? d.cseq[(int64_t)tpp * B * H + bu] : (d.c0 ? d.c0[bu] : 0.f);
-  const float tc = tanh_(c);
-  const float dc = fmaf(dh * og, 1.f - tc * tc, d.dc_carry[bu]);
+  // LSTM: c_{tn-1};  GRU: h_{tn-1} (both fp32 in cseq, c0 = initial state)
+  const float sp = has_prev ? d.cseq[(int64_t)tpp * B * H + bu] : (d.c0 ? d.c0[bu] : 0.f);
   u16x4 dg;
-  dg.x = DT::from_f(dc * gg * ig * (1.f - ig));
-  dg.y = DT::from_f(dc * cp * fg * (1.f - fg));
-  dg.z = DT::from_f(dc * ig * (1.f - gg * gg));
-  dg.w = DT::from_f(dh * tc * og * (1.f - og));
-  // gate-BLOCKED layout (torch's i|f|g|o row order): the next step GEMM pairs
-  // it with W_hh^T as stored, and the weight-gradient GEMMs land directly in
-  // the parameters' layout (no permutation copies)
+  float next;
+  if constexpr (CELL == 0) {
+    const float ig = a0, fg = a1, gg = a2, og = a3;
+    const float tc = tanh_(d.cseq[(int64_t)tn * B * H + bu]);
+    const float dc = fmaf(dh * og, 1.f - tc * tc, carry);
+    dg.x = DT::from_f(dc * gg * ig * (1.f - ig));
+    dg.y = DT::from_f(dc * sp * fg * (1.f - fg));
+    dg.z = DT::from_f(dc * ig * (1.f - gg * gg));
+    dg.w = DT::from_f(dh * tc * og * (1.f - og));
+    next = dc * fg;
+  } else {
+    // h = n + z (h_prev - n), n = tanh(n_x + r n_h):
+    // [dr r(1-r) | dz z(1-z) | dpre_n (x side) | dpre_n r (n_h side)]
+    const float r = a0, z = a1, n = a2, nh = a3;
+    const float dpn = dh * (1.f - z) * (1.f - n * n);
+    dg.x = DT::from_f(dpn * nh * r * (1.f - r));
+    dg.y = DT::from_f(dh * (sp - n) * z * (1.f - z));
+    dg.z = DT::from_f(dpn);
+    dg.w = DT::from_f(dpn * r);
+    next = dh * z;
+  }
+  // gate-BLOCKED layout (torch's row order): the next step GEMM pairs it with
+  // W_hh^T as stored, and the weight-gradient GEMMs land directly in the
+  // parameters' layout (no permutation copies)
   uint16_t* dgp = d.dgates + ((int64_t)tn * B + b) * 4 * H + u;
   dgp[0] = dg.x; dgp[H] = dg.y; dgp[2 * H] = dg.z; dgp[3 * H] = dg.w;
-  d.dc_carry[bu] = dc * fg;
+  d.dc_carry[bu] = next;
 }
 
 // ---------------------------------------------------------------------------
@@ -312,7 +349,7 @@ __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B,
 //   dc_carry = dc f
 // With cell == 0 (after the first forward step): dh0 = acc, dc0 = dc_carry.
 // ---------------------------------------------------------------------------
-template <class DT, int BM, int BN, int WM, int WN, int ST>
+template <class DT, int BM, int BN, int WM, int WN, int ST, int CELL>
 __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(PdrnnLstmLargeStepArgs args) {
   typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
@@ -340,7 +377,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(Pdrnn
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = rbase + r;
-        if (b < B) cell_bwd_elem<DT>(d, B, H, T, rev, tn, cell, b, u, acc[i][j][r]);
+        if (b < B) cell_bwd_elem<DT, CELL>(d, B, H, T, rev, tn, cell, b, u, acc[i][j][r], d.dc_carry[(int64_t)b * H + u]);
       }
     }
   }
@@ -379,7 +416,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_splitk_kernel(Pdr
       }
 }
 
-template <class DT>
+template <class DT, int CELL>
 __global__ void lstm_large_bwd_cell_kernel(PdrnnLstmLargeStepArgs args) {
   const int dir = blockIdx.z;
   const PdrnnLstmLargeDir& d = args.dir[dir];
@@ -393,12 +430,12 @@ __global__ void lstm_large_bwd_cell_kernel(PdrnnLstmLargeStepArgs args) {
   float dh = 0.f;
   for (int sl = 0; sl < S; ++sl) dh += args.ws[((int64_t)sl * 2 + dir) * B * H + e];
   const int b = (int)(e / H), u = (int)(e - (int64_t)b * H);
-  cell_bwd_elem<DT>(d, B, H, T, rev, tn, cell, b, u, dh);
+  cell_bwd_elem<DT, CELL>(d, B, H, T, rev, tn, cell, b, u, dh, d.dc_carry[e]);
 }
 
 // Cell backward of the LAST forward step (no recurrent dh yet):
-// dh = dout_T-1 + dhn, dc = dcn.  One thread per (b, u).
-template <class DT>
+// dh = dout_T-1 + dhn, carry = dcn (LSTM) / 0 (GRU).  One thread per (b, u).
+template <class DT, int CELL>
 __global__ void lstm_large_bwd_first_kernel(PdrnnLstmLargeStepArgs args) {
   const PdrnnLstmLargeDir& d = args.dir[blockIdx.z];
   const int B = args.B, H = args.H, T = args.T;
@@ -407,27 +444,8 @@ __global__ void lstm_large_bwd_first_kernel(PdrnnLstmLargeStepArgs args) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)B * H) return;
   const int b = (int)(e / H), u = (int)(e - (int64_t)b * H);
-  float dh = d.dhn ? d.dhn[e] : 0.f;
-  if (d.dout) dh += DT::to_f(d.dout[(int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u]);
-  const u16x4 av = *reinterpret_cast<const u16x4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u);
-  const float ig = DT::to_f(av.x), fg = DT::to_f(av.y), gg = DT::to_f(av.z), og = DT::to_f(av.w);
-  const float c = d.cseq[(int64_t)tn * B * H + e];
-  const int tpp = rev ? tn + 1 : tn - 1;
-  const bool has_prev = rev ? tpp < T : tpp >= 0;
-  const float cp = has_prev ? d.cseq[(int64_t)tpp * B * H + e] : (d.c0 ? d.c0[e] : 0.f);
-  const float tc = tanh_(c);
-  const float dc = fmaf(dh * og, 1.f - tc * tc, d.dcn ? d.dcn[e] : 0.f);
-  u16x4 dg;
-  dg.x = DT::from_f(dc * gg * ig * (1.f - ig));
-  dg.y = DT::from_f(dc * cp * fg * (1.f - fg));
-  dg.z = DT::from_f(dc * ig * (1.f - gg * gg));
-  dg.w = DT::from_f(dh * tc * og * (1.f - og));
-  // gate-BLOCKED layout (torch's i|f|g|o row order): the next step GEMM pairs
-  // it with W_hh^T as stored, and the weight-gradient GEMMs land directly in
-  // the parameters' layout (no permutation copies)
-  uint16_t* dgp = d.dgates + ((int64_t)tn * B + b) * 4 * H + u;
-  dgp[0] = dg.x; dgp[H] = dg.y; dgp[2 * H] = dg.z; dgp[3 * H] = dg.w;
-  d.dc_carry[e] = dc * fg;
+  const float carry = (CELL == 0 && d.dcn) ? d.dcn[e] : 0.f;
+  cell_bwd_elem<DT, CELL>(d, B, H, T, rev, tn, true, b, u, d.dhn ? d.dhn[e] : 0.f, carry);
 }
 
 // Plain NT GEMM on the same core (tests / fallbacks): C[M,N] fp32 = A Bt^T.
@@ -454,7 +472,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(const uint16_t* A
       }
 }
 
-template <class DT, int BM, int BN, int WM, int WN, int ST>
+template <class DT, int CELL, int BM, int BN, int WM, int WN, int ST>
 hipError_t launch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, hipStream_t st) {
   typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
   const int N = backward ? a->H : 4 * a->H;
@@ -462,9 +480,9 @@ hipError_t launch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward,
   dim3 grid(N / BN, (a->B + BM - 1) / BM, ndir);
   const size_t lds = sizeof(uint16_t) * G::LDS_ELEMS;
   if (backward)
-    hipLaunchKernelGGL((lstm_large_bwd_step_kernel<DT, BM, BN, WM, WN, ST>), grid, dim3(G::NTHREADS), lds, st, *a);
+    hipLaunchKernelGGL((lstm_large_bwd_step_kernel<DT, BM, BN, WM, WN, ST, CELL>), grid, dim3(G::NTHREADS), lds, st, *a);
   else
-    hipLaunchKernelGGL((lstm_large_fwd_step_kernel<DT, BM, BN, WM, WN, ST>), grid, dim3(G::NTHREADS), lds, st, *a);
+    hipLaunchKernelGGL((lstm_large_fwd_step_kernel<DT, BM, BN, WM, WN, ST, CELL>), grid, dim3(G::NTHREADS), lds, st, *a);
   return hipGetLastError();
 }
 
@@ -483,7 +501,7 @@ inline int pick_tile(int M, int N, int ndir) {
   return 4;
 }
 
-template <class DT>
+template <class DT, int CELL>
 hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, int tile, hipStream_t st) {
   const int N = backward ? a->H : 4 * a->H;
   if (backward && a->splitk > 1 && a->ws) {
@@ -504,14 +522,14 @@ hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwar
     }
     PDRNN_HIP_CHECK(hipGetLastError());
     const int64_t n = (int64_t)a->B * a->H;
-    hipLaunchKernelGGL(lstm_large_bwd_cell_kernel<DT>, dim3((unsigned)((n + 255) / 256), 1, ndir), dim3(256), 0, st,
+    hipLaunchKernelGGL((lstm_large_bwd_cell_kernel<DT, CELL>), dim3((unsigned)((n + 255) / 256), 1, ndir), dim3(256), 0, st,
                        *a);
     return hipGetLastError();
   }
   if (tile < 0 || tile > 4) tile = pick_tile(a->B, N, ndir);
   switch (tile) {
 #define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_) \
-  case ID: return launch_step<DT, BM_, BN_, WM_, WN_, ST_>(a, ndir, backward, st);
+  case ID: return launch_step<DT, CELL, BM_, BN_, WM_, WN_, ST_>(a, ndir, backward, st);
     PDRNN_TILE_CFGS(PDRNN_CASE)
 #undef PDRNN_CASE
     default: return hipErrorInvalidValue;
@@ -569,17 +587,26 @@ int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir, int* big) {
 hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
                                  hipStream_t stream) {
   if (!pdrnn_lstm_large_supported(a->H) || ndir < 1 || ndir > 2) return hipErrorInvalidValue;
-  if (dtype == 0) return pdrnn::dispatch_step<pdrnn::BF16>(a, ndir, backward != 0, tile, stream);
-  return pdrnn::dispatch_step<pdrnn::F16>(a, ndir, backward != 0, tile, stream);
+  if (a->cell != 0 && a->cell != 1) return hipErrorInvalidValue;
+  const bool bw = backward != 0;
+  if (dtype == 0)
+    return a->cell ? pdrnn::dispatch_step<pdrnn::BF16, 1>(a, ndir, bw, tile, stream)
+                   : pdrnn::dispatch_step<pdrnn::BF16, 0>(a, ndir, bw, tile, stream);
+  return a->cell ? pdrnn::dispatch_step<pdrnn::F16, 1>(a, ndir, bw, tile, stream)
+                 : pdrnn::dispatch_step<pdrnn::F16, 0>(a, ndir, bw, tile, stream);
 }
 
 hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir, int dtype, hipStream_t stream) {
   const int64_t n = (int64_t)a->B * a->H;
   dim3 grid((unsigned)((n + 255) / 256), 1, ndir);
-  if (dtype == 0)
-    hipLaunchKernelGGL(pdrnn::lstm_large_bwd_first_kernel<pdrnn::BF16>, grid, dim3(256), 0, stream, *a);
-  else
-    hipLaunchKernelGGL(pdrnn::lstm_large_bwd_first_kernel<pdrnn::F16>, grid, dim3(256), 0, stream, *a);
+  if (a->cell != 0 && a->cell != 1) return hipErrorInvalidValue;
+  if (dtype == 0) {
+    if (a->cell) hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::BF16, 1>), grid, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::BF16, 0>), grid, dim3(256), 0, stream, *a);
+  } else {
+    if (a->cell) hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::F16, 1>), grid, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::F16, 0>), grid, dim3(256), 0, stream, *a);
+  }
   return hipGetLastError();
 }
 

@@ -65,7 +65,8 @@ class LSTM(nn.LSTM):
 
 
 class GRU(nn.GRU):
-    """``nn.GRU`` whose forward runs on the fused MI355X GRU kernels."""
+    """``nn.GRU`` whose forward runs on the fused MI355X GRU kernels (small H,
+    fp32) or the MFMA step kernels (16-bit, H % 64 == 0, also bidirectional)."""
 
     def _weights(self):
         ws = []
@@ -77,17 +78,27 @@ class GRU(nn.GRU):
         return ws
 
     def forward(self, input, hx: Optional[Tensor] = None):  # type: ignore[override]
-        if isinstance(input, nn.utils.rnn.PackedSequence) or self.bidirectional:
+        if isinstance(input, nn.utils.rnn.PackedSequence):
             return super().forward(input, hx)
+        if self.bidirectional:
+            from ..ops import gru_large
+            if not gru_large.supported(input if input.dim() == 3 else input.unsqueeze(1), self.hidden_size):
+                return super().forward(input, hx)
         unbatched = input.dim() == 2
         if unbatched:
             input = input.unsqueeze(0 if self.batch_first else 1)
             if hx is not None:
                 hx = hx.unsqueeze(1)
-        out, hn = gru_ops.gru_forward(input, self._weights(), hx, hidden=self.hidden_size,
-                                      num_layers=self.num_layers, batch_first=self.batch_first,
-                                      dropout=self.dropout if self.training else 0.0,
-                                      training=self.training)
+        if self.bidirectional:
+            out, hn = gru_large.gru_large_forward(
+                input, [getattr(self, n) for names in self._all_weights for n in names], hx,
+                hidden=self.hidden_size, num_layers=self.num_layers, batch_first=self.batch_first,
+                bidirectional=True, dropout=self.dropout if self.training else 0.0, training=self.training)
+        else:
+            out, hn = gru_ops.gru_forward(input, self._weights(), hx, hidden=self.hidden_size,
+                                          num_layers=self.num_layers, batch_first=self.batch_first,
+                                          dropout=self.dropout if self.training else 0.0,
+                                          training=self.training)
         if unbatched:
             out, hn = out.squeeze(0 if self.batch_first else 1), hn.squeeze(1)
         return out, hn

@@ -1,4 +1,5 @@
-"""GRU stack operator (fused HIP kernel for small hidden sizes, ATen otherwise).
+"""GRU stack operator: fused HIP kernels for small hidden sizes (fp32), the MFMA
+step kernels for 16-bit inputs with H % 64 == 0 (ops/gru_large.py), ATen otherwise.
 
 New capability (BASELINE.json names an "LSTM/GRU cell"; the reference itself
 only uses nn.LSTM).  Gate order and parameters follow nn.GRU
@@ -37,4 +38,8 @@ def gru_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Ten
     if dropout == 0.0 and fused_small_supported(x, hidden, num_layers):
         from .gru_fused import fused_gru
         return fused_gru(x, weights, h0, hidden=hidden, num_layers=num_layers, batch_first=batch_first)
+    from . import gru_large
+    if gru_large.supported(x, hidden):
+        return gru_large.gru_large_forward(x, weights, h0, hidden=hidden, num_layers=num_layers,
+                                           batch_first=batch_first, dropout=dropout, training=training)
     return gru_reference(x, weights, h0, hidden, num_layers, batch_first, dropout, training)

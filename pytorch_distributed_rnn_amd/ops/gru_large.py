@@ -1,0 +1,152 @@
+"""Large-hidden GRU stack on the MFMA step kernels (csrc/kernels/lstm_large.hip,
+CELL = GRU).
+
+New capability: the reference only builds ``nn.LSTM`` (reference:
+src/motion/model.py:9), BASELINE.json names an "LSTM/GRU cell", and the
+small-H GRU already runs on the fused kernels (ops/gru_fused.py).  This is the
+16-bit, H % 64 == 0 counterpart for the shapes the large-H LSTM serves.
+
+The GRU's gates ride on the LSTM step kernels' four-column quad as
+``[r | z | n_x | n_h]`` (the layout of ops/gru_fused.py)::
+
+    W_ih4 = [W_ir; W_iz; W_in; 0]      b4 = [b_ir + b_hr; b_iz + b_hz; b_in; b_hn]
+    W_hh4 = [W_hr; W_hz; 0;    W_hn]
+
+* forward: one library GEMM projects the input of all timesteps and both
+  directions (``Xp = X W_ih4^T + b4``, gate-interleaved columns), then T
+  launches of the MFMA step kernel whose epilogue applies
+  ``r, z = sigma(.)``, ``n = tanh(n_x + r n_h)``, ``h = n + z (h_prev - n)``
+  with ``h_prev`` kept in fp32;
+* backward: T launches of the MFMA BPTT step (``dh_{t-1} = dgates_t W_hh4 +
+  dh_t z_t``) emitting ``dgates = [dr r(1-r) | dz z(1-z) | dpre_n | dpre_n r]``
+  in gate-blocked order, then ``dW_hh``, ``dW_ih``, the biases and ``dX`` as
+  library GEMMs over all timesteps.
+
+The zero blocks cost a quarter of the recurrent MFMA work; in exchange the GRU
+shares every tile configuration, the split-K backward and the numerics tests
+of the LSTM path.  Parameters stay in ``nn.GRU``'s layout (r, z, n).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+from torch import Tensor
+
+from .. import _ext
+from .lstm_large import _interleave, _mm_f32, _perm, _tile
+
+
+def supported(x: Tensor, hidden: int) -> bool:
+    if x.dtype not in (torch.bfloat16, torch.float16) or x.device.type != "cuda" or x.dim() != 3:
+        return False
+    mod = _ext.native(x.device)
+    return mod is not None and hasattr(mod, "lstm_large_fwd") and bool(mod.lstm_large_supported(hidden))
+
+
+def _hprev(hseq_d: Tensor, h0d: Optional[Tensor], d: int) -> Tensor:
+    """h_{t-1} in processing order for direction d ([T, B, H])."""
+    T, B, H = hseq_d.shape
+    h0d = h0d if h0d is not None else hseq_d.new_zeros(1, B, H)
+    return torch.cat([h0d, hseq_d[:-1]], 0) if d == 0 else torch.cat([hseq_d[1:], h0d], 0)
+
+
+class _LargeGRULayer(torch.autograd.Function):
+    """One layer, 1 or 2 directions.  x: [T, B, I] (compute dtype); weights per
+    direction (w_ih, w_hh, b_ih, b_hh), fp32 masters (biases may be None)."""
+
+    @staticmethod
+    def forward(ctx, x, h0, cfg, *weights):
+        H, ndir, tile = cfg
+        cdt = x.dtype
+        T, B, I = x.shape
+        mod = _ext.native(x.device)
+        perm = _perm(H, x.device)
+        wih, whh4, wih4, b4 = [], [], [], []
+        for d in range(ndir):
+            w_ih, w_hh, b_ih, b_hh = weights[4 * d:4 * d + 4]
+            w_ih16, w_hh16 = w_ih.to(cdt), w_hh.to(cdt)
+            wih.append(w_ih16)
+            wih4.append(_interleave(torch.cat([w_ih16, w_ih16.new_zeros(H, I)]), H))
+            whh4.append(torch.cat([w_hh16[:2 * H], w_hh16.new_zeros(H, H), w_hh16[2 * H:]]))
+            b = torch.zeros(4 * H, device=x.device, dtype=torch.float32)
+            if b_ih is not None:
+                b[:3 * H] += b_ih.float()
+            if b_hh is not None:
+                b[:2 * H] += b_hh[:2 * H].float()
+                b[3 * H:] += b_hh[2 * H:].float()
+            b4.append(b[perm])
+        xp = torch.addmm(torch.cat(b4).to(cdt), x.reshape(T * B, I), torch.cat(wih4).t())
+        xp = xp.view(T, B, ndir * 4 * H)
+        whh_p = [_interleave(w, H).contiguous() for w in whh4]
+        h0c = h0.to(cdt).contiguous() if h0 is not None else None
+        h0f = h0.float().contiguous() if h0 is not None else None
+        rev_mask = 2 if ndir == 2 else 0
+        hseq, hs32, acts = mod.lstm_large_fwd(xp, whh_p, h0c, h0f, H, rev_mask, tile, 1)
+        last = [T - 1, 0][:ndir]
+        hn = torch.stack([hseq[last[d], :, d * H:(d + 1) * H] for d in range(ndir)], 0)
+        ctx.save_for_backward(x, hseq, hs32, acts, h0c, h0f, *wih, *whh4)
+        ctx.cfg = (H, ndir, tile, rev_mask, [w is not None for w in weights], h0 is not None,
+                   h0.dtype if h0 is not None else None)
+        return hseq, hn
+
+    @staticmethod
+    def backward(ctx, dhseq, dhn):
+        H, ndir, tile, rev_mask, has_w, has_h0, h0_dtype = ctx.cfg
+        x, hseq, hs32, acts, h0c, h0f, *ws = ctx.saved_tensors
+        wih, whh4 = ws[:ndir], ws[ndir:]
+        cdt = x.dtype
+        T, B, I = x.shape
+        mod = _ext.native(x.device)
+        dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
+        dhn_f = dhn.float().contiguous() if dhn is not None else None
+        wt = [w.t().contiguous() for w in whh4]                     # [H, 4H], gate-blocked
+        dgates, dh0, _ = mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1)
+        grads: List[Optional[Tensor]] = []
+        dx = None
+        x2 = x.reshape(T * B, I)
+        for d in range(ndir):
+            G = dgates[d].view(T * B, 4 * H)                         # [r | z | dpre_n | dpre_n r]
+            hprev = _hprev(hseq[:, :, d * H:(d + 1) * H], h0c[d:d + 1] if h0c is not None else None, d)
+            dw4 = _mm_f32(G.t(), hprev.reshape(T * B, H))
+            dwhh = torch.cat([dw4[:2 * H], dw4[3 * H:]])
+            Gx = G[:, :3 * H]                                        # x side: [r | z | dpre_n]
+            dwih = _mm_f32(Gx.t(), x2)
+            cs = G.sum(0, dtype=torch.float32)
+            dbih = cs[:3 * H]
+            dbhh = torch.cat([cs[:2 * H], cs[3 * H:]])
+            if dx is None:
+                dx = torch.mm(Gx, wih[d])
+            else:
+                dx.addmm_(Gx, wih[d])
+            grads += [dwih, dwhh, dbih if has_w[4 * d + 2] else None, dbhh if has_w[4 * d + 3] else None]
+        dh0_out = dh0.to(h0_dtype) if has_h0 else None
+        return (dx.view(T, B, I), dh0_out, None, *grads)
+
+
+def gru_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor], *, hidden: int,
+                      num_layers: int, batch_first: bool, bidirectional: bool = False, dropout: float = 0.0,
+                      training: bool = False) -> Tuple[Tensor, Tensor]:
+    """Stacked (bi)GRU on the MFMA step kernels; ``nn.GRU``-compatible outputs.
+
+    ``weights``: ``nn.GRU`` ``_all_weights`` order (per layer and direction
+    w_ih, w_hh[, b_ih, b_hh])."""
+    ndir = 2 if bidirectional else 1
+    per = len(weights) // (num_layers * ndir)
+    seq = (x.transpose(0, 1) if batch_first else x).contiguous()
+    tile = _tile()
+    hns = []
+    for l in range(num_layers):
+        ws: List[Optional[Tensor]] = []
+        for d in range(ndir):
+            chunk = list(weights[(l * ndir + d) * per:(l * ndir + d + 1) * per])
+            if per == 2:
+                chunk += [None, None]
+            ws += chunk
+        h0l = h0[l * ndir:(l + 1) * ndir] if h0 is not None else None
+        seq, hn = _LargeGRULayer.apply(seq, h0l, (hidden, ndir, tile), *ws)
+        hns.append(hn)
+        if dropout > 0 and training and l < num_layers - 1:
+            seq = torch.nn.functional.dropout(seq, dropout, True)
+    out = seq.transpose(0, 1) if batch_first else seq
+    return out, torch.cat(hns, 0)

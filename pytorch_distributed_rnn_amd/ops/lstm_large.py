@@ -100,7 +100,7 @@ class _LargeLSTMLayer(torch.autograd.Function):
         h0c = h0.to(cdt).contiguous() if h0 is not None else None
         c0c = c0.float().contiguous() if c0 is not None else None
         rev_mask = 2 if ndir == 2 else 0
-        hseq, cseq, acts = mod.lstm_large_fwd(xp, whh_p, h0c, c0c, H, rev_mask, tile)
+        hseq, cseq, acts = mod.lstm_large_fwd(xp, whh_p, h0c, c0c, H, rev_mask, tile, 0)
         last = [T - 1, 0][:ndir]
         hn = torch.stack([hseq[last[d], :, d * H:(d + 1) * H] for d in range(ndir)], 0)
         cn = torch.stack([cseq[d, last[d]] for d in range(ndir)], 0)
@@ -124,7 +124,7 @@ class _LargeLSTMLayer(torch.autograd.Function):
         dhn_f = dhn.float().contiguous() if dhn is not None else None
         dcn_f = dcn.float().contiguous() if dcn is not None else None
         wt = [w.t().contiguous() for w in whh]                      # [H, 4H], gate-blocked
-        dgates, dh0, dc0 = mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile)
+        dgates, dh0, dc0 = mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile, 0)
         grads: List[Optional[Tensor]] = []
         dx = None
         x2 = x.reshape(T * B, I)
@@ -135,9 +135,11 @@ class _LargeLSTMLayer(torch.autograd.Function):
             hprev = torch.cat([h0d, hd[:-1]], 0) if d == 0 else torch.cat([hd[1:], h0d], 0)
             dwhh = _mm_f32(G.t(), hprev.reshape(T * B, H))
             dwih = _mm_f32(G.t(), x2)
-            db = G.float().sum(0)
-            part = torch.mm(G, wih[d])
-            dx = part if dx is None else dx + part
+            db = G.sum(0, dtype=torch.float32)  # fp32 accumulation, no fp32 copy of G
+            if dx is None:
+                dx = torch.mm(G, wih[d])
+            else:
+                dx.addmm_(G, wih[d])
             grads += [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
         dx = dx.view(T, B, I)
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
