@@ -22,6 +22,7 @@ SONAME), so there is exactly one HIP runtime and one RCCL in the process.
 Usage::
 
     python -m pytorch_distributed_rnn_amd._build          # incremental
+    PDRNN_DEBUG_BUILD=1 python -m pytorch_distributed_rnn_amd._build   # -O1 -g + device asserts
     python -m pytorch_distributed_rnn_amd._build --clean  # full rebuild
 """
 from __future__ import annotations
@@ -100,14 +101,17 @@ def build(verbose: bool = False, clean: bool = False, jobs: int | None = None) -
     hipcc = ROCM / "bin" / "hipcc"
     py_inc = sysconfig.get_paths()["include"]
     common_inc = [f"-I{CSRC / 'include'}"]
+    debug = os.environ.get("PDRNN_DEBUG_BUILD", "0") == "1"
+    hip_opt = ["-O1", "-g", "-DPDRNN_DEBUG=1"] if debug else ["-O3"]
+    host_opt = ["-O0", "-g", "-DPDRNN_DEBUG=1"] if debug else ["-O2"]
     hip_flags = [
-        "-c", "-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
+        "-c", *hip_opt, "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
         "-munsafe-fp-atomics", "-Wno-unused-result", *common_inc,
         # diagnostics only (e.g. -DPDRNN_ABLATE=N timing ablations); part of the build signature
         *os.environ.get("PDRNN_HIP_EXTRA_FLAGS", "").split(),
     ]
     host_flags = [
-        "-c", "-O2", "-fPIC", "-fvisibility=hidden", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+        "-c", *host_opt, "-fPIC", "-fvisibility=hidden", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
         f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
         "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-deprecated-declarations",
         *common_inc, *[f"-I{p}" for p in inc], f"-I{ROCM / 'include'}", f"-I{py_inc}",

@@ -10,7 +10,8 @@ so fabfile-style command lines keep working:
     torchrun --nproc-per-node 8 main.py ... horovod
     main.py ... parameter-server --world-size 3 --rank 0
 
-Additions (all optional): ``--synthetic``, ``--cell {lstm,gru}``,
+Additions (all optional): ``--synthetic``, ``--cell {lstm,gru}``, ``--dtype
+{fp32,bf16,fp16}``, ``--bidirectional``, ``--trace`` / ``--profile DIR``,
 ``--backend``, ``--bucket-mb``, ``--kernel {hip,torch}``, ``--resume``,
 ``--checkpoint-every``, ``--log-interval``, ``--weak-scaling``,
 ``--fault-delay-ms`` / ``--fault-rank`` (network fault injection stand-in for
@@ -57,8 +58,14 @@ def build_parser(script_dir: Optional[Path] = None) -> argparse.ArgumentParser:
                    help="train on generated UCI-HAR-shaped data (also used when no data is found)")
     p.add_argument("--synthetic-size", default=6912, type=int)
     p.add_argument("--cell", choices=("lstm", "gru"), default="lstm")
-    p.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
-                   help="bf16: bf16 inputs and recurrent weights, fp32 accumulation / masters")
+    p.add_argument("--dtype", choices=("fp32", "bf16", "fp16"), default="fp32",
+                   help="bf16/fp16: 16-bit inputs and recurrent weights, fp32 accumulation / masters")
+    p.add_argument("--bidirectional", action="store_true",
+                   help="bidirectional recurrent stack (head reads out[:, -1, :])")
+    p.add_argument("--trace", action="store_true",
+                   help="roctx / torch.profiler ranges around forward, backward, all-reduce, optimizer")
+    p.add_argument("--profile", default=None, type=Path,
+                   help="torch.profiler capture of the training run into this directory")
     p.add_argument("--backend", default=None, help="nccl|rccl|gloo|mpi (default: RCCL on GPU, gloo on CPU)")
     p.add_argument("--bucket-mb", default=None, type=float)
     p.add_argument("--kernel", choices=("hip", "torch"), default="hip")
@@ -109,6 +116,9 @@ def _apply_common(args) -> None:
     if args.fault_delay_ms > 0:
         from .utils import faults
         faults.configure(delay_ms=args.fault_delay_ms, rank=args.fault_rank)
+    if args.trace:
+        from .utils import tracing
+        tracing.enable(True)
 
 
 def train(args, name: str):
@@ -127,8 +137,8 @@ def train(args, name: str):
     from .models.motion import MotionModel
     model = MotionModel(input_dim=training_set.num_features, hidden_dim=args.hidden_units,
                         layer_dim=args.stacked_layer, output_dim=len(MotionDataset.LABELS),
-                        cell=args.cell,
-                        compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
+                        cell=args.cell, bidirectional=args.bidirectional,
+                        compute_dtype={"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype, torch.float32))
     trainer_cls = _trainer_class(name)
     kw = dict(model=model, training_set=training_set, validation_set=validation_set,
               test_set=test_set, batch_size=args.batch_size, learning_rate=args.learning_rate,
@@ -149,8 +159,10 @@ def train(args, name: str):
         nxt = trainer.resume(args.resume)
         logging.info(f"Resumed from {args.resume} (continuing at epoch {nxt})")
     logging.info(f"Training model for {args.epochs} epochs...")
-    _, train_history, validation_history = trainer.train(epochs=args.epochs)
     rank = getattr(trainer, "rank", 0)
+    from .utils import tracing
+    with tracing.profile(args.profile, rank):
+        _, train_history, validation_history = trainer.train(epochs=args.epochs)
     if rank == 0:
         with open(args.history_file, "w") as f:
             json.dump({"train_history": train_history, "validation_history": validation_history}, f)

@@ -9,6 +9,20 @@
 #include <stdint.h>
 
 #define PDRNN_HOST_DEVICE __host__ __device__
+
+// Debug flavour (PDRNN_DEBUG_BUILD=1 python -m pytorch_distributed_rnn_amd._build):
+// -O1 -g and device-side bounds asserts on data-dependent indices (token ids,
+// labels).  A failing assert aborts the kernel with file:line on stderr --
+// the on-GPU replacement for a sanitizer run, which this pool does not offer.
+#ifndef PDRNN_DEBUG
+#define PDRNN_DEBUG 0
+#endif
+#if PDRNN_DEBUG
+#include <cassert>
+#define PDRNN_DEVICE_ASSERT(cond) assert(cond)
+#else
+#define PDRNN_DEVICE_ASSERT(cond) ((void)0)
+#endif
 #define PDRNN_DEVICE __device__ __forceinline__
 
 namespace pdrnn {

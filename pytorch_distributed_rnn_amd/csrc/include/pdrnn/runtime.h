@@ -43,7 +43,18 @@ class Comm {
   // collective issued so far.
   virtual void wait() = 0;
   virtual void barrier() = 0;
+  // all_reduce whose result is ordered into the caller's current stream, for
+  // call sites with nothing to overlap (the fused motion step): RCCL runs
+  // straight on that stream, no cross-stream event hops.
+  virtual void all_reduce_inline(at::Tensor& t, RedOp op) {
+    all_reduce(t, op);
+    wait();
+  }
 };
+
+// PDRNN_SERIALIZE_COMM=1: every collective completes (device-synchronised)
+// before the call returns -- A/B switch for overlap / stream-ordering bugs.
+bool serialize_comm();
 
 std::shared_ptr<Comm> make_rccl_comm(const std::string& uid, int rank, int world, int device, bool high_priority);
 std::shared_ptr<Comm> make_pg_comm(const pybind11::object& process_group);

@@ -22,6 +22,7 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(const float* __restrict__ 
   for (int64_t r = wave; r < n; r += nwaves) {
     int64_t v = idx[r];
     if (v < 0) v += V;
+    PDRNN_DEVICE_ASSERT(v >= 0 && v < V);
     const float* src = w + v * dim;
     float* dst = out + r * dim;
     if (vec) {
@@ -46,6 +47,7 @@ __global__ void __launch_bounds__(256) emb_fwd16_kernel(const float* __restrict_
   for (int64_t r = wave; r < n; r += nwaves) {
     int64_t v = idx[r];
     if (v < 0) v += V;
+    PDRNN_DEVICE_ASSERT(v >= 0 && v < V);
     const float* src = w + v * dim;
     uint16_t* dst = out + r * dim;
     for (int64_t c = lane; c < dim; c += 64) {

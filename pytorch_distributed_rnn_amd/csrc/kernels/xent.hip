@@ -37,6 +37,7 @@ __global__ void __launch_bounds__(kThreads) xent_rows_kernel(PdrnnXentArgs a, in
   for (int64_t row = row0 + wave; row < row1; row += kWavesPerBlock) {
     const T* x = logits + row * a.ld;
     const int64_t label = a.labels[row];
+    PDRNN_DEVICE_ASSERT(label == a.ignore_index || (label >= 0 && label < a.C));
     // pass 1: max + first argmax
     float m = -INFINITY;
     int64_t am = a.C;

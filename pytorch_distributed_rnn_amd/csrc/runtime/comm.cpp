@@ -145,10 +145,21 @@ class RcclComm final : public Comm {
     NCCL_CHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, stream_));
     leave({t});
   }
+  void all_reduce_inline(at::Tensor& t, RedOp op) override {
+    check(t);
+    // keep this communicator's collectives strictly ordered: join any still
+    // queued on the comm stream first
+    if (pending_) wait();
+    c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
+    hipStream_t cs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_).stream();
+    NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl(op), comm_, cs));
+    if (serialize_comm()) HIP_CHECK(hipStreamSynchronize(cs));
+  }
   void wait() override {
     c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     HIP_CHECK(hipEventRecord(ev_out_, stream_));
     HIP_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_).stream(), ev_out_, 0));
+    pending_ = false;
   }
   void barrier() override {
     auto t = at::zeros({1}, at::TensorOptions().device(at::kCUDA, device_).dtype(at::kFloat));
@@ -165,6 +176,7 @@ class RcclComm final : public Comm {
   }
   // Order the comm stream after everything enqueued on the caller's stream.
   void enter() {
+    pending_ = true;
     c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     HIP_CHECK(hipEventRecord(ev_in_, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_).stream()));
     HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
@@ -174,18 +186,24 @@ class RcclComm final : public Comm {
     for (const auto& t : ts)
       if (t.defined() && t.storage().data_ptr().get())
         c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), s);
+    if (serialize_comm()) HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
   int rank_, world_, device_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  bool pending_ = false;  // collectives on stream_ not yet joined by wait()
 };
 
 // c10d adapter: drives torch.distributed collectives (gloo on CPU, or torch's
 // own RCCL process group) through Python.  Used for the CPU plumbing path and
 // as a fallback; async work handles are waited in wait().
 class ProcessGroupComm final : public Comm {
+  void maybe_serialize() {
+    if (serialize_comm()) wait();
+  }
+
  public:
   explicit ProcessGroupComm(py::object pg) : pg_(std::move(pg)) {
     py::gil_scoped_acquire gil;
@@ -202,16 +220,19 @@ class ProcessGroupComm final : public Comm {
     py::gil_scoped_acquire gil;
     works_.push_back(dist_.attr("all_reduce")(t, py::arg("op") = pyop(op), py::arg("group") = pg_,
                                                py::arg("async_op") = true));
+    maybe_serialize();
   }
   void broadcast(at::Tensor& t, int root) override {
     py::gil_scoped_acquire gil;
     const int groot = dist_.attr("get_global_rank")(pg_, root).cast<int>();
     works_.push_back(dist_.attr("broadcast")(t, py::arg("src") = groot, py::arg("group") = pg_,
                                               py::arg("async_op") = true));
+    maybe_serialize();
   }
   void all_gather(at::Tensor& out, const at::Tensor& in) override {
     py::gil_scoped_acquire gil;
     works_.push_back(dist_.attr("all_gather_into_tensor")(out, in, py::arg("group") = pg_, py::arg("async_op") = true));
+    maybe_serialize();
   }
   void reduce_scatter(at::Tensor& out, const at::Tensor& in, RedOp op) override {
     py::gil_scoped_acquire gil;
@@ -224,10 +245,12 @@ class ProcessGroupComm final : public Comm {
     }
     works_.push_back(dist_.attr("reduce_scatter_tensor")(out, in, py::arg("op") = pyop(op), py::arg("group") = pg_,
                                                          py::arg("async_op") = true));
+    maybe_serialize();
   }
   void all_to_all(at::Tensor& out, const at::Tensor& in) override {
     py::gil_scoped_acquire gil;
     works_.push_back(dist_.attr("all_to_all_single")(out, in, py::arg("group") = pg_, py::arg("async_op") = true));
+    maybe_serialize();
   }
   void send(const at::Tensor& t, int peer) override {
     py::gil_scoped_acquire gil;
@@ -268,6 +291,14 @@ class ProcessGroupComm final : public Comm {
 };
 
 }  // namespace
+
+bool serialize_comm() {
+  static const bool on = [] {
+    const char* e = std::getenv("PDRNN_SERIALIZE_COMM");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
 
 std::string rccl_unique_id() {
   ncclUniqueId id;

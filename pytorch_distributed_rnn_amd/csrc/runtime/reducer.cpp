@@ -158,6 +158,14 @@ class GradReducer {
       for (auto& f : buckets_) f.div_((double)comm_->world());
   }
 
+  // Same, each bucket reduced straight on the caller's stream (nothing to
+  // overlap: the fused motion step produces every gradient in one kernel).
+  void all_reduce_inline() {
+    for (size_t b = 0; b < buckets_.size(); ++b) comm_->all_reduce_inline(buckets_[b], op());
+    if (average_ && !comm_->native_avg() && comm_->world() > 1)
+      for (auto& f : buckets_) f.div_((double)comm_->world());
+  }
+
   int64_t launched() const { return launched_; }
 
  private:
@@ -311,6 +319,8 @@ void register_runtime(py::module_& m) {
       .def("all_to_all", [](Comm& c, at::Tensor out, const at::Tensor& in) { c.all_to_all(out, in); })
       .def("send", &Comm::send)
       .def("recv", [](Comm& c, at::Tensor t, int peer) { c.recv(t, peer); })
+      .def("all_reduce_inline", [](Comm& c, at::Tensor t, const std::string& op) { c.all_reduce_inline(t, parse_op(op)); },
+           py::arg("tensor"), py::arg("op") = "sum")
       .def("wait", &Comm::wait)
       .def("barrier", &Comm::barrier);
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
@@ -331,6 +341,7 @@ void register_runtime(py::module_& m) {
       .def("reset", &GradReducer::reset)
       .def("zero_", &GradReducer::zero_)
       .def("all_reduce_now", &GradReducer::all_reduce_now)
+      .def("all_reduce_inline", &GradReducer::all_reduce_inline)
       .def_property_readonly("launched", &GradReducer::launched);
 
   py::class_<FusionReducer, std::shared_ptr<FusionReducer>>(m, "FusionReducer")

@@ -50,6 +50,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--history-file", default=None)
     p.add_argument("--checkpoint-directory", default=None, help="save <dir>/charlm-epoch<k>.pt after every epoch")
     p.add_argument("--resume", default=None, help="checkpoint to continue from")
+    p.add_argument("--trace", action="store_true", help="roctx / torch.profiler ranges around step phases")
+    p.add_argument("--profile", default=None, help="torch.profiler capture of the run into this directory")
     p.add_argument("mode", choices=("local", "distributed"))
     return p
 
@@ -68,12 +70,16 @@ def main(argv=None):
                         bucket_cap_mb=args.bucket_mb, weak_scaling=args.weak_scaling)
     start = trainer.resume(args.resume) if args.resume else 0
     history = []
-    for e in range(start, start + args.epochs):
-        h = trainer.train_epoch(e, args.max_steps)
-        history.append(h)
-        if args.checkpoint_directory:
-            from pathlib import Path
-            trainer.save(Path(args.checkpoint_directory) / f"charlm-epoch{e}.pt", e, h["loss"])
+    from .utils import tracing
+    if args.trace:
+        tracing.enable(True)
+    with tracing.profile(args.profile, trainer.rank):
+        for e in range(start, start + args.epochs):
+            h = trainer.train_epoch(e, args.max_steps)
+            history.append(h)
+            if args.checkpoint_directory:
+                from pathlib import Path
+                trainer.save(Path(args.checkpoint_directory) / f"charlm-epoch{e}.pt", e, h["loss"])
     if trainer.rank == 0 and args.history_file:
         with open(args.history_file, "w") as f:
             json.dump(history, f)

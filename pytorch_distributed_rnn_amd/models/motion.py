@@ -27,8 +27,10 @@ class MotionModel(nn.Module):
     supports_index_batches = True
 
     def __init__(self, input_dim: int, hidden_dim: int, layer_dim: int, output_dim: int,
-                 cell: str = "lstm", dropout: float = 0.0, compute_dtype: torch.dtype = torch.float32):
+                 cell: str = "lstm", dropout: float = 0.0, compute_dtype: torch.dtype = torch.float32,
+                 bidirectional: bool = False):
         super().__init__()
+        self.bidirectional = bidirectional
         # bf16: inputs and recurrent weights in bf16 storage, fp32 accumulation,
         # cell state and master weights (BASELINE config 2)
         self.compute_dtype = compute_dtype
@@ -37,12 +39,20 @@ class MotionModel(nn.Module):
         self.cell = cell
         rnn_cls = {"lstm": LSTM, "gru": GRU}[cell]
         # attribute name kept as `lstm` for checkpoint compatibility
-        self.lstm = rnn_cls(input_dim, hidden_dim, layer_dim, batch_first=True, dropout=dropout)
-        self.fc = nn.Linear(hidden_dim, output_dim)
+        self.lstm = rnn_cls(input_dim, hidden_dim, layer_dim, batch_first=True, dropout=dropout,
+                            bidirectional=bidirectional)
+        # bidirectional (extension): the head reads out[:, -1, :] = [h_fwd(T-1), h_bwd(T-1)]
+        self.fc = nn.Linear(hidden_dim * (2 if bidirectional else 1), output_dim)
 
     def forward(self, x: Tensor, idx: Optional[Tensor] = None) -> Tensor:
         if self.compute_dtype != torch.float32 and x.dtype != self.compute_dtype:
             x = x.to(self.compute_dtype)
+        if self.bidirectional:
+            if idx is not None:
+                x = x.index_select(0, idx)
+            out, _ = self.lstm(x)
+            h = out[:, -1, :]
+            return self.fc(h if h.dtype == self.fc.weight.dtype else h.to(self.fc.weight.dtype))
         if self.cell == "lstm":
             _, (hn, _) = self.lstm(x, need_out=False, idx=idx)
         else:

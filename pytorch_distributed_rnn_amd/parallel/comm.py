@@ -39,6 +39,10 @@ class _PyComm:
              "min": dist.ReduceOp.MIN}[op]
         self._works.append(dist.all_reduce(t, op=o, group=self.group, async_op=True))
 
+    def all_reduce_inline(self, t, op="sum"):
+        self.all_reduce(t, op)
+        self.wait()
+
     def broadcast(self, t, root):
         self._works.append(dist.broadcast(t, dist.get_global_rank(self.group, root), group=self.group,
                                           async_op=True))

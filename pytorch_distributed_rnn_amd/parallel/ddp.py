@@ -32,6 +32,7 @@ from torch import nn
 
 from .. import _ext
 from ..utils.flat import FlatParameters
+from ..utils.tracing import trace_range
 from .comm import get_comm
 
 DEFAULT_BUCKET_MB = float(os.environ.get("PDRNN_BUCKET_MB", 32))
@@ -72,6 +73,11 @@ class _PyReducer:
 
     def reset(self):
         self.ready = [False] * len(self.params)
+
+    def all_reduce_now(self):
+        self.finalize()
+
+    all_reduce_inline = all_reduce_now
 
 
 class DistributedDataParallel(nn.Module):
@@ -140,7 +146,8 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._finalize_queued = False
-        self.reducer.finalize()
+        with trace_range("pdrnn.grad_allreduce"):
+            self.reducer.finalize()
 
     # -------------------------------------------------------------- api
     def forward(self, *args, **kwargs):

@@ -20,6 +20,7 @@ the weak-scaling benchmark).
 from __future__ import annotations
 
 import logging
+import os
 from typing import Optional
 
 import torch
@@ -86,10 +87,14 @@ class DDPTrainer(DistributedTrainer):
                          checkpoint_dir=checkpoint_dir, device=device, **kwargs)
 
     def _grad_sync(self):
+        # the fused step has nothing to overlap the all-reduce with (every
+        # gradient comes out of one reduction kernel): reduce inline on the
+        # compute stream.  PDRNN_FORCE_GRAD_SYNC=1 keeps the sync at world 1
+        # (diagnostic: the multi-GPU step's launch sequence on one GPU).
         reducer = self.model.reducer
-        if self._world_size == 1:
+        if self._world_size == 1 and os.environ.get("PDRNN_FORCE_GRAD_SYNC", "0") != "1":
             return None
-        return reducer.all_reduce_now
+        return reducer.all_reduce_inline
 
     @staticmethod
     def _device() -> torch.device:

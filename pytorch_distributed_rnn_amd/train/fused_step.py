@@ -29,6 +29,7 @@ from torch import Tensor, nn
 
 from .. import _ext
 from ..utils.flat import contiguous_span
+from ..utils.tracing import trace_range
 
 
 def _inner(model: nn.Module) -> nn.Module:
@@ -102,11 +103,15 @@ class MotionTrainStep:
         r = self.flat.data.to(torch.bfloat16).float()
         return [r[o:o + int(torch.Size(s).numel())].view(s) for o, s in self._offs]
 
-    def _fused_adam(self):
-        """(state, hyper-parameters) when Adam can run inside the reduction tail."""
+    def _flat_adam(self):
+        """(state, hyper-parameters) when the optimizer is a plain single-group
+        FusedAdam over exactly the model's flat buffer: the step then runs as
+        one native launch on the cached flat state (inside the reduction tail
+        for a single process, or right after the gradient all-reduce) instead
+        of going through ``optimizer.step()``.  Advances the step count."""
         from ..ops.adam import FusedAdam
         opt = self.optimizer
-        if self.grad_sync is not None or type(opt) is not FusedAdam or len(opt.param_groups) != 1:
+        if type(opt) is not FusedAdam or len(opt.param_groups) != 1:
             return None
         g = opt.param_groups[0]
         if g.get("amsgrad") or g.get("maximize") or opt._pdrnn_grad_scale != 1.0:
@@ -135,14 +140,23 @@ class MotionTrainStep:
             ws = self.weights
         stats = self.ring[self._slot]
         self._slot = (self._slot + 1) % self.RING
-        fused = self._fused_adam()
-        if fused is not None:
-            self.mod.lstm_head_train_step(features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H,
-                                          self.NL, 0, 0, nb_fwd, nb_bwd, fused[0], fused[1])
+        adam = self._flat_adam()
+        if adam is not None and self.grad_sync is None:
+            with trace_range("pdrnn.fwd_bwd_adam"):
+                self.mod.lstm_head_train_step(features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H,
+                                              self.NL, 0, 0, nb_fwd, nb_bwd, adam[0], adam[1])
             return stats
-        self.mod.lstm_head_train_step(
-            features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd)
+        with trace_range("pdrnn.fwd_bwd"):
+            self.mod.lstm_head_train_step(
+                features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd)
         if self.grad_sync is not None:
-            self.grad_sync()
-        self.optimizer.step()
+            with trace_range("pdrnn.grad_allreduce"):
+                self.grad_sync()
+        with trace_range("pdrnn.optimizer"):
+            if adam is not None:
+                (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
+                self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step, 1.0, bool(dec), False,
+                                   None, None)
+            else:
+                self.optimizer.step()
         return stats

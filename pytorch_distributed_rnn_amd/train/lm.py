@@ -26,6 +26,7 @@ from ..parallel import env
 from ..parallel.ddp import DistributedDataParallel
 from ..utils.flat import flatten_module
 from ..utils.memory import device_peak_mib
+from ..utils.tracing import trace_range
 
 
 class LMTrainer:
@@ -66,11 +67,14 @@ class LMTrainer:
 
     def train_step(self, inp: Tensor, tgt: Tensor) -> Tensor:
         self.optimizer.zero_grad()
-        logits = self.model(inp, carry=True)                                   # [T, B, V]
-        loss = cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt.t().reshape(-1))
-        loss.backward()
-        self._clip()
-        self.optimizer.step()
+        with trace_range("pdrnn.forward"):
+            logits = self.model(inp, carry=True)                               # [T, B, V]
+            loss = cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt.t().reshape(-1))
+        with trace_range("pdrnn.backward"):
+            loss.backward()
+        with trace_range("pdrnn.optimizer"):
+            self._clip()
+            self.optimizer.step()
         return loss.detach()
 
     def train_epoch(self, epoch: int = 0, max_steps: Optional[int] = None) -> Dict[str, float]:

@@ -37,6 +37,7 @@ from ..ops.adam import FusedAdam
 from ..ops.xent import CrossEntropyLoss
 from ..utils import memory as mem
 from ..utils.flat import flatten_module
+from ..utils.tracing import trace_range
 from . import checkpoint as ckpt
 from .formatter import TrainingMessageFormatter
 
@@ -174,12 +175,15 @@ class Trainer:
             data, labels = batch
             return fused(data, labels.reshape(-1).contiguous(), None), labels.shape[0]
         self.optimizer.zero_grad()
-        output, labels = self._forward(batch)
-        labels = labels.long().reshape(-1)
-        loss = self.loss_fn(output, labels)
-        stats = self.loss_fn.last_stats
-        loss.backward()
-        self.optimizer.step()
+        with trace_range("pdrnn.forward"):
+            output, labels = self._forward(batch)
+            labels = labels.long().reshape(-1)
+            loss = self.loss_fn(output, labels)
+            stats = self.loss_fn.last_stats
+        with trace_range("pdrnn.backward"):
+            loss.backward()
+        with trace_range("pdrnn.optimizer"):
+            self.optimizer.step()
         return stats, labels.shape[0]
 
     def _train_step(self, formatter: TrainingMessageFormatter):

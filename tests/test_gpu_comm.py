@@ -55,9 +55,14 @@ def test_rccl_comm_collectives(rccl_group):
     c.wait()
     torch.testing.assert_close(rs, x)
     c.barrier()
+    z = x.clone()
+    c.all_reduce(z, "sum")        # queued on the comm stream ...
+    c.all_reduce_inline(z, "avg")  # ... joined before the inline one (same communicator)
+    torch.testing.assert_close(z, x)
 
 
-def test_ddp_reducer_rccl_step_matches_local(rccl_group):
+@pytest.mark.parametrize("mode", ["all_reduce_now", "all_reduce_inline"])
+def test_ddp_reducer_rccl_step_matches_local(rccl_group, mode):
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
@@ -74,7 +79,7 @@ def test_ddp_reducer_rccl_step_matches_local(rccl_group):
     o1 = FusedAdam(m1.parameters(), lr=2.5e-3)
     flatten_module(m2)
     o2 = FusedAdam(m2.parameters(), lr=2.5e-3)
-    s1 = MotionTrainStep(ddp, o1, ddp.reducer.all_reduce_now)   # RCCL all-reduce in the step
+    s1 = MotionTrainStep(ddp, o1, getattr(ddp.reducer, mode))   # RCCL all-reduce in the step
     s2 = MotionTrainStep(m2, o2, None)                           # local, Adam fused into the reduction
     for i in range(3):
         idx = torch.arange(i * 64, (i + 1) * 64, device="cuda")
