@@ -1,0 +1,43 @@
+"""World > 1 on the GPU path, rehearsed on one MI355X: two ranks share cuda:0
+over the gloo backend (RCCL refuses two ranks on one device; the driver's
+8-GPU run covers RCCL with distinct devices).  This exercises the fused
+multi-rank step the 2/4/8-GPU benchmark runs -- fused LSTM forward + BPTT on
+each rank's shard, gradient all-reduce through the native communicator,
+flat Adam -- and checks the reference's correctness oracle: the
+mean over ranks of the per-step loss equals the single-process loss."""
+import os
+import sys
+
+import pytest
+
+from _mp import ROOT, batch_losses, free_port, run
+
+pytestmark = pytest.mark.gpu
+
+MAIN = os.path.join(ROOT, "src", "motion", "main.py")
+COMMON = ["--seed", "1", "--epochs", "1", "--batch-size", "480", "--no-validation", "--synthetic",
+          "--synthetic-size", "960", "--log-interval", "1"]
+
+
+def _gpu_env(extra=None):
+    env = dict(os.environ)
+    env.update({"MASTER_ADDR": "127.0.0.1", "OMP_NUM_THREADS": "1",
+                "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "PDRNN_FORCE_CPU"):
+        env.pop(k, None)
+    env.update(extra or {})
+    return env
+
+
+@pytest.mark.parametrize("mode", ["distributed", "horovod"])
+def test_two_ranks_one_gpu_match_single_process(tmp_path, mode):
+    local = batch_losses(run([sys.executable, MAIN] + COMMON + ["local"], cwd=str(tmp_path), env=_gpu_env(),
+                             timeout=110))[0]
+    out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={free_port()}", MAIN] + COMMON + [mode],
+              cwd=str(tmp_path), env=_gpu_env({"PDRNN_BACKEND": "gloo"}), timeout=110)
+    per = batch_losses(out)
+    assert sorted(per) == [0, 1] and len(per[0]) == len(local) == 2
+    mean = [(a + b) / 2 for a, b in zip(per[0], per[1])]
+    for a, b in zip(mean, local):
+        assert abs(a - b) < 1e-5, (mean, local)
