@@ -341,6 +341,82 @@ __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B,
   d.dc_carry[bu] = next;
 }
 
+// cell_bwd_elem for 8 consecutive units u0 .. u0+7 of row b (u0 % 8 == 0):
+// the same math with 16-byte accesses.  dh: the recurrent dh of the 8 units.
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+}
+__device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+template <class DT, int CELL>
+__device__ __forceinline__ void cell_bwd_vec8(const PdrnnLstmLargeDir& d, int B, int H, int T, bool rev, int tn,
+                                              bool cell, int b, int u0, float (&dh)[8]) {
+  const int64_t bu = (int64_t)b * H + u0;
+  float carry[8];
+  ld8(d.dc_carry + bu, carry);
+  if constexpr (CELL == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dh[k] += carry[k];
+  }
+  if (!cell) {
+    if (d.dh0) st8(d.dh0 + bu, dh);
+    if (CELL == 0 && d.dc0) st8(d.dc0 + bu, carry);
+    return;
+  }
+  if (d.dout) {
+    const uint4 dv = *reinterpret_cast<const uint4*>(d.dout + (int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u0);
+    const uint16_t* dh16 = reinterpret_cast<const uint16_t*>(&dv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dh[k] += DT::to_f(dh16[k]);
+  }
+  uint4 av[4];
+  const uint4* ap = reinterpret_cast<const uint4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) av[q] = ap[q];
+  const uint16_t* a16 = reinterpret_cast<const uint16_t*>(av);  // unit k: a16[4k .. 4k+3]
+  const int tpp = rev ? tn + 1 : tn - 1;
+  const bool has_prev = rev ? tpp < T : tpp >= 0;
+  float sp[8];
+  if (has_prev) ld8(d.cseq + (int64_t)tpp * B * H + bu, sp);
+  else if (d.c0) ld8(d.c0 + bu, sp);
+  else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sp[k] = 0.f;
+  }
+  float cur[8];
+  if constexpr (CELL == 0) ld8(d.cseq + (int64_t)tn * B * H + bu, cur);
+  uint16_t g[4][8];
+  float next[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float a0 = DT::to_f(a16[4 * k]), a1 = DT::to_f(a16[4 * k + 1]);
+    const float a2 = DT::to_f(a16[4 * k + 2]), a3 = DT::to_f(a16[4 * k + 3]);
+    if constexpr (CELL == 0) {
+      const float tc = tanh_(cur[k]);
+      const float dc = fmaf(dh[k] * a3, 1.f - tc * tc, carry[k]);
+      g[0][k] = DT::from_f(dc * a2 * a0 * (1.f - a0));
+      g[1][k] = DT::from_f(dc * sp[k] * a1 * (1.f - a1));
+      g[2][k] = DT::from_f(dc * a0 * (1.f - a2 * a2));
+      g[3][k] = DT::from_f(dh[k] * tc * a3 * (1.f - a3));
+      next[k] = dc * a1;
+    } else {
+      const float dpn = dh[k] * (1.f - a1) * (1.f - a2 * a2);
+      g[0][k] = DT::from_f(dpn * a3 * a0 * (1.f - a0));
+      g[1][k] = DT::from_f(dh[k] * (sp[k] - a2) * a1 * (1.f - a1));
+      g[2][k] = DT::from_f(dpn);
+      g[3][k] = DT::from_f(dpn * a0);
+      next[k] = dh[k] * a1;
+    }
+  }
+  uint16_t* dgp = d.dgates + ((int64_t)tn * B + b) * 4 * H + u0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) *reinterpret_cast<uint4*>(dgp + q * H) = *reinterpret_cast<const uint4*>(g[q]);
+  st8(d.dc_carry + bu, next);
+}
+
 // ---------------------------------------------------------------------------
 // Backward step: dh_{t'} = dgates_t Wp  (t' = the step processed before t in
 // forward order) fused with the cell backward of step t':
@@ -366,20 +442,37 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(Pdrnn
   f32x4 acc[G::MT][G::NT];
   G::run(d.dgates + (int64_t)t * B * 4 * H, 4 * H, d.wt, 4 * H, B, 4 * H, m0, n0, smem_u16, acc);
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid / WN, wn = wid % WN;
+  // Epilogue through LDS (as in the forward): the dh tile is parked as fp32
+  // [BM][BN+4] in the idle staging ring, then each thread runs the cell
+  // backward of 8 consecutive units of one row with 16-byte loads / stores
+  // (acts, c, carry, dout, and one store per gate block of dgates) instead of
+  // per-element 2-byte accesses straight from the MFMA C layout.
+  constexpr int LDC = BN + 4;
+  static_assert(BM * LDC * 4 <= G::LDS_ELEMS * 2, "C tile must fit in the staging ring");
+  float* cs = reinterpret_cast<float*>(smem_u16);
+  {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid / WN, wn = wid % WN;
 #pragma unroll
-  for (int i = 0; i < G::MT; ++i) {
-    const int rbase = m0 + wm * G::WTM + i * 16 + (lane >> 4) * 4;
+    for (int i = 0; i < G::MT; ++i)
 #pragma unroll
-    for (int j = 0; j < G::NT; ++j) {
-      const int u = n0 + wn * G::WTN + j * 16 + (lane & 15);
+      for (int j = 0; j < G::NT; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = rbase + r;
-        if (b < B) cell_bwd_elem<DT, CELL>(d, B, H, T, rev, tn, cell, b, u, acc[i][j][r], d.dc_carry[(int64_t)b * H + u]);
-      }
-    }
+        for (int r = 0; r < 4; ++r)
+          cs[(wm * G::WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * G::WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+  }
+  __syncthreads();
+  constexpr int C8 = BN / 8;
+  for (int e = threadIdx.x; e < BM * C8; e += G::NTHREADS) {
+    const int row = e / C8, c8 = e - row * C8;
+    const int b = m0 + row;
+    if (b >= B) continue;
+    float dh[8];
+    const float4 z0 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8);
+    const float4 z1 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8 + 4);
+    dh[0] = z0.x; dh[1] = z0.y; dh[2] = z0.z; dh[3] = z0.w;
+    dh[4] = z1.x; dh[5] = z1.y; dh[6] = z1.z; dh[7] = z1.w;
+    cell_bwd_vec8<DT, CELL>(d, B, H, T, rev, tn, cell, b, n0 + c8 * 8, dh);
   }
 }
 
@@ -536,10 +629,18 @@ hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwar
   }
 }
 
+// Tile shapes reachable only through the plain GEMM entry (tile-shape
+// experiments for the large-batch step GEMMs; ids >= 10).
+#define PDRNN_GEMM_ONLY_CFGS(X) \
+  X(10, 256, 256, 2, 4, 2)      \
+  X(11, 128, 128, 2, 2, 4)      \
+  X(12, 128, 256, 2, 4, 3)      \
+  X(13, 128, 128, 2, 2, 2)
+
 template <class DT>
 hipError_t gemm_nt_dispatch(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
                             int M, int N, int K, int tile, hipStream_t st) {
-  if (tile < 0 || tile > 4) tile = pick_tile(M, N, 1);
+  if (tile < 0 || (tile > 4 && tile < 10) || tile > 13) tile = pick_tile(M, N, 1);
   switch (tile) {
 #define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_)                                                      \
   case ID: {                                                                                        \
@@ -551,6 +652,7 @@ hipError_t gemm_nt_dispatch(const uint16_t* A, int64_t lda, const uint16_t* Bt, 
     return hipGetLastError();                                                                        \
   }
     PDRNN_TILE_CFGS(PDRNN_CASE)
+    PDRNN_GEMM_ONLY_CFGS(PDRNN_CASE)
 #undef PDRNN_CASE
     default: return hipErrorInvalidValue;
   }

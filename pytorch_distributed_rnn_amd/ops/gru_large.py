@@ -104,6 +104,7 @@ class _LargeGRULayer(torch.autograd.Function):
         dgates, dh0, _ = mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1)
         grads: List[Optional[Tensor]] = []
         dx = None
+        need_dx = ctx.needs_input_grad[0]
         x2 = x.reshape(T * B, I)
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # [r | z | dpre_n | dpre_n r]
@@ -115,13 +116,15 @@ class _LargeGRULayer(torch.autograd.Function):
             cs = G.sum(0, dtype=torch.float32)
             dbih = cs[:3 * H]
             dbhh = torch.cat([cs[:2 * H], cs[3 * H:]])
-            if dx is None:
+            if not need_dx:
+                pass  # layer input without grad (e.g. the data): no dX GEMM
+            elif dx is None:
                 dx = torch.mm(Gx, wih[d])
             else:
                 dx.addmm_(Gx, wih[d])
             grads += [dwih, dwhh, dbih if has_w[4 * d + 2] else None, dbhh if has_w[4 * d + 3] else None]
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
-        return (dx.view(T, B, I), dh0_out, None, *grads)
+        return (dx.view(T, B, I) if dx is not None else None, dh0_out, None, *grads)
 
 
 def gru_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor], *, hidden: int,

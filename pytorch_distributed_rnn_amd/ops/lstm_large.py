@@ -127,6 +127,7 @@ class _LargeLSTMLayer(torch.autograd.Function):
         dgates, dh0, dc0 = mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile, 0)
         grads: List[Optional[Tensor]] = []
         dx = None
+        need_dx = ctx.needs_input_grad[0]
         x2 = x.reshape(T * B, I)
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
@@ -136,12 +137,14 @@ class _LargeLSTMLayer(torch.autograd.Function):
             dwhh = _mm_f32(G.t(), hprev.reshape(T * B, H))
             dwih = _mm_f32(G.t(), x2)
             db = G.sum(0, dtype=torch.float32)  # fp32 accumulation, no fp32 copy of G
-            if dx is None:
+            if not need_dx:
+                pass  # layer input without grad (e.g. the data): no dX GEMM
+            elif dx is None:
                 dx = torch.mm(G, wih[d])
             else:
                 dx.addmm_(G, wih[d])
             grads += [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
-        dx = dx.view(T, B, I)
+        dx = dx.view(T, B, I) if dx is not None else None
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         dc0_out = dc0.to(c0_dtype) if has_c0 else None
         return (dx, dh0_out, dc0_out, None, *grads)
