@@ -152,6 +152,13 @@ class RcclComm final : public Comm {
     if (pending_) wait();
     c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     hipStream_t cs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_).stream();
+    if (cs == nullptr) {
+      // never put RCCL on the legacy NULL stream (it synchronises with every
+      // blocking stream): go through the comm stream instead
+      all_reduce(t, op);
+      wait();
+      return;
+    }
     NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl(op), comm_, cs));
     if (serialize_comm()) HIP_CHECK(hipStreamSynchronize(cs));
   }

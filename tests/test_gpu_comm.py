@@ -59,6 +59,14 @@ def test_rccl_comm_collectives(rccl_group):
     c.all_reduce(z, "sum")        # queued on the comm stream ...
     c.all_reduce_inline(z, "avg")  # ... joined before the inline one (same communicator)
     torch.testing.assert_close(z, x)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # a real (non-NULL) stream: RCCL runs on it directly
+        w = z * 2
+        c.all_reduce_inline(w, "sum")
+        w += 1
+    torch.cuda.current_stream().wait_stream(side)
+    torch.testing.assert_close(w, 2 * x + 1)
 
 
 @pytest.mark.parametrize("mode", ["all_reduce_now", "all_reduce_inline"])
