@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--trainer", choices=("distributed", "horovod"), default="distributed")
     ap.add_argument("--cell", choices=("lstm", "gru"), default="lstm")
     ap.add_argument("--seed", type=int, default=123456789)
+    ap.add_argument("--cuda-graph", action="store_true",
+                    help="replay the synced step (fwd/BPTT, RCCL all-reduce, Adam) from a HIP graph")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
                     help="bf16: BASELINE config 2 (bf16 inputs/weights, fp32 accumulate)")
     return ap.parse_args(argv)
@@ -84,7 +86,8 @@ def main(argv=None):
                         compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     cls = DDPTrainer if args.trainer == "distributed" else HorovodTrainer
     trainer = cls(model=model, training_set=train_set, batch_size=args.global_batch,
-                  learning_rate=0.0025, weak_scaling=args.scaling == "weak", device=dev)
+                  learning_rate=0.0025, weak_scaling=args.scaling == "weak", device=dev,
+                  cuda_graph=True if args.cuda_graph else None)
     per_rank = trainer.train_loader.batch_size
 
     loader = trainer.train_loader

@@ -12,7 +12,7 @@ so fabfile-style command lines keep working:
 
 Additions (all optional): ``--synthetic``, ``--cell {lstm,gru}``, ``--dtype
 {fp32,bf16,fp16}``, ``--bidirectional``, ``--trace`` / ``--profile DIR``,
-``--backend``, ``--bucket-mb``, ``--kernel {hip,torch}``, ``--resume``,
+``--backend``, ``--bucket-mb``, ``--cuda-graph``, ``--kernel {hip,torch}``, ``--resume``,
 ``--checkpoint-every``, ``--log-interval``, ``--weak-scaling``,
 ``--fault-delay-ms`` / ``--fault-rank`` (network fault injection stand-in for
 tc-netem), ``--history-file``.  Deviations from the reference, documented:
@@ -68,6 +68,8 @@ def build_parser(script_dir: Optional[Path] = None) -> argparse.ArgumentParser:
                    help="torch.profiler capture of the training run into this directory")
     p.add_argument("--backend", default=None, help="nccl|rccl|gloo|mpi (default: RCCL on GPU, gloo on CPU)")
     p.add_argument("--bucket-mb", default=None, type=float)
+    p.add_argument("--cuda-graph", action="store_true",
+                   help="replay the synced fused step (fwd/BPTT + RCCL all-reduce + Adam) from a HIP graph")
     p.add_argument("--kernel", choices=("hip", "torch"), default="hip")
     p.add_argument("--device", default=None, help="cpu to force the CPU path")
     p.add_argument("--resume", default=None, type=Path)
@@ -143,7 +145,7 @@ def train(args, name: str):
     kw = dict(model=model, training_set=training_set, validation_set=validation_set,
               test_set=test_set, batch_size=args.batch_size, learning_rate=args.learning_rate,
               checkpoint_dir=args.checkpoint_directory, log_interval=args.log_interval,
-              checkpoint_every=args.checkpoint_every)
+              checkpoint_every=args.checkpoint_every, cuda_graph=True if args.cuda_graph else None)
     if args.device == "cpu":
         kw["device"] = torch.device("cpu")
     if name != "local":

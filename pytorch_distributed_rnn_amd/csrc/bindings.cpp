@@ -434,7 +434,7 @@ Tensor xent_bwd(const Tensor& dlogits, const Tensor& grad_out, const Tensor& sta
 void adam_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_sq,
                const optional<Tensor>& max_exp_avg_sq, double lr, double beta1, double beta2, double eps,
                double weight_decay, double step, double grad_scale, bool decoupled, bool maximize,
-               const optional<Tensor>& lr_t, const optional<Tensor>& step_t) {
+               const optional<Tensor>& lr_t, const optional<Tensor>& step_t, const optional<Tensor>& ticket) {
   CHECK_HIP_TENSOR(param);
   for (const Tensor* t : std::initializer_list<const Tensor*>{&param, &grad, &exp_avg, &exp_avg_sq}) {
     CHECK_F32(*t);
@@ -457,6 +457,15 @@ void adam_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_
   a.maximize = maximize ? 1 : 0;
   a.lr_ptr = opt_ptr(lr_t);
   a.step_ptr = opt_ptr(step_t);
+  if (ticket.has_value() && ticket->defined()) {
+    // advance mode: step_t holds the count BEFORE this step and is bumped in-kernel
+    TORCH_CHECK(step_t.has_value() && step_t->defined(), "adam_flat: ticket needs the device step tensor");
+    TORCH_CHECK(ticket->is_cuda() && ticket->scalar_type() == at::kInt && ticket->numel() >= 1,
+                "adam_flat: ticket must be a device int32 tensor (zero-initialised)");
+    a.step_advance = step_t->data_ptr<float>();
+    a.ticket = reinterpret_cast<unsigned int*>(ticket->data_ptr<int>());
+    a.step_ptr = nullptr;
+  }
   HIP_LAUNCH_CHECK(pdrnn_adam_flat(&a, cur_stream()));
 }
 
@@ -668,7 +677,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("adam_hp") = py::none());
   m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
-  m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer");
+  m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer", py::arg("param"), py::arg("grad"),
+        py::arg("exp_avg"), py::arg("exp_avg_sq"), py::arg("max_exp_avg_sq"), py::arg("lr"), py::arg("beta1"),
+        py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"), py::arg("grad_scale"),
+        py::arg("decoupled"), py::arg("maximize"), py::arg("lr_t") = py::none(), py::arg("step_t") = py::none(),
+        py::arg("ticket") = py::none());
   m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
   m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
   m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });

@@ -151,6 +151,11 @@ typedef struct {
   int maximize;
   const float* lr_ptr;       // optional device lr (graph-capturable); overrides lr
   const float* step_ptr;     // optional device step count for bias correction (capturable)
+  // optional: advance the device step count in-kernel (graph replay needs no
+  // separate increment launch): the step used is *step_advance + 1, written
+  // back by the last workgroup to finish (arrival ticket, reset to 0 after)
+  float* step_advance;
+  unsigned int* ticket;
 } PdrnnAdamArgs;
 hipError_t pdrnn_adam_flat(const PdrnnAdamArgs* a, hipStream_t stream);
 

@@ -43,7 +43,11 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(PdrnnAdamArgs a) {
   AdamScalars s;
   s.lr = a.lr_ptr ? *a.lr_ptr : a.lr;
   s.b1 = a.beta1; s.b2 = a.beta2; s.eps = a.eps; s.wd = a.weight_decay;
-  if (a.step_ptr) {
+  const float st_new = a.step_advance ? *a.step_advance + 1.f : 0.f;
+  if (a.step_advance) {
+    s.bc1 = 1.f - powf(a.beta1, st_new);
+    s.bc2_sqrt = sqrtf(1.f - powf(a.beta2, st_new));
+  } else if (a.step_ptr) {
     const float st = *a.step_ptr;
     s.bc1 = 1.f - powf(a.beta1, st);
     s.bc2_sqrt = sqrtf(1.f - powf(a.beta2, st));
@@ -82,6 +86,16 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(PdrnnAdamArgs a) {
     float p = a.param[i], m = a.exp_avg[i], v = a.exp_avg_sq[i];
     adam_elem(p, a.grad[i], m, v, s.amsgrad ? a.max_exp_avg_sq + i : nullptr, s);
     a.param[i] = p; a.exp_avg[i] = m; a.exp_avg_sq[i] = v;
+  }
+  if (a.step_advance) {
+    // every workgroup read the old count above (it fed bc1/bc2); the last one
+    // to arrive publishes the new count and re-arms the ticket for the next
+    // launch (kernel-boundary visibility)
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(a.ticket, 1u) == gridDim.x - 1) {
+      *a.step_advance = st_new;
+      *a.ticket = 0u;
+    }
   }
 }
 

@@ -56,8 +56,11 @@ class Trainer:
     def __init__(self, model: nn.Module, training_set, batch_size: int, learning_rate: float,
                  validation_set=None, test_set=None, checkpoint_dir: Optional[Path] = None,
                  sampler: Optional[ShardedSampler] = None, *, device: Optional[torch.device] = None,
-                 log_interval: int = 0, checkpoint_every: int = 0, flatten: bool = True):
+                 log_interval: int = 0, checkpoint_every: int = 0, flatten: bool = True,
+                 cuda_graph: Optional[bool] = None):
         self.device = torch.device(device) if device is not None else default_device()
+        # replay the synced fused step from a HIP graph (None: PDRNN_CUDA_GRAPH)
+        self.cuda_graph = cuda_graph
         self.model = model.to(self.device)
         inner = getattr(self.model, "module", self.model)
         if flatten and not getattr(inner, "_pdrnn_flat", None):
@@ -158,7 +161,8 @@ class Trainer:
         if os.environ.get("PDRNN_FUSED_STEP", "1") != "0":
             from . import fused_step
             if fused_step.supported(self.model, self.optimizer, self.device):
-                self._fused = fused_step.MotionTrainStep(self.model, self.optimizer, self._grad_sync())
+                self._fused = fused_step.MotionTrainStep(self.model, self.optimizer, self._grad_sync(),
+                                                         cuda_graph=self.cuda_graph)
         return self._fused
 
     def train_batch(self, batch) -> Tuple[Tensor, int]:

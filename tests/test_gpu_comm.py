@@ -98,6 +98,46 @@ def test_ddp_reducer_rccl_step_matches_local(rccl_group, mode):
         torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
 
 
+def test_graph_replayed_rccl_step_matches_local(rccl_group):
+    """The synced step captured into a HIP graph (fwd/BPTT/reductions + inline
+    RCCL all-reduce + Adam with a device step count) and replayed with fresh
+    batch indices reproduces the eager local step, step for step, including
+    after an eager step in between (device step count re-seeded)."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_rnn_amd.train.fused_step import MotionTrainStep
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    from pytorch_distributed_rnn_amd.utils.flat import flatten_module
+    torch.manual_seed(3)
+    train, _, _ = synthetic_motion(n_train=512, n_validation=1, n_test=1, seed=3)
+    feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
+    m1 = MotionModel(9, 32, 2, 6).cuda()
+    m2 = copy.deepcopy(m1)
+    ddp = DistributedDataParallel(m1)
+    o1 = FusedAdam(m1.parameters(), lr=2.5e-3)
+    flatten_module(m2)
+    o2 = FusedAdam(m2.parameters(), lr=2.5e-3)
+    s1 = MotionTrainStep(ddp, o1, ddp.reducer.all_reduce_inline, cuda_graph=True)
+    s2 = MotionTrainStep(m2, o2, None)
+    g = torch.Generator().manual_seed(0)
+    outs = []
+    for i in range(7):
+        idx = torch.randperm(512, generator=g)[:64].cuda()
+        if i == 5:  # a host-gathered batch in between runs eagerly
+            a = s1(feats.index_select(0, idx), labels.index_select(0, idx), None)
+        else:
+            a = s1(feats, labels, idx)
+        b = s2(feats, labels, idx)
+        outs.append((a.clone(), b.clone()))
+    assert s1._graph is not None, "the synced step was never captured"
+    for a, b in outs:
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+    assert o1.state_dict()["state"][0]["step"] == o2.state_dict()["state"][0]["step"]
+
+
 def test_ddp_autograd_hooks_rccl(rccl_group):
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel

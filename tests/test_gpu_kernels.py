@@ -124,6 +124,32 @@ def test_fused_adam_matches_torch():
     assert set(sd["state"][0].keys()) >= {"step", "exp_avg", "exp_avg_sq"}
 
 
+def test_adam_flat_device_step_advance():
+    """Advance mode (graph replay): the kernel uses device step + 1 for the bias
+    corrections and the last workgroup writes it back -- over many workgroups,
+    matching host-step launches, with the ticket re-armed every launch."""
+    from pytorch_distributed_rnn_amd import _ext
+    mod = _ext.require()
+    torch.manual_seed(0)
+    n = 1 << 20  # 1024 workgroups
+    p0 = torch.randn(n, device="cuda")
+    p1, p2 = p0.clone(), p0.clone()
+    m1, v1 = torch.zeros_like(p0), torch.zeros_like(p0)
+    m2, v2 = torch.zeros_like(p0), torch.zeros_like(p0)
+    step_t = torch.zeros(1, device="cuda")
+    ticket = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for s in range(1, 5):
+        g = torch.randn(n, device="cuda")
+        mod.adam_flat(p1, g, m1, v1, None, 1e-2, 0.9, 0.999, 1e-8, 0.0, float(s), 1.0, False, False)
+        mod.adam_flat(p2, g, m2, v2, None, 1e-2, 0.9, 0.999, 1e-8, 0.0, 0.0, 1.0, False, False,
+                      None, step_t, ticket)
+        torch.cuda.synchronize()
+        assert float(step_t) == float(s) and int(ticket) == 0
+    # bias corrections in fp32 on the device vs double on the host
+    torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(v2, v1, rtol=0, atol=0)
+
+
 def test_embedding_matches_torch():
     C = _C()
     V, D, N = 97, 64, 5000
