@@ -16,7 +16,7 @@ layout and are unpacked here to nn.GRU's.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor
@@ -34,23 +34,67 @@ def supported(x: Tensor, hidden: int, num_layers: int) -> bool:
     return num_layers * 4 * hidden <= 512 and num_layers * hidden * lanes <= 512
 
 
+_ZEROS: Dict[Tuple[torch.device, torch.dtype], Tensor] = {}
+_UNPACK: Dict[Tuple[int, Tuple[int, ...], torch.device], Tensor] = {}
+
+
+def _zeros(like: Tensor, n: int) -> Tensor:
+    """Slice of a cached zero vector (the packed layout's empty blocks)."""
+    key = (like.device, like.dtype)
+    z = _ZEROS.get(key)
+    if z is None or z.numel() < n:
+        z = like.new_zeros(max(n, 1024))
+        _ZEROS[key] = z
+    return z[:n]
+
+
 def _pack(weights: Sequence[Optional[Tensor]], num_layers: int, hidden: int, like: Tensor) -> List[Tensor]:
+    """All layers' 4-block stacks as views of ONE buffer built by a single
+    batched cat launch (the zero blocks are slices of a cached zero vector),
+    instead of a cat + zero fill per tensor per step."""
     H = hidden
-    out = []
+    pieces: List[Tensor] = []
+    shapes: List[Tuple[int, ...]] = []
     with torch.no_grad():
         for l in range(num_layers):
             w_ih, w_hh, b_ih, b_hh = weights[4 * l:4 * l + 4]
             I = w_ih.shape[1]
-            z_ih = like.new_zeros(H, I)
-            z_hh = like.new_zeros(H, H)
-            zb = like.new_zeros(H)
-            b_ih = b_ih if b_ih is not None else like.new_zeros(3 * H)
-            b_hh = b_hh if b_hh is not None else like.new_zeros(3 * H)
-            out += [torch.cat([w_ih, z_ih]).contiguous(),
-                    torch.cat([w_hh[:2 * H], z_hh, w_hh[2 * H:]]).contiguous(),
-                    torch.cat([b_ih, zb]).contiguous(),
-                    torch.cat([b_hh[:2 * H], zb, b_hh[2 * H:]]).contiguous()]
+            zb = _zeros(like, H)
+            b_ih = b_ih.reshape(-1) if b_ih is not None else _zeros(like, 3 * H)
+            b_hh = b_hh.reshape(-1) if b_hh is not None else _zeros(like, 3 * H)
+            pieces += [w_ih.reshape(-1), _zeros(like, H * I),
+                       w_hh[:2 * H].reshape(-1), _zeros(like, H * H), w_hh[2 * H:].reshape(-1),
+                       b_ih, zb, b_hh[:2 * H], zb, b_hh[2 * H:]]
+            shapes += [(4 * H, I), (4 * H, H), (4 * H,), (4 * H,)]
+        flat = torch.cat(pieces)
+    out, off = [], 0
+    for s in shapes:
+        n = 1
+        for d in s:
+            n *= d
+        out.append(flat[off:off + n].view(s))
+        off += n
     return out
+
+
+def _unpack_index(hidden: int, in_dims: Tuple[int, ...], device: torch.device) -> Tensor:
+    """Gather map from the packed gradient vector to nn.GRU's parameter order
+    (per layer: dW_ih = rows [0, 3H) of its block, dW_hh / db_hh = rows
+    [0, 2H) and [3H, 4H), db_ih = [0, 3H)); one index_select per step."""
+    key = (hidden, in_dims, device)
+    idx = _UNPACK.get(key)
+    if idx is None:
+        H, parts, off = hidden, [], 0
+        for I in in_dims:
+            parts.append(torch.arange(off, off + 3 * H * I)); off += 4 * H * I
+            parts += [torch.arange(off, off + 2 * H * H), torch.arange(off + 3 * H * H, off + 4 * H * H)]
+            off += 4 * H * H
+            parts.append(torch.arange(off, off + 3 * H)); off += 4 * H
+            parts += [torch.arange(off, off + 2 * H), torch.arange(off + 3 * H, off + 4 * H)]
+            off += 4 * H
+        idx = torch.cat(parts).to(device)
+        _UNPACK[key] = idx
+    return idx
 
 
 class _FusedSmallGRU(torch.autograd.Function):
@@ -83,19 +127,15 @@ class _FusedSmallGRU(torch.autograd.Function):
         dhn = dhn.contiguous() if dhn is not None else None
         dparams, dx, dh0, _ = mod.lstm_small_bwd(x, None, packed, h0, None, hseq, act, dout, dhn, None, H,
                                                  num_layers, batch_first, need_dx, need_dh0, 1, 1, None, cell=1)
+        in_dims = tuple(int(packed[4 * l].shape[1]) for l in range(num_layers))
+        g = dparams.index_select(0, _unpack_index(H, in_dims, dparams.device))
         grads: List[Optional[Tensor]] = []
         off = 0
-        for l in range(num_layers):
-            views = []
-            for w in packed[4 * l:4 * l + 4]:
-                views.append(dparams[off:off + w.numel()].view_as(w))
-                off += w.numel()
-            dwih4, dwhh4, dbih4, dbhh4 = views
-            gl = [dwih4[:3 * H],
-                  torch.cat([dwhh4[:2 * H], dwhh4[3 * H:]]),
-                  dbih4[:3 * H],
-                  torch.cat([dbhh4[:2 * H], dbhh4[3 * H:]])]
-            grads += [g if present[4 * l + k] else None for k, g in enumerate(gl)]
+        for l, I in enumerate(in_dims):
+            for k, s in enumerate(((3 * H, I), (3 * H, H), (3 * H,), (3 * H,))):
+                n = s[0] * (s[1] if len(s) > 1 else 1)
+                grads.append(g[off:off + n].view(s) if present[4 * l + k] else None)
+                off += n
         return (dx if need_dx else None, dh0 if need_dh0 else None, None, *grads)
 
 
