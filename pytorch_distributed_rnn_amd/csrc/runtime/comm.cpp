@@ -93,6 +93,10 @@ class RcclComm final : public Comm {
 
   void all_reduce(at::Tensor& t, RedOp op) override {
     check(t);
+    // an in-place reduction over one rank is the identity: no collective, no
+    // comm-stream hop (the autograd DDP path at N = 1).  The inline variant
+    // below still issues it, so forced-sync timing runs keep the RCCL kernel.
+    if (world_ == 1) return;
     enter();
     NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl(op), comm_, stream_));
     leave({t});
