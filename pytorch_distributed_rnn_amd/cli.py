@@ -80,7 +80,9 @@ def build_parser(script_dir: Optional[Path] = None) -> argparse.ArgumentParser:
                    help="--batch-size is per rank instead of global")
     p.add_argument("--fault-delay-ms", default=0.0, type=float,
                    help="inject a host delay before every gradient sync (netem stand-in)")
-    p.add_argument("--fault-rank", default=-1, type=int, help="only this rank is delayed (-1: all)")
+    p.add_argument("--fault-rank", default=-1, type=int, help="only this rank is delayed / dropped (-1: all)")
+    p.add_argument("--fault-drop-step", default=-1, type=int,
+                   help="the --fault-rank rank(s) exit abruptly at this training step (failure-detection test)")
     p.add_argument("--history-file", default="history.json", type=Path)
 
     sub = p.add_subparsers(title="Available commands", metavar="command [options ...]")
@@ -115,9 +117,14 @@ def _apply_common(args) -> None:
         os.environ["PDRNN_KERNELS"] = "torch"
     if args.device == "cpu":
         os.environ["PDRNN_FORCE_CPU"] = "1"
-    if args.fault_delay_ms > 0:
+    if args.fault_delay_ms > 0 or args.fault_drop_step >= 0:
         from .utils import faults
-        faults.configure(delay_ms=args.fault_delay_ms, rank=args.fault_rank)
+        kw = {"rank": args.fault_rank}
+        if args.fault_delay_ms > 0:
+            kw["delay_ms"] = args.fault_delay_ms
+        if args.fault_drop_step >= 0:
+            kw["drop_step"] = args.fault_drop_step
+        faults.configure(**kw)
     if args.trace:
         from .utils import tracing
         tracing.enable(True)
@@ -154,8 +161,8 @@ def train(args, name: str):
         if name == "distributed":
             kw["bucket_cap_mb"] = args.bucket_mb
     trainer = trainer_cls(**kw)
-    if args.fault_delay_ms > 0:
-        from .utils import faults
+    from .utils import faults
+    if faults.active():  # flags above or PDRNN_FAULT_* environment
         faults.install(trainer)
     if args.resume is not None:
         nxt = trainer.resume(args.resume)

@@ -225,6 +225,10 @@ hipError_t pdrnn_gemm_nt(const uint16_t* A, int64_t lda, const uint16_t* Bt, int
 hipError_t pdrnn_adam_partials(const PdrnnAdamArgs* a, const float* work, int split, int64_t P_total,
                                float* grad_out, float* stats_out, int n_stats, hipStream_t stream);
 
+// Diagnostics: a single wave that spins for `microseconds` (bounded, <= 60 s).
+// Communicator-watchdog tests only.
+hipError_t pdrnn_debug_spin(uint64_t microseconds, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,13 +50,28 @@ class Comm {
     all_reduce(t, op);
     wait();
   }
+  // ---- failure detection (RcclComm: watchdog thread; others: their
+  // backend's own timeouts) ----
+  virtual bool aborted() const { return false; }
+  virtual double timeout_s() const { return 0.0; }
+  virtual int64_t tracked() const { return 0; }  // collectives the watchdog has followed
+  // test hook: occupy the comm stream for `seconds` like a collective whose
+  // peer never arrives (bounded spin kernel)
+  virtual void debug_stall(double seconds) {
+    (void)seconds;
+    TORCH_CHECK(false, "debug_stall: only the native RCCL communicator has a device-side stall");
+  }
 };
+
+// exit status of a process whose communicator watchdog fired (see comm.cpp)
+constexpr int kWatchdogExit = 86;
 
 // PDRNN_SERIALIZE_COMM=1: every collective completes (device-synchronised)
 // before the call returns -- A/B switch for overlap / stream-ordering bugs.
 bool serialize_comm();
 
-std::shared_ptr<Comm> make_rccl_comm(const std::string& uid, int rank, int world, int device, bool high_priority);
+std::shared_ptr<Comm> make_rccl_comm(const std::string& uid, int rank, int world, int device, bool high_priority,
+                                     double timeout_s);
 std::shared_ptr<Comm> make_pg_comm(const pybind11::object& process_group);
 std::string rccl_unique_id();
 

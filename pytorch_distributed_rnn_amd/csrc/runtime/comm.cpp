@@ -6,20 +6,41 @@
 // src/example/example_distributed.py:18-19):
 //  * bootstrapped from an ncclUniqueId that the Python side distributes
 //    through the torch.distributed TCPStore rendezvous,
-//  * every collective runs on ONE dedicated high-priority HIP stream per
-//    communicator, fenced against the caller's compute stream with events, so
-//    gradient all-reduce overlaps the BPTT kernels still running on the
-//    compute stream,
+//  * asynchronous collectives (all_reduce, broadcast, all_gather, ...) run on
+//    ONE dedicated high-priority HIP stream per communicator, fenced against
+//    the caller's compute stream with events, so gradient all-reduce overlaps
+//    the BPTT kernels still running on the compute stream; all_reduce_inline
+//    runs straight on the caller's stream (nothing to overlap),
 //  * payloads are torch tensors; their storage is recorded on the comm stream
-//    so the caching allocator never recycles memory a collective still reads.
+//    so the caching allocator never recycles memory a collective still reads,
+//  * an in-place all_reduce over ONE rank is the identity and issues nothing
+//    (PDRNN_FORCE_COLLECTIVE=1 keeps issuing it: tests and forced-sync timing),
+//  * a watchdog thread bounds every collective: each one is followed by a
+//    completion event; a collective still pending after `timeout_s` (or an
+//    asynchronous RCCL error) aborts the communicator (ncclCommAbort makes
+//    the spinning RCCL kernels exit, so a host blocked in a device
+//    synchronize wakes up), every later call raises, and -- unless
+//    PDRNN_COMM_WATCHDOG_EXIT=0 -- the process exits with kWatchdogExit after
+//    a grace period.  This is the native counterpart of the reference's
+//    bounded waits (RPC timeout 60 s, master.py:56 / worker.py:105;
+//    horovodrun --start-timeout 300, fabfile.py:227).
 #include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <stdexcept>
+#include <thread>
 
+#include "pdrnn/api.h"
 #include "pdrnn/runtime.h"
 
 namespace pdrnn {
@@ -63,10 +84,26 @@ ncclRedOp_t to_nccl(RedOp op) {
   return ncclSum;
 }
 
+bool env_flag(const char* name, bool dflt) {
+  const char* e = std::getenv(name);
+  if (e == nullptr || e[0] == '\0') return dflt;
+  return e[0] == '1' || e[0] == 'y' || e[0] == 'Y' || e[0] == 't' || e[0] == 'T';
+}
+
+double env_double(const char* name, double dflt) {
+  const char* e = std::getenv(name);
+  if (e == nullptr || e[0] == '\0') return dflt;
+  char* end = nullptr;
+  const double v = std::strtod(e, &end);
+  return end != e ? v : dflt;
+}
+
+using Clock = std::chrono::steady_clock;
+
 class RcclComm final : public Comm {
  public:
-  RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority)
-      : rank_(rank), world_(world), device_(device) {
+  RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority, double timeout_s)
+      : rank_(rank), world_(world), device_(device), timeout_s_(timeout_s > 0 ? timeout_s : 600.0) {
     TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
@@ -76,13 +113,27 @@ class RcclComm final : public Comm {
     HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo));
     HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+    // every peer has just joined the torch.distributed rendezvous that carried
+    // the unique id, so a blocking init cannot wait on a dead rank for long
     NCCL_CHECK(ncclCommInitRank(&comm_, world_, id, rank_));
+    exit_on_abort_ = env_flag("PDRNN_COMM_WATCHDOG_EXIT", true);
+    grace_s_ = env_double("PDRNN_COMM_WATCHDOG_GRACE_S", 5.0);
+    poll_ms_ = std::max(1.0, env_double("PDRNN_COMM_WATCHDOG_POLL_MS", 100.0));
+    watchdog_ = std::thread([this] { watchdog_loop(); });
   }
   ~RcclComm() override {
-    if (comm_) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (watchdog_.joinable()) watchdog_.join();
+    if (comm_ && !aborted_.load()) {
       hipStreamSynchronize(stream_);
       ncclCommDestroy(comm_);
     }
+    for (auto& w : works_) hipEventDestroy(w.ev);
+    for (auto ev : free_events_) hipEventDestroy(ev);
     if (ev_in_) hipEventDestroy(ev_in_);
     if (ev_out_) hipEventDestroy(ev_out_);
     if (stream_) hipStreamDestroy(stream_);
@@ -94,33 +145,52 @@ class RcclComm final : public Comm {
   void all_reduce(at::Tensor& t, RedOp op) override {
     check(t);
     // an in-place reduction over one rank is the identity: no collective, no
-    // comm-stream hop (the autograd DDP path at N = 1).  The inline variant
-    // below still issues it, so forced-sync timing runs keep the RCCL kernel.
-    if (world_ == 1) return;
-    enter();
-    NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl(op), comm_, stream_));
-    leave({t});
+    // comm-stream hop (the autograd DDP path at N = 1) -- unless forced
+    if (world_ == 1 && !force_collective()) return;
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      live();
+      enter();
+      NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl(op), comm_, stream_));
+      leave({t}, "all_reduce");
+    }
+    if (serialize_comm()) host_wait(stream_, "all_reduce");
   }
   void broadcast(at::Tensor& t, int root) override {
     check(t);
-    enter();
-    NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, stream_));
-    leave({t});
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      live();
+      enter();
+      NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, stream_));
+      leave({t}, "broadcast");
+    }
+    if (serialize_comm()) host_wait(stream_, "broadcast");
   }
   void all_gather(at::Tensor& out, const at::Tensor& in) override {
     check(out); check(in);
     TORCH_CHECK(out.numel() == in.numel() * world_, "all_gather: out must hold world * in elements");
-    enter();
-    NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, stream_));
-    leave({out, in});
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      live();
+      enter();
+      NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, stream_));
+      leave({out, in}, "all_gather");
+    }
+    if (serialize_comm()) host_wait(stream_, "all_gather");
   }
   void reduce_scatter(at::Tensor& out, const at::Tensor& in, RedOp op) override {
     check(out); check(in);
     TORCH_CHECK(in.numel() == out.numel() * world_, "reduce_scatter: in must hold world * out elements");
-    enter();
-    NCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl(in.scalar_type()), to_nccl(op),
-                                 comm_, stream_));
-    leave({out, in});
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      live();
+      enter();
+      NCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl(in.scalar_type()), to_nccl(op),
+                                   comm_, stream_));
+      leave({out, in}, "reduce_scatter");
+    }
+    if (serialize_comm()) host_wait(stream_, "reduce_scatter");
   }
   void all_to_all(at::Tensor& out, const at::Tensor& in) override {
     check(out); check(in);
@@ -128,26 +198,41 @@ class RcclComm final : public Comm {
     const int64_t chunk = in.numel() / world_;
     const size_t esz = in.element_size();
     const auto dt = to_nccl(in.scalar_type());
-    enter();
-    NCCL_CHECK(ncclGroupStart());
-    for (int p = 0; p < world_; ++p) {
-      NCCL_CHECK(ncclSend(static_cast<const char*>(in.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, stream_));
-      NCCL_CHECK(ncclRecv(static_cast<char*>(out.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, stream_));
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      live();
+      enter();
+      NCCL_CHECK(ncclGroupStart());
+      for (int p = 0; p < world_; ++p) {
+        NCCL_CHECK(ncclSend(static_cast<const char*>(in.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, stream_));
+        NCCL_CHECK(ncclRecv(static_cast<char*>(out.data_ptr()) + p * chunk * esz, chunk, dt, p, comm_, stream_));
+      }
+      NCCL_CHECK(ncclGroupEnd());
+      leave({out, in}, "all_to_all");
     }
-    NCCL_CHECK(ncclGroupEnd());
-    leave({out, in});
+    if (serialize_comm()) host_wait(stream_, "all_to_all");
   }
   void send(const at::Tensor& t, int peer) override {
     check(t);
-    enter();
-    NCCL_CHECK(ncclSend(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, stream_));
-    leave({t});
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      live();
+      enter();
+      NCCL_CHECK(ncclSend(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, stream_));
+      leave({t}, "send");
+    }
+    if (serialize_comm()) host_wait(stream_, "send");
   }
   void recv(at::Tensor& t, int peer) override {
     check(t);
-    enter();
-    NCCL_CHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, stream_));
-    leave({t});
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      live();
+      enter();
+      NCCL_CHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, stream_));
+      leave({t}, "recv");
+    }
+    if (serialize_comm()) host_wait(stream_, "recv");
   }
   void all_reduce_inline(at::Tensor& t, RedOp op) override {
     check(t);
@@ -163,10 +248,16 @@ class RcclComm final : public Comm {
       wait();
       return;
     }
-    NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl(op), comm_, cs));
-    if (serialize_comm()) HIP_CHECK(hipStreamSynchronize(cs));
+    {
+      std::lock_guard<std::mutex> api(api_mu_);
+      live();
+      NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl(op), comm_, cs));
+      track(cs, "all_reduce_inline");
+    }
+    if (serialize_comm()) host_wait(cs, "all_reduce_inline");
   }
   void wait() override {
+    live();
     c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
     HIP_CHECK(hipEventRecord(ev_out_, stream_));
     HIP_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_).stream(), ev_out_, 0));
@@ -174,16 +265,52 @@ class RcclComm final : public Comm {
   }
   void barrier() override {
     auto t = at::zeros({1}, at::TensorOptions().device(at::kCUDA, device_).dtype(at::kFloat));
-    all_reduce(t, RedOp::kSum);
+    if (world_ > 1 || force_collective()) {
+      {
+        std::lock_guard<std::mutex> api(api_mu_);
+        live();
+        enter();
+        NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), 1, ncclFloat32, ncclSum, comm_, stream_));
+        leave({t}, "barrier");
+      }
+    }
     wait();
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    host_wait(stream_, "barrier");
   }
+  void debug_stall(double seconds) override {
+    // a stand-in for a collective whose peer never arrives: bounded spin on
+    // the comm stream, tracked like a collective (watchdog tests)
+    std::lock_guard<std::mutex> api(api_mu_);
+    live();
+    enter();
+    HIP_CHECK(pdrnn_debug_spin((uint64_t)(seconds * 1e6), stream_));
+    leave({}, "debug_stall");
+  }
+  bool aborted() const override { return aborted_.load(); }
+  double timeout_s() const override { return timeout_s_; }
+  int64_t tracked() const override { return tracked_.load(); }
   hipStream_t stream() const { return stream_; }
 
  private:
+  struct Work {
+    hipEvent_t ev;
+    Clock::time_point t;
+    const char* what;
+  };
+
+  // read per call (a getenv): tests flip it inside one process
+  static bool force_collective() { return env_flag("PDRNN_FORCE_COLLECTIVE", false); }
   void check(const at::Tensor& t) const {
     TORCH_CHECK(t.is_cuda() && t.get_device() == device_, "RCCL tensors must live on device ", device_);
     TORCH_CHECK(t.is_contiguous(), "RCCL tensors must be contiguous");
+  }
+  // raise once the watchdog has aborted the communicator
+  void live() const {
+    if (aborted_.load()) {
+      std::lock_guard<std::mutex> lk(mu_);
+      TORCH_CHECK(false, "RCCL communicator (rank ", rank_, "/", world_, ") was aborted by the watchdog: ",
+                  abort_reason_);
+    }
   }
   // Order the comm stream after everything enqueued on the caller's stream.
   void enter() {
@@ -192,19 +319,148 @@ class RcclComm final : public Comm {
     HIP_CHECK(hipEventRecord(ev_in_, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_).stream()));
     HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
   }
-  void leave(std::initializer_list<at::Tensor> ts) {
+  void leave(std::initializer_list<at::Tensor> ts, const char* what) {
     auto s = c10::hip::getStreamFromExternalMasqueradingAsCUDA(stream_, (c10::DeviceIndex)device_);
     for (const auto& t : ts)
       if (t.defined() && t.storage().data_ptr().get())
         c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), s);
-    if (serialize_comm()) HIP_CHECK(hipStreamSynchronize(stream_));
+    track(stream_, what);
+  }
+  // completion event after the collective just enqueued on `st` (skipped while
+  // `st` is being captured into a graph: a captured event cannot be queried)
+  void track(hipStream_t st, const char* what) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) return;
+    hipEvent_t ev = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!free_events_.empty()) {
+        ev = free_events_.back();
+        free_events_.pop_back();
+      }
+    }
+    if (ev == nullptr) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(ev, st));
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      works_.push_back({ev, Clock::now(), what});
+    }
+    tracked_.fetch_add(1);
+  }
+  // host-side wait that raises (instead of hanging) once the watchdog aborts
+  void host_wait(hipStream_t st, const char* what) {
+    hipEvent_t ev;
+    HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(ev, st));
+    int spins = 0;
+    for (;;) {
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) {
+        hipEventDestroy(ev);
+        TORCH_CHECK(false, "HIP error while waiting for ", what, ": ", hipGetErrorString(q));
+      }
+      if (aborted_.load()) {
+        hipEventDestroy(ev);
+        live();
+      }
+      if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    hipEventDestroy(ev);
+  }
+
+  void watchdog_loop() {
+    hipSetDevice(device_);
+    std::unique_lock<std::mutex> lk(mu_);
+    while (!stop_) {
+      cv_.wait_for(lk, std::chrono::microseconds((int64_t)(poll_ms_ * 1000)));
+      if (stop_) break;
+      // retire completed work (FIFO: collectives of one communicator complete in order per stream)
+      std::string reason;
+      while (!works_.empty()) {
+        const hipError_t q = hipEventQuery(works_.front().ev);
+        if (q == hipSuccess) {
+          free_events_.push_back(works_.front().ev);
+          works_.pop_front();
+          continue;
+        }
+        if (q != hipErrorNotReady) reason = std::string("HIP error on ") + works_.front().what + ": " + hipGetErrorString(q);
+        break;
+      }
+      if (reason.empty() && !works_.empty()) {
+        const double age = std::chrono::duration<double>(Clock::now() - works_.front().t).count();
+        if (age > timeout_s_) {
+          char buf[256];
+          std::snprintf(buf, sizeof(buf), "%s did not complete within %.1f s (%zu collective(s) pending)",
+                        works_.front().what, timeout_s_, works_.size());
+          reason = buf;
+        }
+      }
+      if (reason.empty() && comm_ != nullptr) {
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+          reason = std::string("asynchronous RCCL error: ") + ncclGetErrorString(ae);
+      }
+      if (!reason.empty()) {
+        abort_reason_ = reason;
+        lk.unlock();
+        abort_and_maybe_exit();
+        return;
+      }
+    }
+  }
+
+  void abort_and_maybe_exit() {
+    std::fprintf(stderr, "[pdrnn] RCCL watchdog (rank %d/%d): %s -- aborting the communicator\n", rank_, world_,
+                 abort_reason_.c_str());
+    std::fflush(stderr);
+    aborted_.store(true);
+    // never abort while the main thread is inside an RCCL enqueue; a thread
+    // stuck inside one for seconds is itself the hang: exit without abort
+    bool locked = false;
+    for (int i = 0; i < 50 && !locked; ++i) {
+      locked = api_mu_.try_lock();
+      if (!locked) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+    if (locked) {
+      ncclCommAbort(comm_);  // in-flight RCCL kernels observe the abort flag and exit
+      api_mu_.unlock();
+    }
+    if (!exit_on_abort_) return;
+    // give the main thread a chance to raise out of its next call (clean
+    // Python exit with a traceback); otherwise end the process non-zero
+    const auto until = Clock::now() + std::chrono::duration<double>(grace_s_);
+    while (Clock::now() < until) {
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (stop_) return;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    std::fprintf(stderr, "[pdrnn] RCCL watchdog (rank %d/%d): exiting with status %d\n", rank_, world_, kWatchdogExit);
+    std::fflush(stderr);
+    std::_Exit(kWatchdogExit);
   }
 
   int rank_, world_, device_;
+  double timeout_s_;
+  double grace_s_ = 5.0, poll_ms_ = 100.0;
+  bool exit_on_abort_ = true;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
   bool pending_ = false;  // collectives on stream_ not yet joined by wait()
+  // watchdog state (mu_ guards works_, free_events_, stop_, abort_reason_)
+  mutable std::mutex mu_;
+  std::mutex api_mu_;  // held around every RCCL enqueue (abort never races one)
+  std::condition_variable cv_;
+  std::deque<Work> works_;
+  std::vector<hipEvent_t> free_events_;
+  bool stop_ = false;
+  std::string abort_reason_;
+  std::atomic<bool> aborted_{false};
+  std::atomic<int64_t> tracked_{0};
+  std::thread watchdog_;
 };
 
 // c10d adapter: drives torch.distributed collectives (gloo on CPU, or torch's
@@ -317,8 +573,9 @@ std::string rccl_unique_id() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-std::shared_ptr<Comm> make_rccl_comm(const std::string& uid, int rank, int world, int device, bool high_priority) {
-  return std::make_shared<RcclComm>(uid, rank, world, device, high_priority);
+std::shared_ptr<Comm> make_rccl_comm(const std::string& uid, int rank, int world, int device, bool high_priority,
+                                     double timeout_s) {
+  return std::make_shared<RcclComm>(uid, rank, world, device, high_priority, timeout_s);
 }
 
 std::shared_ptr<Comm> make_pg_comm(const pybind11::object& process_group) {

@@ -322,11 +322,17 @@ void register_runtime(py::module_& m) {
       .def("all_reduce_inline", [](Comm& c, at::Tensor t, const std::string& op) { c.all_reduce_inline(t, parse_op(op)); },
            py::arg("tensor"), py::arg("op") = "sum")
       .def("wait", &Comm::wait)
-      .def("barrier", &Comm::barrier);
+      .def("barrier", &Comm::barrier)
+      .def("debug_stall", &Comm::debug_stall, py::arg("seconds"))
+      .def_property_readonly("aborted", &Comm::aborted)
+      .def_property_readonly("timeout_s", &Comm::timeout_s)
+      .def_property_readonly("tracked", &Comm::tracked);
+  m.attr("WATCHDOG_EXIT") = kWatchdogExit;
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
-  m.def("make_rccl_comm", [](py::bytes uid, int rank, int world, int device, bool high_priority) {
-    return make_rccl_comm(std::string(uid), rank, world, device, high_priority);
-  }, py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("high_priority") = true);
+  m.def("make_rccl_comm", [](py::bytes uid, int rank, int world, int device, bool high_priority, double timeout_s) {
+    return make_rccl_comm(std::string(uid), rank, world, device, high_priority, timeout_s);
+  }, py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("high_priority") = true,
+     py::arg("timeout_s") = 600.0);
   m.def("make_pg_comm", &make_pg_comm, py::arg("process_group"));
 
   py::class_<GradReducer, std::shared_ptr<GradReducer>>(m, "GradReducer")

@@ -6,7 +6,9 @@ group:
 * GPU + RCCL group -> :class:`RcclComm` (csrc/runtime/comm.cpp): its own
   ncclComm created from a unique id that rank 0 draws and every rank receives
   through the already-initialised torch.distributed group (TCPStore
-  rendezvous), its own high-priority HIP stream;
+  rendezvous), its own high-priority HIP stream, and a watchdog thread that
+  aborts it (and, by default, ends the process with status
+  ``WATCHDOG_EXIT``) when a collective outlives ``collective_timeout_s()``;
 * otherwise (gloo / CPU plumbing) -> the same interface over torch.distributed.
 
 Communicators are cached per group.
@@ -32,6 +34,8 @@ class _PyComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.native_avg = dist.get_backend(group) == "nccl"
+        self.aborted = False
+        self.tracked = 0
         self._works = []
 
     def all_reduce(self, t, op="sum"):
@@ -82,7 +86,9 @@ def get_comm(group=None, prefer_native: bool = True):
         world = dist.get_world_size(g)
         uid = [mod.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=dist.get_global_rank(g, 0), group=g)
-        comm = mod.make_rccl_comm(uid[0], rank, world, torch.cuda.current_device(), True)
+        from .env import collective_timeout_s
+        comm = mod.make_rccl_comm(uid[0], rank, world, torch.cuda.current_device(), True,
+                                  collective_timeout_s())
     elif mod is not None:
         comm = mod.make_pg_comm(g)
     else:

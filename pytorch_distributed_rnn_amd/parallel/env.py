@@ -107,9 +107,31 @@ def setup_device(info: Optional[ProcessInfo] = None) -> torch.device:
     return torch.device("cpu")
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0,
+_TIMEOUT_S = 600.0
+
+
+def collective_timeout_s() -> float:
+    """Bound on any single collective: the process group's timeout
+    (``PDRNN_DIST_TIMEOUT_S`` / ``init_distributed(timeout_s=...)``), used by
+    gloo itself and by the native RCCL communicator's watchdog
+    (``PDRNN_COMM_TIMEOUT_S`` overrides the latter)."""
+    v = os.environ.get("PDRNN_COMM_TIMEOUT_S")
+    return float(v) if v not in (None, "") else _TIMEOUT_S
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None,
                      use_gpu: Optional[bool] = None) -> ProcessInfo:
-    """Initialise the default process group (idempotent) and the device."""
+    """Initialise the default process group (idempotent) and the device.
+
+    Every distributed wait is bounded by ``timeout_s`` (default 600 s or
+    ``PDRNN_DIST_TIMEOUT_S``): gloo raises, torch's RCCL group and the native
+    communicator's watchdog abort -- a dead peer fails the job instead of
+    hanging it (the reference bounds its waits too: RPC timeout 60 s,
+    src/motion/param_server/master.py:56; horovodrun --start-timeout 300,
+    fabfile.py:227)."""
+    global _TIMEOUT_S
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("PDRNN_DIST_TIMEOUT_S", 600.0) or 600.0)
     info = discover()
     if use_gpu is None:
         use_gpu = torch.cuda.is_available() and os.environ.get("PDRNN_FORCE_CPU", "0") != "1"
@@ -125,6 +147,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0,
             os.environ["MASTER_PORT"] = "29500"
         else:
             os.environ["MASTER_PORT"] = str(_free_port())
+    _TIMEOUT_S = float(timeout_s)
     kwargs = dict(backend=be, rank=info.rank, world_size=info.world_size,
                   timeout=datetime.timedelta(seconds=timeout_s))
     if be == "nccl" and use_gpu:

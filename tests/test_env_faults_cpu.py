@@ -57,3 +57,45 @@ def test_fault_delay_is_injected():
         assert t.calls == 1
     finally:
         faults.configure(**old)
+
+
+def test_dropped_rank_fails_survivors_fast(tmp_path):
+    """A rank that dies mid-epoch must make every survivor exit non-zero within
+    the collective timeout instead of hanging (the reference bounds its waits:
+    RPC timeout 60 s, src/motion/param_server/master.py:56; horovodrun
+    --start-timeout 300, fabfile.py:227).  Ranks are started directly (no
+    torchrun agent that would kill the survivors for us)."""
+    import os
+    import subprocess
+    import sys
+
+    from _mp import ROOT, cpu_env, free_port
+
+    world, timeout_s = 3, 20
+    main = os.path.join(ROOT, "src", "motion", "main.py")
+    port = str(free_port())
+    procs = []
+    t0 = time.perf_counter()
+    for r in range(world):
+        e = cpu_env({"RANK": str(r), "WORLD_SIZE": str(world), "LOCAL_RANK": str(r), "MASTER_PORT": port,
+                     "PDRNN_DIST_TIMEOUT_S": str(timeout_s)})
+        cmd = [sys.executable, main, "--seed", "1", "--epochs", "50", "--batch-size", "96", "--no-validation",
+               "--synthetic", "--synthetic-size", "384", "--device", "cpu", "--hidden-units", "8",
+               "--fault-rank", "1", "--fault-drop-step", "3", "distributed"]
+        procs.append(subprocess.Popen(cmd, cwd=str(tmp_path), env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    codes, outs = [], []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout_s * 4 + 60)
+            codes.append(p.returncode)
+            outs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.perf_counter() - t0
+    assert codes[1] == 17, (codes, outs[1][-2000:])  # the injected drop
+    for r in (0, 2):
+        assert codes[r] != 0, f"survivor rank {r} exited 0:\n{outs[r][-2000:]}"
+    assert elapsed < timeout_s * 4 + 60, elapsed

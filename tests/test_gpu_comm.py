@@ -2,10 +2,21 @@
 horovod-mode fusion reducer on a one-rank RCCL group (the driver's 2/4/8-GPU
 runs exercise the same code with more ranks; here: that it initialises,
 launches on its own stream, orders against the compute stream and computes
-the right thing)."""
+the right thing).
+
+The fixture sets PDRNN_FORCE_COLLECTIVE=1, so the one-rank all_reduce is a
+real ncclAllReduce on the comm stream (event fences, recordStream lifetime,
+the pending-work join before an inline reduction), not the world-1 identity;
+every test checks that the watchdog followed real collectives.  The watchdog
+itself is exercised in a child process (a stalled comm stream must abort the
+communicator and end that process with WATCHDOG_EXIT)."""
 import copy
 import os
 import socket
+import subprocess
+import sys
+import textwrap
+import time
 
 import pytest
 import torch
@@ -23,8 +34,10 @@ def _port():
 @pytest.fixture(scope="module")
 def rccl_group():
     from pytorch_distributed_rnn_amd.parallel import comm, env
-    old = {k: os.environ.get(k) for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
-    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    old = {k: os.environ.get(k) for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+                                          "PDRNN_FORCE_COLLECTIVE")}
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
+                      PDRNN_FORCE_COLLECTIVE="1")
     env.init_distributed("nccl")
     assert dist.get_backend() == "nccl"
     yield
@@ -41,11 +54,21 @@ def test_rccl_comm_collectives(rccl_group):
     from pytorch_distributed_rnn_amd.parallel.comm import get_comm
     c = get_comm()
     assert type(c).__name__ != "_PyComm" and c.world == 1 and c.rank == 0
+    assert not c.aborted and c.timeout_s > 0
+    n0 = c.tracked
     x = torch.arange(1000, dtype=torch.float32, device="cuda")
     y = x.clone()
     c.all_reduce(y, "sum")
     c.wait()
     torch.testing.assert_close(y, x)
+    assert c.tracked == n0 + 1, "forced one-rank all_reduce must issue a real collective"
+    tmp = torch.full((1 << 16,), 3.0, device="cuda")
+    c.all_reduce(tmp, "avg")       # the tensor dies before the comm stream runs:
+    del tmp                        # recordStream keeps its block out of the allocator
+    junk = torch.zeros(1 << 16, device="cuda")
+    c.wait()
+    torch.cuda.synchronize()
+    assert float(junk.abs().sum()) == 0.0
     c.all_reduce(y, "avg")
     c.broadcast(y, 0)
     out = torch.empty_like(x)
@@ -82,8 +105,8 @@ def test_ddp_reducer_rccl_step_matches_local(rccl_group, mode):
     feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
     m1 = MotionModel(9, 32, 2, 6).cuda()
     m2 = copy.deepcopy(m1)
-    ddp = DistributedDataParallel(m1, bucket_cap_mb=0.01)  # several buckets
-    assert len(ddp.bucket_layout()) >= 1
+    ddp = DistributedDataParallel(m1, bucket_cap_mb=0.01, first_bucket_cap_mb=0.01)  # several buckets
+    assert len(ddp.bucket_layout()) >= 2
     o1 = FusedAdam(m1.parameters(), lr=2.5e-3)
     flatten_module(m2)
     o2 = FusedAdam(m2.parameters(), lr=2.5e-3)
@@ -96,6 +119,7 @@ def test_ddp_reducer_rccl_step_matches_local(rccl_group, mode):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
     for p, q in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+    assert ddp.comm.tracked >= 3 * len(ddp.bucket_layout()), "every bucket must go through RCCL"
 
 
 def test_graph_replayed_rccl_step_matches_local(rccl_group):
@@ -144,14 +168,61 @@ def test_ddp_autograd_hooks_rccl(rccl_group):
     torch.manual_seed(1)
     m1 = MotionModel(9, 16, 2, 6).cuda()
     m2 = copy.deepcopy(m1)
-    ddp = DistributedDataParallel(m1)
+    ddp = DistributedDataParallel(m1, bucket_cap_mb=0.01, first_bucket_cap_mb=0.01)
     x = torch.randn(8, 20, 9, device="cuda")
     y = torch.randint(0, 6, (8,), device="cuda")
+    n0 = ddp.comm.tracked
     torch.nn.functional.cross_entropy(ddp(x), y).backward()
     torch.nn.functional.cross_entropy(m2(x), y).backward()
     torch.cuda.synchronize()
     for p, q in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-6)
+    # hook-driven buckets were launched asynchronously on the comm stream,
+    # one real collective per bucket
+    assert ddp.comm.tracked - n0 == len(ddp.bucket_layout()) >= 2
+
+
+_WATCHDOG_CHILD = textwrap.dedent("""
+    import os, sys, time, torch
+    sys.path.insert(0, os.environ["PDRNN_ROOT"])
+    from pytorch_distributed_rnn_amd.parallel import env
+    from pytorch_distributed_rnn_amd.parallel.comm import get_comm
+    env.init_distributed("nccl")
+    c = get_comm()
+    print("timeout", c.timeout_s, flush=True)
+    x = torch.ones(4, device="cuda")
+    c.all_reduce(x, "sum"); c.wait(); torch.cuda.synchronize()
+    c.debug_stall(3.0)          # the comm stream never finishes 'this collective' in time
+    c.wait()
+    torch.cuda.synchronize()    # the host blocks here, as it would behind a dead peer
+    print("synchronize returned", flush=True)
+    try:
+        c.all_reduce(x, "sum")
+    except RuntimeError as e:
+        print("raised:", str(e).splitlines()[0], flush=True)
+    time.sleep(30)              # the watchdog's grace period ends the process
+    print("still alive", flush=True)
+""")
+
+
+def test_watchdog_aborts_stalled_collective(tmp_path):
+    from pytorch_distributed_rnn_amd import _ext
+    script = tmp_path / "child.py"
+    script.write_text(_WATCHDOG_CHILD)
+    e = dict(os.environ)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
+             PDRNN_ROOT=root, PDRNN_COMM_TIMEOUT_S="1", PDRNN_COMM_WATCHDOG_GRACE_S="6",
+             PDRNN_FORCE_COLLECTIVE="1")
+    t0 = time.perf_counter()
+    p = subprocess.run([sys.executable, "-u", str(script)], env=e, capture_output=True, text=True, timeout=100)
+    elapsed = time.perf_counter() - t0
+    out = p.stdout + p.stderr
+    assert p.returncode == _ext.require().WATCHDOG_EXIT, (p.returncode, out[-3000:])
+    assert "RCCL watchdog (rank 0/1): debug_stall did not complete within 1.0 s" in out, out[-3000:]
+    assert "synchronize returned" in out and "raised:" in out and "aborted by the watchdog" in out, out[-3000:]
+    assert "still alive" not in out
+    assert elapsed < 60, elapsed
 
 
 def test_horovod_mode_rccl(rccl_group):
