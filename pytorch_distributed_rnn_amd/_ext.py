@@ -8,7 +8,9 @@ Policy (so that GPU runs never silently fall back to eager PyTorch):
 * On a CPU-only machine (this container, CI) the torch reference path is used
   and :func:`native` returns ``None``.
 * ``PDRNN_KERNELS=torch`` forces the reference path everywhere (testing aid,
-  mirrors the ``--kernel torch`` CLI flag).
+  mirrors the ``--kernel torch`` CLI flag); ``PDRNN_KERNELS=hip-strict``
+  (``--kernel hip``) turns every remaining ATen/MIOpen fallback into an error,
+  otherwise such a fallback warns once (:func:`fallback`).
 """
 from __future__ import annotations
 
@@ -65,6 +67,33 @@ def native(device: Optional[torch.device] = None):
             "or set PDRNN_ALLOW_FALLBACK=1 to run the (slow) torch reference path."
         )
     return mod
+
+
+_WARNED = set()
+
+
+def strict_kernels() -> bool:
+    """``PDRNN_KERNELS=hip-strict`` (CLI ``--kernel hip``): a shape that no HIP
+    kernel covers raises instead of falling back to ATen/MIOpen."""
+    return kernels_mode() in ("hip-strict", "strict")
+
+
+def fallback(what: str, device=None) -> None:
+    """Called right before an op runs the ATen/MIOpen reference on a GPU
+    because no HIP kernel covers the configuration: warns once per ``what``
+    (never silent), raises under :func:`strict_kernels`.  No-op on CPU runs and
+    under ``PDRNN_KERNELS=torch`` (the reference path was asked for)."""
+    if kernels_mode() == "torch" or not gpu_available():
+        return
+    if device is not None and torch.device(device).type != "cuda":
+        return
+    msg = f"pytorch_distributed_rnn_amd: no HIP kernel for {what}; running the ATen/MIOpen reference"
+    if strict_kernels():
+        raise RuntimeError(msg + " (strict kernel mode: PDRNN_KERNELS=hip-strict / --kernel hip)")
+    if what not in _WARNED:
+        _WARNED.add(what)
+        import warnings
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
 def require():

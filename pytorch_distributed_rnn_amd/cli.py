@@ -70,7 +70,9 @@ def build_parser(script_dir: Optional[Path] = None) -> argparse.ArgumentParser:
     p.add_argument("--bucket-mb", default=None, type=float)
     p.add_argument("--cuda-graph", action="store_true",
                    help="replay the synced fused step (fwd/BPTT + RCCL all-reduce + Adam) from a HIP graph")
-    p.add_argument("--kernel", choices=("hip", "torch"), default="hip")
+    p.add_argument("--kernel", choices=("auto", "hip", "torch"), default="auto",
+                   help="auto: HIP kernels, ATen fallback warns; hip: strict (uncovered shapes raise); "
+                        "torch: ATen reference (tests)")
     p.add_argument("--device", default=None, help="cpu to force the CPU path")
     p.add_argument("--resume", default=None, type=Path)
     p.add_argument("--checkpoint-every", default=0, type=int)
@@ -115,6 +117,8 @@ def _trainer_class(name: str):
 def _apply_common(args) -> None:
     if args.kernel == "torch":
         os.environ["PDRNN_KERNELS"] = "torch"
+    elif args.kernel == "hip":
+        os.environ["PDRNN_KERNELS"] = "hip-strict"
     if args.device == "cpu":
         os.environ["PDRNN_FORCE_CPU"] = "1"
     if args.fault_delay_ms > 0 or args.fault_drop_step >= 0:

@@ -279,7 +279,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
                           Tensor flat_grad, Tensor stats, int64_t H, int64_t NL, int64_t split_fwd,
                           int64_t split_bwd, int64_t nb_fwd, int64_t nb_bwd,
                           const optional<std::vector<Tensor>>& adam_state,
-                          const optional<std::vector<double>>& adam_hp) {
+                          const optional<std::vector<double>>& adam_hp, int64_t cell,
+                          const optional<Tensor>& grad_colmap) {
   CHECK_HIP_TENSOR(x);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be float32 or bfloat16");
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [N, T, I] with contiguous rows");
@@ -295,11 +296,20 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   TORCH_CHECK(head_w.dim() == 2 && head_w.size(1) == H && head_w.is_contiguous() && C <= 16, "head weight [C<=16, H]");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous(), "labels must be int64");
   StackLayout L = stack_layout(w, NL, true);
-  const int64_t P_params = L.P + C * H + (head_b.has_value() && head_b->defined() ? C : 0);
+  // GRU: `w` is the packed 4-block stack; the flat gradient buffer holds
+  // nn.GRU's parameters, reached from the packed slab through grad_colmap
+  const bool mapped = grad_colmap.has_value() && grad_colmap->defined();
+  TORCH_CHECK(cell == 0 || mapped, "GRU train step needs the packed->nn.GRU gradient column map");
+  const int64_t P_rnn = mapped ? grad_colmap->numel() : L.P;
+  if (mapped)
+    TORCH_CHECK(grad_colmap->scalar_type() == at::kInt && grad_colmap->is_contiguous() &&
+                grad_colmap->device() == x.device(), "grad_colmap must be a contiguous int32 device tensor");
+  const int* colmap = mapped ? grad_colmap->data_ptr<int>() : nullptr;
+  const int64_t P_params = P_rnn + C * H + (head_b.has_value() && head_b->defined() ? C : 0);
   TORCH_CHECK(flat_grad.numel() == P_params && flat_grad.is_contiguous() && flat_grad.scalar_type() == at::kFloat,
               "flat_grad must be the model's flat fp32 gradient buffer (", P_params, " elements)");
   TORCH_CHECK(stats.numel() >= 3 && stats.is_contiguous() && stats.scalar_type() == at::kFloat);
-  const int64_t P_head = P_params - L.P;      // head weight (+ bias)
+  const int64_t P_head = P_params - P_rnn;    // head weight (+ bias)
   const int64_t PH = P_head + 3;              // + [loss, count, correct]
   auto opts = x.options().dtype(at::kFloat);
   Tensor hseq = at::empty({NL, B, T, H}, opts);
@@ -336,7 +346,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   f.slab_P = PH; f.head_off_w = 0; f.head_off_b = C * H; f.stat_off = P_head;
   f.inv_batch = 1.f / (float)std::max<int64_t>(B, 1);
   f.C = (int)C;
-  f.B = (int)B; f.T = (int)T; f.I = (int)I; f.NL = (int)NL;
+  f.B = (int)B; f.T = (int)T; f.I = (int)I; f.NL = (int)NL; f.cell = (int)cell;
   hipStream_t st = cur_stream();
   Tensor st_f, st_b;
   if (stamps_enabled()) {
@@ -356,7 +366,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.hseq = f.hseq; bk.act = f.act;
   bk.dhn = dh_top.data_ptr<float>(); bk.dhn_top_only = 1;
   bk.slab = slab.data_ptr<float>(); bk.P = L.P;
-  bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL;
+  bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL; bk.cell = (int)cell;
   if (st_b.defined()) bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
   HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
   if (st_f.defined()) {
@@ -365,7 +375,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   }
 
   const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, gridb / 16));
-  Tensor work = at::empty({split, L.P + PH}, opts);
+  Tensor work = at::empty({split, P_rnn + PH}, opts);
   if (adam_state.has_value() && adam_hp.has_value()) {
     // single-process step: the second reduction pass runs inside Adam
     const auto& as = *adam_state;
@@ -373,8 +383,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     TORCH_CHECK(as.size() == 3 && hp.size() == 7, "adam_state = [param, exp_avg, exp_avg_sq], 7 hyper-parameters");
     for (const auto& t : as)
       TORCH_CHECK(t.is_contiguous() && t.numel() == P_params && t.scalar_type() == at::kFloat, "flat fp32 Adam buffers");
-    HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), gridb, L.P, head_slab.data_ptr<float>(), B, PH,
-                                              work.data_ptr<float>(), split, st));
+    HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,
+                                              work.data_ptr<float>(), split, colmap, L.P, st));
     PdrnnAdamArgs ad{};
     ad.param = as[0].data_ptr<float>(); ad.exp_avg = as[1].data_ptr<float>(); ad.exp_avg_sq = as[2].data_ptr<float>();
     ad.n = P_params;
@@ -383,13 +393,13 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     ad.bias_correction1 = (float)(1.0 - std::pow(hp[1], hp[5]));
     ad.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(hp[2], hp[5]));
     ad.grad_scale = 1.f; ad.decoupled = hp[6] != 0.0 ? 1 : 0; ad.maximize = 0;
-    HIP_LAUNCH_CHECK(pdrnn_adam_partials(&ad, work.data_ptr<float>(), split, L.P + PH, flat_grad.data_ptr<float>(),
+    HIP_LAUNCH_CHECK(pdrnn_adam_partials(&ad, work.data_ptr<float>(), split, P_rnn + PH, flat_grad.data_ptr<float>(),
                                          stats.data_ptr<float>(), 3, st));
     return;
   }
-  HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), gridb, L.P, head_slab.data_ptr<float>(), B, PH,
+  HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,
                                       P_params, flat_grad.data_ptr<float>(), stats.data_ptr<float>(),
-                                      work.data_ptr<float>(), split, st));
+                                      work.data_ptr<float>(), split, colmap, L.P, st));
 }
 
 std::vector<Tensor> xent_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore_index, bool need_grad) {
@@ -674,7 +684,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("idx"), py::arg("labels"), py::arg("w"), py::arg("head_w"), py::arg("head_b"),
         py::arg("flat_grad"), py::arg("stats"), py::arg("H"), py::arg("NL"), py::arg("split_fwd"),
         py::arg("split_bwd"), py::arg("nb_fwd"), py::arg("nb_bwd"), py::arg("adam_state") = py::none(),
-        py::arg("adam_hp") = py::none());
+        py::arg("adam_hp") = py::none(), py::arg("cell") = 0, py::arg("grad_colmap") = py::none());
   m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
   m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer", py::arg("param"), py::arg("grad"),

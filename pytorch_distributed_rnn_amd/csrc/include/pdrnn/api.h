@@ -104,11 +104,15 @@ hipError_t pdrnn_slab_reduce(const float* slab, int64_t rows, int64_t P, float* 
 // Two slabs reduced side by side (columns of A then of B); the first n_out
 // summed columns go to out, the rest to out_tail.
 hipError_t pdrnn_slab2_reduce(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB, int64_t PB,
-                              int64_t n_out, float* out, float* out_tail, float* work, int split, hipStream_t stream);
+                              int64_t n_out, float* out, float* out_tail, float* work, int split, const int* colmap,
+                              int64_t ldA, hipStream_t stream);
 // First pass only (work[split][PA+PB] partial column sums); the second pass
 // can be fused into its consumer (pdrnn_adam_partials).
+// colmap (optional, with ldA = A's leading dimension): output column p < PA
+// reads A column colmap[p] (GRU packed layout -> nn.GRU order); NULL = identity
 hipError_t pdrnn_slab2_reduce_pass1(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB,
-                                   int64_t PB, float* work, int split, hipStream_t stream);
+                                   int64_t PB, float* work, int split, const int* colmap, int64_t ldA,
+                                   hipStream_t stream);
 // Same, with columns [P_a, P) written to out_b instead (e.g. loss statistics).
 hipError_t pdrnn_slab_reduce2(const float* slab, int64_t rows, int64_t P, int64_t P_a, float* out_a,
                               float* out_b, float* work, int split, hipStream_t stream);

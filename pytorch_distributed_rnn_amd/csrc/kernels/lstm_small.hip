@@ -1134,17 +1134,21 @@ __global__ void slab_reduce_pass2(const float* __restrict__ work, int64_t P, int
   out[p] = beta == 0.f ? acc : fmaf(beta, out[p], acc);
 }
 
-// pass 1 over two slabs side by side: columns [0, PA) from A, [PA, PA+PB) from B
+// pass 1 over two slabs side by side: columns [0, PA) from A, [PA, PA+PB) from B.
+// colmap (optional): output column p < PA reads A column colmap[p] of an A
+// slab with leading dimension ldA (the GRU's packed 4-block layout -> nn.GRU
+// parameter order, zero blocks dropped).
 __global__ void slab2_reduce_pass1(const float* __restrict__ A, int64_t rowsA, int64_t PA,
                                    const float* __restrict__ Bs, int64_t rowsB, int64_t PB,
-                                   float* __restrict__ work, int split) {
+                                   float* __restrict__ work, int split, const int* __restrict__ colmap,
+                                   int64_t ldA) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int sp = blockIdx.y;
   const int64_t P = PA + PB;
   if (p >= P) return;
   const bool inA = p < PA;
-  const float* src = inA ? A + p : Bs + (p - PA);
-  const int64_t ld = inA ? PA : PB;
+  const float* src = inA ? A + (colmap ? colmap[p] : p) : Bs + (p - PA);
+  const int64_t ld = inA ? ldA : PB;
   const int64_t rows = inA ? rowsA : rowsB;
   const int64_t r0 = rows * sp / split, r1 = rows * (sp + 1) / split;
   float acc0 = 0.f, acc1 = 0.f;
@@ -1184,15 +1188,25 @@ hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
 template <int H, int NB, bool SAVE>
 hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st);
 
-// GRU forward: one sequence per workgroup, no fused head.
+// GRU forward: one sequence per workgroup; the classifier head + CE epilogue
+// of the fused training step (SAVE + head_w) is shared with the LSTM.
 template <int H, bool SAVE>
 hipError_t launch_fwd_gs_gru(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   const int grid = a->B;
   const int block = a->NL * 4 * H;
   const size_t lds = sizeof(float) * a->NL * 2 * (2 * H);
   const size_t xbytes = sizeof(float) * (size_t)a->T * H;
-  if (a->head_w) return hipErrorInvalidValue;
-  if (xbytes <= (size_t)kXldsBytes)
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  if (a->head_w) {
+    if constexpr (SAVE) {
+      if (a->C > 16) return hipErrorInvalidValue;
+      if (xl) hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, 1, true, true, true, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+      else hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, 1, true, false, true, 1>), dim3(grid), dim3(block), lds, st, *a);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
+  if (xl)
     hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, 1, SAVE, true, false, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
   else
     hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, 1, SAVE, false, false, 1>), dim3(grid), dim3(block), lds, st, *a);
@@ -1280,10 +1294,14 @@ hipError_t launch_bwd_gs_gru(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int
   const int block = a->NL * H * L;
   const size_t lds = bwd_gs_lds<H, 1>(a->NL), xbytes = bwd_gs_xbytes<H, 1>(a->T);
   if (grid <= 0) grid = bwd_gs_grid<H, L, 1>(a);
-  if (xbytes <= (size_t)kXldsBytes)
-    hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, 1, true, false, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
-  else
-    hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, 1, false, false, 1>), dim3(grid), dim3(block), lds, st, *a);
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  if (bwd_lean(a)) {  // fused training step: zero initial state, loss through h_T only
+    if (xl) hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, 1, true, true, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+    else hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, 1, false, true, 1>), dim3(grid), dim3(block), lds, st, *a);
+  } else {
+    if (xl) hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, 1, true, false, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+    else hipLaunchKernelGGL((lstm_small_bwd_gs_kernel<H, L, 1, false, false, 1>), dim3(grid), dim3(block), lds, st, *a);
+  }
   return hipGetLastError();
 }
 
@@ -1530,24 +1548,28 @@ hipError_t pdrnn_slab_reduce2(const float* slab, int64_t rows, int64_t P, int64_
 }
 
 hipError_t pdrnn_slab2_reduce_pass1(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB,
-                                   int64_t PB, float* work, int split, hipStream_t stream) {
+                                   int64_t PB, float* work, int split, const int* colmap, int64_t ldA,
+                                   hipStream_t stream) {
   if (split < 1) split = 1;
   if (split > 64) split = 64;
   const int64_t P = PA + PB;
   const int threads = 256;
   dim3 g1((unsigned)((P + threads - 1) / threads), (unsigned)split);
-  hipLaunchKernelGGL(pdrnn::slab2_reduce_pass1, g1, dim3(threads), 0, stream, A, rowsA, PA, Bs, rowsB, PB, work, split);
+  hipLaunchKernelGGL(pdrnn::slab2_reduce_pass1, g1, dim3(threads), 0, stream, A, rowsA, PA, Bs, rowsB, PB, work, split,
+                     colmap, colmap ? ldA : PA);
   return hipGetLastError();
 }
 
 hipError_t pdrnn_slab2_reduce(const float* A, int64_t rowsA, int64_t PA, const float* Bs, int64_t rowsB, int64_t PB,
-                              int64_t n_out, float* out, float* out_tail, float* work, int split, hipStream_t stream) {
+                              int64_t n_out, float* out, float* out_tail, float* work, int split, const int* colmap,
+                              int64_t ldA, hipStream_t stream) {
   if (split < 1) split = 1;
   if (split > 64) split = 64;
   const int64_t P = PA + PB;
   const int threads = 256;
   dim3 g1((unsigned)((P + threads - 1) / threads), (unsigned)split);
-  hipLaunchKernelGGL(pdrnn::slab2_reduce_pass1, g1, dim3(threads), 0, stream, A, rowsA, PA, Bs, rowsB, PB, work, split);
+  hipLaunchKernelGGL(pdrnn::slab2_reduce_pass1, g1, dim3(threads), 0, stream, A, rowsA, PA, Bs, rowsB, PB, work, split,
+                     colmap, colmap ? ldA : PA);
   PDRNN_HIP_CHECK(hipGetLastError());
   dim3 g2((unsigned)((P + threads - 1) / threads));
   hipLaunchKernelGGL(pdrnn::slab_reduce_pass2_split, g2, dim3(threads), 0, stream, work, P, n_out, split, out, out_tail);

@@ -35,11 +35,39 @@ def fused_small_supported(x: Tensor, hidden: int, num_layers: int) -> bool:
 def gru_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor] = None, *,
                 hidden: int, num_layers: int, batch_first: bool = False, dropout: float = 0.0,
                 training: bool = False) -> Tuple[Tensor, Tensor]:
-    if dropout == 0.0 and fused_small_supported(x, hidden, num_layers):
+    drop = dropout if training else 0.0
+    if x.dtype == torch.float32:
         from .gru_fused import fused_gru
-        return fused_gru(x, weights, h0, hidden=hidden, num_layers=num_layers, batch_first=batch_first)
+        from .lstm import _pad_state, pad_gate_rows, small_plan
+        plan = small_plan(x, hidden, num_layers, cell="gru", per_layer=drop > 0, batch_first=batch_first)
+        if plan is not None:
+            hp, chunks = plan
+            if hp == hidden and len(chunks) == 1:
+                return fused_gru(x, weights, h0, hidden=hidden, num_layers=num_layers, batch_first=batch_first)
+            # zero-padded units: r = z = 1/2, n = tanh(0) = 0 -> h stays exactly 0
+            h, hns = x, []
+            for k, (l0, n) in enumerate(chunks):
+                ws = list(weights[4 * l0:4 * (l0 + n)])
+                if hp != hidden:
+                    for j in range(n):
+                        in_pad = None if l0 + j == 0 else hp
+                        ws[4 * j:4 * j + 4] = [pad_gate_rows(ws[4 * j], hidden, hp, 3, in_pad),
+                                               pad_gate_rows(ws[4 * j + 1], hidden, hp, 3, hp),
+                                               pad_gate_rows(ws[4 * j + 2], hidden, hp, 3),
+                                               pad_gate_rows(ws[4 * j + 3], hidden, hp, 3)]
+                hh = _pad_state(h0[l0:l0 + n], hidden, hp) if h0 is not None else None
+                out, hn = fused_gru(h, ws, hh, hidden=hp, num_layers=n, batch_first=batch_first)
+                hns.append(hn)
+                if k < len(chunks) - 1 and drop > 0:
+                    out = torch.nn.functional.dropout(out, drop, True)
+                h = out
+            hn = torch.cat(hns)
+            if hp != hidden:
+                h, hn = h[..., :hidden], hn[..., :hidden]
+            return h, hn
     from . import gru_large
     if gru_large.supported(x, hidden):
         return gru_large.gru_large_forward(x, weights, h0, hidden=hidden, num_layers=num_layers,
                                            batch_first=batch_first, dropout=dropout, training=training)
+    _ext.fallback(f"GRU(H={hidden}, I={x.shape[-1]}, layers={num_layers}, {x.dtype})", x.device)
     return gru_reference(x, weights, h0, hidden, num_layers, batch_first, dropout, training)

@@ -35,6 +35,9 @@ def supported(x: Tensor, hidden: int, num_layers: int) -> bool:
 
 
 _ZEROS: Dict[Tuple[torch.device, torch.dtype], Tensor] = {}
+# superseded zero vectors stay referenced: a cat on another stream may still
+# be reading one (they are never written, so sharing is safe; a few KB each)
+_RETIRED: List[Tensor] = []
 _UNPACK: Dict[Tuple[int, Tuple[int, ...], torch.device], Tensor] = {}
 
 
@@ -43,6 +46,8 @@ def _zeros(like: Tensor, n: int) -> Tensor:
     key = (like.device, like.dtype)
     z = _ZEROS.get(key)
     if z is None or z.numel() < n:
+        if z is not None:
+            _RETIRED.append(z)
         z = like.new_zeros(max(n, 1024))
         _ZEROS[key] = z
     return z[:n]

@@ -159,6 +159,89 @@ def lstm_reference(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[
     return out, hn, cn
 
 
+_SMALL_H = (16, 32, 64)
+
+
+def small_plan(x: Tensor, hidden: int, num_layers: int, *, cell: str = "lstm", per_layer: bool = False,
+               batch_first: bool = True) -> Optional[Tuple[int, List[Tuple[int, int]]]]:
+    """How the fused small-H kernels cover an arbitrary unidirectional stack:
+    ``(H_pad, [(first_layer, n_layers), ...])`` or None.
+
+    * hidden sizes the kernels are not instantiated for (8, 24, 48, ...) run
+      zero-padded to the next of 16/32/64: padded units have zero weights and
+      bias, so i=f=o=1/2, g=0 -> c and h stay exactly 0 and never touch a real
+      unit (their W columns are zero); padded gradients are dropped;
+    * stacks deeper than one launch holds (4 layers, 512 lanes) run as chunks
+      of layers, each chunk's top output feeding the next (``per_layer``: one
+      layer per launch, e.g. nn.LSTM dropout between layers)."""
+    if x.dim() != 3 or x.dtype not in (torch.float32, torch.bfloat16):
+        return None
+    mod = _ext.native(x.device)
+    if mod is None:
+        return None
+    I = x.shape[-1]
+    T = x.shape[1 if batch_first else 0]
+    for hp in _SMALL_H:
+        if hp < hidden or hp < I:
+            continue
+        if x.dtype == torch.bfloat16 and T * hp * 4 > 48 * 1024:
+            continue  # bf16 x is widened while staging into LDS: the sequence must fit there
+        chunks, l = [], 0
+        while l < num_layers:
+            n = 1 if per_layer else min(4, num_layers - l)
+            while n > 0 and not _chunk_ok(mod, cell, hp, I if l == 0 else hp, n):
+                n -= 1
+            if n == 0:
+                break
+            chunks.append((l, n))
+            l += n
+        if l == num_layers:
+            return hp, chunks
+    return None
+
+
+def _chunk_ok(mod, cell: str, hp: int, in_dim: int, n: int) -> bool:
+    if not mod.lstm_small_supported(hp, in_dim, n):
+        return False
+    if cell == "gru":  # GRU: gate-split forward and unit-group backward maps only
+        return n * 4 * hp <= 512 and n * hp * (8 if hp >= 64 else 4) <= 512
+    return True
+
+
+def pad_gate_rows(w: Optional[Tensor], hidden: int, hp: int, gates: int, in_pad: Optional[int] = None):
+    """[gates*H, I] -> [gates*hp, in_pad] (or [gates*H] -> [gates*hp]) with zero
+    rows/columns; differentiable (the gradient of the real block flows back)."""
+    if w is None:
+        return None
+    if w.dim() == 1:
+        return torch.nn.functional.pad(w.view(gates, hidden), (0, hp - hidden)).reshape(gates * hp)
+    i = w.shape[1]
+    ip = i if in_pad is None else in_pad
+    return torch.nn.functional.pad(w.view(gates, hidden, i), (0, ip - i, 0, hp - hidden)).reshape(gates * hp, ip)
+
+
+def _pad_state(s: Optional[Tensor], hidden: int, hp: int) -> Optional[Tensor]:
+    if s is None or hp == hidden:
+        return s
+    return torch.nn.functional.pad(s, (0, hp - hidden))
+
+
+def _run_small_chunk(x, idx, h0, c0, ws, hidden, n, batch_first, need_out):
+    flat = _flat_weights(ws, n, hidden, x)
+    needs_grad = torch.is_grad_enabled() and (
+        x.requires_grad or any(w.requires_grad for w in flat)
+        or (h0 is not None and h0.requires_grad) or (c0 is not None and c0.requires_grad))
+    if needs_grad:
+        return _FusedSmallLSTM.apply(x, idx, h0, c0, (hidden, n, batch_first, need_out), *flat)
+    mod = _ext.native(x.device)
+    nb_fwd, sp_fwd, _, _ = small_launch_config(
+        idx.numel() if idx is not None else (x.shape[0] if batch_first else x.shape[1]), hidden, n)
+    out, hn, cn, _ = mod.lstm_small_fwd(
+        x, idx, flat, h0.contiguous() if h0 is not None else None,
+        c0.contiguous() if c0 is not None else None, hidden, n, batch_first, False, need_out, nb_fwd, sp_fwd)
+    return out, hn, cn
+
+
 def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor] = None,
                  c0: Optional[Tensor] = None, *, hidden: int, num_layers: int,
                  batch_first: bool = False, need_out: bool = True, idx: Optional[Tensor] = None,
@@ -169,25 +252,39 @@ def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Te
     ``idx`` (optional) gathers batch rows from ``x`` (a device-resident dataset)
     inside the kernel; ``need_out=False`` lets inference skip the per-timestep
     output stream when only h_n is consumed."""
-    if (not bidirectional and dropout == 0.0
-            and fused_small_supported(x, hidden, num_layers, bidirectional, batch_first=batch_first)):
-        flat = _flat_weights(weights, num_layers, hidden, x)
-        needs_grad = torch.is_grad_enabled() and (
-            x.requires_grad or any(w.requires_grad for w in flat)
-            or (h0 is not None and h0.requires_grad) or (c0 is not None and c0.requires_grad))
-        if needs_grad:
-            out, hn, cn = _FusedSmallLSTM.apply(
-                x, idx, h0, c0, (hidden, num_layers, batch_first, need_out), *flat)
-            return out, hn, cn
-        mod = _ext.native(x.device)
-        nb_fwd, sp_fwd, _, _ = small_launch_config(
-            idx.numel() if idx is not None else (x.shape[0] if batch_first else x.shape[1]), hidden,
-            num_layers)
-        out, hn, cn, _ = mod.lstm_small_fwd(
-            x, idx, flat, h0.contiguous() if h0 is not None else None,
-            c0.contiguous() if c0 is not None else None, hidden, num_layers, batch_first, False,
-            need_out, nb_fwd, sp_fwd)
-        return out, hn, cn
+    drop = dropout if training else 0.0
+    plan = None if bidirectional else small_plan(x, hidden, num_layers, per_layer=drop > 0,
+                                                 batch_first=batch_first)
+    if plan is not None:
+        hp, chunks = plan
+        if hp == hidden and len(chunks) == 1:
+            return _run_small_chunk(x, idx, h0, c0, list(weights), hidden, num_layers, batch_first, need_out)
+        h, hns, cns = x, [], []
+        for k, (l0, n) in enumerate(chunks):
+            ws = list(weights[4 * l0:4 * (l0 + n)])
+            if hp != hidden:
+                for j in range(n):
+                    in_pad = None if l0 + j == 0 else hp
+                    ws[4 * j:4 * j + 4] = [pad_gate_rows(ws[4 * j], hidden, hp, 4, in_pad),
+                                           pad_gate_rows(ws[4 * j + 1], hidden, hp, 4, hp),
+                                           pad_gate_rows(ws[4 * j + 2], hidden, hp, 4),
+                                           pad_gate_rows(ws[4 * j + 3], hidden, hp, 4)]
+            last = k == len(chunks) - 1
+            out, hn, cn = _run_small_chunk(
+                h, idx if l0 == 0 else None,
+                _pad_state(h0[l0:l0 + n], hidden, hp) if h0 is not None else None,
+                _pad_state(c0[l0:l0 + n], hidden, hp) if c0 is not None else None,
+                ws, hp, n, batch_first, need_out or not last)
+            hns.append(hn)
+            cns.append(cn)
+            if not last and drop > 0:
+                out = torch.nn.functional.dropout(out, drop, True)
+            h = out
+        hn, cn = torch.cat(hns), torch.cat(cns)
+        if hp != hidden:
+            hn, cn = hn[..., :hidden], cn[..., :hidden]
+            h = h[..., :hidden] if h is not None else None
+        return h, hn, cn
     from . import lstm_large
     if lstm_large.supported(x, hidden, num_layers):
         if idx is not None:
@@ -196,10 +293,64 @@ def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Te
                                              num_layers=num_layers, batch_first=batch_first,
                                              bidirectional=bidirectional, dropout=dropout,
                                              training=training)
+    _ext.fallback(f"LSTM(H={hidden}, I={x.shape[-1]}, layers={num_layers}, {x.dtype}, "
+                  f"bidirectional={bidirectional})", x.device)
     if idx is not None:
         x = x.index_select(0, idx)
     return lstm_reference(x, weights, h0, c0, hidden, num_layers, batch_first, dropout, training,
                           bidirectional)
+
+
+def _bidir_small_hp(x: Tensor, hidden: int, num_layers: int, batch_first: bool) -> Optional[int]:
+    """Padded hidden size for a bidirectional stack on the small-H kernels
+    (layer >= 1 consumes [fwd | bwd] = 2H features, which must fit the
+    kernel's input width <= H_pad), or None."""
+    if x.dim() != 3 or x.dtype not in (torch.float32, torch.bfloat16):
+        return None
+    mod = _ext.native(x.device)
+    if mod is None:
+        return None
+    I, T = x.shape[-1], x.shape[1 if batch_first else 0]
+    for hp in _SMALL_H:
+        if hp < hidden or hp < I or (num_layers > 1 and hp < 2 * hidden):
+            continue
+        if x.dtype == torch.bfloat16 and T * hp * 4 > 48 * 1024:
+            continue
+        if all(_chunk_ok(mod, "lstm", hp, I if l == 0 else hp, 1) for l in range(num_layers)):
+            return hp
+    return None
+
+
+def _bidir_small(x, ws, h0, c0, hidden, hp, num_layers, batch_first, drop):
+    """Stacked bidirectional LSTM on the fused kernels: per layer, the forward
+    direction runs on x and the reverse direction on time-reversed x (one
+    single-layer launch each), outputs concatenated [fwd | bwd] like nn.LSTM."""
+    tdim = 1 if batch_first else 0
+    h, hns, cns = x, [], []
+    for l in range(num_layers):
+        outs = []
+        for d in range(2):
+            k = 2 * l + d
+            w = ws[4 * k:4 * k + 4]
+            in_pad = None if l == 0 else hp
+            w = [pad_gate_rows(w[0], hidden, hp, 4, in_pad if in_pad != w[0].shape[1] else None),
+                 pad_gate_rows(w[1], hidden, hp, 4, hp),
+                 pad_gate_rows(w[2], hidden, hp, 4), pad_gate_rows(w[3], hidden, hp, 4)]
+            inp = h if d == 0 else h.flip(tdim)
+            hh = _pad_state(h0[k:k + 1], hidden, hp) if h0 is not None else None
+            cc = _pad_state(c0[k:k + 1], hidden, hp) if c0 is not None else None
+            out, hn, cn = _run_small_chunk(inp, None, hh, cc, w, hp, 1, batch_first, True)
+            out = out[..., :hidden]
+            outs.append(out if d == 0 else out.flip(tdim))
+            hns.append(hn[..., :hidden])
+            cns.append(cn[..., :hidden])
+        h = torch.cat(outs, dim=-1)
+        if l < num_layers - 1:
+            if h.shape[-1] < hp:  # next layer's input width: zero columns up to H_pad
+                h = torch.nn.functional.pad(h, (0, hp - h.shape[-1]))
+            if drop > 0:
+                h = torch.nn.functional.dropout(h, drop, True)
+    return h, torch.cat(hns), torch.cat(cns)
 
 
 def lstm_bidirectional_forward(x: Tensor, all_weights: Sequence[Tensor], h0: Optional[Tensor],
@@ -221,5 +372,9 @@ def lstm_bidirectional_forward(x: Tensor, all_weights: Sequence[Tensor], h0: Opt
         if not has_bias:
             chunk += [None, None]
         ws += chunk
+    hp = _bidir_small_hp(x, hidden, num_layers, batch_first)
+    if hp is not None:
+        return _bidir_small(x, ws, h0, c0, hidden, hp, num_layers, batch_first, dropout if training else 0.0)
+    _ext.fallback(f"bidirectional LSTM(H={hidden}, I={x.shape[-1]}, layers={num_layers}, {x.dtype})", x.device)
     return lstm_reference(x, ws, h0, c0, hidden, num_layers, batch_first, dropout, training,
                           bidirectional=True)
