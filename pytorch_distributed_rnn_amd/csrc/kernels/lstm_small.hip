@@ -827,11 +827,16 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
   float* const dc0p = LEAN ? nullptr : a.dc0;
   const bool top_only = LEAN ? true : a.dhn_top_only;
 
-  // LDS: dg[NB][NL][2][R] | dha[NB][NL][2][H] | xs[NB][T][H]
+  // LDS: dg[NB][NL][2][RP] | dha[NB][NL][2][H] | xs[NB][T][H]
+  // The gate-gradient vector is stored with a 4-float pad after every RS-row
+  // slice: the L lanes of a unit read slices j*RS.. as float4s, and with an
+  // unpadded RS = 32 slices j and j + 2 hit the same banks (2-way conflict,
+  // ~150 cycles per step, profiles/r2_small_kernels_pmc.md).
+  constexpr int RP = R + L * 4;
   float* dg_s = smem;
-  float* dha_s = dg_s + NB * NL * 2 * R;
+  float* dha_s = dg_s + NB * NL * 2 * RP;
   float* xs = dha_s + NB * NL * 2 * H;
-  auto dgbuf = [&](int n, int l, int p) { return dg_s + ((n * NL + l) * 2 + p) * R; };
+  auto dgbuf = [&](int n, int l, int p) { return dg_s + ((n * NL + l) * 2 + p) * RP; };
   auto dhabuf = [&](int n, int l, int p) { return dha_s + ((n * NL + l) * 2 + p) * H; };
 
   // ---- W columns (u) for rows j*RS.., as float2 pairs along rows ----------
@@ -985,7 +990,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
         dgv = active ? dgv : 0.f;  // inactive: zero gate gradients (dW, db, dh unaffected)
         dc[n] = active ? dcn : dc[n];
         if (L == 4 || rowlane) {
-          dgbuf(n, layer, p)[q * H + u] = dgv;
+          dgbuf(n, layer, p)[q * H + u + ((q * H + u) / RS) * 4] = dgv;
           db += valid[n] ? dgv : 0.f;
         }
       }
@@ -1003,7 +1008,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
         const float xin = (XLDS && layer == 0) ? xsv : xgv;
         // an invalid slot still runs the recurrence but contributes nothing to dW
         const float hw = valid[n] ? hprev : 0.f, xw = valid[n] ? xin : 0.f;
-        const float4* g4 = reinterpret_cast<const float4*>(dgbuf(n, layer, p) + r0);
+        const float4* g4 = reinterpret_cast<const float4*>(dgbuf(n, layer, p) + r0 + j * 4);
         // all of this lane's gate-gradient slice in flight at once: one
         // LDS latency per step instead of one per read batch
         float4 gv[RS / 4];
@@ -1268,7 +1273,10 @@ int bwd_gs_resident(int NL, size_t lds) {
 }
 
 template <int H, int NB>
-size_t bwd_gs_lds(int NL) { return sizeof(float) * NB * NL * 2 * (4 * H + H); }
+size_t bwd_gs_lds(int NL) {
+  // dg slices padded by 4 floats per lane slice (L <= 8 lanes per unit)
+  return sizeof(float) * NB * NL * 2 * (4 * H + 8 * 4 + H);
+}
 template <int H, int NB>
 size_t bwd_gs_xbytes(int T) { return sizeof(float) * (size_t)NB * T * H; }
 
@@ -1366,6 +1374,7 @@ hipError_t dispatch_fwd(const PdrnnLstmSmallFwdArgs* a, int nb, int split, int s
   if (a->cell == 1 && split != 1) return hipErrorInvalidConfiguration;  // GRU: gate-split map only
   if (split == 1) {  // gate-split map (4 lanes per unit, one gate each)
     if (a->NL * 4 * H > 512) return hipErrorInvalidConfiguration;
+
     if (a->cell == 1) return save ? launch_fwd_gs_gru<H, true>(a, st) : launch_fwd_gs_gru<H, false>(a, st);
     if (save) return nb == 2 ? launch_fwd_gs<H, 2, true>(a, st) : launch_fwd_gs<H, 1, true>(a, st);
     return nb == 2 ? launch_fwd_gs<H, 2, false>(a, st) : launch_fwd_gs<H, 1, false>(a, st);

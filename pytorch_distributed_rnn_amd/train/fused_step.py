@@ -41,8 +41,10 @@ def supported(model: nn.Module, optimizer, device: torch.device) -> bool:
     from ..models.motion import MotionModel
     from ..ops.adam import FusedAdam
     m = _inner(model)
-    if device.type != "cuda" or not isinstance(m, MotionModel) or m.cell != "lstm":
+    if device.type != "cuda" or not isinstance(m, MotionModel) or m.cell not in ("lstm", "gru"):
         return False
+    if m.cell == "gru" and getattr(m, "compute_dtype", torch.float32) != torch.float32:
+        return False  # the GRU step runs the fp32 kernels only
     if not isinstance(optimizer, FusedAdam):
         return False
     mod = _ext.native(device)
@@ -56,6 +58,10 @@ def supported(model: nn.Module, optimizer, device: torch.device) -> bool:
     if mod.lstm_small_max_split(lstm.hidden_size, lstm.num_layers, False) != 1 or \
             mod.lstm_small_max_split(lstm.hidden_size, lstm.num_layers, True) != 1:
         return False
+    if m.cell == "gru":
+        H, NL = lstm.hidden_size, lstm.num_layers
+        if NL * 4 * H > 512 or NL * H * (8 if H >= 64 else 4) > 512:
+            return False
     params = list(m.parameters())
     if any(p.dtype != torch.float32 for p in params):
         return False
@@ -94,6 +100,10 @@ class MotionTrainStep:
         self.mod = _ext.native(next(self.m.parameters()).device)
         lstm = self.m.lstm
         self.H, self.NL = lstm.hidden_size, lstm.num_layers
+        # GRU: the kernels run nn.GRU's parameters packed as [r | z | n_x | n_h]
+        # 4-block stacks (ops/gru_fused.py); the reduction writes gradients
+        # back in nn.GRU order through a column map
+        self.gru = getattr(self.m, "cell", "lstm") == "gru"
         self.weights = []
         for l in range(self.NL):
             self.weights += [getattr(lstm, f"weight_ih_l{l}"), getattr(lstm, f"weight_hh_l{l}"),
@@ -109,6 +119,11 @@ class MotionTrainStep:
         # bf16 model: recurrent weights used rounded to bf16 (one cast of the
         # flat master buffer per step); gradients land on the fp32 masters
         self.bf16 = getattr(self.m, "compute_dtype", torch.float32) == torch.bfloat16
+        self.colmap = None
+        if self.gru:
+            from ..ops.gru_fused import _unpack_index
+            in_dims = tuple(int(self.weights[4 * l].shape[1]) for l in range(self.NL))
+            self.colmap = _unpack_index(self.H, in_dims, self.flat.grad.device).to(torch.int32)
         base = self.flat.data.data_ptr()
         self._offs = [((w.data_ptr() - base) // 4, w.shape) for w in self.weights]
         if cuda_graph is None:
@@ -150,27 +165,34 @@ class MotionTrainStep:
         self.flat.attach_grads()
         batch = idx.numel() if idx is not None else features.shape[0]
         nb_fwd, _, nb_bwd, _ = small_launch_config(batch, self.H, self.NL)
+        if self.gru:
+            nb_fwd = nb_bwd = 1
         hw, hb = self.m.fc.weight, self.m.fc.bias  # the classifier head stays fp32
         if self.bf16:
             ws = self._rounded()
             if features.dtype != torch.bfloat16:
                 features = features.to(torch.bfloat16)
+        elif self.gru:
+            from ..ops.gru_fused import _pack
+            ws = _pack(self.weights, self.NL, self.H, self.flat.data)
         else:
             ws = self.weights
+        cell = 1 if self.gru else 0
         stats = self.ring[self._slot]
         self._slot = (self._slot + 1) % self.RING
         adam = self._flat_adam()
         if adam is not None and self.grad_sync is None:
             with trace_range("pdrnn.fwd_bwd_adam"):
                 self.mod.lstm_head_train_step(features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H,
-                                              self.NL, 0, 0, nb_fwd, nb_bwd, adam[0], adam[1])
+                                              self.NL, 0, 0, nb_fwd, nb_bwd, adam[0], adam[1], cell, self.colmap)
             return stats
         if self.grad_sync is not None and adam is not None and self.cuda_graph:
             if self._graph_step(features, labels, idx, ws, nb_fwd, nb_bwd, adam, stats):
                 return stats
         with trace_range("pdrnn.fwd_bwd"):
             self.mod.lstm_head_train_step(
-                features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd)
+                features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd,
+                None, None, cell, self.colmap)
         if self.grad_sync is not None:
             with trace_range("pdrnn.grad_allreduce"):
                 self.grad_sync()
@@ -190,8 +212,8 @@ class MotionTrainStep:
         the bf16 model (its per-step weight cast allocates), and the first two
         steps after a (re)configuration, so that RCCL's lazy connection setup
         and the kernels' first-use allocations happen outside the capture."""
-        if self.bf16:
-            return False
+        if self.bf16 or self.gru:
+            return False  # per-step weight cast / packing allocates
         (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
         key = (features.data_ptr(), tuple(features.shape), features.dtype, labels.data_ptr(), labels.numel(),
                None if idx is None else (idx.numel(), idx.dtype), nb_fwd, nb_bwd, lr, b1, b2, eps, wd, dec,

@@ -15,12 +15,13 @@ def _trainer(model, data, fused: bool):
     return t
 
 
-def test_fused_step_matches_autograd():
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+def test_fused_step_matches_autograd(cell):
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     torch.manual_seed(0)
     train, _, _ = synthetic_motion(n_train=384, n_validation=2, n_test=2, seed=3)
-    m1 = MotionModel(9, 32, 2, 6)
+    m1 = MotionModel(9, 32, 2, 6, cell=cell)
     m2 = copy.deepcopy(m1)
     t1, t2 = _trainer(m1, train, True), _trainer(m2, train, False)
     assert t1._fused_step() is not None, "fused step not selected on GPU"
