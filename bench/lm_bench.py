@@ -49,6 +49,10 @@ def parse(argv=None):
     ap.add_argument("--hidden", type=int, default=None)
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--input-dim", type=int, default=1024, help="bilstm input features")
+    ap.add_argument("--ddp", action="store_true",
+                    help="charlm: bucketed DDP reducer even at one rank (overlap traces with "
+                         "PDRNN_FORCE_COLLECTIVE=1)")
+    ap.add_argument("--bucket-mb", type=float, default=None)
     return ap.parse_args(argv)
 
 
@@ -62,7 +66,8 @@ def main(argv=None):
         B, T, H = a.batch or 128, a.seq_len or 512, a.hidden or 1024
         corpus = CharCorpus.synthetic(B * world * T * (a.steps + a.warmup + 2) + 1, 256, seed=0)
         tr = LMTrainer(CharLM(256, 256, H, a.layers, 0.0, torch.bfloat16), corpus, B, T, 2e-3, device=dev,
-                       distributed=world > 1, weak_scaling=True)
+                       distributed=world > 1 or a.ddp, weak_scaling=True, force_ddp=a.ddp,
+                       bucket_cap_mb=a.bucket_mb)
         segs = list(CharCorpus.segments(tr.streams, T, a.steps + a.warmup))
         tr.inner.reset_hidden_state()
         step = lambda i: tr.train_step(*segs[i])  # noqa: E731
@@ -111,7 +116,8 @@ def main(argv=None):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
             "data": "synthetic", "config": {"model": model_name, "global_batch": B * world, "seq_len": T,
                                             "parallelism": f"dp{world}"},
-            "final_loss": round(float(loss), 5), "device_peak_mib": round(device_peak_mib(dev), 1)}), flush=True)
+            "final_loss": round(float(loss), 5), "device_peak_mib": round(device_peak_mib(dev), 1),
+            "ddp_reducer": a.config == "charlm" and isinstance(tr.model, DistributedDataParallel)}), flush=True)
     env.shutdown()
 
 

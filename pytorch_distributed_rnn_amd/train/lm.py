@@ -34,7 +34,7 @@ class LMTrainer:
                  learning_rate: float = 2e-3, device: Optional[torch.device] = None,
                  distributed: bool = False, backend: Optional[str] = None, grad_clip: float = 1.0,
                  log_interval: int = 50, bucket_cap_mb: Optional[float] = None,
-                 weak_scaling: bool = False):
+                 weak_scaling: bool = False, force_ddp: bool = False):
         self.rank, self.world = 0, 1
         if distributed:
             info = env.init_distributed(backend)
@@ -47,8 +47,11 @@ class LMTrainer:
         self.device = device
         self.inner = model.to(device)
         flatten_module(self.inner)
+        # force_ddp: keep the bucketed reducer at world size 1 (with
+        # PDRNN_FORCE_COLLECTIVE=1 every bucket is a real RCCL collective on
+        # the comm stream -- the overlap trace of profiles/r2_charlm_overlap.md)
         self.model = (DistributedDataParallel(self.inner, bucket_cap_mb=bucket_cap_mb)
-                      if distributed and self.world > 1 else self.inner)
+                      if distributed and (self.world > 1 or force_ddp) else self.inner)
         self.flat = next(iter(self.inner._pdrnn_flat.values()))
         self.optimizer = FusedAdam(self.inner.parameters(), lr=learning_rate)
         self.seq_len = seq_len
