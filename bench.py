@@ -103,6 +103,10 @@ def main(argv=None):
 
     stream = index_stream()
     trainer.model.train()
+    # one-time device setup (kernel code-object load, workspace sizing): the
+    # trainer's gradient-only pre-pass, no parameter update -- the same
+    # preparation the CLI runs before its timed epochs
+    trainer.prepare()
     for _ in range(args.warmup):
         trainer.train_batch(loader.make_batch(next(stream)))
     # the sampler's host-side permutations are drawn up front; the batch

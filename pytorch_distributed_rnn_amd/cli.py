@@ -86,6 +86,8 @@ def build_parser(script_dir: Optional[Path] = None) -> argparse.ArgumentParser:
     p.add_argument("--fault-drop-step", default=-1, type=int,
                    help="the --fault-rank rank(s) exit abruptly at this training step (failure-detection test)")
     p.add_argument("--history-file", default="history.json", type=Path)
+    p.add_argument("--no-warmup", action="store_true",
+                   help="charge kernel loading / workspace sizing to the first timed epoch")
 
     sub = p.add_subparsers(title="Available commands", metavar="command [options ...]")
     sub.required = True
@@ -156,7 +158,8 @@ def train(args, name: str):
     kw = dict(model=model, training_set=training_set, validation_set=validation_set,
               test_set=test_set, batch_size=args.batch_size, learning_rate=args.learning_rate,
               checkpoint_dir=args.checkpoint_directory, log_interval=args.log_interval,
-              checkpoint_every=args.checkpoint_every, cuda_graph=True if args.cuda_graph else None)
+              checkpoint_every=args.checkpoint_every, cuda_graph=True if args.cuda_graph else None,
+              warmup=not args.no_warmup)
     if args.device == "cpu":
         kw["device"] = torch.device("cpu")
     if name != "local":

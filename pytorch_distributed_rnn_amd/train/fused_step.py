@@ -205,6 +205,32 @@ class MotionTrainStep:
                 self.optimizer.step()
         return stats
 
+    def warmup(self, features: Tensor, labels: Tensor, idx: Optional[Tensor]) -> None:
+        """Forward + BPTT + gradient reduction of one batch with the result
+        discarded: loads the kernels' code objects and sizes the allocator's
+        workspace for this batch shape.  Parameters and optimizer state are not
+        touched; the flat gradient (fully rewritten by every step) is zeroed."""
+        from ..ops.lstm import small_launch_config
+        self.flat.attach_grads()
+        batch = idx.numel() if idx is not None else features.shape[0]
+        nb_fwd, _, nb_bwd, _ = small_launch_config(batch, self.H, self.NL)
+        if self.gru:
+            nb_fwd = nb_bwd = 1
+        if self.bf16:
+            ws = self._rounded()
+            if features.dtype != torch.bfloat16:
+                features = features.to(torch.bfloat16)
+        elif self.gru:
+            from ..ops.gru_fused import _pack
+            ws = _pack(self.weights, self.NL, self.H, self.flat.data)
+        else:
+            ws = self.weights
+        stats = torch.zeros(3, dtype=torch.float32, device=self.flat.grad.device)
+        self.mod.lstm_head_train_step(features, idx, labels, ws, self.m.fc.weight, self.m.fc.bias, self.flat.grad,
+                                      stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd, None, None,
+                                      1 if self.gru else 0, self.colmap)
+        self.flat.grad.zero_()
+
     # ------------------------------------------------------------ HIP graph
     def _graph_step(self, features: Tensor, labels: Tensor, idx: Optional[Tensor], ws, nb_fwd: int,
                     nb_bwd: int, adam, stats: Tensor) -> bool:

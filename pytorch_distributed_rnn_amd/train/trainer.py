@@ -57,8 +57,9 @@ class Trainer:
                  validation_set=None, test_set=None, checkpoint_dir: Optional[Path] = None,
                  sampler: Optional[ShardedSampler] = None, *, device: Optional[torch.device] = None,
                  log_interval: int = 0, checkpoint_every: int = 0, flatten: bool = True,
-                 cuda_graph: Optional[bool] = None):
+                 cuda_graph: Optional[bool] = None, warmup: bool = True):
         self.device = torch.device(device) if device is not None else default_device()
+        self.warmup = warmup
         # replay the synced fused step from a HIP graph (None: PDRNN_CUDA_GRAPH)
         self.cuda_graph = cuda_graph
         self.model = model.to(self.device)
@@ -123,6 +124,11 @@ class Trainer:
                 if self.checkpoint_every and (epoch + 1) % self.checkpoint_every == 0:
                     self._save_checkpoint(epoch, train_loss, best=False)
 
+        if self.warmup:
+            t0 = time.perf_counter()
+            self.prepare()
+            logging.info(f"Warm-up (kernel load, workspace sizing; no parameter update): "
+                         f"{time.perf_counter() - t0:.4f} s")
         mem.reset_device_peak(self.device if self.device.type == "cuda" else None)
         self.sequences_seen = 0
         mem.synchronize()
@@ -141,6 +147,31 @@ class Trainer:
 
     def world_size(self) -> int:
         return 1
+
+    def prepare(self) -> None:
+        """One-time device setup before the timed epochs: the fused step runs
+        a gradient-only pass (no optimizer update, gradients discarded) for
+        each batch shape of the epoch -- the full batch and the short last one
+        -- so that kernel code-object loading and the caching allocator's
+        first allocations are not charged to the first epoch.  A no-op on the
+        CPU / autograd path.  Disable with ``warmup=False`` (CLI
+        ``--no-warmup``)."""
+        fused = self._fused_step()
+        if fused is None:
+            return
+        loader = self.train_loader
+        n = loader.num_items
+        sizes = sorted({min(loader.batch_size, n), n % loader.batch_size or loader.batch_size})
+        self.model.train()
+        for b in sizes:
+            batch = loader.make_batch(torch.arange(b, device=loader.device))
+            if len(batch) == 3:
+                features, labels_all, idx = batch
+                fused.warmup(features, labels_all, idx)
+            else:
+                data, labels = batch
+                fused.warmup(data, labels.reshape(-1).contiguous(), None)
+        mem.synchronize()
 
     def _forward(self, batch) -> Tuple[Tensor, Tensor]:
         if len(batch) == 3:
