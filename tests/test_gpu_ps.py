@@ -1,0 +1,48 @@
+"""GPU: parameter-server mode with device-resident RPC payloads (TensorPipe
+device maps, trainer GPU <-> server GPU; reference hot path:
+src/motion/param_server/worker.py:46,52,91-94): the server's model runs on
+the HIP kernels, both trainers step it, the loss goes down.  Three processes
+share the box's one GPU (PS + 2 trainers)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from _mp import ROOT, batch_losses, free_port  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+MAIN = os.path.join(ROOT, "src", "motion", "main.py")
+
+
+@pytest.mark.parametrize("payload", ["device", "host"])
+def test_parameter_server_gpu_loss_decreases(tmp_path, payload):
+    port = str(free_port())
+    common = ["--seed", "1", "--epochs", "4", "--batch-size", "96", "--no-validation", "--synthetic",
+              "--synthetic-size", "384", "--log-interval", "1", "parameter-server", "--world-size", "3",
+              "--master-address", "127.0.0.1", "--master-port", port]
+    if payload == "host":
+        common.append("--ps-host-payloads")
+    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    procs = [subprocess.Popen([sys.executable, MAIN] + common + ["--rank", str(r)], cwd=str(tmp_path),
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(3)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=100)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in procs), "\n".join(o[-2500:] for o in outs)
+    per = batch_losses("\n".join(outs))
+    assert set(per) == {1, 2}, per  # both trainers stepped
+    for r, losses in per.items():
+        assert all(x == x for x in losses)
+        k = max(1, len(losses) // 4)
+        assert sum(losses[-k:]) / k < sum(losses[:k]) / k, (r, losses)  # learning on the server
