@@ -131,8 +131,25 @@ def main(argv=None):
     value = seqs / elapsed
     ms = elapsed / args.steps * 1e3
     base = BASELINE_SEQ_PER_S.get(world)
+    # one real epoch after the timed steps (every batch of the sampler's
+    # permutation, the short last one included), timed the same way: the
+    # reference's own metric is a 1-epoch duration (fabfile.py:48-66)
+    trainer.sampler.set_epoch(10_000)
+    epoch_batches = loader.batch_indices()
+    env.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for bidx in epoch_batches:
+        stats, _ = trainer.train_batch(loader.make_batch(bidx))
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    env.barrier()
+    te = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                      device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(te, op=dist.ReduceOp.MAX)
+    epoch_s = float(te.item())
     # sanity: loss must be finite after training
-    stats, _ = trainer.train_batch(loader.make_batch(timed[0]))
     loss = float(stats[0])
     if rank == 0:
         out = {
@@ -156,7 +173,8 @@ def main(argv=None):
                 "trainer": args.trainer,
                 "per_gpu_batch": per_rank,
             },
-            "epoch_time_s": round(EPOCH_SEQUENCES / value, 6),
+            "epoch_time_s": round(epoch_s, 6),
+            "epoch_sequences": n_train,
             "final_loss": round(loss, 6),
             "baseline_seq_per_s": base,
         }

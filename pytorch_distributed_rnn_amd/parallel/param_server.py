@@ -11,14 +11,13 @@ its gradients immediately (asynchronous, Hogwild-style -- no averaging).
 
 MI355X-native differences:
 
-* the server keeps the model (and the fused HIP LSTM kernels) on its GPU, and
-  on GPU nodes the RPC tensor payloads stay device tensors end to end: each
-  trainer holds its data shard on its own GPU, and TensorPipe device maps
-  (trainer GPU <-> server GPU) move the batch, the logits and the logits'
-  gradient of ``dist_autograd.backward`` GPU to GPU (over xGMI between GPUs
-  of one node) instead of staging them through host memory.  RPC stays the
-  control plane.  ``--ps-host-payloads`` (or ``PDRNN_PS_PAYLOAD=host``)
-  restores host-staged payloads;
+* the server keeps the model (and the fused HIP LSTM kernels) on its GPU.
+  The RPC tensor payloads (batch in, logits out, the logits' gradient of
+  ``dist_autograd.backward``) are host-staged: TensorPipe in torch-ROCm 2.10
+  has no device channel -- a CUDA tensor in an RPC fails with "Attempting to
+  send a Tensor with unexpected device type cuda:0"
+  (profiles/r2_ps_device_payload_tried.md) -- so there is no GPU-to-GPU
+  path under RPC semantics on this stack;
 * fixes of reference quirks, each behind a flag: trainers
   shard the data over the W-1 trainers (``--ps-legacy-sharding`` restores the
   reference's ``num_replicas=W`` sharding that never trains on shard 0);
@@ -84,8 +83,6 @@ class ServerModel:
             self.step_lock.release()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if x.is_cuda:  # device payload: the response goes back GPU to GPU
-            return self.model(x.to(self.device))
         return self.model(x.to(self.device)).cpu()
 
     def get_dist_gradients(self, cid: int):
@@ -116,29 +113,10 @@ def get_parameter_network(input_dim, hidden_dim, layer_dim, output_dim, cell="ls
         return _server_model
 
 
-def device_payloads() -> bool:
-    """Device-resident RPC payloads (TensorPipe device maps) on GPU nodes."""
-    return torch.cuda.is_available() and os.environ.get("PDRNN_PS_PAYLOAD", "device") != "host"
-
-
-def worker_device(rank: int) -> torch.device:
-    """Trainer rank r (1..W-1) uses GPU r mod #GPUs; the server uses GPU 0."""
-    n = max(1, torch.cuda.device_count())
-    return torch.device("cuda", rank % n)
-
-
-def _rpc_options(address: str, port: str, rank: int = 0, world_size: int = 1):
+def _rpc_options(address: str, port: str):
     import torch.distributed.rpc as rpc
-    opts = rpc.TensorPipeRpcBackendOptions(init_method=f"tcp://{address}:{port}",
+    return rpc.TensorPipeRpcBackendOptions(init_method=f"tcp://{address}:{port}",
                                            rpc_timeout=RPC_TIMEOUT_S)
-    if device_payloads():
-        # device maps in both directions (responses use the inverse map)
-        if rank == 0:
-            for r in range(1, world_size):
-                opts.set_device_map(f"trainer_{r}", {0: worker_device(r).index})
-        else:
-            opts.set_device_map(PS_NAME, {worker_device(rank).index: 0})
-    return opts
 
 
 def run_parameter_server(rank: int, world_size: int, address: str = "127.0.0.1",
@@ -148,7 +126,7 @@ def run_parameter_server(rank: int, world_size: int, address: str = "127.0.0.1",
         torch.cuda.set_device(0)
     logging.info("PS master initializing RPC")
     rpc.init_rpc(name=PS_NAME, rank=rank, world_size=world_size,
-                 rpc_backend_options=_rpc_options(address, port, rank, world_size))
+                 rpc_backend_options=_rpc_options(address, port))
     logging.info("RPC initialized! Running parameter server...")
     rpc.shutdown(graceful=True)  # returns when every trainer has finished
     logging.info("RPC shutdown on parameter server.")
@@ -190,13 +168,11 @@ def _make_worker_trainer_cls():
             else:
                 sampler = ShardedSampler(len(training_set), num_replicas=world_size - 1, rank=rank - 1)
             eval_ok = rank == 0
-            # the shard lives on this trainer's GPU when payloads are device tensors
-            dev = worker_device(rank) if device_payloads() else torch.device("cpu")
             super().__init__(model=model, training_set=training_set, batch_size=batch_size,
                              learning_rate=learning_rate,
                              validation_set=validation_set if eval_ok else None,
                              test_set=test_set if eval_ok else None, checkpoint_dir=checkpoint_dir,
-                             sampler=sampler, device=dev, flatten=False, warmup=False)
+                             sampler=sampler, device=torch.device("cpu"), flatten=False, warmup=False)
 
         def world_size(self):
             return self._world
@@ -257,10 +233,8 @@ def run_worker(rank, world_size, epochs, batch_size, learning_rate, input_dim, h
                hogwild: bool = False):
     import torch.distributed.rpc as rpc
     logging.info(f"Worker rank {rank} initializing RPC")
-    if device_payloads():
-        torch.cuda.set_device(worker_device(rank))
     rpc.init_rpc(name=f"trainer_{rank}", rank=rank, world_size=world_size,
-                 rpc_backend_options=_rpc_options(address, port, rank, world_size))
+                 rpc_backend_options=_rpc_options(address, port))
     logging.info(f"Worker {rank} done initializing RPC")
     model = RemoteModel(input_dim, hidden_dim, layer_dim, output_dim, cell)
     cls = _make_worker_trainer_cls()
@@ -286,9 +260,6 @@ def add_sub_command(parent_parser):
     p.add_argument("--master-port", type=str, default="29500", help="Port of the server.")
     p.add_argument("--ps-legacy-sharding", action="store_true",
                    help="shard over all W ranks like the reference (shard 0 never trained)")
-    p.add_argument("--ps-host-payloads", action="store_true",
-                   help="stage RPC tensor payloads through host memory (default on GPU nodes: "
-                        "device tensors via TensorPipe device maps)")
     p.add_argument("--ps-hogwild", action="store_true",
                    help="let trainers' forward/backward/step interleave on the server (reference "
                         "behaviour; races on in-place parameter updates)")
@@ -300,8 +271,6 @@ def execute(args):
     os.environ["MASTER_ADDR"] = args.master_address
     os.environ["MASTER_PORT"] = args.master_port
     address = "127.0.0.1" if args.master_address == "localhost" else args.master_address
-    if args.ps_host_payloads:
-        os.environ["PDRNN_PS_PAYLOAD"] = "host"
     if args.rank == 0:
         run_parameter_server(0, args.world_size, address, args.master_port)
         return None

@@ -10,3 +10,5 @@ done
 timeout -k 10 180 python src/motion/main.py --epochs 1 --seed 123456789 --no-validation --synthetic --no-warmup local > gpurun_out/r2p_cli_nowarm.log 2>&1
 grep "Training Duration" gpurun_out/r2p_cli_nowarm.log
 for i in 1 2 3; do timeout -k 10 180 python bench.py --steps 20 --warmup 5 > gpurun_out/r2p_bench_driver$i.log 2>&1; tail -1 gpurun_out/r2p_bench_driver$i.log | cut -c1-190; done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ps.py -x -v --timeout 150 --timeout-method thread > gpurun_out/r2p_ps.log 2>&1 || { tail -60 gpurun_out/r2p_ps.log; exit 1; }
+tail -4 gpurun_out/r2p_ps.log
