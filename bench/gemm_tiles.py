@@ -21,7 +21,10 @@ def bench(fn, it=10):
 
 mod = _ext.require()
 for (M, N, K, what) in [(4096, 4096, 16384, "bwd step B4096 H4096"), (4096, 16384, 4096, "fwd step B4096 H4096"),
-                        (256, 4096, 16384, "bwd step B256"), (128, 4096, 1024, "charlm fwd step")]:
+                        (256, 4096, 16384, "bwd step B256"), (128, 4096, 1024, "charlm fwd step"),
+                        # input projections Xp = X W_ih^T of the bi-LSTM (both directions, M = T*B rows;
+                        # 1/8 of the B4096 x T64 rows keeps the sweep short, same per-tile work)
+                        (32768, 32768, 1024, "Xp layer0 (I1024)"), (32768, 32768, 8192, "Xp layer1 (I8192)")]:
     a = torch.randn(M, K, device="cuda").half()
     b = torch.randn(N, K, device="cuda").half()
     fl = 2.0 * M * N * K

@@ -106,6 +106,12 @@ class FusedAdam(torch.optim.Adam):
                           float(group["lr"]), beta1, beta2, group["eps"], group["weight_decay"],
                           step, self._pdrnn_grad_scale, bool(group.get("decoupled_weight_decay", False)),
                           bool(group.get("maximize", False)), None, None)
+            # the native kernel wrote the parameters through raw pointers: move
+            # their version counters like any in-place torch update would, so
+            # derived copies keyed on versions (16-bit shadow weights of the
+            # large-H LSTM, ops/lstm_large.py) see the change
+            for p in params:
+                torch.autograd.graph.increment_version(p)
         return loss
 
     def _reference_group_step(self, group):

@@ -68,6 +68,67 @@ def _mm_f32(a: Tensor, b: Tensor) -> Tensor:
         return torch.mm(a.float(), b.float())
 
 
+def _addmm_f32_(c: Tensor, a: Tensor, b: Tensor) -> Tensor:
+    """c += a @ b, fp32 c, 16-bit a / b."""
+    try:
+        return c.copy_(torch.addmm(c, a, b, out_dtype=torch.float32))
+    except (RuntimeError, TypeError):
+        return c.add_(torch.mm(a.float(), b.float()))
+
+
+def shadow(w: Tensor, kind: str, cdt: torch.dtype, hidden: int) -> Tensor:
+    """16-bit copy of an fp32 master weight in the layout a kernel reads,
+    cached on the parameter and rebuilt only when the master changed: its
+    version counter moves on every in-place update (FusedAdam's native step
+    bumps it explicitly).  Replaces the per-forward casts / interleaves /
+    transposes (a cast, an interleave copy and a second cast for the backward
+    per weight per step before).
+
+    kind: "i" gate-interleaved rows (forward step GEMM / input projection),
+          "p" stored layout (dX GEMM), "t" transposed [I, 4H] (BPTT step GEMM)."""
+    key = (kind, cdt)
+    ver = (w._version, w.data_ptr())
+    cache = getattr(w, "_pdrnn_shadow", None)
+    if cache is None:
+        cache = {}
+        w._pdrnn_shadow = cache
+    ent = cache.get(key)
+    if ent is not None and ent[0] == ver:
+        return ent[1]
+    with torch.no_grad():
+        src = w.detach()
+        if kind == "i":
+            t = _interleave(src.to(cdt), hidden).contiguous()
+        elif kind == "p":
+            t = src.to(cdt)
+        elif kind == "t":
+            t = src.t().to(cdt).contiguous()
+        else:
+            raise ValueError(kind)
+    cache[key] = (ver, t)
+    return t
+
+
+def _shadow_cat(ws: List[Tensor], cdt: torch.dtype, hidden: int) -> Tensor:
+    """Both directions' interleaved input weights stacked [ndir*4H, I] (one
+    input-projection GEMM for both), cached on the first weight."""
+    if len(ws) == 1:
+        return shadow(ws[0], "i", cdt, hidden)
+    key = ("icat", cdt, tuple(id(w) for w in ws))
+    ver = tuple((w._version, w.data_ptr()) for w in ws)
+    cache = getattr(ws[0], "_pdrnn_shadow", None)
+    if cache is None:
+        cache = {}
+        ws[0]._pdrnn_shadow = cache
+    ent = cache.get(key)
+    if ent is not None and ent[0] == ver:
+        return ent[1]
+    with torch.no_grad():
+        t = torch.cat([_interleave(w.detach().to(cdt), hidden) for w in ws], 0)
+    cache[key] = (ver, t)
+    return t
+
+
 class _LargeLSTMLayer(torch.autograd.Function):
     """One layer, 1 or 2 directions.  x: [T, B, I] (compute dtype).
 
@@ -93,10 +154,10 @@ class _LargeLSTMLayer(torch.autograd.Function):
             if b_hh is not None:
                 b = b + b_hh.float()
             bias.append(b[perm])
-        wih_p = torch.cat([_interleave(w.to(cdt), H) for w in w_ih], 0)     # [ndir*4H, I]
+        wih_p = _shadow_cat(w_ih, cdt, H)                                  # [ndir*4H, I]
         bias_p = torch.cat(bias, 0).to(cdt)
         xp = torch.addmm(bias_p, x.reshape(T * B, I), wih_p.t()).view(T, B, ndir * 4 * H)
-        whh_p = [_interleave(w.to(cdt), H).contiguous() for w in w_hh]
+        whh_p = [shadow(w, "i", cdt, H) for w in w_hh]
         h0c = h0.to(cdt).contiguous() if h0 is not None else None
         c0c = c0.float().contiguous() if c0 is not None else None
         rev_mask = 2 if ndir == 2 else 0
@@ -104,9 +165,10 @@ class _LargeLSTMLayer(torch.autograd.Function):
         last = [T - 1, 0][:ndir]
         hn = torch.stack([hseq[last[d], :, d * H:(d + 1) * H] for d in range(ndir)], 0)
         cn = torch.stack([cseq[d, last[d]] for d in range(ndir)], 0)
-        # backward works in torch's gate-blocked order: weights as stored (cast)
-        ctx.save_for_backward(x, hseq, cseq, acts, h0c, c0c, *[w.to(cdt) for w in w_ih],
-                              *[w.to(cdt) for w in w_hh])
+        # backward works in torch's gate-blocked order: W_ih as stored (dX GEMM),
+        # W_hh transposed (BPTT step GEMM), both 16-bit shadows
+        ctx.save_for_backward(x, hseq, cseq, acts, h0c, c0c, *[shadow(w, "p", cdt, H) for w in w_ih],
+                              *[shadow(w, "t", cdt, H) for w in w_hh])
         ctx.cfg = (H, ndir, tile, rev_mask, [w is not None for w in weights], h0 is not None,
                    c0 is not None, h0.dtype if h0 is not None else None,
                    c0.dtype if c0 is not None else None)
@@ -123,7 +185,7 @@ class _LargeLSTMLayer(torch.autograd.Function):
         dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
         dhn_f = dhn.float().contiguous() if dhn is not None else None
         dcn_f = dcn.float().contiguous() if dcn is not None else None
-        wt = [w.t().contiguous() for w in whh]                      # [H, 4H], gate-blocked
+        wt = list(whh)                                              # [H, 4H], gate-blocked
         dgates, dh0, dc0 = mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile, 0)
         grads: List[Optional[Tensor]] = []
         dx = None
@@ -131,10 +193,20 @@ class _LargeLSTMLayer(torch.autograd.Function):
         x2 = x.reshape(T * B, I)
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
-            hd = hseq[:, :, d * H:(d + 1) * H]
-            h0d = h0c[d:d + 1] if h0c is not None else torch.zeros(1, B, H, device=x.device, dtype=cdt)
-            hprev = torch.cat([h0d, hd[:-1]], 0) if d == 0 else torch.cat([hd[1:], h0d], 0)
-            dwhh = _mm_f32(G.t(), hprev.reshape(T * B, H))
+            hd = hseq[:, :, d * H:(d + 1) * H]                       # strided view, row stride ndir*H
+            # dW_hh = sum_t dgates_t^T h_prev(t) over shifted views of the output
+            # sequence (no [T, B, H] h_prev copy): forward h_prev(t) = h_{t-1},
+            # reverse h_{t+1}; the step next to the initial state pairs with h0
+            if T > 1:
+                if d == 0:
+                    dwhh = _mm_f32(G[B:].t(), hd[:-1].reshape((T - 1) * B, H))
+                else:
+                    dwhh = _mm_f32(G[:(T - 1) * B].t(), hd[1:].reshape((T - 1) * B, H))
+            else:
+                dwhh = torch.zeros(4 * H, H, device=x.device, dtype=torch.float32)
+            if h0c is not None:
+                g0 = G[:B] if d == 0 else G[(T - 1) * B:]
+                _addmm_f32_(dwhh, g0.t(), h0c[d])
             dwih = _mm_f32(G.t(), x2)
             db = G.sum(0, dtype=torch.float32)  # fp32 accumulation, no fp32 copy of G
             if not need_dx:

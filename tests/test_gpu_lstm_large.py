@@ -138,3 +138,36 @@ def test_embedding_bwd_csr8(dt):
     w = torch.randn(V, D, device="cuda")
     out = mod.embedding_fwd(w, idx, torch.bfloat16)
     assert out.dtype == torch.bfloat16 and torch.equal(out, w[idx].to(torch.bfloat16))
+
+
+def test_shadow_weights_follow_optimizer_steps():
+    """16-bit shadow weights (ops/lstm_large.shadow) are rebuilt whenever the
+    fp32 master changes -- FusedAdam's native step bumps the version counters
+    -- so training with the cache equals training with the cache dropped
+    before every step; bidirectional with h0 covers the shifted dW_hh GEMMs."""
+    import copy
+
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    from pytorch_distributed_rnn_amd.utils.flat import flatten_module
+    torch.manual_seed(7)
+    m1 = LSTM(64, 128, 2, bidirectional=True).cuda()
+    m2 = copy.deepcopy(m1)
+    flatten_module(m1)
+    flatten_module(m2)
+    o1, o2 = FusedAdam(m1.parameters(), lr=1e-2), FusedAdam(m2.parameters(), lr=1e-2)
+    x = torch.randn(9, 6, 64, device="cuda").to(torch.bfloat16)
+    h0 = torch.randn(4, 6, 128, device="cuda").to(torch.bfloat16)
+    c0 = torch.randn(4, 6, 128, device="cuda")
+    for _ in range(3):
+        for m, o, drop in ((m1, o1, False), (m2, o2, True)):
+            if drop:
+                for p in m.parameters():
+                    if hasattr(p, "_pdrnn_shadow"):
+                        del p._pdrnn_shadow
+            o.zero_grad()
+            out, _ = m(x, (h0, c0))
+            out.float().square().mean().backward()
+            o.step()
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q, rtol=0, atol=0, msg=k)
+    assert any(hasattr(p, "_pdrnn_shadow") for p in m1.parameters())
