@@ -245,16 +245,35 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
   uint16_t* hout = d.hseq + (int64_t)t * d.hseq_st;
   uint16_t* acts = d.acts + (int64_t)t * B * 4 * H;
   constexpr int C8 = BN / 8;
-  for (int e = threadIdx.x; e < BM * C8; e += G::NTHREADS) {
+  // Every item's global operands (xp, c_prev) and C-tile slice are loaded
+  // first, then the cell math and stores run: the loads of all items are in
+  // flight together instead of one HBM round trip per item (with one
+  // workgroup per CU the epilogue is not hidden behind another workgroup's
+  // MFMA loop).
+  constexpr int ITEMS = (BM * C8 + G::NTHREADS - 1) / G::NTHREADS;
+  uint4 xv[ITEMS];
+  float2 cpv[ITEMS];
+  float4 za[ITEMS], zb[ITEMS];
+#pragma unroll
+  for (int it = 0; it < ITEMS; ++it) {
+    const int e = min((int)threadIdx.x + it * G::NTHREADS, BM * C8 - 1);
+    const int row = e / C8, c8 = e - row * C8;
+    const int b = min(m0 + row, B - 1);
+    const int col = n0 + c8 * 8;
+    xv[it] = *reinterpret_cast<const uint4*>(xp + (int64_t)b * d.xp_sb + col);
+    cpv[it] = cprev ? *reinterpret_cast<const float2*>(cprev + (int64_t)b * H + (col >> 2)) : make_float2(0.f, 0.f);
+    za[it] = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8);
+    zb[it] = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8 + 4);
+  }
+#pragma unroll
+  for (int it = 0; it < ITEMS; ++it) {
+    const int e = threadIdx.x + it * G::NTHREADS;
     const int row = e / C8, c8 = e - row * C8;
     const int b = m0 + row;
-    if (b >= B) continue;
+    if (e >= BM * C8 || b >= B) continue;
     const int col = n0 + c8 * 8;
-    const float4 z0 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8);
-    const float4 z1 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8 + 4);
-    const uint4 xv = *reinterpret_cast<const uint4*>(xp + (int64_t)b * d.xp_sb + col);
-    const uint16_t* xh = reinterpret_cast<const uint16_t*>(&xv);
-    const float z[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+    const uint16_t* xh = reinterpret_cast<const uint16_t*>(&xv[it]);
+    const float z[8] = {za[it].x, za[it].y, za[it].z, za[it].w, zb[it].x, zb[it].y, zb[it].z, zb[it].w};
     float g[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -263,8 +282,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
       else g[k] = (k & 3) < 2 ? sigm(zz) : zz;  // GRU: r, z activated; n_x, n_h linear
     }
     const int u = col >> 2;
-    float2 cp = make_float2(0.f, 0.f);
-    if (cprev) cp = *reinterpret_cast<const float2*>(cprev + (int64_t)b * H + u);
+    const float2 cp = cpv[it];
     float s0, s1, h0v, h1v;
     if constexpr (CELL == 0) {
       s0 = fmaf(g[1], cp.x, g[0] * g[2]);
@@ -341,8 +359,7 @@ __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B,
   d.dc_carry[bu] = next;
 }
 
-// cell_bwd_elem for 8 consecutive units u0 .. u0+7 of row b (u0 % 8 == 0):
-// the same math with 16-byte accesses.  dh: the recurrent dh of the 8 units.
+// 8-float (2 x 16-byte) row accesses
 __device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
   const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
@@ -351,12 +368,46 @@ __device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
+
+// Cell backward of 8 consecutive units u0 .. u0+7 of row b (u0 % 8 == 0):
+// cell_bwd_elem's math with 16-byte accesses, split into a load phase and a
+// compute phase so that the epilogue of the backward step kernel puts the
+// global loads of several items in flight before the first one is consumed.
+struct CellBwdOps8 {
+  float carry[8], sp[8], cur[8];
+  uint4 av[4];
+  uint4 dv;
+};
+
 template <class DT, int CELL>
-__device__ __forceinline__ void cell_bwd_vec8(const PdrnnLstmLargeDir& d, int B, int H, int T, bool rev, int tn,
-                                              bool cell, int b, int u0, float (&dh)[8]) {
+__device__ __forceinline__ void cell_bwd_load8(const PdrnnLstmLargeDir& d, int B, int H, int T, bool rev, int tn,
+                                               bool cell, int b, int u0, CellBwdOps8& o) {
+  const int64_t bu = (int64_t)b * H + u0;
+  ld8(d.dc_carry + bu, o.carry);
+  if (!cell) return;
+  o.dv = d.dout ? *reinterpret_cast<const uint4*>(d.dout + (int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u0)
+                : make_uint4(0u, 0u, 0u, 0u);
+  const uint4* ap = reinterpret_cast<const uint4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o.av[q] = ap[q];
+  const int tpp = rev ? tn + 1 : tn - 1;
+  const bool has_prev = rev ? tpp < T : tpp >= 0;
+  if (has_prev) ld8(d.cseq + (int64_t)tpp * B * H + bu, o.sp);
+  else if (d.c0) ld8(d.c0 + bu, o.sp);
+  else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.sp[k] = 0.f;
+  }
+  if constexpr (CELL == 0) ld8(d.cseq + (int64_t)tn * B * H + bu, o.cur);
+}
+
+template <class DT, int CELL>
+__device__ __forceinline__ void cell_bwd_compute8(const PdrnnLstmLargeDir& d, int B, int H, bool cell, int tn, int b,
+                                                  int u0, float (&dh)[8], const CellBwdOps8& o) {
   const int64_t bu = (int64_t)b * H + u0;
   float carry[8];
-  ld8(d.dc_carry + bu, carry);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) carry[k] = o.carry[k];
   if constexpr (CELL == 1) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) dh[k] += carry[k];
@@ -367,27 +418,11 @@ __device__ __forceinline__ void cell_bwd_vec8(const PdrnnLstmLargeDir& d, int B,
     return;
   }
   if (d.dout) {
-    const uint4 dv = *reinterpret_cast<const uint4*>(d.dout + (int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u0);
-    const uint16_t* dh16 = reinterpret_cast<const uint16_t*>(&dv);
+    const uint16_t* dh16 = reinterpret_cast<const uint16_t*>(&o.dv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) dh[k] += DT::to_f(dh16[k]);
   }
-  uint4 av[4];
-  const uint4* ap = reinterpret_cast<const uint4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u0);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) av[q] = ap[q];
-  const uint16_t* a16 = reinterpret_cast<const uint16_t*>(av);  // unit k: a16[4k .. 4k+3]
-  const int tpp = rev ? tn + 1 : tn - 1;
-  const bool has_prev = rev ? tpp < T : tpp >= 0;
-  float sp[8];
-  if (has_prev) ld8(d.cseq + (int64_t)tpp * B * H + bu, sp);
-  else if (d.c0) ld8(d.c0 + bu, sp);
-  else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sp[k] = 0.f;
-  }
-  float cur[8];
-  if constexpr (CELL == 0) ld8(d.cseq + (int64_t)tn * B * H + bu, cur);
+  const uint16_t* a16 = reinterpret_cast<const uint16_t*>(o.av);  // unit k: a16[4k .. 4k+3]
   uint16_t g[4][8];
   float next[8];
 #pragma unroll
@@ -395,17 +430,17 @@ __device__ __forceinline__ void cell_bwd_vec8(const PdrnnLstmLargeDir& d, int B,
     const float a0 = DT::to_f(a16[4 * k]), a1 = DT::to_f(a16[4 * k + 1]);
     const float a2 = DT::to_f(a16[4 * k + 2]), a3 = DT::to_f(a16[4 * k + 3]);
     if constexpr (CELL == 0) {
-      const float tc = tanh_(cur[k]);
+      const float tc = tanh_(o.cur[k]);
       const float dc = fmaf(dh[k] * a3, 1.f - tc * tc, carry[k]);
       g[0][k] = DT::from_f(dc * a2 * a0 * (1.f - a0));
-      g[1][k] = DT::from_f(dc * sp[k] * a1 * (1.f - a1));
+      g[1][k] = DT::from_f(dc * o.sp[k] * a1 * (1.f - a1));
       g[2][k] = DT::from_f(dc * a0 * (1.f - a2 * a2));
       g[3][k] = DT::from_f(dh[k] * tc * a3 * (1.f - a3));
       next[k] = dc * a1;
     } else {
       const float dpn = dh[k] * (1.f - a1) * (1.f - a2 * a2);
       g[0][k] = DT::from_f(dpn * a3 * a0 * (1.f - a0));
-      g[1][k] = DT::from_f(dh[k] * (sp[k] - a2) * a1 * (1.f - a1));
+      g[1][k] = DT::from_f(dh[k] * (o.sp[k] - a2) * a1 * (1.f - a1));
       g[2][k] = DT::from_f(dpn);
       g[3][k] = DT::from_f(dpn * a0);
       next[k] = dh[k] * a1;
@@ -463,16 +498,32 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(Pdrnn
   }
   __syncthreads();
   constexpr int C8 = BN / 8;
-  for (int e = threadIdx.x; e < BM * C8; e += G::NTHREADS) {
-    const int row = e / C8, c8 = e - row * C8;
-    const int b = m0 + row;
-    if (b >= B) continue;
-    float dh[8];
-    const float4 z0 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8);
-    const float4 z1 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8 + 4);
-    dh[0] = z0.x; dh[1] = z0.y; dh[2] = z0.z; dh[3] = z0.w;
-    dh[4] = z1.x; dh[5] = z1.y; dh[6] = z1.z; dh[7] = z1.w;
-    cell_bwd_vec8<DT, CELL>(d, B, H, T, rev, tn, cell, b, n0 + c8 * 8, dh);
+  // items in batches of IB: every item's global operands of a batch are in
+  // flight together (see the forward epilogue)
+  constexpr int ITEMS = (BM * C8 + G::NTHREADS - 1) / G::NTHREADS;
+  constexpr int IB = ITEMS < 2 ? ITEMS : 2;
+#pragma unroll
+  for (int i0 = 0; i0 < ITEMS; i0 += IB) {
+    CellBwdOps8 ops[IB];
+#pragma unroll
+    for (int ib = 0; ib < IB; ++ib) {
+      const int e = min((int)threadIdx.x + (i0 + ib) * G::NTHREADS, BM * C8 - 1);
+      const int row = e / C8, c8 = e - row * C8;
+      cell_bwd_load8<DT, CELL>(d, B, H, T, rev, tn, cell, min(m0 + row, B - 1), n0 + c8 * 8, ops[ib]);
+    }
+#pragma unroll
+    for (int ib = 0; ib < IB; ++ib) {
+      const int e = threadIdx.x + (i0 + ib) * G::NTHREADS;
+      const int row = e / C8, c8 = e - row * C8;
+      const int b = m0 + row;
+      if (e >= BM * C8 || b >= B) continue;
+      float dh[8];
+      const float4 z0 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8);
+      const float4 z1 = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8 + 4);
+      dh[0] = z0.x; dh[1] = z0.y; dh[2] = z0.z; dh[3] = z0.w;
+      dh[4] = z1.x; dh[5] = z1.y; dh[6] = z1.z; dh[7] = z1.w;
+      cell_bwd_compute8<DT, CELL>(d, B, H, cell, tn, b, n0 + c8 * 8, dh, ops[ib]);
+    }
   }
 }
 
