@@ -322,7 +322,12 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   TORCH_CHECK(split_fwd == 1 && split_bwd == 1, "fused train step runs on the gate-split / unit-group kernels");
   if (nb_fwd <= 0) nb_fwd = 1;
   if (nb_bwd <= 0) nb_bwd = 1;
-  const int gridb = pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb_bwd, (int)split_bwd);
+  // nb_bwd >= 2: the throughput backward (several sequences per workgroup,
+  // operands DMA-staged through LDS; lstm_small_tp.hip) when it covers the shape
+  const bool tp = nb_bwd >= 2 && pdrnn_lstm_small_bwd_tp_ok((int)H, (int)NL, (int)T, (int)I, (int)B, (int)nb_bwd);
+  if (!tp && cell == 1) nb_bwd = 1;  // the GRU latency backward is single-sequence
+  const int gridb = tp ? pdrnn_lstm_small_bwd_tp_grid((int)H, (int)NL, (int)T, (int)I, (int)B, (int)nb_bwd, (int)cell)
+                       : pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb_bwd, (int)split_bwd);
   TORCH_CHECK(gridb > 0, "unsupported backward tile nb=", nb_bwd);
   Tensor slab = at::empty({gridb, L.P}, opts);
 
@@ -368,7 +373,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.slab = slab.data_ptr<float>(); bk.P = L.P;
   bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL; bk.cell = (int)cell;
   if (st_b.defined()) bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
-  HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
+  if (tp) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_tp(&bk, (int)H, (int)nb_bwd, gridb, st));
+  else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
   if (st_f.defined()) {
     report_stamps("fwd(head step)", st_f, (int)(T + NL - 1));
     report_stamps("bwd(head step, lean)", st_b, (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)gridb * nb_bwd - 1) / ((int64_t)gridb * nb_bwd)));
@@ -677,6 +683,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_small_max_split", [](int64_t H, int64_t NL, bool backward) {
     return pdrnn_lstm_small_max_split((int)H, (int)NL, backward ? 1 : 0);
   });
+  m.def("lstm_small_bwd_tp_ok", [](int64_t H, int64_t NL, int64_t T, int64_t I, int64_t B, int64_t nb) {
+    return pdrnn_lstm_small_bwd_tp_ok((int)H, (int)NL, (int)T, (int)I, (int)B, (int)nb) != 0;
+  }, "the throughput (multi-sequence) fused-step backward covers this shape");
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });

@@ -118,6 +118,42 @@ PDRNN_DEVICE uint16_t f32_to_bf16(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// ---------------------------------------------------------------------------
+// Shared by the small-H recurrent kernels (lstm_small.hip, lstm_small_tp.hip)
+// ---------------------------------------------------------------------------
+// Buffer descriptor for a wave-uniform base pointer: the halves go through
+// readfirstlane so the compiler can keep the descriptor in SGPRs (no
+// waterfall loop around each buffer op).
+PDRNN_DEVICE __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  void* up = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(up, 0, 0x7FFFFFFF, 0x00020000);
+}
+PDRNN_DEVICE float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff_bytes, uint32_t soff_bytes) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff_bytes, soff_bytes, 0));
+}
+
+// x element i as fp32 (x may be stored in bf16: mixed-precision inputs are
+// widened once, while staging into LDS)
+PDRNN_DEVICE float ldx(const float* x, int64_t i, int bf) {
+  return bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(x)[i]) : x[i];
+}
+
+typedef float pdrnn_f2 __attribute__((ext_vector_type(2)));
+
+PDRNN_DEVICE float quad_bcast(float v, int q) {
+  // quad_perm [q,q,q,q]: every lane of the quad reads lane q of the quad
+  switch (q) {
+    case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x00, 0xF, 0xF, false));
+    case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x55, 0xF, 0xF, false));
+    case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xAA, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xFF, 0xF, 0xF, false));
+  }
+}
+
+
 }  // namespace pdrnn
 
 #define PDRNN_HIP_CHECK(expr)                                                   \

@@ -49,26 +49,6 @@ constexpr int kXldsBytes = 48 * 1024;
 #endif
 constexpr bool kFwdBulkLds = PDRNN_FWD_BULK_LDS;
 
-// Buffer descriptor for a wave-uniform base pointer: the halves go through
-// readfirstlane so the compiler can keep the descriptor in SGPRs (no
-// waterfall loop around each buffer op).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
-  void* up = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(up, 0, 0x7FFFFFFF, 0x00020000);
-}
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff_bytes, uint32_t soff_bytes) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff_bytes, soff_bytes, 0));
-}
-
-// x element i as fp32 (x may be stored in bf16: mixed-precision inputs are
-// widened once, while staging into LDS)
-__device__ __forceinline__ float ldx(const float* x, int64_t i, int bf) {
-  return bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(x)[i]) : x[i];
-}
-
 // Stage one sequence's inputs x[t][0..I) into the LDS image xs[t][0..H)
 // (columns >= I zero): only the I real columns are loaded (not H), 4 loads
 // in flight per thread, so the prologue is one memory round trip instead of
@@ -267,18 +247,6 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
 // per-timestep dependency chain (the recurrence is latency-bound: one wave per
 // SIMD at motion batch sizes).
 // ---------------------------------------------------------------------------
-typedef float pdrnn_f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ float quad_bcast(float v, int q) {
-  // quad_perm [q,q,q,q]: every lane of the quad reads lane q of the quad
-  switch (q) {
-    case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x00, 0xF, 0xF, false));
-    case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x55, 0xF, 0xF, false));
-    case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xAA, 0xF, 0xF, false));
-    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xFF, 0xF, 0xF, false));
-  }
-}
-
 constexpr float kNegLog2e = -1.4426950408889634f;
 
 // CELL 1 = GRU on the same lane map: the quad's four rows are [r | z | n_x |

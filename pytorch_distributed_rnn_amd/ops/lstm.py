@@ -51,6 +51,24 @@ def small_launch_config(batch: int, hidden: int, num_layers: int = 2) -> Tuple[i
     return nb_fwd, sp_fwd, nb_bwd, sp_bwd  # split 0 = widest valid (chosen natively)
 
 
+def fused_bwd_nb(batch: int, hidden: int, num_layers: int) -> int:
+    """Sequences per workgroup of the fused training step's backward.
+
+    1 = the latency kernel (lstm_small.hip: one sequence per workgroup, two
+    resident per CU).  2..3 = the throughput kernel (lstm_small_tp.hip:
+    several sequences share the register-resident W / dW, operands DMA-staged
+    through LDS; B = 1440 runs in one residency round instead of three).  The
+    throughput kernel is correct but measured SLOWER at every motion batch
+    size (profiles/r2_tp_backward_tried.md: the backward is VALU-issue bound,
+    so interleaving sequences in a wave buys no latency hiding and the LDS
+    operand reads cost more than register prefetch); it stays opt-in for
+    sweeps via PDRNN_LSTM_NB_BWD."""
+    env = _env_int("PDRNN_LSTM_NB_BWD", 0)
+    if env in (1, 2, 3, 4):
+        return env
+    return 1
+
+
 def fused_small_supported(x: Tensor, hidden: int, num_layers: int, bidirectional: bool,
                           proj_size: int = 0, batch_first: bool = True) -> bool:
     if bidirectional or proj_size:

@@ -36,6 +36,53 @@ def test_fused_step_matches_autograd(cell):
         assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
 
 
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+@pytest.mark.parametrize("nb", [2, 3])
+def test_fused_throughput_backward_matches_autograd(cell, nb, monkeypatch):
+    """The multi-sequence (LDS-DMA staged) backward of the fused step
+    (csrc/kernels/lstm_small_tp.hip) against the autograd path; 380 samples in
+    batches of 96 leave a last batch of 92, so tiles with unused slots run."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.setenv("PDRNN_LSTM_NB_BWD", str(nb))
+    assert _ext.native(torch.device("cuda")).lstm_small_bwd_tp_ok(32, 2, 128, 9, 96, nb)
+    torch.manual_seed(1)
+    train, _, _ = synthetic_motion(n_train=380, n_validation=2, n_test=2, seed=4)
+    m1 = MotionModel(9, 32, 2, 6, cell=cell)
+    m2 = copy.deepcopy(m1)
+    t1, t2 = _trainer(m1, train, True), _trainer(m2, train, False)
+    assert t1._fused_step() is not None
+    for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
+        s1, _ = t1.train_batch(x1)
+        s2, _ = t2.train_batch(x2)
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
+
+
+@pytest.mark.parametrize("nb", [1, 3])
+def test_fused_step_headline_batch_matches_autograd(nb, monkeypatch):
+    """B = 1440 (the headline per-GPU batch), latency and throughput backward."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.train.trainer import Trainer
+    monkeypatch.setenv("PDRNN_LSTM_NB_BWD", str(nb))
+    torch.manual_seed(2)
+    train, _, _ = synthetic_motion(n_train=2880, n_validation=2, n_test=2, seed=5)
+    m1 = MotionModel(9, 32, 2, 6)
+    m2 = copy.deepcopy(m1)
+    t1 = Trainer(m1, train, batch_size=1440, learning_rate=2.5e-3, device=torch.device("cuda"))
+    t2 = Trainer(m2, train, batch_size=1440, learning_rate=2.5e-3, device=torch.device("cuda"))
+    t2._fused = None
+    for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
+        s1, _ = t1.train_batch(x1)
+        s2, _ = t2.train_batch(x2)
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
+
+
 def test_local_trainer_epoch_on_gpu(tmp_path):
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
