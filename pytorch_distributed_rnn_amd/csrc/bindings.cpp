@@ -54,6 +54,16 @@ int dtype_code(const Tensor& t) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "16-bit (bf16/fp16) tensor expected");
   return t.scalar_type() == at::kBFloat16 ? 0 : 1;
 }
+// large-H LSTM storage: 0 bf16, 1 fp16, 2 fp32
+int large_dtype(const Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return 2;
+  return dtype_code(t);
+}
+// element `off` of t, as an untyped pointer (large-H kernels take void* storage)
+const void* eptr(const Tensor& t, int64_t off = 0) {
+  return static_cast<const char*>(t.data_ptr()) + off * (int64_t)t.element_size();
+}
+void* eptrm(const Tensor& t, int64_t off = 0) { return static_cast<char*>(t.data_ptr()) + off * (int64_t)t.element_size(); }
 const uint16_t* u16(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
 uint16_t* u16m(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 const uint16_t* opt_u16(const optional<Tensor>& t) {
@@ -542,7 +552,7 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
                                    int64_t cell) {
   CHECK_HIP_TENSOR(xp);
   const c10::DeviceGuard guard(xp.device());
-  const int dt = dtype_code(xp);
+  const int dt = large_dtype(xp);
   const int ndir = (int)w.size();
   TORCH_CHECK(ndir == 1 || ndir == 2, "1 or 2 directions");
   TORCH_CHECK(pdrnn_lstm_large_supported((int)H), "large LSTM path needs H % 64 == 0");
@@ -550,7 +560,7 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
   const int64_t T = xp.size(0), B = xp.size(1);
   TORCH_CHECK(xp.stride(1) == ndir * 4 * H && xp.stride(0) == B * ndir * 4 * H, "xp must be contiguous");
   for (auto& t : w) {
-    TORCH_CHECK(t.is_contiguous() && t.size(0) == 4 * H && t.size(1) == H && dtype_code(t) == dt, "w: [4H, H] contiguous");
+    TORCH_CHECK(t.is_contiguous() && t.size(0) == 4 * H && t.size(1) == H && large_dtype(t) == dt, "w: [4H, H] contiguous");
   }
   auto o16 = xp.options();
   auto o32 = xp.options().dtype(at::kFloat);
@@ -559,7 +569,7 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
   Tensor acts = at::empty({ndir, T, B, 4 * H}, o16);
   const bool has_h0 = h0.has_value() && h0->defined();
   const bool has_c0 = c0.has_value() && c0->defined();
-  if (has_h0) TORCH_CHECK(h0->is_contiguous() && dtype_code(*h0) == dt && h0->numel() == ndir * B * H, "h0 [ndir,B,H]");
+  if (has_h0) TORCH_CHECK(h0->is_contiguous() && large_dtype(*h0) == dt && h0->numel() == ndir * B * H, "h0 [ndir,B,H]");
   if (has_c0) TORCH_CHECK(c0->is_contiguous() && c0->scalar_type() == at::kFloat && c0->numel() == ndir * B * H, "c0");
   PdrnnLstmLargeStepArgs a{};
   a.B = (int)B; a.H = (int)H; a.T = (int)T; a.reverse_mask = (int)reverse_mask;
@@ -567,13 +577,13 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
   a.cell = (int)cell;
   for (int d = 0; d < ndir; ++d) {
     PdrnnLstmLargeDir& dd = a.dir[d];
-    dd.w = u16(w[d]);
-    dd.xp = u16(xp) + d * 4 * H; dd.xp_sb = ndir * 4 * H; dd.xp_st = B * ndir * 4 * H;
-    dd.h0 = has_h0 ? u16(*h0) + d * B * H : nullptr;
+    dd.w = eptr(w[d]);
+    dd.xp = eptr(xp, d * 4 * H); dd.xp_sb = ndir * 4 * H; dd.xp_st = B * ndir * 4 * H;
+    dd.h0 = has_h0 ? eptr(*h0, d * B * H) : nullptr;
     dd.c0 = has_c0 ? c0->data_ptr<float>() + d * B * H : nullptr;
-    dd.hseq = u16m(hseq) + d * H; dd.hseq_sb = ndir * H; dd.hseq_st = B * ndir * H;
+    dd.hseq = eptrm(hseq, d * H); dd.hseq_sb = ndir * H; dd.hseq_st = B * ndir * H;
     dd.cseq = cseq.data_ptr<float>() + d * T * B * H;
-    dd.acts = u16m(acts) + d * T * B * 4 * H;
+    dd.acts = eptrm(acts, d * T * B * 4 * H);
   }
   hipStream_t st = cur_stream();
   for (int64_t s = 0; s < T; ++s) {
@@ -591,15 +601,15 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
                                    int64_t tile, int64_t cell) {
   CHECK_HIP_TENSOR(acts);
   const c10::DeviceGuard guard(acts.device());
-  const int dt = dtype_code(acts);
+  const int dt = large_dtype(acts);
   const int ndir = (int)wt.size();
   const int64_t T = acts.size(1), B = acts.size(2);
   TORCH_CHECK(acts.is_contiguous() && acts.size(0) == ndir && acts.size(3) == 4 * H, "acts [ndir, T, B, 4H]");
   TORCH_CHECK(cseq.is_contiguous() && cseq.scalar_type() == at::kFloat, "cseq f32");
-  for (auto& t : wt) TORCH_CHECK(t.is_contiguous() && t.size(0) == H && t.size(1) == 4 * H && dtype_code(t) == dt, "wt [H, 4H]");
+  for (auto& t : wt) TORCH_CHECK(t.is_contiguous() && t.size(0) == H && t.size(1) == 4 * H && large_dtype(t) == dt, "wt [H, 4H]");
   const bool has_dout = dout.has_value() && dout->defined();
   if (has_dout) {
-    TORCH_CHECK(dtype_code(*dout) == dt && dout->dim() == 3 && dout->size(2) == ndir * H && dout->stride(2) == 1,
+    TORCH_CHECK(large_dtype(*dout) == dt && dout->dim() == 3 && dout->size(2) == ndir * H && dout->stride(2) == 1,
                 "dout [T, B, ndir*H]");
   }
   auto o16 = acts.options();
@@ -621,13 +631,13 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   a.cell = (int)cell;
   for (int d = 0; d < ndir; ++d) {
     PdrnnLstmLargeDir& dd = a.dir[d];
-    dd.wt = u16(wt[d]);
+    dd.wt = eptr(wt[d]);
     dd.c0 = c0_p ? c0_p + d * B * H : nullptr;
     dd.cseq = cseq.data_ptr<float>() + d * T * B * H;
-    dd.acts = u16m(acts) + d * T * B * 4 * H;
-    dd.dgates = u16m(dgates) + d * T * B * 4 * H;
+    dd.acts = eptrm(acts, d * T * B * 4 * H);
+    dd.dgates = eptrm(dgates, d * T * B * 4 * H);
     if (has_dout) {
-      dd.dout = u16(*dout) + d * H; dd.dout_sb = dout->stride(1); dd.dout_st = dout->stride(0);
+      dd.dout = eptr(*dout, d * H); dd.dout_sb = dout->stride(1); dd.dout_st = dout->stride(0);
     }
     dd.dhn = dhn_p ? dhn_p + d * B * H : nullptr;
     dd.dcn = dcn_p ? dcn_p + d * B * H : nullptr;
@@ -661,11 +671,11 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
 Tensor gemm_nt(const Tensor& A, const Tensor& Bt, int64_t tile) {
   CHECK_HIP_TENSOR(A);
   const c10::DeviceGuard guard(A.device());
-  const int dt = dtype_code(A);
-  TORCH_CHECK(A.is_contiguous() && Bt.is_contiguous() && A.size(1) == Bt.size(1) && dtype_code(Bt) == dt);
+  const int dt = large_dtype(A);
+  TORCH_CHECK(A.is_contiguous() && Bt.is_contiguous() && A.size(1) == Bt.size(1) && large_dtype(Bt) == dt);
   const int64_t M = A.size(0), K = A.size(1), N = Bt.size(0);
   Tensor C = at::empty({M, N}, A.options().dtype(at::kFloat));
-  HIP_LAUNCH_CHECK(pdrnn_gemm_nt(u16(A), K, u16(Bt), K, C.data_ptr<float>(), N, (int)M, (int)N, (int)K, dt,
+  HIP_LAUNCH_CHECK(pdrnn_gemm_nt(eptr(A), K, eptr(Bt), K, C.data_ptr<float>(), N, (int)M, (int)N, (int)K, dt,
                                  (int)tile, cur_stream()));
   return C;
 }

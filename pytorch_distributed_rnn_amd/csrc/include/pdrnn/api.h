@@ -185,22 +185,24 @@ hipError_t pdrnn_embedding_bwd_csr(const float* dout, const int64_t* perm, const
                                    float* dweight, int64_t num_embeddings, int64_t dim,
                                    int64_t padding_idx, hipStream_t stream);
 
-// ---- large-H LSTM (MFMA per-step kernels, 16-bit storage) -----------------
+// ---- large-H LSTM (MFMA per-step kernels; bf16 / fp16 / fp32 storage) ------
+// Storage pointers are void*: elements of the dtype passed to the launchers
+// (0 bf16, 1 fp16, 2 fp32).
 // One direction of a layer.  Gate-interleaved layouts: column / row 4u+q is
 // gate q (i, f, g, o) of unit u.
 typedef struct {
-  const uint16_t* w;       // [4H, H] W_hh, gate-interleaved rows (forward GEMM: h Wp^T)
-  const uint16_t* wt;      // [H, 4H] W_hh^T, torch gate-blocked order (backward GEMM: dgates W_hh)
-  const uint16_t* xp;      // input projection incl. bias, [t, b, col] at t*xp_st + b*xp_sb + col
+  const void* w;           // [4H, H] W_hh, gate-interleaved rows (forward GEMM: h Wp^T)
+  const void* wt;          // [H, 4H] W_hh^T, torch gate-blocked order (backward GEMM: dgates W_hh)
+  const void* xp;          // input projection incl. bias, [t, b, col] at t*xp_st + b*xp_sb + col
   int64_t xp_sb, xp_st;
-  const uint16_t* h0;      // [B, H] or null
+  const void* h0;          // [B, H] or null
   const float* c0;         // [B, H] or null
-  uint16_t* hseq;          // outputs h_t at t*hseq_st + b*hseq_sb + u
+  void* hseq;              // outputs h_t at t*hseq_st + b*hseq_sb + u
   int64_t hseq_sb, hseq_st;
   float* cseq;             // [T, B, H] fp32 cell states
-  uint16_t* acts;          // [T, B, 4H] activated gates
-  uint16_t* dgates;        // [T, B, 4H] pre-activation gate gradients, gate-blocked (i|f|g|o)
-  const uint16_t* dout;    // grad of hseq (same strides as dout_sb / dout_st) or null
+  void* acts;              // [T, B, 4H] activated gates
+  void* dgates;            // [T, B, 4H] pre-activation gate gradients, gate-blocked (i|f|g|o)
+  const void* dout;        // grad of hseq (same strides as dout_sb / dout_st) or null
   int64_t dout_sb, dout_st;
   const float* dhn;        // [B, H] or null
   const float* dcn;        // [B, H] or null
@@ -222,12 +224,12 @@ typedef struct {
 
 int pdrnn_lstm_large_supported(int H);
 int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir, int* big);
-// dtype 0 = bf16, 1 = fp16; tile -1 = auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
+// dtype 0 = bf16, 1 = fp16, 2 = fp32; tile -1 = auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
                                  hipStream_t stream);
 hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir, int dtype, hipStream_t stream);
 // tile: -1 auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
-hipError_t pdrnn_gemm_nt(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
+hipError_t pdrnn_gemm_nt(const void* A, int64_t lda, const void* Bt, int64_t ldb, float* C, int64_t ldc,
                          int M, int N, int K, int dtype, int tile, hipStream_t stream);
 
 // Adam whose gradient is the fixed-order sum of `split` rows of work[split][P_total]

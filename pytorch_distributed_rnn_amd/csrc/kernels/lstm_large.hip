@@ -1,5 +1,6 @@
-// Large-hidden LSTM (H = 256 ... 4096+, bf16 / fp16 storage, fp32 accumulation
-// and cell state) for gfx950.
+// Large-hidden LSTM (H = 64k: bf16 / fp16 storage on v_mfma_f32_16x16x32, or
+// fp32 storage on v_mfma_f32_16x16x4_f32; fp32 accumulation and cell state)
+// for gfx950.
 //
 // A layer is split into
 //   * one big input-projection GEMM over all timesteps (library GEMM, issued
@@ -35,11 +36,13 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
-// storage type tags
+// storage type tags.  S: element type in HBM / LDS; EPC: elements per 16-byte
+// chunk (an LDS tile row is 8 chunks = 128 bytes: BK = 8 * EPC elements);
+// mfma: one 16-byte chunk per operand and lane -> one K-slab of the tile.
 struct BF16 {
-  typedef bf16x8 frag;
+  typedef uint16_t S;
+  static constexpr int EPC = 8;
   static __device__ __forceinline__ float to_f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
   static __device__ __forceinline__ uint16_t from_f(float f) {
     const __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN-preserving
@@ -51,7 +54,8 @@ struct BF16 {
   }
 };
 struct F16 {
-  typedef f16x8 frag;
+  typedef uint16_t S;
+  static constexpr int EPC = 8;
   static __device__ __forceinline__ float to_f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
   static __device__ __forceinline__ uint16_t from_f(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
   static __device__ __forceinline__ f32x4 mfma(const uint4& a, const uint4& b, f32x4 c) {
@@ -59,8 +63,36 @@ struct F16 {
                                                   c, 0, 0, 0);
   }
 };
+// fp32 storage on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32
+// accumulation; 157 TF/s dense = the fp32 vector peak, reached by the matrix
+// pipe without VALU issue pressure).  A lane's 16-byte chunk holds 4
+// consecutive k; the k-slab of chunk c is split into 4 MFMAs, MFMA m taking
+// component m -- lane group fq of MFMA m then covers k = 4 (ks*4 + fq) + m,
+// identical for A and B, so the 4 MFMAs sum the slab exactly once.
+struct F32 {
+  typedef float S;
+  static constexpr int EPC = 4;
+  static __device__ __forceinline__ float to_f(float v) { return v; }
+  static __device__ __forceinline__ float from_f(float f) { return f; }
+  static __device__ __forceinline__ f32x4 mfma(const uint4& a, const uint4& b, f32x4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
+  }
+};
 
-constexpr int BK = 64;  // K elements per LDS tile (8 x 16-byte chunks per row)
+// 8 consecutive elements of storage type DT (16 or 32 bytes)
+template <class DT>
+struct V8 {
+  uint4 v[sizeof(typename DT::S) / 2];
+  __device__ __forceinline__ float get(int k) const { return DT::to_f(reinterpret_cast<const typename DT::S*>(v)[k]); }
+  __device__ __forceinline__ void set(int k, float f) { reinterpret_cast<typename DT::S*>(v)[k] = DT::from_f(f); }
+};
+template <class DT>
+__device__ __forceinline__ V8<DT> ld_v8(const typename DT::S* p) { return *reinterpret_cast<const V8<DT>*>(p); }
+template <class DT>
+__device__ __forceinline__ void st_v8(typename DT::S* p, const V8<DT>& v) { *reinterpret_cast<V8<DT>*>(p) = v; }
 
 __device__ __forceinline__ float sigm(float x) { return fast_rcp(1.f + __expf(-x)); }
 __device__ __forceinline__ float tanh_(float x) {
@@ -76,15 +108,19 @@ __device__ __forceinline__ float qbcast(float v, int q) {
   }
 }
 
-// LDS image of a [ROWS x 64] 16-bit tile: 16-byte chunk c of row r lives at
-// chunk slot (c ^ (r & 7)) -- the XOR swizzle spreads the 16 rows an MFMA
-// fragment read touches over all bank groups.
-__device__ __forceinline__ int lds_off(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
+// LDS image of a [ROWS x 8 chunks] tile (128 bytes per row): 16-byte chunk c
+// of row r lives at chunk slot (c ^ (r & 7)) -- the XOR swizzle spreads the
+// 16 rows an MFMA fragment read touches over all bank groups.  Offsets in
+// elements of DT::S.
+template <class DT>
+__device__ __forceinline__ int lds_off(int row, int chunk) {
+  return row * 8 * DT::EPC + (chunk ^ (row & 7)) * DT::EPC;
+}
 
 // C[M, N] = A[M, K] * Bt[N, K]^T for one BM x BN block tile, WM x WN waves,
-// each wave (BM/WM) x (BN/WN) = MT x NT MFMA 16x16x32 sub-tiles.  A / Bt are
-// 16-bit, K-contiguous (lda / ldb).  Rows of A beyond M are clamped (the
-// caller discards their results).  K % 64 == 0.
+// each wave (BM/WM) x (BN/WN) = MT x NT 16x16 MFMA sub-tiles.  A / Bt are
+// DT::S, K-contiguous (lda / ldb).  Rows of A beyond M are clamped (the
+// caller discards their results).  K % BK == 0 (BK = 64 16-bit / 32 fp32).
 //
 // Staging: direct global->LDS DMA (global_load_lds_dwordx4, 1 KiB per wave
 // instruction) into a STAGES-deep ring of [BM+BN][64] tiles, prefetch distance
@@ -96,6 +132,8 @@ __device__ __forceinline__ int lds_off(int row, int chunk) { return row * BK + (
 // every ds_read).
 template <class DT, int BM, int BN, int WM, int WN, int STAGES>
 struct GemmPipe {
+  typedef typename DT::S S;
+  static constexpr int BK = 8 * DT::EPC;        // K elements per LDS tile row
   static constexpr int NWAVES = WM * WN, NTHREADS = NWAVES * 64;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int MT = WTM / 16, NT = WTN / 16;
@@ -112,8 +150,8 @@ struct GemmPipe {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
   }
 
-  __device__ static void run(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ Bt,
-                             int64_t ldb, int M, int K, int m0, int n0, uint16_t* smem, f32x4 (&acc)[MT][NT]) {
+  __device__ static void run(const S* __restrict__ A, int64_t lda, const S* __restrict__ Bt,
+                             int64_t ldb, int M, int K, int m0, int n0, S* smem, f32x4 (&acc)[MT][NT]) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -123,21 +161,22 @@ struct GemmPipe {
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const uint16_t* src[G];
+    const S* src[G];
 #pragma unroll
     for (int i = 0; i < G; ++i) {
       const int cid = (wid * G + i) * 64 + lane;
       const int row = cid >> 3, slot = cid & 7;
       const int lc = slot ^ (row & 7);
-      src[i] = row < BM ? A + (int64_t)min(m0 + row, M - 1) * lda + lc * 8
-                        : Bt + (int64_t)(n0 + row - BM) * ldb + lc * 8;
+      src[i] = row < BM ? A + (int64_t)min(m0 + row, M - 1) * lda + lc * DT::EPC
+                        : Bt + (int64_t)(n0 + row - BM) * ldb + lc * DT::EPC;
     }
     auto issue = [&](int kt, int st) {
-      uint16_t* base = smem + st * STAGE_ELEMS + wid * G * 512;
+      constexpr int GE = 64 * DT::EPC;  // elements per 1 KiB DMA group
+      S* base = smem + st * STAGE_ELEMS + wid * G * GE;
 #pragma unroll
       for (int i = 0; i < G; ++i)
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[i] + kt * BK),
-                                         (__attribute__((address_space(3))) void*)(base + i * 512), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(base + i * GE), 16, 0, 0);
     };
     const int KT = K / BK;
 #pragma unroll
@@ -158,17 +197,17 @@ struct GemmPipe {
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (kt + STAGES - 1 < KT) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
-      const uint16_t* sA = smem + (kt % STAGES) * STAGE_ELEMS;
-      const uint16_t* sB = sA + BM * BK;
+      const S* sA = smem + (kt % STAGES) * STAGE_ELEMS;
+      const S* sB = sA + BM * BK;
 #pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
+      for (int ks = 0; ks < 2; ++ks) {  // 2 k-slabs of 4 chunks per tile row
         uint4 fa[MT], fb[NT];
 #pragma unroll
         for (int i = 0; i < MT; ++i)
-          fa[i] = *reinterpret_cast<const uint4*>(sA + lds_off(wm * WTM + i * 16 + fr, ks * 4 + fq));
+          fa[i] = *reinterpret_cast<const uint4*>(sA + lds_off<DT>(wm * WTM + i * 16 + fr, ks * 4 + fq));
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          fb[j] = *reinterpret_cast<const uint4*>(sB + lds_off(wn * WTN + j * 16 + fr, ks * 4 + fq));
+          fb[j] = *reinterpret_cast<const uint4*>(sB + lds_off<DT>(wn * WTN + j * 16 + fr, ks * 4 + fq));
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -198,7 +237,9 @@ struct GemmPipe {
 template <class DT, int BM, int BN, int WM, int WN, int ST, int CELL>
 __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(PdrnnLstmLargeStepArgs args) {
   typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
+  typedef typename DT::S S;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  S* const smem = reinterpret_cast<S*>(smem_raw);
   const PdrnnLstmLargeDir& d = args.dir[blockIdx.z];
   const int B = args.B, H = args.H;
   const int t = args.reverse_mask & (1 << blockIdx.z) ? args.T - 1 - args.step : args.step;
@@ -207,7 +248,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
 
   // A operand: h_{prev} rows of the output sequence (or h0)
-  const uint16_t* hA = first ? d.h0 : d.hseq + (int64_t)tp * d.hseq_st;
+  const S* hA = first ? static_cast<const S*>(d.h0) : static_cast<const S*>(d.hseq) + (int64_t)tp * d.hseq_st;
   const int64_t lda = first ? H : d.hseq_sb;
   f32x4 acc[G::MT][G::NT];
   if (first && d.h0 == nullptr) {
@@ -216,7 +257,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
 #pragma unroll
       for (int j = 0; j < G::NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   } else {
-    G::run(hA, lda, d.w, H, B, H, m0, n0, smem_u16, acc);
+    G::run(hA, lda, static_cast<const S*>(d.w), H, B, H, m0, n0, smem, acc);
   }
 
   // Epilogue through LDS: the C tile is parked as fp32 [BM][BN+4] in the
@@ -225,8 +266,8 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
   // stores of the activated gates, 8-byte c and 4-byte h -- instead of
   // 2-byte scattered accesses straight from the MFMA C layout.
   constexpr int LDC = BN + 4;
-  static_assert(BM * LDC * 4 <= G::LDS_ELEMS * 2, "C tile must fit in the staging ring");
-  float* cs = reinterpret_cast<float*>(smem_u16);
+  static_assert(BM * LDC * 4 <= G::LDS_ELEMS * sizeof(S), "C tile must fit in the staging ring");
+  float* cs = reinterpret_cast<float*>(smem_raw);
   {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid / WN, wn = wid % WN;
@@ -239,11 +280,11 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
           cs[(wm * G::WTM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * G::WTN + j * 16 + (lane & 15)] = acc[i][j][r];
   }
   __syncthreads();
-  const uint16_t* xp = d.xp + (int64_t)t * d.xp_st;
+  const S* xp = static_cast<const S*>(d.xp) + (int64_t)t * d.xp_st;
   const float* cprev = first ? d.c0 : d.cseq + (int64_t)tp * B * H;
   float* cout = d.cseq + (int64_t)t * B * H;
-  uint16_t* hout = d.hseq + (int64_t)t * d.hseq_st;
-  uint16_t* acts = d.acts + (int64_t)t * B * 4 * H;
+  S* hout = static_cast<S*>(d.hseq) + (int64_t)t * d.hseq_st;
+  S* acts = static_cast<S*>(d.acts) + (int64_t)t * B * 4 * H;
   constexpr int C8 = BN / 8;
   // Every item's global operands (xp, c_prev) and C-tile slice are loaded
   // first, then the cell math and stores run: the loads of all items are in
@@ -251,7 +292,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
   // workgroup per CU the epilogue is not hidden behind another workgroup's
   // MFMA loop).
   constexpr int ITEMS = (BM * C8 + G::NTHREADS - 1) / G::NTHREADS;
-  uint4 xv[ITEMS];
+  V8<DT> xv[ITEMS];
   float2 cpv[ITEMS];
   float4 za[ITEMS], zb[ITEMS];
 #pragma unroll
@@ -260,7 +301,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
     const int row = e / C8, c8 = e - row * C8;
     const int b = min(m0 + row, B - 1);
     const int col = n0 + c8 * 8;
-    xv[it] = *reinterpret_cast<const uint4*>(xp + (int64_t)b * d.xp_sb + col);
+    xv[it] = ld_v8<DT>(xp + (int64_t)b * d.xp_sb + col);
     cpv[it] = cprev ? *reinterpret_cast<const float2*>(cprev + (int64_t)b * H + (col >> 2)) : make_float2(0.f, 0.f);
     za[it] = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8);
     zb[it] = *reinterpret_cast<const float4*>(cs + row * LDC + c8 * 8 + 4);
@@ -272,12 +313,11 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
     const int b = m0 + row;
     if (e >= BM * C8 || b >= B) continue;
     const int col = n0 + c8 * 8;
-    const uint16_t* xh = reinterpret_cast<const uint16_t*>(&xv[it]);
     const float z[8] = {za[it].x, za[it].y, za[it].z, za[it].w, zb[it].x, zb[it].y, zb[it].z, zb[it].w};
     float g[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float zz = z[k] + DT::to_f(xh[k]);
+      const float zz = z[k] + xv[it].get(k);
       if constexpr (CELL == 0) g[k] = (k & 3) == 2 ? tanh_(zz) : sigm(zz);
       else g[k] = (k & 3) < 2 ? sigm(zz) : zz;  // GRU: r, z activated; n_x, n_h linear
     }
@@ -297,14 +337,17 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
       s0 = h0v = fmaf(g[1], cp.x - g[2], g[2]);
       s1 = h1v = fmaf(g[5], cp.y - g[6], g[6]);
     }
-    uint4 av;
-    uint16_t* ah = reinterpret_cast<uint16_t*>(&av);
+    V8<DT> av;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) ah[k] = DT::from_f(g[k]);
-    *reinterpret_cast<uint4*>(acts + (int64_t)b * 4 * H + col) = av;
+    for (int k = 0; k < 8; ++k) av.set(k, g[k]);
+    st_v8<DT>(acts + (int64_t)b * 4 * H + col, av);
     *reinterpret_cast<float2*>(cout + (int64_t)b * H + u) = make_float2(s0, s1);
-    const uint32_t hv = (uint32_t)DT::from_f(h0v) | ((uint32_t)DT::from_f(h1v) << 16);
-    *reinterpret_cast<uint32_t*>(hout + (int64_t)b * d.hseq_sb + u) = hv;
+    if constexpr (sizeof(S) == 2) {
+      const uint32_t hv = (uint32_t)DT::from_f(h0v) | ((uint32_t)DT::from_f(h1v) << 16);
+      *reinterpret_cast<uint32_t*>(hout + (int64_t)b * d.hseq_sb + u) = hv;
+    } else {
+      *reinterpret_cast<float2*>(hout + (int64_t)b * d.hseq_sb + u) = make_float2(h0v, h1v);
+    }
   }
 }
 
@@ -322,14 +365,15 @@ __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B,
     if (CELL == 0 && d.dc0) d.dc0[bu] = carry;
     return;
   }
-  if (d.dout) dh += DT::to_f(d.dout[(int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u]);
-  const u16x4 av = *reinterpret_cast<const u16x4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u);
-  const float a0 = DT::to_f(av.x), a1 = DT::to_f(av.y), a2 = DT::to_f(av.z), a3 = DT::to_f(av.w);
+  typedef typename DT::S S;
+  if (d.dout) dh += DT::to_f(static_cast<const S*>(d.dout)[(int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u]);
+  const S* ap = static_cast<const S*>(d.acts) + ((int64_t)tn * B + b) * 4 * H + 4 * u;
+  const float a0 = DT::to_f(ap[0]), a1 = DT::to_f(ap[1]), a2 = DT::to_f(ap[2]), a3 = DT::to_f(ap[3]);
   const int tpp = rev ? tn + 1 : tn - 1;
   const bool has_prev = rev ? tpp < T : tpp >= 0;
   // LSTM: c_{tn-1};  GRU: h_{tn-1} (both fp32 in cseq, c0 = initial state)
   const float sp = has_prev ? d.cseq[(int64_t)tpp * B * H + bu] : (d.c0 ? d.c0[bu] : 0.f);
-  u16x4 dg;
+  struct { S x, y, z, w; } dg;
   float next;
   if constexpr (CELL == 0) {
     const float ig = a0, fg = a1, gg = a2, og = a3;
@@ -354,7 +398,7 @@ __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B,
   // gate-BLOCKED layout (torch's row order): the next step GEMM pairs it with
   // W_hh^T as stored, and the weight-gradient GEMMs land directly in the
   // parameters' layout (no permutation copies)
-  uint16_t* dgp = d.dgates + ((int64_t)tn * B + b) * 4 * H + u;
+  S* dgp = static_cast<S*>(d.dgates) + ((int64_t)tn * B + b) * 4 * H + u;
   dgp[0] = dg.x; dgp[H] = dg.y; dgp[2 * H] = dg.z; dgp[3 * H] = dg.w;
   d.dc_carry[bu] = next;
 }
@@ -373,23 +417,25 @@ __device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
 // cell_bwd_elem's math with 16-byte accesses, split into a load phase and a
 // compute phase so that the epilogue of the backward step kernel puts the
 // global loads of several items in flight before the first one is consumed.
+template <class DT>
 struct CellBwdOps8 {
   float carry[8], sp[8], cur[8];
-  uint4 av[4];
-  uint4 dv;
+  V8<DT> av[4];  // 8 units x 4 gates
+  V8<DT> dv;
 };
 
 template <class DT, int CELL>
 __device__ __forceinline__ void cell_bwd_load8(const PdrnnLstmLargeDir& d, int B, int H, int T, bool rev, int tn,
-                                               bool cell, int b, int u0, CellBwdOps8& o) {
+                                               bool cell, int b, int u0, CellBwdOps8<DT>& o) {
+  typedef typename DT::S S;
   const int64_t bu = (int64_t)b * H + u0;
   ld8(d.dc_carry + bu, o.carry);
   if (!cell) return;
-  o.dv = d.dout ? *reinterpret_cast<const uint4*>(d.dout + (int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u0)
-                : make_uint4(0u, 0u, 0u, 0u);
-  const uint4* ap = reinterpret_cast<const uint4*>(d.acts + ((int64_t)tn * B + b) * 4 * H + 4 * u0);
+  if (d.dout) o.dv = ld_v8<DT>(static_cast<const S*>(d.dout) + (int64_t)tn * d.dout_st + (int64_t)b * d.dout_sb + u0);
+  else o.dv = V8<DT>{};
+  const S* ap = static_cast<const S*>(d.acts) + ((int64_t)tn * B + b) * 4 * H + 4 * u0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) o.av[q] = ap[q];
+  for (int q = 0; q < 4; ++q) o.av[q] = ld_v8<DT>(ap + 8 * q);
   const int tpp = rev ? tn + 1 : tn - 1;
   const bool has_prev = rev ? tpp < T : tpp >= 0;
   if (has_prev) ld8(d.cseq + (int64_t)tpp * B * H + bu, o.sp);
@@ -403,7 +449,8 @@ __device__ __forceinline__ void cell_bwd_load8(const PdrnnLstmLargeDir& d, int B
 
 template <class DT, int CELL>
 __device__ __forceinline__ void cell_bwd_compute8(const PdrnnLstmLargeDir& d, int B, int H, bool cell, int tn, int b,
-                                                  int u0, float (&dh)[8], const CellBwdOps8& o) {
+                                                  int u0, float (&dh)[8], const CellBwdOps8<DT>& o) {
+  typedef typename DT::S S;
   const int64_t bu = (int64_t)b * H + u0;
   float carry[8];
 #pragma unroll
@@ -418,17 +465,17 @@ __device__ __forceinline__ void cell_bwd_compute8(const PdrnnLstmLargeDir& d, in
     return;
   }
   if (d.dout) {
-    const uint16_t* dh16 = reinterpret_cast<const uint16_t*>(&o.dv);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) dh[k] += DT::to_f(dh16[k]);
+    for (int k = 0; k < 8; ++k) dh[k] += o.dv.get(k);
   }
-  const uint16_t* a16 = reinterpret_cast<const uint16_t*>(o.av);  // unit k: a16[4k .. 4k+3]
-  uint16_t g[4][8];
+  // unit k: gates 4k .. 4k+3 of the 32 loaded (V8 q holds units 2q, 2q+1)
+  auto act = [&](int e) { return o.av[e >> 3].get(e & 7); };
+  alignas(16) S g[4][8];
   float next[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const float a0 = DT::to_f(a16[4 * k]), a1 = DT::to_f(a16[4 * k + 1]);
-    const float a2 = DT::to_f(a16[4 * k + 2]), a3 = DT::to_f(a16[4 * k + 3]);
+    const float a0 = act(4 * k), a1 = act(4 * k + 1);
+    const float a2 = act(4 * k + 2), a3 = act(4 * k + 3);
     if constexpr (CELL == 0) {
       const float tc = tanh_(o.cur[k]);
       const float dc = fmaf(dh[k] * a3, 1.f - tc * tc, carry[k]);
@@ -446,9 +493,9 @@ __device__ __forceinline__ void cell_bwd_compute8(const PdrnnLstmLargeDir& d, in
       next[k] = dh[k] * a1;
     }
   }
-  uint16_t* dgp = d.dgates + ((int64_t)tn * B + b) * 4 * H + u0;
+  S* dgp = static_cast<S*>(d.dgates) + ((int64_t)tn * B + b) * 4 * H + u0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) *reinterpret_cast<uint4*>(dgp + q * H) = *reinterpret_cast<const uint4*>(g[q]);
+  for (int q = 0; q < 4; ++q) st_v8<DT>(dgp + q * H, *reinterpret_cast<const V8<DT>*>(g[q]));
   st8(d.dc_carry + bu, next);
 }
 
@@ -463,7 +510,9 @@ __device__ __forceinline__ void cell_bwd_compute8(const PdrnnLstmLargeDir& d, in
 template <class DT, int BM, int BN, int WM, int WN, int ST, int CELL>
 __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(PdrnnLstmLargeStepArgs args) {
   typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
+  typedef typename DT::S S;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  S* const smem = reinterpret_cast<S*>(smem_raw);
   const PdrnnLstmLargeDir& d = args.dir[blockIdx.z];
   const int B = args.B, H = args.H, T = args.T;
   const bool rev = args.reverse_mask & (1 << blockIdx.z);
@@ -475,7 +524,8 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(Pdrnn
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
 
   f32x4 acc[G::MT][G::NT];
-  G::run(d.dgates + (int64_t)t * B * 4 * H, 4 * H, d.wt, 4 * H, B, 4 * H, m0, n0, smem_u16, acc);
+  G::run(static_cast<const S*>(d.dgates) + (int64_t)t * B * 4 * H, 4 * H, static_cast<const S*>(d.wt), 4 * H, B,
+         4 * H, m0, n0, smem, acc);
 
   // Epilogue through LDS (as in the forward): the dh tile is parked as fp32
   // [BM][BN+4] in the idle staging ring, then each thread runs the cell
@@ -483,8 +533,8 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(Pdrnn
   // (acts, c, carry, dout, and one store per gate block of dgates) instead of
   // per-element 2-byte accesses straight from the MFMA C layout.
   constexpr int LDC = BN + 4;
-  static_assert(BM * LDC * 4 <= G::LDS_ELEMS * 2, "C tile must fit in the staging ring");
-  float* cs = reinterpret_cast<float*>(smem_u16);
+  static_assert(BM * LDC * 4 <= G::LDS_ELEMS * sizeof(S), "C tile must fit in the staging ring");
+  float* cs = reinterpret_cast<float*>(smem_raw);
   {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid / WN, wn = wid % WN;
@@ -504,7 +554,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(Pdrnn
   constexpr int IB = ITEMS < 2 ? ITEMS : 2;
 #pragma unroll
   for (int i0 = 0; i0 < ITEMS; i0 += IB) {
-    CellBwdOps8 ops[IB];
+    CellBwdOps8<DT> ops[IB];
 #pragma unroll
     for (int ib = 0; ib < IB; ++ib) {
       const int e = min((int)threadIdx.x + (i0 + ib) * G::NTHREADS, BM * C8 - 1);
@@ -534,7 +584,8 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_step_kernel(Pdrnn
 template <class DT, int BM, int BN, int WM, int WN, int ST>
 __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_splitk_kernel(PdrnnLstmLargeStepArgs args) {
   typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
+  typedef typename DT::S Sd;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int S = args.splitk;
   const int dir = blockIdx.z / S, sl = blockIdx.z - dir * S;
   const PdrnnLstmLargeDir& d = args.dir[dir];
@@ -544,7 +595,8 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_bwd_splitk_kernel(Pdr
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int Ks = 4 * H / S, k0 = sl * Ks;
   f32x4 acc[G::MT][G::NT];
-  G::run(d.dgates + (int64_t)t * B * 4 * H + k0, 4 * H, d.wt + k0, 4 * H, B, Ks, m0, n0, smem_u16, acc);
+  G::run(static_cast<const Sd*>(d.dgates) + (int64_t)t * B * 4 * H + k0, 4 * H, static_cast<const Sd*>(d.wt) + k0,
+         4 * H, B, Ks, m0, n0, reinterpret_cast<Sd*>(smem_raw), acc);
   float* ws = args.ws + ((int64_t)sl * 2 + dir) * B * H;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -594,14 +646,14 @@ __global__ void lstm_large_bwd_first_kernel(PdrnnLstmLargeStepArgs args) {
 
 // Plain NT GEMM on the same core (tests / fallbacks): C[M,N] fp32 = A Bt^T.
 template <class DT, int BM, int BN, int WM, int WN, int ST>
-__global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(const uint16_t* A, int64_t lda, const uint16_t* Bt,
-                                                               int64_t ldb, float* C, int64_t ldc, int M, int N,
-                                                               int K) {
+__global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(const typename DT::S* A, int64_t lda,
+                                                               const typename DT::S* Bt, int64_t ldb, float* C,
+                                                               int64_t ldc, int M, int N, int K) {
   typedef GemmPipe<DT, BM, BN, WM, WN, ST> G;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem_u16[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   f32x4 acc[G::MT][G::NT];
-  G::run(A, lda, Bt, ldb, M, K, m0, n0, smem_u16, acc);
+  G::run(A, lda, Bt, ldb, M, K, m0, n0, reinterpret_cast<typename DT::S*>(smem_raw), acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WN, wn = wid % WN;
 #pragma unroll
@@ -622,7 +674,7 @@ hipError_t launch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward,
   const int N = backward ? a->H : 4 * a->H;
   if (N % BN) return hipErrorInvalidValue;
   dim3 grid(N / BN, (a->B + BM - 1) / BM, ndir);
-  const size_t lds = sizeof(uint16_t) * G::LDS_ELEMS;
+  const size_t lds = sizeof(typename DT::S) * G::LDS_ELEMS;
   if (backward)
     hipLaunchKernelGGL((lstm_large_bwd_step_kernel<DT, BM, BN, WM, WN, ST, CELL>), grid, dim3(G::NTHREADS), lds, st, *a);
   else
@@ -656,13 +708,13 @@ hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwar
       typedef GemmPipe<DT, 128, 128, 2, 2, 3> G;
       dim3 grid(N / 128, (a->B + 127) / 128, ndir * a->splitk);
       hipLaunchKernelGGL((lstm_large_bwd_splitk_kernel<DT, 128, 128, 2, 2, 3>), grid, dim3(G::NTHREADS),
-                         sizeof(uint16_t) * G::LDS_ELEMS, st, *a);
+                         sizeof(typename DT::S) * G::LDS_ELEMS, st, *a);
     } else {
       typedef GemmPipe<DT, 32, 32, 2, 2, 4> G;
       if (N % 32) return hipErrorInvalidValue;
       dim3 grid(N / 32, (a->B + 31) / 32, ndir * a->splitk);
       hipLaunchKernelGGL((lstm_large_bwd_splitk_kernel<DT, 32, 32, 2, 2, 4>), grid, dim3(G::NTHREADS),
-                         sizeof(uint16_t) * G::LDS_ELEMS, st, *a);
+                         sizeof(typename DT::S) * G::LDS_ELEMS, st, *a);
     }
     PDRNN_HIP_CHECK(hipGetLastError());
     const int64_t n = (int64_t)a->B * a->H;
@@ -689,8 +741,10 @@ hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwar
   X(13, 128, 128, 2, 2, 2)
 
 template <class DT>
-hipError_t gemm_nt_dispatch(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
+hipError_t gemm_nt_dispatch(const void* Av, int64_t lda, const void* Btv, int64_t ldb, float* C, int64_t ldc,
                             int M, int N, int K, int tile, hipStream_t st) {
+  const typename DT::S* A = static_cast<const typename DT::S*>(Av);
+  const typename DT::S* Bt = static_cast<const typename DT::S*>(Btv);
   if (tile < 0 || (tile > 4 && tile < 10) || tile > 13) tile = pick_tile(M, N, 1);
   switch (tile) {
 #define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_)                                                      \
@@ -699,7 +753,7 @@ hipError_t gemm_nt_dispatch(const uint16_t* A, int64_t lda, const uint16_t* Bt, 
     if (N % BN_) return hipErrorInvalidValue;                                                        \
     dim3 grid(N / BN_, (M + BM_ - 1) / BM_);                                                         \
     hipLaunchKernelGGL((gemm_nt_kernel<DT, BM_, BN_, WM_, WN_, ST_>), grid, dim3(G::NTHREADS),       \
-                       sizeof(uint16_t) * G::LDS_ELEMS, st, A, lda, Bt, ldb, C, ldc, M, N, K);       \
+                       sizeof(typename DT::S) * G::LDS_ELEMS, st, A, lda, Bt, ldb, C, ldc, M, N, K); \
     return hipGetLastError();                                                                        \
   }
     PDRNN_TILE_CFGS(PDRNN_CASE)
@@ -745,6 +799,9 @@ hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int 
   if (dtype == 0)
     return a->cell ? pdrnn::dispatch_step<pdrnn::BF16, 1>(a, ndir, bw, tile, stream)
                    : pdrnn::dispatch_step<pdrnn::BF16, 0>(a, ndir, bw, tile, stream);
+  if (dtype == 2)
+    return a->cell ? pdrnn::dispatch_step<pdrnn::F32, 1>(a, ndir, bw, tile, stream)
+                   : pdrnn::dispatch_step<pdrnn::F32, 0>(a, ndir, bw, tile, stream);
   return a->cell ? pdrnn::dispatch_step<pdrnn::F16, 1>(a, ndir, bw, tile, stream)
                  : pdrnn::dispatch_step<pdrnn::F16, 0>(a, ndir, bw, tile, stream);
 }
@@ -756,6 +813,9 @@ hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir,
   if (dtype == 0) {
     if (a->cell) hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::BF16, 1>), grid, dim3(256), 0, stream, *a);
     else hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::BF16, 0>), grid, dim3(256), 0, stream, *a);
+  } else if (dtype == 2) {
+    if (a->cell) hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::F32, 1>), grid, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::F32, 0>), grid, dim3(256), 0, stream, *a);
   } else {
     if (a->cell) hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::F16, 1>), grid, dim3(256), 0, stream, *a);
     else hipLaunchKernelGGL((pdrnn::lstm_large_bwd_first_kernel<pdrnn::F16, 0>), grid, dim3(256), 0, stream, *a);
@@ -763,10 +823,11 @@ hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir,
   return hipGetLastError();
 }
 
-hipError_t pdrnn_gemm_nt(const uint16_t* A, int64_t lda, const uint16_t* Bt, int64_t ldb, float* C, int64_t ldc,
+hipError_t pdrnn_gemm_nt(const void* A, int64_t lda, const void* Bt, int64_t ldb, float* C, int64_t ldc,
                          int M, int N, int K, int dtype, int tile, hipStream_t stream) {
   if (K % 64 || N % 32) return hipErrorInvalidValue;
   if (dtype == 0) return pdrnn::gemm_nt_dispatch<pdrnn::BF16>(A, lda, Bt, ldb, C, ldc, M, N, K, tile, stream);
+  if (dtype == 2) return pdrnn::gemm_nt_dispatch<pdrnn::F32>(A, lda, Bt, ldb, C, ldc, M, N, K, tile, stream);
   return pdrnn::gemm_nt_dispatch<pdrnn::F16>(A, lda, Bt, ldb, C, ldc, M, N, K, tile, stream);
 }
 

@@ -38,7 +38,7 @@ from .lstm_large import _interleave, _mm_f32, _perm, _tile
 
 
 def supported(x: Tensor, hidden: int) -> bool:
-    if x.dtype not in (torch.bfloat16, torch.float16) or x.device.type != "cuda" or x.dim() != 3:
+    if x.dtype not in (torch.bfloat16, torch.float16, torch.float32) or x.device.type != "cuda" or x.dim() != 3:
         return False
     mod = _ext.native(x.device)
     return mod is not None and hasattr(mod, "lstm_large_fwd") and bool(mod.lstm_large_supported(hidden))

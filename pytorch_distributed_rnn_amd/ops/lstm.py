@@ -311,6 +311,21 @@ def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Te
                                              num_layers=num_layers, batch_first=batch_first,
                                              bidirectional=bidirectional, dropout=dropout,
                                              training=training)
+    hp = -(-hidden // 64) * 64  # large-H kernels: H % 64 == 0 -> zero-pad the hidden size
+    if not bidirectional and hidden > 64 and lstm_large.supported(x, hp, num_layers):
+        if idx is not None:
+            x = x.index_select(0 if batch_first else 1, idx)
+        per = len(weights) // num_layers
+        ws: List[Optional[Tensor]] = []
+        for l in range(num_layers):
+            w = list(weights[l * per:(l + 1) * per]) + ([None, None] if per == 2 else [])
+            in_pad = None if l == 0 else hp
+            ws += [pad_gate_rows(w[0], hidden, hp, 4, in_pad), pad_gate_rows(w[1], hidden, hp, 4, hp),
+                   pad_gate_rows(w[2], hidden, hp, 4), pad_gate_rows(w[3], hidden, hp, 4)]
+        out, hn, cn = lstm_large.lstm_large_forward(
+            x, ws, _pad_state(h0, hidden, hp), _pad_state(c0, hidden, hp), hidden=hp,
+            num_layers=num_layers, batch_first=batch_first, dropout=dropout, training=training)
+        return out[..., :hidden], hn[..., :hidden], cn[..., :hidden]
     _ext.fallback(f"LSTM(H={hidden}, I={x.shape[-1]}, layers={num_layers}, {x.dtype}, "
                   f"bidirectional={bidirectional})", x.device)
     if idx is not None:

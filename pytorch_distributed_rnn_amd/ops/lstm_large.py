@@ -1,8 +1,11 @@
 """Large-hidden LSTM stack on the MFMA step kernels (csrc/kernels/lstm_large.hip).
 
-Used for 16-bit inputs (bf16 / fp16 compute, fp32 master weights, fp32 cell
-state and weight gradients) when ``H % 64 == 0`` -- the char-LM (H = 1024) and
-stacked bidirectional (H = 4096) configurations.  Per layer:
+Used when ``H % 64 == 0`` (other H >= 64 are zero-padded up by ops/lstm.py):
+16-bit inputs (bf16 / fp16 compute on v_mfma_f32_16x16x32, fp32 master
+weights, fp32 cell state and weight gradients) -- the char-LM (H = 1024) and
+stacked bidirectional (H = 4096) configurations -- and fp32 inputs (exact fp32
+products on v_mfma_f32_16x16x4_f32, e.g. the motion CLI with
+``--hidden-units 128``).  Per layer:
 
 * input projection for ALL timesteps and both directions in one library GEMM
   (``Xp = X [W_ih_fwd; W_ih_rev]^T + b``, gate-interleaved columns);
@@ -54,7 +57,7 @@ def _tile() -> int:
 
 
 def supported(x: Tensor, hidden: int, num_layers: int, bidirectional: bool = False) -> bool:
-    if x.dtype not in (torch.bfloat16, torch.float16) or x.device.type != "cuda" or x.dim() != 3:
+    if x.dtype not in (torch.bfloat16, torch.float16, torch.float32) or x.device.type != "cuda" or x.dim() != 3:
         return False
     mod = _ext.native(x.device)
     return mod is not None and hasattr(mod, "lstm_large_fwd") and bool(mod.lstm_large_supported(hidden))
@@ -77,7 +80,7 @@ def _addmm_f32_(c: Tensor, a: Tensor, b: Tensor) -> Tensor:
 
 
 def shadow(w: Tensor, kind: str, cdt: torch.dtype, hidden: int) -> Tensor:
-    """16-bit copy of an fp32 master weight in the layout a kernel reads,
+    """Compute-dtype copy (16-bit, or fp32 for the fp32 path) of an fp32 master weight in the layout a kernel reads,
     cached on the parameter and rebuilt only when the master changed: its
     version counter moves on every in-place update (FusedAdam's native step
     bumps it explicitly).  Replaces the per-forward casts / interleaves /

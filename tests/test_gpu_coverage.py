@@ -2,7 +2,7 @@
 --stacked-layer into nn.LSTM, reference src/motion/main.py:20-21,
 src/motion/model.py:9) run on the HIP kernels -- zero-padded hidden units,
 layer chunks, per-direction bidirectional launches, dropout between layer
-chunks -- under strict kernel mode (PDRNN_KERNELS=hip-strict: an ATen/MIOpen
+chunks, fp32 large hidden sizes on the MFMA step kernels -- under strict kernel mode (PDRNN_KERNELS=hip-strict: an ATen/MIOpen
 fallback raises), checked against fp64 torch modules."""
 import pytest
 import torch
@@ -37,6 +37,10 @@ def _check(mod_ref, mod, x, h0=None, tol=2e-4):
 @pytest.mark.parametrize("cell,H,L,bidir", [
     ("lstm", 8, 2, False), ("lstm", 48, 2, False), ("lstm", 24, 3, False), ("lstm", 32, 5, False),
     ("lstm", 32, 2, True), ("lstm", 16, 1, True), ("gru", 8, 2, False), ("gru", 48, 3, False),
+    # fp32 large-H: MFMA 16x16x4 f32 step kernels (lstm_large.hip, F32 storage);
+    # H = 100 is zero-padded to 128
+    ("lstm", 128, 2, False), ("lstm", 100, 1, False), ("lstm", 128, 1, True), ("gru", 128, 2, False),
+    ("gru", 192, 1, True),
 ])
 def test_uncovered_shapes_run_on_hip(cell, H, L, bidir):
     from pytorch_distributed_rnn_amd.models.rnn import GRU, LSTM
@@ -53,7 +57,7 @@ def test_motion_cli_shapes_train_on_hip(tmp_path):
     """main.py-equivalent model builds with the reference's flags train a step
     through the kernels (strict mode), dropout between layer chunks included."""
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    for H, L, bidir in ((48, 2, False), (8, 2, False), (32, 2, True)):
+    for H, L, bidir in ((48, 2, False), (8, 2, False), (32, 2, True), (128, 2, False), (256, 1, True)):
         torch.manual_seed(1)
         m = MotionModel(9, H, L, 6, bidirectional=bidir).cuda()
         m.lstm.dropout = 0.1
