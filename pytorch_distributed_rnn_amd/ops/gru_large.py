@@ -34,7 +34,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-from .lstm_large import _interleave, _mm_f32, _perm, _tile
+from .lstm_large import _interleave, _mm_f32, _mm_tn_f32, _perm, _tile
 
 
 def supported(x: Tensor, hidden: int) -> bool:
@@ -109,10 +109,10 @@ class _LargeGRULayer(torch.autograd.Function):
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # [r | z | dpre_n | dpre_n r]
             hprev = _hprev(hseq[:, :, d * H:(d + 1) * H], h0c[d:d + 1] if h0c is not None else None, d)
-            dw4 = _mm_f32(G.t(), hprev.reshape(T * B, H))
+            dw4 = _mm_tn_f32(G, hprev.reshape(T * B, H), T)
             dwhh = torch.cat([dw4[:2 * H], dw4[3 * H:]])
             Gx = G[:, :3 * H]                                        # x side: [r | z | dpre_n]
-            dwih = _mm_f32(Gx.t(), x2)
+            dwih = _mm_tn_f32(Gx, x2, T)
             cs = G.sum(0, dtype=torch.float32)
             dbih = cs[:3 * H]
             dbhh = torch.cat([cs[:2 * H], cs[3 * H:]])

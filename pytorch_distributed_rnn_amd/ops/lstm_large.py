@@ -71,6 +71,34 @@ def _mm_f32(a: Tensor, b: Tensor) -> Tensor:
         return torch.mm(a.float(), b.float())
 
 
+def _mm_tn_f32(g: Tensor, x: Tensor, steps: int) -> Tensor:
+    """g^T x with fp32 output for g [K, M], x [K, N], K = steps * rows.
+
+    Weight-gradient GEMMs of small layers have a tiny output and a huge K
+    (fp32 motion model, H = 128, B = 1440, T = 128: 512 x 128 outputs, K =
+    184k), so a single library GEMM has too few output tiles to fill the GPU
+    (measured 632 us at 38 TF/s, `profiles/r2_fp32_large_h128.md`).  Those are
+    split along K at step boundaries into one strided-batched GEMM plus a sum."""
+    K, M = g.shape
+    N = x.shape[1]
+    c = 1
+    if M * N <= (1 << 20) and K >= (1 << 14) and steps > 1:
+        for d in range(min(steps, 128), 1, -1):
+            if steps % d == 0 and K // d >= 1024:
+                c = d
+                break
+    if c == 1:
+        return _mm_f32(g.t(), x)
+    gb = g.reshape(c, K // c, M).transpose(1, 2)
+    xb = x.reshape(c, K // c, N)
+    if g.dtype == torch.float32:
+        return torch.bmm(gb, xb).sum(0)
+    try:
+        return torch.bmm(gb, xb, out_dtype=torch.float32).sum(0)
+    except (RuntimeError, TypeError):
+        return _mm_f32(g.t(), x)
+
+
 def _addmm_f32_(c: Tensor, a: Tensor, b: Tensor) -> Tensor:
     """c += a @ b, fp32 c, 16-bit a / b."""
     try:
@@ -202,15 +230,15 @@ class _LargeLSTMLayer(torch.autograd.Function):
             # reverse h_{t+1}; the step next to the initial state pairs with h0
             if T > 1:
                 if d == 0:
-                    dwhh = _mm_f32(G[B:].t(), hd[:-1].reshape((T - 1) * B, H))
+                    dwhh = _mm_tn_f32(G[B:], hd[:-1].reshape((T - 1) * B, H), T - 1)
                 else:
-                    dwhh = _mm_f32(G[:(T - 1) * B].t(), hd[1:].reshape((T - 1) * B, H))
+                    dwhh = _mm_tn_f32(G[:(T - 1) * B], hd[1:].reshape((T - 1) * B, H), T - 1)
             else:
                 dwhh = torch.zeros(4 * H, H, device=x.device, dtype=torch.float32)
             if h0c is not None:
                 g0 = G[:B] if d == 0 else G[(T - 1) * B:]
                 _addmm_f32_(dwhh, g0.t(), h0c[d])
-            dwih = _mm_f32(G.t(), x2)
+            dwih = _mm_tn_f32(G, x2, T)
             db = G.sum(0, dtype=torch.float32)  # fp32 accumulation, no fp32 copy of G
             if not need_dx:
                 pass  # layer input without grad (e.g. the data): no dX GEMM
