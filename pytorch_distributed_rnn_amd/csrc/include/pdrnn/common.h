@@ -142,7 +142,6 @@ PDRNN_DEVICE float ldx(const float* x, int64_t i, int bf) {
 }
 
 typedef float pdrnn_f2 __attribute__((ext_vector_type(2)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 PDRNN_DEVICE float quad_bcast(float v, int q) {
   // quad_perm [q,q,q,q]: every lane of the quad reads lane q of the quad

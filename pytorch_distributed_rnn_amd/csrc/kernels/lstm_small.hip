@@ -44,11 +44,6 @@ constexpr int kXldsBytes = 48 * 1024;
 #ifndef PDRNN_ABLATE
 #define PDRNN_ABLATE 0
 #endif
-// BPTT weight gradients on the matrix pipe (v_mfma_f32_16x16x4_f32 over 4
-// buffered timesteps) instead of per-step rank-1 VALU updates; 0 = VALU.
-#ifndef PDRNN_BWD_DW_MFMA
-#define PDRNN_BWD_DW_MFMA 1
-#endif
 #ifndef PDRNN_FWD_BULK_LDS
 #define PDRNN_FWD_BULK_LDS 1
 #endif
@@ -778,15 +773,6 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
   constexpr int RS = R / L;          // rows per lane
   constexpr int LANES = H * L;
   static_assert(L >= 4 && RS % 4 == 0, "need >= 4 lanes per unit, float4 row slices");
-  // dW on MFMA (one sequence per workgroup, 4 lanes per unit): the gate
-  // gradients and the layer inputs of the last steps stay in LDS rings of DGR
-  // slots, and every 4th step each wave accumulates its dW tiles with
-  // v_mfma_f32_16x16x4_f32 (K = the 4 timesteps), one row tile per step
-  // during the next group.  The ring holds 16 steps so that the slot a row
-  // phase writes is never one a lagging wave of the same workgroup still
-  // reads (reads reach back at most 7 steps, writes run at most 1 ahead).
-  constexpr bool DWM = PDRNN_BWD_DW_MFMA && L == 4 && NB == 1 && (H == 16 || H == 32);
-  constexpr int DGR = DWM ? 16 : 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
   const int NL = a.NL, B = a.B, T = a.T, I = a.I;
@@ -816,12 +802,9 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
   // ~150 cycles per step, profiles/r2_small_kernels_pmc.md).
   constexpr int RP = R + L * 4;
   float* dg_s = smem;
-  float* dha_s = dg_s + NB * NL * DGR * RP;
-  float* hring = dha_s + NB * NL * 2 * H;          // DWM: [NL][DGR][H] h_{t-1} per step
-  float* xring = hring + (DWM ? NL * DGR * H : 0);  // DWM: [NL][DGR][H] layer input per step
-  float* xs = xring + (DWM ? NL * DGR * H : 0);
-  // gate-gradient slot of iteration `it` (ring of DGR; DGR = 2: parity)
-  auto dgbuf = [&](int n, int l, int it) { return dg_s + ((n * NL + l) * DGR + (it & (DGR - 1))) * RP; };
+  float* dha_s = dg_s + NB * NL * 2 * RP;
+  float* xs = dha_s + NB * NL * 2 * H;
+  auto dgbuf = [&](int n, int l, int p) { return dg_s + ((n * NL + l) * 2 + p) * RP; };
   auto dhabuf = [&](int n, int l, int p) { return dha_s + ((n * NL + l) * 2 + p) * H; };
 
   // ---- W columns (u) for rows j*RS.., as float2 pairs along rows ----------
@@ -831,18 +814,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
   // slab row however many sequences it processed.
   const int r0 = j * RS;
   const bool ih_live = u < Iin;
-  pdrnn_f2 whh[RS / 2], wih[RS / 2], dwhh[DWM ? 1 : RS / 2], dwih[DWM ? 1 : RS / 2];
-  // DWM accumulators: wave wl of the layer group owns row tiles 4 wl .. 4 wl + 3
-  // of dW_hh (col tiles 0 .. H/16-1) and dW_ih (col tiles 0 .. H/16-1, the
-  // ones beyond the layer's input width skipped)
-  constexpr int CT = H / 16;
-  f32x4_t dwacc[DWM ? 4 : 1][DWM ? 2 * CT : 1];
-  if constexpr (DWM) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < 2 * CT; ++c) dwacc[i][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  }
+  pdrnn_f2 whh[RS / 2], wih[RS / 2], dwhh[RS / 2], dwih[RS / 2];
   {
     const float* ph = a.w_hh[layer] + (int64_t)r0 * H + u;
     const float* pi = a.w_ih[layer] + (int64_t)r0 * Iin + min(u, Iin - 1);
@@ -851,18 +823,13 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       whh[rr] = pdrnn_f2{ph[(2 * rr) * H], ph[(2 * rr + 1) * H]};
       const float x0 = pi[(int64_t)(2 * rr) * Iin], x1 = pi[(int64_t)(2 * rr + 1) * Iin];
       wih[rr] = ih_live ? pdrnn_f2{x0, x1} : pdrnn_f2{0.f, 0.f};
-      if constexpr (!DWM) {
-        dwhh[rr] = pdrnn_f2{0.f, 0.f};
-        dwih[rr] = pdrnn_f2{0.f, 0.f};
-      }
+      dwhh[rr] = pdrnn_f2{0.f, 0.f};
+      dwih[rr] = pdrnn_f2{0.f, 0.f};
     }
   }
   float db = 0.f;
   uint64_t st0 = 0, sr0 = 0;
   if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
-  const int wl = __builtin_amdgcn_readfirstlane(lg >> 6);  // wave within the layer group
-  const int lane = tid & 63;
-  const int ct_ih = __builtin_amdgcn_readfirstlane((Iin + 15) / 16);  // live dW_ih col tiles
 
   struct Ops { float aq, ct, cp, dout, hprev, xin; };
   for (int b0 = blockIdx.x * NB; b0 < B; b0 += gridDim.x * NB) {
@@ -957,35 +924,6 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
     // join makes the waitcnt pass conservative, and every conservative
     // vmcnt here would wait for the prefetches of the next two steps.
     const int dha_tgt = layer > 0 ? layer - 1 : NL - 1;  // top layer's dha slots are never read
-    // DWM: dW += G^T [h | x] for row tile i of this wave over the 4 steps
-    // g0 .. g0+3 (MFMA K index k <-> step g0+k): lane (c16, k) feeds
-    // A[row c16][k] = dg_{g0+k}[row] and B[k][col c16] = h / x_{g0+k}[col].
-    // Spread over the steps of the next group (one row tile per step, 2 CT
-    // MFMAs) so the matrix pipe overlaps the column phase's VALU work.
-    auto dw_tile = [&](int g0, int i) {
-      if constexpr (DWM) {
-        const int k = lane >> 4, c16 = lane & 15;
-        const int sl = (g0 + k) & (DGR - 1);
-        const float* dgk = dg_s + (layer * DGR + sl) * RP;
-        const float* hk = hring + (layer * DGR + sl) * H;
-        const float* xk = xring + (layer * DGR + sl) * H;
-        const int row = (4 * wl + i) * 16 + c16;
-        const float av = dgk[row + (row / RS) * 4];
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          const float bh = hk[c * 16 + c16], bx = xk[c * 16 + c16];
-          // i is wave-uniform but runtime: select the accumulator tile by a
-          // switch so dwacc stays in registers
-#pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            if (ii == i) {
-              dwacc[ii][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bh, dwacc[ii][c], 0, 0, 0);
-              if (c < ct_ih) dwacc[ii][CT + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bx, dwacc[ii][CT + c], 0, 0, 0);
-            }
-          }
-        }
-      }
-    };
     auto step = [&](int it, Ops* op) {
       const int t = t_first - it;
       const bool active = t >= 0 && t < T;
@@ -1020,20 +958,8 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
         dgv = active ? dgv : 0.f;  // inactive: zero gate gradients (dW, db, dh unaffected)
         dc[n] = active ? dcn : dc[n];
         if (L == 4 || rowlane) {
-          dgbuf(n, layer, it)[q * H + u + ((q * H + u) / RS) * 4] = dgv;
+          dgbuf(n, layer, p)[q * H + u + ((q * H + u) / RS) * 4] = dgv;
           db += valid[n] ? dgv : 0.f;
-        }
-        if constexpr (DWM) {
-          // this step's dW operands (h_{t-1}, layer input) into the rings,
-          // published by the barrier below
-          if (j == 0) {
-            const float hprev = (t > 0 || h0p) ? op[n].hprev : 0.f;
-            const int tcl = min(max(t, 0), T - 1);
-            const float xsv = XLDS ? xs[((int64_t)n * T + tcl) * H + u] : 0.f;
-            const float xgv = (layer > 0 || u < I) ? op[n].xin : 0.f;
-            hring[(layer * DGR + (it & (DGR - 1))) * H + u] = hprev;
-            xring[(layer * DGR + (it & (DGR - 1))) * H + u] = (XLDS && layer == 0) ? xsv : xgv;
-          }
         }
       }
       if constexpr (PDRNN_ABLATE & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1050,7 +976,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
         const float xin = (XLDS && layer == 0) ? xsv : xgv;
         // an invalid slot still runs the recurrence but contributes nothing to dW
         const float hw = valid[n] ? hprev : 0.f, xw = valid[n] ? xin : 0.f;
-        const float4* g4 = reinterpret_cast<const float4*>(dgbuf(n, layer, it) + r0 + j * 4);
+        const float4* g4 = reinterpret_cast<const float4*>(dgbuf(n, layer, p) + r0 + j * 4);
         // all of this lane's gate-gradient slice in flight at once: one
         // LDS latency per step instead of one per read batch
         float4 gv[RS / 4];
@@ -1071,7 +997,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
           } else {
             sh[0] += g01; sx[1] += g23;
           }
-          if constexpr (!(PDRNN_ABLATE & 1) && !DWM) {
+          if constexpr (!(PDRNN_ABLATE & 1)) {
             dwhh[2 * r4] = __builtin_elementwise_fma(g01, hb, dwhh[2 * r4]);
             dwhh[2 * r4 + 1] = __builtin_elementwise_fma(g23, hb, dwhh[2 * r4 + 1]);
             dwih[2 * r4] = __builtin_elementwise_fma(g01, xb, dwih[2 * r4]);
@@ -1096,10 +1022,6 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
 #pragma unroll
         for (int n = 0; n < NB; ++n) dha_r[n] = dhabuf(n, layer, (it + 1) & 1)[u];
       }
-      if constexpr (DWM) {
-        // one row tile of the group of 4 steps that ended 1..4 steps ago
-        if (it >= 4) dw_tile(it - 4 - (it & 3), it & 3);
-      }
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         if constexpr (PDRNN_ABLATE & 4) {
@@ -1110,20 +1032,13 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
       }
     };
 
-    // DWM: whole groups of 4 steps (the extra steps are inactive: zero gate
-    // gradients, state unchanged)
-    const int iters = DWM ? (T + 2 * (NL - 1) + 3) / 4 * 4 : T + 2 * (NL - 1);
+    const int iters = T + 2 * (NL - 1);
     int it = 0;
     for (; it + 1 < iters; it += 2) {
       step(it, opA);
       step(it + 1, opB);
     }
     if (it < iters) step(it, opA);
-    if constexpr (DWM) {
-      // the last group of 4 steps (its ring slots are no longer written)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dw_tile(iters - 4, i);
-    }
 
     if (j == 0) {
 #pragma unroll
@@ -1142,34 +1057,20 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
 
   // ---------------- epilogue: this workgroup's partial dW / db ----------
   float* slab = a.slab + (int64_t)blockIdx.x * a.P;
-  if constexpr (DWM) {
-    // MFMA C layout: lane holds rows 4 (lane / 16) .. +3 of column lane % 16
+  {
+    float* dst = slab + a.off_whh[layer] + (int64_t)r0 * H + u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < CT; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = (4 * wl + i) * 16 + 4 * (lane >> 4) + r, col = c * 16 + (lane & 15);
-          slab[a.off_whh[layer] + (int64_t)row * H + col] = dwacc[i][c][r];
-          if (col < Iin) slab[a.off_wih[layer] + (int64_t)row * Iin + col] = dwacc[i][CT + c][r];
-        }
-  } else {
-    {
-      float* dst = slab + a.off_whh[layer] + (int64_t)r0 * H + u;
-#pragma unroll
-      for (int rr = 0; rr < RS / 2; ++rr) {
-        dst[(2 * rr) * H] = dwhh[rr].x;
-        dst[(2 * rr + 1) * H] = dwhh[rr].y;
-      }
+    for (int rr = 0; rr < RS / 2; ++rr) {
+      dst[(2 * rr) * H] = dwhh[rr].x;
+      dst[(2 * rr + 1) * H] = dwhh[rr].y;
     }
-    if (ih_live) {
-      float* dst = slab + a.off_wih[layer] + (int64_t)r0 * Iin + u;
+  }
+  if (ih_live) {
+    float* dst = slab + a.off_wih[layer] + (int64_t)r0 * Iin + u;
 #pragma unroll
-      for (int rr = 0; rr < RS / 2; ++rr) {
-        dst[(int64_t)(2 * rr) * Iin] = dwih[rr].x;
-        dst[(int64_t)(2 * rr + 1) * Iin] = dwih[rr].y;
-      }
+    for (int rr = 0; rr < RS / 2; ++rr) {
+      dst[(int64_t)(2 * rr) * Iin] = dwih[rr].x;
+      dst[(int64_t)(2 * rr + 1) * Iin] = dwih[rr].y;
     }
   }
   if (rowlane) {
@@ -1339,14 +1240,10 @@ int bwd_gs_resident(int NL, size_t lds) {
   return c_val;
 }
 
-template <int H, int L, int NB>
+template <int H, int NB>
 size_t bwd_gs_lds(int NL) {
-  // mirrors the kernel's LDS layout: dg ring (slices padded by 4 floats per
-  // lane slice) | dha parity buffers | DWM rings of h and x
-  constexpr bool DWM = PDRNN_BWD_DW_MFMA && L == 4 && NB == 1 && (H == 16 || H == 32);
-  constexpr int DGR = DWM ? 16 : 2;
-  return sizeof(float) * ((size_t)NB * NL * DGR * (4 * H + L * 4) + (size_t)NB * NL * 2 * H +
-                          (DWM ? (size_t)2 * NL * DGR * H : 0));
+  // dg slices padded by 4 floats per lane slice (L <= 8 lanes per unit)
+  return sizeof(float) * NB * NL * 2 * (4 * H + 8 * 4 + H);
 }
 template <int H, int NB>
 size_t bwd_gs_xbytes(int T) { return sizeof(float) * (size_t)NB * T * H; }
@@ -1357,7 +1254,7 @@ inline bool bwd_lean(const PdrnnLstmSmallBwdArgs* a) {
 
 template <int H, int L, int NB>
 int bwd_gs_grid(const PdrnnLstmSmallBwdArgs* a) {
-  const size_t lds = bwd_gs_lds<H, L, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
+  const size_t lds = bwd_gs_lds<H, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
   const bool xl = xbytes <= (size_t)kXldsBytes;
   int cap;
   if (bwd_lean(a)) cap = xl ? bwd_gs_resident<H, L, NB, true, true>(a->NL, lds + xbytes)
@@ -1371,7 +1268,7 @@ int bwd_gs_grid(const PdrnnLstmSmallBwdArgs* a) {
 template <int H, int L>
 hipError_t launch_bwd_gs_gru(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid) {
   const int block = a->NL * H * L;
-  const size_t lds = bwd_gs_lds<H, L, 1>(a->NL), xbytes = bwd_gs_xbytes<H, 1>(a->T);
+  const size_t lds = bwd_gs_lds<H, 1>(a->NL), xbytes = bwd_gs_xbytes<H, 1>(a->T);
   if (grid <= 0) grid = bwd_gs_grid<H, L, 1>(a);
   const bool xl = xbytes <= (size_t)kXldsBytes;
   if (bwd_lean(a)) {  // fused training step: zero initial state, loss through h_T only
@@ -1387,7 +1284,7 @@ hipError_t launch_bwd_gs_gru(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int
 template <int H, int L, int NB>
 hipError_t launch_bwd_gs(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid) {
   const int block = a->NL * H * L;
-  const size_t lds = bwd_gs_lds<H, L, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
+  const size_t lds = bwd_gs_lds<H, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
   if (grid <= 0) grid = bwd_gs_grid<H, L, NB>(a);
   const bool xl = xbytes <= (size_t)kXldsBytes;
   if (bwd_lean(a)) {
