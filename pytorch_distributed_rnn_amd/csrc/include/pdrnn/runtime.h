@@ -55,6 +55,10 @@ class Comm {
   virtual bool aborted() const { return false; }
   virtual double timeout_s() const { return 0.0; }
   virtual int64_t tracked() const { return 0; }  // collectives the watchdog has followed
+  // bound the work enqueued so far on the caller's current stream like a
+  // collective (a replayed graph that contains collectives: captured
+  // collectives carry no completion event of their own)
+  virtual void track_current() {}
   // test hook: occupy the comm stream for `seconds` like a collective whose
   // peer never arrives (bounded spin kernel)
   virtual void debug_stall(double seconds) {

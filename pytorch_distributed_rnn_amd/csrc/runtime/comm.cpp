@@ -326,6 +326,10 @@ class RcclComm final : public Comm {
         c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), s);
     track(stream_, what);
   }
+  void track_current() override {
+    hipStream_t cs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device_).stream();
+    track(cs, "graph replay");
+  }
   // completion event after the collective just enqueued on `st` (skipped while
   // `st` is being captured into a graph: a captured event cannot be queried)
   void track(hipStream_t st, const char* what) {

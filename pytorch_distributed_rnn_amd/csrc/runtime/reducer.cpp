@@ -326,7 +326,8 @@ void register_runtime(py::module_& m) {
       .def("debug_stall", &Comm::debug_stall, py::arg("seconds"))
       .def_property_readonly("aborted", &Comm::aborted)
       .def_property_readonly("timeout_s", &Comm::timeout_s)
-      .def_property_readonly("tracked", &Comm::tracked);
+      .def_property_readonly("tracked", &Comm::tracked)
+      .def("track_current", &Comm::track_current);
   m.attr("WATCHDOG_EXIT") = kWatchdogExit;
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("make_rccl_comm", [](py::bytes uid, int rank, int world, int device, bool high_priority, double timeout_s) {

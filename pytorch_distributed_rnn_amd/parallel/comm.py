@@ -47,6 +47,9 @@ class _PyComm:
         self.all_reduce(t, op)
         self.wait()
 
+    def track_current(self):
+        pass  # gloo / torch process groups bound their own waits
+
     def broadcast(self, t, root):
         self._works.append(dist.broadcast(t, dist.get_global_rank(self.group, root), group=self.group,
                                           async_op=True))

@@ -127,7 +127,17 @@ class MotionTrainStep:
         base = self.flat.data.data_ptr()
         self._offs = [((w.data_ptr() - base) // 4, w.shape) for w in self.weights]
         if cuda_graph is None:
-            cuda_graph = os.environ.get("PDRNN_CUDA_GRAPH", "0") == "1"
+            # default: graph replay for the synced multi-GPU step (RCCL's eager
+            # enqueue leaves ~13 us idle on each side of the all-reduce; at the
+            # 8-GPU per-rank batch that is ~10 % of a step --
+            # profiles/r1_v5_graph_step.md); PDRNN_CUDA_GRAPH=0/1 overrides
+            env = os.environ.get("PDRNN_CUDA_GRAPH")
+            if env is not None:
+                cuda_graph = env == "1"
+            else:
+                import torch.distributed as dist
+                cuda_graph = grad_sync is not None and dist.is_available() and dist.is_initialized() \
+                    and dist.get_world_size() > 1
         self.cuda_graph = bool(cuda_graph)
         self._graph = None       # captured synced step (torch.cuda.CUDAGraph = hipGraph)
         self._graph_key = None
@@ -254,13 +264,23 @@ class MotionTrainStep:
             self._eager_steps += 1
             if self._eager_steps <= 2:
                 return False
-            self._capture(features, labels, idx, ws, nb_fwd, nb_bwd, adam)
+            try:
+                self._capture(features, labels, idx, ws, nb_fwd, nb_bwd, adam)
+            except Exception as exc:  # capture unsupported here: stay eager for good
+                import warnings
+                warnings.warn(f"HIP graph capture of the synced step failed ({exc!r}); running eagerly")
+                torch.cuda.synchronize(self.flat.grad.device)
+                self._graph, self.cuda_graph = None, False
+                return False
         # the graph's Adam launch uses (device step count + 1) and stores it back
         if self._g_step_host != step - 1.0:
             self._g_step.fill_(step - 1.0)
         self._g_idx.copy_(idx, non_blocking=True)
         with trace_range("pdrnn.graph_step"):
             self._graph.replay()
+        comm = getattr(self.model, "comm", None)
+        if comm is not None and hasattr(comm, "track_current"):
+            comm.track_current()  # the communicator's watchdog bounds the replay
         self._g_step_host = step
         stats.copy_(self._g_stats, non_blocking=True)
         return True

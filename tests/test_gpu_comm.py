@@ -122,6 +122,18 @@ def test_ddp_reducer_rccl_step_matches_local(rccl_group, mode):
     assert ddp.comm.tracked >= 3 * len(ddp.bucket_layout()), "every bucket must go through RCCL"
 
 
+def test_graph_step_is_default_only_for_multi_rank(rccl_group):
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_rnn_amd.train.fused_step import MotionTrainStep
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    m = MotionModel(9, 32, 2, 6).cuda()
+    ddp = DistributedDataParallel(m)
+    o = FusedAdam(m.parameters(), lr=2.5e-3)
+    # one rank: eager by default; the graph is the default for world > 1
+    assert MotionTrainStep(ddp, o, ddp.reducer.all_reduce_inline).cuda_graph is False
+
+
 def test_graph_replayed_rccl_step_matches_local(rccl_group):
     """The synced step captured into a HIP graph (fwd/BPTT/reductions + inline
     RCCL all-reduce + Adam with a device step count) and replayed with fresh
@@ -146,6 +158,7 @@ def test_graph_replayed_rccl_step_matches_local(rccl_group):
     s2 = MotionTrainStep(m2, o2, None)
     g = torch.Generator().manual_seed(0)
     outs = []
+    n0 = ddp.comm.tracked
     for i in range(7):
         idx = torch.randperm(512, generator=g)[:64].cuda()
         if i == 5:  # a host-gathered batch in between runs eagerly
@@ -155,6 +168,9 @@ def test_graph_replayed_rccl_step_matches_local(rccl_group):
         b = s2(feats, labels, idx)
         outs.append((a.clone(), b.clone()))
     assert s1._graph is not None, "the synced step was never captured"
+    # eager steps track their all-reduce, replays are tracked as a whole
+    # (captured collectives have no completion event): one per step
+    assert ddp.comm.tracked - n0 == 7
     for a, b in outs:
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
     for p, q in zip(m1.parameters(), m2.parameters()):
