@@ -153,9 +153,12 @@ class Trainer:
         a gradient-only pass (no optimizer update, gradients discarded) for
         each batch shape of the epoch -- the full batch and the short last one
         -- so that kernel code-object loading and the caching allocator's
-        first allocations are not charged to the first epoch.  A no-op on the
-        CPU / autograd path.  Disable with ``warmup=False`` (CLI
-        ``--no-warmup``)."""
+        first allocations are not charged to the first epoch; then repeats
+        the full-batch pass until the GPU has been busy for
+        ``PDRNN_WARMUP_MS`` (default 40 ms): after host-side setup the GPU
+        clocks ramp up under load and kernel times fall by ~12 % over the
+        first ~25 ms (profiles/r2_clock_ramp.md).  A no-op on the CPU /
+        autograd path.  Disable with ``warmup=False`` (CLI ``--no-warmup``)."""
         fused = self._fused_step()
         if fused is None:
             return
@@ -163,7 +166,8 @@ class Trainer:
         n = loader.num_items
         sizes = sorted({min(loader.batch_size, n), n % loader.batch_size or loader.batch_size})
         self.model.train()
-        for b in sizes:
+
+        def one_pass(b):
             batch = loader.make_batch(torch.arange(b, device=loader.device))
             if len(batch) == 3:
                 features, labels_all, idx = batch
@@ -171,7 +175,20 @@ class Trainer:
             else:
                 data, labels = batch
                 fused.warmup(data, labels.reshape(-1).contiguous(), None)
+
+        for b in sizes:
+            one_pass(b)
         mem.synchronize()
+        try:
+            budget = float(os.environ.get("PDRNN_WARMUP_MS", "40")) / 1e3
+        except ValueError:
+            budget = 0.04
+        t0 = time.perf_counter()
+        for _ in range(1000):
+            if time.perf_counter() - t0 >= budget:
+                break
+            one_pass(max(sizes))
+            mem.synchronize()
 
     def _forward(self, batch) -> Tuple[Tensor, Tensor]:
         if len(batch) == 3:
