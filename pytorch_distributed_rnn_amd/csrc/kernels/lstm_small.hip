@@ -814,6 +814,9 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
   // slab row however many sequences it processed.
   const int r0 = j * RS;
   const bool ih_live = u < Iin;
+  float gm[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) gm[g] = q == g ? 1.f : 0.f;
   pdrnn_f2 whh[RS / 2], wih[RS / 2], dwhh[RS / 2], dwih[RS / 2];
   {
     const float* ph = a.w_hh[layer] + (int64_t)r0 * H + u;
@@ -935,24 +938,30 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
         if (!top) dht += dha_r[n];  // dh from the layer above (prefetched, see the column phase)
         const float ig = quad_bcast(op[n].aq, 0), fg = quad_bcast(op[n].aq, 1);
         const float gg = quad_bcast(op[n].aq, 2), og = quad_bcast(op[n].aq, 3);
+        // this lane's gate gradient by arithmetic with 0/1 lane masks
+        // (gm[q] = [q == lane's gate]): a select chain over q compiles into
+        // divergent exec-masked branches inside the recurrence
+        const float own = op[n].aq;
         float dgv, dcn;
         if constexpr (CELL == 0) {
           const float cp = (t > 0 || c0p) ? op[n].cp : 0.f;
           const float tc = (PDRNN_ABLATE & 16) ? op[n].ct : tanhf_fast(op[n].ct);
           const float dcp = fmaf(dht * og, 1.f - tc * tc, dc[n]);
-          const float d_i = dcp * gg * ig * (1.f - ig);
-          const float d_f = dcp * cp * fg * (1.f - fg);
-          const float d_g = dcp * ig * (1.f - gg * gg);
-          const float d_o = dht * tc * og * (1.f - og);
-          dgv = q == 0 ? d_i : (q == 1 ? d_f : (q == 2 ? d_g : d_o));
+          // i: dcp gg s'(i)  f: dcp cp s'(f)  g: dcp ig t'(g)  o: dht tc s'(o)
+          const float oth = fmaf(gm[0], gg, fmaf(gm[1], cp, fmaf(gm[2], ig, gm[3] * tc)));
+          const float src = fmaf(gm[3], dht - dcp, dcp);
+          const float der = fmaf(gm[2], 1.f - own, own) - own * own;
+          dgv = src * oth * der;
           dcn = dcp * fg;
         } else {  // GRU: ig = r, fg = z, og = n_h, ct = n
           const float hp = (t > 0 || h0p) ? op[n].hprev : 0.f;
           const float nn = op[n].ct;
           const float dpn = dht * (1.f - fg) * (1.f - nn * nn);
-          const float d_r = dpn * og * ig * (1.f - ig);
-          const float d_z = dht * (hp - nn) * fg * (1.f - fg);
-          dgv = q == 0 ? d_r : (q == 1 ? d_z : (q == 2 ? dpn : dpn * ig));
+          // r: dpn n_h s'(r)  z: dht (h - n) s'(z)  n_x: dpn  n_h: dpn r
+          const float a0 = fmaf(gm[1], dht - dpn, dpn);
+          const float a1 = fmaf(gm[0], og, fmaf(gm[1], hp - nn, fmaf(gm[3], ig, gm[2])));
+          const float a2 = fmaf(gm[0] + gm[1], own - own * own - 1.f, 1.f);
+          dgv = a0 * a1 * a2;
           dcn = dht * fg;  // direct path into dh_{t-1}
         }
         dgv = active ? dgv : 0.f;  // inactive: zero gate gradients (dW, db, dh unaffected)
