@@ -1133,14 +1133,16 @@ __global__ void slab2_reduce_pass1(const float* __restrict__ A, int64_t rowsA, i
   const int64_t ld = inA ? ldA : PB;
   const int64_t rows = inA ? rowsA : rowsB;
   const int64_t r0 = rows * sp / split, r1 = rows * (sp + 1) / split;
-  float acc0 = 0.f, acc1 = 0.f;
+  // 8 independent loads in flight per thread (the head slab has B rows over
+  // ~200 columns: few threads, long columns -- latency-bound otherwise)
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int64_t r = r0;
-  for (; r + 2 <= r1; r += 2) {
-    acc0 += src[r * ld];
-    acc1 += src[(r + 1) * ld];
+  for (; r + 8 <= r1; r += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += src[(r + k) * ld];
   }
-  if (r < r1) acc0 += src[r * ld];
-  work[(int64_t)sp * P + p] = acc0 + acc1;
+  for (int k = 0; r < r1; ++r, ++k) acc[k] += src[r * ld];
+  work[(int64_t)sp * P + p] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 }
 
 __global__ void slab_reduce_pass2_split(const float* __restrict__ work, int64_t P, int64_t Pa, int split,
