@@ -44,6 +44,9 @@ constexpr int kXldsBytes = 48 * 1024;
 #ifndef PDRNN_ABLATE
 #define PDRNN_ABLATE 0
 #endif
+#ifndef PDRNN_BWD_PIN_DW
+#define PDRNN_BWD_PIN_DW 1
+#endif
 #ifndef PDRNN_FWD_BULK_LDS
 #define PDRNN_FWD_BULK_LDS 1
 #endif
@@ -1012,6 +1015,13 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
             dwih[2 * r4] = __builtin_elementwise_fma(g01, xb, dwih[2 * r4]);
             dwih[2 * r4 + 1] = __builtin_elementwise_fma(g23, xb, dwih[2 * r4 + 1]);
           }
+        }
+        // pin this step's dW updates here: they feed nothing until the
+        // epilogue, and left free the scheduler sinks them into the next
+        // step (keeping this step's gate-gradient slice live across it)
+        if constexpr (PDRNN_BWD_PIN_DW) {
+#pragma unroll
+          for (int rr = 0; rr < RS / 2; ++rr) asm volatile("" : "+v"(dwhh[rr]), "+v"(dwih[rr]));
         }
         const pdrnn_f2 shs = sh[0] + sh[1], sxs = sx[0] + sx[1];
         float dhn_ = group_sum<L>(shs.x + shs.y);  // dh_{t-1}[u] on every lane of the unit
