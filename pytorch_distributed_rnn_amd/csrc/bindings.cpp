@@ -329,7 +329,9 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   Tensor head_slab = at::empty({B, PH}, opts);
   if (split_fwd <= 0) split_fwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 0);
   if (split_bwd <= 0) split_bwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 1);
-  TORCH_CHECK(split_fwd == 1 && split_bwd == 1, "fused train step runs on the gate-split / unit-group kernels");
+  if (cell == 1) split_fwd = 1;  // GRU: gate-split forward only
+  TORCH_CHECK((split_fwd == 1 || split_fwd == 2) && split_bwd == 1,
+              "fused train step runs on the gate-split or 2-lane K-split forward and the unit-group backward");
   if (nb_fwd <= 0) nb_fwd = 1;
   if (nb_bwd <= 0) nb_bwd = 1;
   // nb_bwd >= 2: the throughput backward (several sequences per workgroup,

@@ -92,7 +92,67 @@ __device__ __forceinline__ void preload_x(float* xs, const PdrnnLstmSmallFwdArgs
     stage_x<H>(xs + (int64_t)n * a.T * H, a.x, (int64_t)bsrc[n] * a.x_sb, a.x_st, a.T, a.I, a.x_bf16, valid[n]);
 }
 
-template <int H, int S, int NB, bool SAVE, bool XLDS>
+// Fused classifier head + cross-entropy on the top layer's h_T (motion
+// training step), shared by the gate-split and K-split forward kernels: both
+// leave h_T in the top layer's hidden slot of the LDS operand buffers
+// ([NB][NL][2][2H], parity T & 1).  Wave n handles sequence n of the tile.
+template <int H, int NB>
+__device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a, const float* smem, int bbase) {
+  constexpr int K = 2 * H;
+  const int NL = a.NL, B = a.B, T = a.T;
+  const int tid = threadIdx.x;
+  auto vin = [&](int n, int l, int p) -> const float* { return smem + ((n * NL + l) * 2 + p) * K; };
+  static_assert(NB <= 4, "one wave per sequence of the tile");
+  const int n = tid >> 6;
+  const int b = bbase + n;
+  if (n < NB && b < B) {
+    const int lane = tid & 63;
+    const float* hT = vin(n, NL - 1, T & 1) + H;
+    const float hv = lane < H ? hT[lane] : 0.f;
+    const int64_t lab = a.labels[a.idx ? a.idx[b] : b];
+    const int C = a.C;
+    float m = -INFINITY, logit_y = 0.f;
+    int amax = 0;
+    float lg_c[16];
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      if (cc < C) {
+        const float wv = lane < H ? a.head_w[cc * H + lane] : 0.f;
+        float z = wave_sum(wv * hv) + (a.head_b ? a.head_b[cc] : 0.f);
+        lg_c[cc] = z;
+        if (z > m) { m = z; amax = cc; }
+        if (cc == lab) logit_y = z;
+      }
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc)
+      if (cc < C) se += expf(lg_c[cc] - m);
+    const float lse = m + logf(se);
+    const float inv_se = 1.f / se;
+    float* srow = a.slab + (int64_t)b * a.slab_P;
+    float dh = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      if (cc < C) {
+        const float d = (expf(lg_c[cc] - m) * inv_se - (cc == lab ? 1.f : 0.f)) * a.inv_batch;
+        if (lane < H) {
+          dh = fmaf(a.head_w[cc * H + lane], d, dh);
+          srow[a.head_off_w + cc * H + lane] = d * hv;
+        }
+        if (lane == 0 && a.head_b) srow[a.head_off_b + cc] = d;
+      }
+    }
+    if (lane < H) a.dh_top[(int64_t)b * H + lane] = dh;
+    if (lane == 0) {  // [mean-loss contribution, count, correct] -> column sums are the batch stats
+      srow[a.stat_off + 0] = (lse - logit_y) * a.inv_batch;
+      srow[a.stat_off + 1] = 1.f;
+      srow[a.stat_off + 2] = amax == lab ? 1.f : 0.f;
+    }
+  }
+}
+
+template <int H, int S, int NB, bool SAVE, bool XLDS, bool HEAD = false>
 __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   constexpr int K = 2 * H;
   constexpr int KS = K / S;
@@ -236,6 +296,7 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
       a.cn[((int64_t)layer * B + b) * H + u] = c[n];
     }
   }
+  if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase);
 }
 
 // ---------------------------------------------------------------------------
@@ -438,59 +499,7 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
       if (CELL == 0) a.cn[((int64_t)layer * B + b) * H + u] = c[n];
     }
   }
-  if constexpr (HEAD) {
-    // Fused classifier head + cross-entropy on the top layer's h_T; wave n
-    // handles sequence n of the tile.  h_T sits in the top layer's
-    // next-parity hidden slot after the loop.
-    static_assert(NB <= 4, "one wave per sequence of the tile");
-    const int n = tid >> 6;
-    const int b = bbase + n;
-    if (n < NB && b < B) {
-      const int lane = tid & 63;
-      const float* hT = vin(n, NL - 1, T & 1) + H;
-      const float hv = lane < H ? hT[lane] : 0.f;
-      const int64_t lab = a.labels[a.idx ? a.idx[b] : b];
-      const int C = a.C;
-      float m = -INFINITY, logit_y = 0.f;
-      int amax = 0;
-      float lg_c[16];
-#pragma unroll
-      for (int cc = 0; cc < 16; ++cc) {
-        if (cc < C) {
-          const float wv = lane < H ? a.head_w[cc * H + lane] : 0.f;
-          float z = wave_sum(wv * hv) + (a.head_b ? a.head_b[cc] : 0.f);
-          lg_c[cc] = z;
-          if (z > m) { m = z; amax = cc; }
-          if (cc == lab) logit_y = z;
-        }
-      }
-      float se = 0.f;
-#pragma unroll
-      for (int cc = 0; cc < 16; ++cc)
-        if (cc < C) se += expf(lg_c[cc] - m);
-      const float lse = m + logf(se);
-      const float inv_se = 1.f / se;
-      float* srow = a.slab + (int64_t)b * a.slab_P;
-      float dh = 0.f;
-#pragma unroll
-      for (int cc = 0; cc < 16; ++cc) {
-        if (cc < C) {
-          const float d = (expf(lg_c[cc] - m) * inv_se - (cc == lab ? 1.f : 0.f)) * a.inv_batch;
-          if (lane < H) {
-            dh = fmaf(a.head_w[cc * H + lane], d, dh);
-            srow[a.head_off_w + cc * H + lane] = d * hv;
-          }
-          if (lane == 0 && a.head_b) srow[a.head_off_b + cc] = d;
-        }
-      }
-      if (lane < H) a.dh_top[(int64_t)b * H + lane] = dh;
-      if (lane == 0) {  // [mean-loss contribution, count, correct] -> column sums are the batch stats
-        srow[a.stat_off + 0] = (lse - logit_y) * a.inv_batch;
-        srow[a.stat_off + 1] = 1.f;
-        srow[a.stat_off + 2] = amax == lab ? 1.f : 0.f;
-      }
-    }
-  }
+  if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase);
 }
 
 template <int H, int S2, int NB, bool XLDS>
@@ -1172,6 +1181,16 @@ hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   const int block = a->NL * LANES;
   const size_t lds = sizeof(float) * NB * a->NL * 2 * (2 * H);
   const size_t xbytes = sizeof(float) * (size_t)NB * a->T * H;
+  if constexpr (SAVE) {
+    if (a->head_w) {  // fused training step: classifier head + CE epilogue
+      if (a->C > 16) return hipErrorInvalidValue;
+      if (xbytes <= (size_t)kXldsBytes)
+        hipLaunchKernelGGL((lstm_small_fwd_kernel<H, S, NB, true, true, true>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+      else
+        hipLaunchKernelGGL((lstm_small_fwd_kernel<H, S, NB, true, false, true>), dim3(grid), dim3(block), lds, st, *a);
+      return hipGetLastError();
+    }
+  }
   if (xbytes <= (size_t)kXldsBytes)
     hipLaunchKernelGGL((lstm_small_fwd_kernel<H, S, NB, SAVE, true>), dim3(grid), dim3(block), lds + xbytes, st, *a);
   else

@@ -42,10 +42,16 @@ def small_launch_config(batch: int, hidden: int, num_layers: int = 2) -> Tuple[i
     sp_fwd = _env_int("PDRNN_LSTM_SPLIT_FWD", 0)
     sp_bwd = _env_int("PDRNN_LSTM_SPLIT_BWD", 0)
     if nb_fwd not in (1, 2):
-        # two sequences per forward workgroup once the batch exceeds one
-        # resident wave of single-sequence workgroups (measured: B=1440 on one
-        # MI355X 0.545 -> 0.540 ms/step; B<=1024 stays latency-bound at nb=1)
-        nb_fwd = 2 if batch > 1024 and hidden <= 32 else 1
+        # Large batches are LDS-bandwidth bound in the gate-split forward
+        # (every lane reads the whole [x | h] operand vector): above one
+        # resident round of single-sequence workgroups the 2-lane K-split map
+        # (each lane reads half the vector) is faster -- B=1440: 164 us vs
+        # 178 us for gate-split with 2 sequences per workgroup, 204 us with 1
+        # (bench/fwd_split.py, profiles/r2_fwd_split.log); B<=1024 stays on
+        # the latency-optimal gate-split map with one sequence per workgroup
+        nb_fwd = 1
+        if batch > 1024 and hidden == 32 and sp_fwd == 0:
+            sp_fwd = 2
     if nb_bwd not in (1, 2, 3):
         nb_bwd = 1
     return nb_fwd, sp_fwd, nb_bwd, sp_bwd  # split 0 = widest valid (chosen natively)

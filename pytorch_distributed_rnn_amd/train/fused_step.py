@@ -174,10 +174,10 @@ class MotionTrainStep:
         from ..ops.lstm import fused_bwd_nb, small_launch_config
         self.flat.attach_grads()
         batch = idx.numel() if idx is not None else features.shape[0]
-        nb_fwd, _, _, _ = small_launch_config(batch, self.H, self.NL)
+        nb_fwd, sp_fwd, _, _ = small_launch_config(batch, self.H, self.NL)
         nb_bwd = fused_bwd_nb(batch, self.H, self.NL)
         if self.gru:
-            nb_fwd = 1
+            nb_fwd, sp_fwd = 1, 1
         hw, hb = self.m.fc.weight, self.m.fc.bias  # the classifier head stays fp32
         if self.bf16:
             ws = self._rounded()
@@ -195,14 +195,14 @@ class MotionTrainStep:
         if adam is not None and self.grad_sync is None:
             with trace_range("pdrnn.fwd_bwd_adam"):
                 self.mod.lstm_head_train_step(features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H,
-                                              self.NL, 0, 0, nb_fwd, nb_bwd, adam[0], adam[1], cell, self.colmap)
+                                              self.NL, sp_fwd, 0, nb_fwd, nb_bwd, adam[0], adam[1], cell, self.colmap)
             return stats
         if self.grad_sync is not None and adam is not None and self.cuda_graph:
-            if self._graph_step(features, labels, idx, ws, nb_fwd, nb_bwd, adam, stats):
+            if self._graph_step(features, labels, idx, ws, (nb_fwd, sp_fwd), nb_bwd, adam, stats):
                 return stats
         with trace_range("pdrnn.fwd_bwd"):
             self.mod.lstm_head_train_step(
-                features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd,
+                features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, sp_fwd, 0, nb_fwd, nb_bwd,
                 None, None, cell, self.colmap)
         if self.grad_sync is not None:
             with trace_range("pdrnn.grad_allreduce"):
@@ -224,10 +224,10 @@ class MotionTrainStep:
         from ..ops.lstm import fused_bwd_nb, small_launch_config
         self.flat.attach_grads()
         batch = idx.numel() if idx is not None else features.shape[0]
-        nb_fwd, _, _, _ = small_launch_config(batch, self.H, self.NL)
+        nb_fwd, sp_fwd, _, _ = small_launch_config(batch, self.H, self.NL)
         nb_bwd = fused_bwd_nb(batch, self.H, self.NL)
         if self.gru:
-            nb_fwd = 1
+            nb_fwd, sp_fwd = 1, 1
         if self.bf16:
             ws = self._rounded()
             if features.dtype != torch.bfloat16:
@@ -239,12 +239,12 @@ class MotionTrainStep:
             ws = self.weights
         stats = torch.zeros(3, dtype=torch.float32, device=self.flat.grad.device)
         self.mod.lstm_head_train_step(features, idx, labels, ws, self.m.fc.weight, self.m.fc.bias, self.flat.grad,
-                                      stats, self.H, self.NL, 0, 0, nb_fwd, nb_bwd, None, None,
+                                      stats, self.H, self.NL, sp_fwd, 0, nb_fwd, nb_bwd, None, None,
                                       1 if self.gru else 0, self.colmap)
         self.flat.grad.zero_()
 
     # ------------------------------------------------------------ HIP graph
-    def _graph_step(self, features: Tensor, labels: Tensor, idx: Optional[Tensor], ws, nb_fwd: int,
+    def _graph_step(self, features: Tensor, labels: Tensor, idx: Optional[Tensor], ws, nb_fwd,
                     nb_bwd: int, adam, stats: Tensor) -> bool:
         """Run the synced step as a graph replay.  False: run it eagerly --
         the bf16 model (its per-step weight cast allocates), and the first two
@@ -285,7 +285,7 @@ class MotionTrainStep:
         stats.copy_(self._g_stats, non_blocking=True)
         return True
 
-    def _capture(self, features: Tensor, labels: Tensor, idx: Tensor, ws, nb_fwd: int, nb_bwd: int, adam):
+    def _capture(self, features: Tensor, labels: Tensor, idx: Tensor, ws, nb_fwd, nb_bwd: int, adam):
         (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
         dev = self.flat.grad.device
         hw, hb = self.m.fc.weight, self.m.fc.bias
@@ -297,8 +297,9 @@ class MotionTrainStep:
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            nb, sp = nb_fwd  # (sequences per forward workgroup, forward lanes per unit)
             self.mod.lstm_head_train_step(features, self._g_idx, labels, ws, hw, hb, self.flat.grad, self._g_stats,
-                                          self.H, self.NL, 0, 0, nb_fwd, nb_bwd)
+                                          self.H, self.NL, sp, 0, nb, nb_bwd)
             self.grad_sync()
             self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step, 1.0, bool(dec), False,
                                None, self._g_step, self._g_ticket)
