@@ -136,12 +136,13 @@ class MotionTrainStep:
                 cuda_graph = env == "1"
             else:
                 import torch.distributed as dist
+                # RCCL only: a gloo collective copies through the host and
+                # cannot be captured
                 cuda_graph = grad_sync is not None and dist.is_available() and dist.is_initialized() \
-                    and dist.get_world_size() > 1
+                    and dist.get_world_size() > 1 and dist.get_backend() == "nccl"
         self.cuda_graph = bool(cuda_graph)
-        self._graph = None       # captured synced step (torch.cuda.CUDAGraph = hipGraph)
-        self._graph_key = None
-        self._eager_steps = 0
+        self._graph = None       # last replayed synced step (torch.cuda.CUDAGraph = hipGraph)
+        self._graphs = {}        # configuration key -> captured step
 
     def _rounded(self):
         r = self.flat.data.to(torch.bfloat16).float()
@@ -244,63 +245,74 @@ class MotionTrainStep:
         self.flat.grad.zero_()
 
     # ------------------------------------------------------------ HIP graph
+    # captured steps are kept per configuration (full and short last batch of
+    # an epoch alternate: no re-capture every epoch)
+    _GRAPHS_MAX = 4
+
     def _graph_step(self, features: Tensor, labels: Tensor, idx: Optional[Tensor], ws, nb_fwd,
                     nb_bwd: int, adam, stats: Tensor) -> bool:
         """Run the synced step as a graph replay.  False: run it eagerly --
         the bf16 model (its per-step weight cast allocates), and the first two
-        steps after a (re)configuration, so that RCCL's lazy connection setup
-        and the kernels' first-use allocations happen outside the capture."""
+        steps of a configuration, so that RCCL's lazy connection setup and the
+        kernels' first-use allocations happen outside the capture."""
         if self.bf16 or self.gru:
             return False  # per-step weight cast / packing allocates
-        (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
-        key = (features.data_ptr(), tuple(features.shape), features.dtype, labels.data_ptr(), labels.numel(),
-               None if idx is None else (idx.numel(), idx.dtype), nb_fwd, nb_bwd, lr, b1, b2, eps, wd, dec,
-               p.data_ptr(), m.data_ptr(), v.data_ptr(), self.flat.grad.data_ptr())
         if idx is None:
             return False  # host-gathered batches change pointers every step
-        if key != self._graph_key:
-            self._graph, self._graph_key, self._eager_steps = None, key, 0
-        if self._graph is None:
-            self._eager_steps += 1
-            if self._eager_steps <= 2:
+        (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
+        key = (features.data_ptr(), tuple(features.shape), features.dtype, labels.data_ptr(), labels.numel(),
+               (idx.numel(), idx.dtype), nb_fwd, nb_bwd, lr, b1, b2, eps, wd, dec,
+               p.data_ptr(), m.data_ptr(), v.data_ptr(), self.flat.grad.data_ptr())
+        graphs = self.__dict__.setdefault("_graphs", {})
+        ent = graphs.get(key)
+        if ent is None:
+            ent = {"graph": None, "eager": 0}
+            if len(graphs) >= self._GRAPHS_MAX:
+                graphs.pop(next(iter(graphs)))
+            graphs[key] = ent
+        if ent["graph"] is None:
+            ent["eager"] += 1
+            if ent["eager"] <= 2:
                 return False
             try:
-                self._capture(features, labels, idx, ws, nb_fwd, nb_bwd, adam)
+                self._capture(ent, features, labels, idx, ws, nb_fwd, nb_bwd, adam)
             except Exception as exc:  # capture unsupported here: stay eager for good
                 import warnings
                 warnings.warn(f"HIP graph capture of the synced step failed ({exc!r}); running eagerly")
                 torch.cuda.synchronize(self.flat.grad.device)
-                self._graph, self.cuda_graph = None, False
+                graphs.clear()
+                self.cuda_graph = False
                 return False
+        self._graph = ent["graph"]
         # the graph's Adam launch uses (device step count + 1) and stores it back
-        if self._g_step_host != step - 1.0:
-            self._g_step.fill_(step - 1.0)
-        self._g_idx.copy_(idx, non_blocking=True)
+        if ent["step_host"] != step - 1.0:
+            ent["step"].fill_(step - 1.0)
+        ent["idx"].copy_(idx, non_blocking=True)
         with trace_range("pdrnn.graph_step"):
-            self._graph.replay()
+            ent["graph"].replay()
         comm = getattr(self.model, "comm", None)
         if comm is not None and hasattr(comm, "track_current"):
             comm.track_current()  # the communicator's watchdog bounds the replay
-        self._g_step_host = step
-        stats.copy_(self._g_stats, non_blocking=True)
+        ent["step_host"] = step
+        stats.copy_(ent["stats"], non_blocking=True)
         return True
 
-    def _capture(self, features: Tensor, labels: Tensor, idx: Tensor, ws, nb_fwd, nb_bwd: int, adam):
+    def _capture(self, ent: dict, features: Tensor, labels: Tensor, idx: Tensor, ws, nb_fwd, nb_bwd: int, adam):
         (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
         dev = self.flat.grad.device
         hw, hb = self.m.fc.weight, self.m.fc.bias
-        self._g_idx = idx.clone()
-        self._g_stats = torch.zeros(3, dtype=torch.float32, device=dev)
-        self._g_step = torch.zeros(1, dtype=torch.float32, device=dev)
-        self._g_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
-        self._g_step_host = None
+        ent["idx"] = idx.clone()
+        ent["stats"] = torch.zeros(3, dtype=torch.float32, device=dev)
+        ent["step"] = torch.zeros(1, dtype=torch.float32, device=dev)
+        ent["ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
+        ent["step_host"] = None
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             nb, sp = nb_fwd  # (sequences per forward workgroup, forward lanes per unit)
-            self.mod.lstm_head_train_step(features, self._g_idx, labels, ws, hw, hb, self.flat.grad, self._g_stats,
+            self.mod.lstm_head_train_step(features, ent["idx"], labels, ws, hw, hb, self.flat.grad, ent["stats"],
                                           self.H, self.NL, sp, 0, nb, nb_bwd)
             self.grad_sync()
             self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step, 1.0, bool(dec), False,
-                               None, self._g_step, self._g_ticket)
-        self._graph = g
+                               None, ent["step"], ent["ticket"])
+        ent["graph"] = g
