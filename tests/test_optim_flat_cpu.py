@@ -52,3 +52,14 @@ def test_fused_adam_state_dict_is_torch_compatible():
     st = sd["state"][0]
     assert set(st.keys()) >= {"step", "exp_avg", "exp_avg_sq"}
     assert float(st["step"]) == 2.0
+
+
+def test_stats_to_host_ring_slice_and_fallback():
+    """Epoch statistics read-back: consecutive rows of the fused step's ring
+    come back as one slice copy; wrapped or unrelated rows are stacked."""
+    from pytorch_distributed_rnn_amd.train.trainer import stats_to_host
+    ring = torch.arange(30.).view(10, 3)
+    assert torch.equal(stats_to_host([ring[2], ring[3], ring[4]]), ring[2:5])
+    assert torch.equal(stats_to_host([ring[9], ring[0]]), torch.stack([ring[9], ring[0]]))
+    a, b = torch.ones(3), torch.zeros(3)
+    assert torch.equal(stats_to_host([a, b]), torch.stack([a, b]))
