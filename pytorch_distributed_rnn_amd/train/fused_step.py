@@ -155,8 +155,15 @@ class MotionTrainStep:
         for a single process, or right after the gradient all-reduce) instead
         of going through ``optimizer.step()``.  Advances the step count."""
         from ..ops.adam import FusedAdam
+        from ..parallel.horovod import _DistributedOptimizerMixin
         opt = self.optimizer
-        if type(opt) is not FusedAdam or len(opt.param_groups) != 1:
+        # a Horovod-wrapped FusedAdam qualifies too: its step() only adds the
+        # hook-driven synchronize, which the fused step replaces (no autograd
+        # hooks fire; the flat gradient is reduced by ``grad_sync``)
+        cls = type(opt)
+        if cls is not FusedAdam and cls.__bases__ != (_DistributedOptimizerMixin, FusedAdam):
+            return None
+        if len(opt.param_groups) != 1:
             return None
         g = opt.param_groups[0]
         if g.get("amsgrad") or g.get("maximize") or opt._pdrnn_grad_scale != 1.0:
