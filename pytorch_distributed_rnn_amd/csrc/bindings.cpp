@@ -541,6 +541,47 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 
 
 // ---------------------------------------------------------------------------
+// Persistent recurrence (one cooperative launch per layer direction set,
+// W_hh register-resident; lstm_large.hip) when the shape is covered and
+// PDRNN_LSTM_PERSIST != 0; false -> the caller runs the per-step kernels.
+// PDRNN_LSTM_PERSIST_CHECK=1 synchronises and fails loudly if a grid-sync
+// spin timed out (tests).
+bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int dt, int64_t tile,
+                   const at::TensorOptions& opts, hipStream_t st) {
+  static const int env = [] {
+    const char* e = std::getenv("PDRNN_LSTM_PERSIST");
+    return e ? std::atoi(e) : 1;
+  }();
+  static const bool check = [] {
+    const char* e = std::getenv("PDRNN_LSTM_PERSIST_CHECK");
+    return e && std::atoi(e) != 0;
+  }();
+  static const int mode = [] {  // timing diagnostics only: results are wrong
+    const char* e = std::getenv("PDRNN_PS_MODE");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (env == 0 || tile >= 0) return false;
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
+  int cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
+  const int mt = pdrnn_lstm_large_persist_mt(a.B, a.H, ndir, dt, cus);
+  if (mt == 0) return false;
+  const int nmb = (a.B + 16 * mt - 1) / (16 * mt);
+  Tensor sync = at::zeros({ndir * nmb + 1}, opts.dtype(at::kInt));
+  int* cnt = sync.data_ptr<int>();
+  const hipError_t e = pdrnn_lstm_large_persist(&a, ndir, backward ? 1 : 0, dt, mt, cnt, cnt + ndir * nmb, mode, st);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // e.g. cooperative grid too large: per-step path
+    return false;
+  }
+  if (check) {
+    const int err = sync[ndir * nmb].item<int>();
+    TORCH_CHECK(err == 0, "persistent LSTM grid sync timed out");
+  }
+  return true;
+}
+
 // Large-H LSTM layer (both directions in one launch per step).
 // ---------------------------------------------------------------------------
 
@@ -588,9 +629,11 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
     dd.acts = eptrm(acts, d * T * B * 4 * H);
   }
   hipStream_t st = cur_stream();
-  for (int64_t s = 0; s < T; ++s) {
-    a.step = (int)s;
-    HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 0, dt, (int)tile, st));
+  if (!large_persist(a, ndir, false, dt, tile, o32, st)) {
+    for (int64_t s = 0; s < T; ++s) {
+      a.step = (int)s;
+      HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 0, dt, (int)tile, st));
+    }
   }
   return {hseq, cseq, acts};
 }
@@ -662,9 +705,11 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   }
   hipStream_t st = cur_stream();
   HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, ndir, dt, st));
-  for (int64_t s = 0; s < T; ++s) {
-    a.step = (int)s;
-    HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 1, dt, (int)tile, st));
+  if (!large_persist(a, ndir, true, dt, tile, o32, st)) {
+    for (int64_t s = 0; s < T; ++s) {
+      a.step = (int)s;
+      HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 1, dt, (int)tile, st));
+    }
   }
   return {dgates, dh0, dc0};
 }
@@ -716,6 +761,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
   m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
   m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });
+  m.def("lstm_large_persist_mt", [](int64_t B, int64_t H, int64_t ndir, int64_t dtype) {
+    int dev = 0, cus = 0;
+    TORCH_CHECK(hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess);
+    return pdrnn_lstm_large_persist_mt((int)B, (int)H, (int)ndir, (int)dtype, cus);
+  }, "persistent large-H recurrence: rows-per-workgroup / 16 for this shape on the current device (0 = not covered)");
   m.def("gemm_nt", &gemm_nt, "C = A Bt^T (bf16/fp16 in, f32 out) on the MFMA tile core", py::arg("A"),
         py::arg("Bt"), py::arg("tile") = -1);
   m.def("embedding_fwd", &embedding_fwd, py::arg("weight"), py::arg("idx"), py::arg("out_dtype") = py::none());

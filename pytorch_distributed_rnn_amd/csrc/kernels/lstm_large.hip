@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(WM * WN * 64) lstm_large_fwd_step_kernel(Pdrnn
 // step GEMM and the carry of the step after tn (LSTM: dc; GRU: the direct
 // path dh_{tn+1} z_{tn+1}): emits dgates_tn and the new carry; after the
 // first forward step (cell == false) it emits dh0 / dc0 instead.
-template <class DT, int CELL>
+template <class DT, int CELL, bool COH = false>
 __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B, int H, int T, bool rev, int tn,
                                               bool cell, int b, int u, float dh, float carry) {
   const int64_t bu = (int64_t)b * H + u;
@@ -399,7 +399,18 @@ __device__ __forceinline__ void cell_bwd_elem(const PdrnnLstmLargeDir& d, int B,
   // W_hh^T as stored, and the weight-gradient GEMMs land directly in the
   // parameters' layout (no permutation copies)
   S* dgp = static_cast<S*>(d.dgates) + ((int64_t)tn * B + b) * 4 * H + u;
-  dgp[0] = dg.x; dgp[H] = dg.y; dgp[2 * H] = dg.z; dgp[3 * H] = dg.w;
+  if constexpr (COH) {
+    // persistent kernel: read by the other workgroups of the batch block
+    // within the launch (device-coherent stores, see ps_ld16)
+    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(static_cast<S*>(d.dgates) + (int64_t)tn * B * 4 * H);
+    const uint32_t o = (uint32_t)(((int64_t)b * 4 * H + u) * sizeof(S));
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, dg.x), r, o, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, dg.y), r, o + H * sizeof(S), 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, dg.z), r, o + 2 * H * sizeof(S), 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, dg.w), r, o + 3 * H * sizeof(S), 0, 16);
+  } else {
+    dgp[0] = dg.x; dgp[H] = dg.y; dgp[2 * H] = dg.z; dgp[3 * H] = dg.w;
+  }
   d.dc_carry[bu] = next;
 }
 
@@ -763,6 +774,426 @@ hipError_t gemm_nt_dispatch(const void* Av, int64_t lda, const void* Btv, int64_
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Persistent recurrence (one cooperative launch for all T steps of a layer).
+//
+// The per-step kernels above re-stream W_hh (8 MB at H = 1024 bf16) from
+// L2 / MALL every timestep and pay a launch per step; at small batch (char-LM
+// B = 128) that is what a step costs, not the MFMA work.  Here each workgroup
+// keeps its slice of W_hh in REGISTERS for the whole sequence -- 8 waves x 32
+// KiB of MFMA B fragments -- and the grid synchronises per timestep through a
+// per-(direction, batch-block) arrival counter instead of kernel boundaries.
+//
+//   * workgroup = 512 threads (8 waves), owns NU = 32 hidden units x 16*MT
+//     batch rows; the K dimension of the step GEMM is split over the 8 waves
+//     (forward K = H, backward K = 4H), partial tiles are summed through LDS;
+//   * forward: gates[16 MT x 128] = h_{t-1} W_slice^T, then the cell of the
+//     block's 16 MT x 32 (row, unit) pairs, one per thread (c stays fp32);
+//   * backward: dh[16 MT x 32] = dgates_t W_hh[:, units], then the cell
+//     backward (cell_bwd_elem above) of the same pairs;
+//   * grid sync: h_t / dgates_t are written and read with device-coherent
+//     (SC1) buffer accesses; every thread drains its stores (vmcnt 0), the
+//     workgroup barriers, and one thread bumps the arrival counter of its
+//     batch block (relaxed agent-scope atomic); before the next step one
+//     thread spins on that counter until all NCB column blocks of the batch
+//     block have arrived.  No L2 write-back / invalidate per step (an
+//     acquire/release pair costs a whole-L2 maintenance operation on every
+//     spin and arrival: measured 2x slower than the per-step kernels).  Only the 32 workgroups that share rows wait for
+//     each other; the spin is bounded (~2 s of wall clock; *err is set) so a
+//     fault can never hang the GPU;
+//   * blockIdx -> (column block, batch block) puts the batch block in the
+//     low bits: workgroups are dispatched round-robin over the 8 XCDs, so the
+//     workgroups of one XCD read the same A rows out of their shared L2.
+// Launched cooperatively (the runtime refuses a grid that cannot be
+// co-resident); the host falls back to the per-step kernels otherwise.
+// ---------------------------------------------------------------------------
+constexpr int PS_NU = 32;       // hidden units per workgroup
+constexpr int PS_WAVES = 8;
+constexpr int PS_THREADS = PS_WAVES * 64;
+
+struct PersistSync {
+  int* cnt;   // [ndir][NMB] arrival counters, zero at launch
+  int* err;   // set to 1 when a spin timed out
+  int mode;   // diagnostics (wrong results): bit 0 no waits, bit 1 no step GEMM
+};
+
+__device__ __forceinline__ void ps_arrive(int* c) {
+  // every wave's device-coherent stores are complete before the count moves
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void ps_wait(int* c, int target, int* err) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      // once any workgroup has timed out nobody waits any more (the launch
+      // drains in ~2 s instead of 2 s per remaining step)
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if (wall_clock64() - t0 > 200000000ull) {  // 100 MHz constant clock: 2 s
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Device-coherent (SC1 = agent scope) 16-byte loads / 2-byte stores for the
+// data exchanged between workgroups inside the launch (h_t, dgates_t): they
+// bypass the per-CU L1 and the XCD-private L2 copies, so no cache
+// write-back / invalidate is needed around the arrival counter.
+constexpr int PS_SC1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ps_rsrc(const void* p) { return uniform_rsrc(p); }
+__device__ __forceinline__ uint4 ps_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, PS_SC1);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void ps_st2(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes, uint16_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16(v, r, off_bytes, 0, PS_SC1);
+}
+
+// workgroup -> (direction, column block, batch block)
+__device__ __forceinline__ void ps_coords(int NCB, int NMB, int& dir, int& cb, int& mb) {
+  const int per_dir = NCB * NMB;
+  dir = blockIdx.x / per_dir;
+  const int l = blockIdx.x - dir * per_dir;
+  mb = l % NMB;
+  cb = l / NMB;
+}
+
+// Per-step epilogue state lives in registers: the cell state c (forward) and
+// the carry (backward) never leave the thread that owns the (row, unit) pair;
+// the operands of the next step that do not depend on other workgroups (xp;
+// acts / c / dout) are loaded right after the arrival, so their latency hides
+// behind the wait; only the exchanged stores (h_t / dgates_t) precede the
+// arrival -- the saved activations and c_t are stored after it.
+template <class DT, int CELL, int KS, int MT>
+__global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(PdrnnLstmLargeStepArgs args,
+                                                                            PersistSync sync) {
+  typedef typename DT::S S;
+  constexpr int CT = 4 * PS_NU / 16;  // 8 column tiles of 16 gate columns
+  constexpr int LDR = 4 * PS_NU + 4;  // partial-tile row stride (floats)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  float* red = reinterpret_cast<float*>(smem_raw);  // [wave][MT][16][LDR]
+  const int B = args.B, H = args.H, T = args.T;
+  const int NCB = H / PS_NU, NMB = (B + 16 * MT - 1) / (16 * MT);
+  int dir, cb, mb;
+  ps_coords(NCB, NMB, dir, cb, mb);
+  const PdrnnLstmLargeDir& d = args.dir[dir];
+  const bool rev = args.reverse_mask & (1 << dir);
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = cb * 4 * PS_NU;        // first gate column (gate-interleaved)
+  const int k0 = wid * (H / PS_WAVES);  // this wave's K range
+  int* cnt = sync.cnt + dir * NMB + mb;
+
+  // W_hh slice as MFMA B fragments, resident for the whole sequence
+  uint4 wf[KS][CT];
+  {
+    const S* w = static_cast<const S*>(d.w);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < CT; ++j)
+        wf[ks][j] = *reinterpret_cast<const uint4*>(w + (int64_t)(n0 + j * 16 + fr) * H + k0 + ks * 32 + fq * 8);
+  }
+  // this thread's (row, unit) pairs of the cell epilogue: 16 rows x 32 units
+  const int eu = threadIdx.x & (PS_NU - 1), er = threadIdx.x / PS_NU;
+  const int u = cb * PS_NU + eu;
+  int brow[MT];
+  float cst[MT];   // cell state (LSTM c / GRU h), fp32, register-resident
+  uint2 xpn[MT];   // next step's 4 gate pre-activations (16-bit x 4)
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    brow[mt] = min(mb * 16 * MT + mt * 16 + er, B - 1);
+    cst[mt] = d.c0 ? d.c0[(int64_t)brow[mt] * H + u] : 0.f;
+  }
+  auto load_xp = [&](int t) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      xpn[mt] = *reinterpret_cast<const uint2*>(static_cast<const S*>(d.xp) + (int64_t)t * d.xp_st +
+                                                (int64_t)brow[mt] * d.xp_sb + 4 * u);
+  };
+  load_xp(rev ? T - 1 : 0);
+
+  for (int s = 0; s < T; ++s) {
+    const int t = rev ? T - 1 - s : s;
+    const int tp = rev ? t + 1 : t - 1;
+    const bool first = s == 0;
+    uint2 xcur[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) xcur[mt] = xpn[mt];
+    if (!first && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err);
+
+    f32x4 acc[MT][CT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const S* hA = first ? static_cast<const S*>(d.h0) : static_cast<const S*>(d.hseq) + (int64_t)tp * d.hseq_st;
+    if (hA != nullptr && !(sync.mode & 2)) {
+      const int64_t lda = first ? H : d.hseq_sb;
+      const __amdgpu_buffer_rsrc_t ra = ps_rsrc(hA);
+      uint4 af[MT][KS];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int row = min(mb * 16 * MT + mt * 16 + fr, B - 1);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          af[mt][ks] = ps_ld16(ra, (uint32_t)((row * lda + k0 + ks * 32 + fq * 8) * sizeof(S)));
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int j = 0; j < CT; ++j) acc[mt][j] = DT::mfma(af[mt][ks], wf[ks][j], acc[mt][j]);
+    }
+    // partial tiles -> LDS
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < CT; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          red[((wid * MT + mt) * 16 + fq * 4 + i) * LDR + j * 16 + fr] = acc[mt][j][i];
+    __syncthreads();
+    float gs[MT][4];
+    const __amdgpu_buffer_rsrc_t rh = ps_rsrc(static_cast<S*>(d.hseq) + (int64_t)t * d.hseq_st);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const S* xv = reinterpret_cast<const S*>(&xcur[mt]);
+      float z[4] = {DT::to_f(xv[0]), DT::to_f(xv[1]), DT::to_f(xv[2]), DT::to_f(xv[3])};
+#pragma unroll
+      for (int w = 0; w < PS_WAVES; ++w) {
+        const float4 p = *reinterpret_cast<const float4*>(red + ((w * MT + mt) * 16 + er) * LDR + 4 * eu);
+        z[0] += p.x; z[1] += p.y; z[2] += p.z; z[3] += p.w;
+      }
+      float* g = gs[mt];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if constexpr (CELL == 0) g[k] = k == 2 ? tanh_(z[k]) : sigm(z[k]);
+        else g[k] = k < 2 ? sigm(z[k]) : z[k];
+      }
+      float hv;
+      if constexpr (CELL == 0) {
+        cst[mt] = fmaf(g[1], cst[mt], g[0] * g[2]);
+        hv = g[3] * tanh_(cst[mt]);
+      } else {
+        g[2] = tanh_(fmaf(g[0], g[3], g[2]));
+        cst[mt] = hv = fmaf(g[1], cst[mt] - g[2], g[2]);
+      }
+      const int b = mb * 16 * MT + mt * 16 + er;
+      if (b < B) ps_st2(rh, (uint32_t)((b * d.hseq_sb + u) * sizeof(S)), DT::from_f(hv));
+    }
+    if (s + 1 < T) ps_arrive(cnt);
+    else __syncthreads();  // (LDS reuse only; nothing waits for the last step)
+    if (s + 1 < T) load_xp(rev ? t - 1 : t + 1);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int b = mb * 16 * MT + mt * 16 + er;
+      if (b >= B) continue;
+      const int64_t bu = (int64_t)b * H + u;
+      const float* g = gs[mt];
+      const uint32_t lo = (uint32_t)DT::from_f(g[0]) | ((uint32_t)DT::from_f(g[1]) << 16);
+      const uint32_t hi = (uint32_t)DT::from_f(g[2]) | ((uint32_t)DT::from_f(g[3]) << 16);
+      *reinterpret_cast<uint2*>(static_cast<S*>(d.acts) + (int64_t)t * B * 4 * H + 4 * bu) = make_uint2(lo, hi);
+      d.cseq[(int64_t)t * B * H + bu] = cst[mt];
+    }
+  }
+}
+
+// Backward: step s consumes dgates_t (t = T-1-s forward order) and runs the
+// cell backward of tn (the step before t), or emits dh0 / dc0 after the
+// first forward step.  dgates_{T-1} and the initial carry come from
+// lstm_large_bwd_first_kernel.  Same cell math as cell_bwd_elem.
+template <class DT, int CELL, int KS, int MT>
+__global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(PdrnnLstmLargeStepArgs args,
+                                                                            PersistSync sync) {
+  typedef typename DT::S S;
+  constexpr int CT = PS_NU / 16;  // 2 column tiles of 16 units
+  constexpr int LDR = PS_NU + 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  float* red = reinterpret_cast<float*>(smem_raw);  // [wave][MT][16][LDR]
+  const int B = args.B, H = args.H, T = args.T;
+  const int NCB = H / PS_NU, NMB = (B + 16 * MT - 1) / (16 * MT);
+  int dir, cb, mb;
+  ps_coords(NCB, NMB, dir, cb, mb);
+  const PdrnnLstmLargeDir& d = args.dir[dir];
+  const bool rev = args.reverse_mask & (1 << dir);
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = cb * PS_NU;
+  const int k0 = wid * (4 * H / PS_WAVES);
+  int* cnt = sync.cnt + dir * NMB + mb;
+
+  uint4 wf[KS][CT];
+  {
+    const S* wt = static_cast<const S*>(d.wt);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < CT; ++j)
+        wf[ks][j] = *reinterpret_cast<const uint4*>(wt + (int64_t)(n0 + j * 16 + fr) * 4 * H + k0 + ks * 32 + fq * 8);
+  }
+  const int eu = threadIdx.x & (PS_NU - 1), er = threadIdx.x / PS_NU;
+  const int u = cb * PS_NU + eu;
+  int brow[MT];
+  float carry[MT];
+  // next cell-backward operands: dout, the 4 saved gates, c_tn, c_{tn-1}
+  float nd[MT], ncur[MT], nsp[MT];
+  uint2 nact[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    brow[mt] = min(mb * 16 * MT + mt * 16 + er, B - 1);
+    carry[mt] = d.dc_carry[(int64_t)brow[mt] * H + u];
+  }
+  auto load_ops = [&](int tn) {
+    const int tpp = rev ? tn + 1 : tn - 1;
+    const bool has_prev = rev ? tpp < T : tpp >= 0;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int64_t bu = (int64_t)brow[mt] * H + u;
+      nd[mt] = d.dout ? DT::to_f(static_cast<const S*>(d.dout)[(int64_t)tn * d.dout_st +
+                                                                (int64_t)brow[mt] * d.dout_sb + u])
+                      : 0.f;
+      nact[mt] = *reinterpret_cast<const uint2*>(static_cast<const S*>(d.acts) + ((int64_t)tn * B) * 4 * H + 4 * bu);
+      ncur[mt] = CELL == 0 ? d.cseq[(int64_t)tn * B * H + bu] : 0.f;
+      nsp[mt] = has_prev ? d.cseq[(int64_t)tpp * B * H + bu] : (d.c0 ? d.c0[bu] : 0.f);
+    }
+  };
+  {
+    const int t0 = rev ? 0 : T - 1, tn0 = rev ? t0 + 1 : t0 - 1;
+    if (rev ? tn0 < T : tn0 >= 0) load_ops(tn0);
+  }
+
+  for (int s = 0; s < T; ++s) {
+    const int t = rev ? s : T - 1 - s;
+    const int tn = rev ? t + 1 : t - 1;
+    const bool cell = rev ? tn < T : tn >= 0;
+    float od[MT], ocur[MT], osp[MT];
+    uint2 oact[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) { od[mt] = nd[mt]; ocur[mt] = ncur[mt]; osp[mt] = nsp[mt]; oact[mt] = nact[mt]; }
+    // dgates_t of the whole batch block: written by every column block (the
+    // first one by the separate first-step kernel, ordered by the launch)
+    if (s > 0 && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err);
+    f32x4 acc[MT][CT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) acc[mt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const __amdgpu_buffer_rsrc_t ra = ps_rsrc(static_cast<const S*>(d.dgates) + (int64_t)t * B * 4 * H);
+    // K loop in 4 chunks: a chunk's loads are all in flight before its MFMAs
+    constexpr int KC = KS >= 4 ? KS / 4 : 1;
+    if (!(sync.mode & 2)) {
+#pragma unroll
+      for (int kc = 0; kc < KS; kc += KC) {
+        uint4 af[MT][KC];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int row = min(mb * 16 * MT + mt * 16 + fr, B - 1);
+#pragma unroll
+          for (int k = 0; k < KC; ++k)
+            af[mt][k] = ps_ld16(ra, (uint32_t)((row * 4 * H + k0 + (kc + k) * 32 + fq * 8) * sizeof(S)));
+        }
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int j = 0; j < CT; ++j) acc[mt][j] = DT::mfma(af[mt][k], wf[kc + k][j], acc[mt][j]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < CT; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          red[((wid * MT + mt) * 16 + fq * 4 + i) * LDR + j * 16 + fr] = acc[mt][j][i];
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rg = ps_rsrc(static_cast<S*>(d.dgates) + (int64_t)(cell ? tn : 0) * B * 4 * H);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float dh = 0.f;
+#pragma unroll
+      for (int w = 0; w < PS_WAVES; ++w) dh += red[((w * MT + mt) * 16 + er) * LDR + eu];
+      const int b = mb * 16 * MT + mt * 16 + er;
+      if (b >= B) continue;
+      const int64_t bu = (int64_t)b * H + u;
+      if constexpr (CELL == 1) dh += carry[mt];
+      if (!cell) {
+        if (d.dh0) d.dh0[bu] = dh;
+        if (CELL == 0 && d.dc0) d.dc0[bu] = carry[mt];
+        continue;
+      }
+      dh += od[mt];
+      const S* av = reinterpret_cast<const S*>(&oact[mt]);
+      const float a0 = DT::to_f(av[0]), a1 = DT::to_f(av[1]), a2 = DT::to_f(av[2]), a3 = DT::to_f(av[3]);
+      float g0, g1, g2, g3;
+      if constexpr (CELL == 0) {
+        const float tc = tanh_(ocur[mt]);
+        const float dc = fmaf(dh * a3, 1.f - tc * tc, carry[mt]);
+        g0 = dc * a2 * a0 * (1.f - a0);
+        g1 = dc * osp[mt] * a1 * (1.f - a1);
+        g2 = dc * a0 * (1.f - a2 * a2);
+        g3 = dh * tc * a3 * (1.f - a3);
+        carry[mt] = dc * a1;
+      } else {
+        const float dpn = dh * (1.f - a1) * (1.f - a2 * a2);
+        g0 = dpn * a3 * a0 * (1.f - a0);
+        g1 = dh * (osp[mt] - a2) * a1 * (1.f - a1);
+        g2 = dpn;
+        g3 = dpn * a0;
+        carry[mt] = dh * a1;
+      }
+      // gate-blocked dgates_tn (read by the batch block's other workgroups
+      // at the next step: device-coherent stores)
+      const uint32_t o = (uint32_t)(((int64_t)b * 4 * H + u) * sizeof(S));
+      ps_st2(rg, o, DT::from_f(g0));
+      ps_st2(rg, o + H * sizeof(S), DT::from_f(g1));
+      ps_st2(rg, o + 2 * H * sizeof(S), DT::from_f(g2));
+      ps_st2(rg, o + 3 * H * sizeof(S), DT::from_f(g3));
+    }
+    if (s + 1 < T) {
+      ps_arrive(cnt);
+      const int tn2 = rev ? tn + 1 : tn - 1;  // cell-backward step of s + 1
+      if (rev ? tn2 < T : tn2 >= 0) load_ops(tn2);
+    }
+  }
+}
+
+template <class DT, int CELL, int MT>
+hipError_t persist_launch(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, PersistSync sy, hipStream_t st) {
+  const int NCB = a->H / PS_NU, NMB = (a->B + 16 * MT - 1) / (16 * MT);
+  dim3 grid(NCB * NMB * ndir), block(PS_THREADS);
+  PdrnnLstmLargeStepArgs args = *a;
+  void* kargs[] = {&args, &sy};
+  if (backward) {
+    const size_t lds = (size_t)PS_WAVES * MT * 16 * (PS_NU + 4) * 4;
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_large_persist_bwd_kernel<DT, CELL, 16, MT>),
+                                      grid, block, kargs, (unsigned)lds, st);
+  }
+  const size_t lds = (size_t)PS_WAVES * MT * 16 * (4 * PS_NU + 4) * 4;
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_large_persist_fwd_kernel<DT, CELL, 4, MT>),
+                                    grid, block, kargs, (unsigned)lds, st);
+}
+
+// H = 1024 only: forward K-steps per wave H/256 = 4, backward 4H/256 = 16
+// (32 B fragments per wave either way = 128 VGPRs).
+template <class DT, int CELL>
+hipError_t persist_dispatch(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, int mt, PersistSync sy,
+                            hipStream_t st) {
+  return mt == 1 ? persist_launch<DT, CELL, 1>(a, ndir, backward, sy, st)
+                 : persist_launch<DT, CELL, 2>(a, ndir, backward, sy, st);
+}
+
 }  // namespace
 }  // namespace pdrnn
 
@@ -804,6 +1235,32 @@ hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int 
                    : pdrnn::dispatch_step<pdrnn::F32, 0>(a, ndir, bw, tile, stream);
   return a->cell ? pdrnn::dispatch_step<pdrnn::F16, 1>(a, ndir, bw, tile, stream)
                  : pdrnn::dispatch_step<pdrnn::F16, 0>(a, ndir, bw, tile, stream);
+}
+
+// Persistent recurrence (see above): batch rows per workgroup / 16 (1 or 2)
+// for a grid that fits one workgroup per CU, or 0 when the shape is not
+// covered (16-bit storage, H = 1024, grid <= cus).
+int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus) {
+  if (dtype != 0 && dtype != 1) return 0;
+  if (H != 1024 || ndir < 1 || ndir > 2) return 0;
+  for (int mt = 1; mt <= 2; ++mt) {
+    const int64_t grid = (int64_t)(H / pdrnn::PS_NU) * ((B + 16 * mt - 1) / (16 * mt)) * ndir;
+    if (grid <= cus) return mt;
+  }
+  return 0;
+}
+
+hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int mt,
+                                    int* counters, int* err, int mode, hipStream_t stream) {
+  if (a->H != 1024 || (mt != 1 && mt != 2) || (dtype != 0 && dtype != 1)) return hipErrorInvalidValue;
+  if (a->cell != 0 && a->cell != 1) return hipErrorInvalidValue;
+  const pdrnn::PersistSync sy{counters, err, mode};
+  const bool bw = backward != 0;
+  if (dtype == 0)
+    return a->cell ? pdrnn::persist_dispatch<pdrnn::BF16, 1>(a, ndir, bw, mt, sy, stream)
+                   : pdrnn::persist_dispatch<pdrnn::BF16, 0>(a, ndir, bw, mt, sy, stream);
+  return a->cell ? pdrnn::persist_dispatch<pdrnn::F16, 1>(a, ndir, bw, mt, sy, stream)
+                 : pdrnn::persist_dispatch<pdrnn::F16, 0>(a, ndir, bw, mt, sy, stream);
 }
 
 hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir, int dtype, hipStream_t stream) {

@@ -6,6 +6,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# persistent large-H LSTM kernels: fail loudly if a grid-sync spin timed out
+os.environ.setdefault("PDRNN_LSTM_PERSIST_CHECK", "1")
 
 
 def pytest_configure(config):

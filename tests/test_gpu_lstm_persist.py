@@ -1,0 +1,79 @@
+"""Persistent large-H recurrence (one cooperative launch per layer, W_hh
+register-resident, per-batch-block grid sync; csrc/kernels/lstm_large.hip)
+against the per-step MFMA kernels on identical inputs, and the char-LM-shaped
+layer against the fp32 torch reference.  PDRNN_LSTM_PERSIST_CHECK=1
+(conftest) makes every persistent launch check its sync-timeout flag."""
+import pytest
+import torch
+
+from pytorch_distributed_rnn_amd import _ext
+from pytorch_distributed_rnn_amd.models.rnn import LSTM
+
+pytestmark = pytest.mark.gpu
+
+H = 1024
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+def _run(mod, tile, xp, w, wt, h0, c0, dout, dhn, dcn, rev, cell):
+    hseq, cseq, acts = mod.lstm_large_fwd(xp, w, h0, c0, H, rev, tile, cell)
+    dg, dh0, dc0 = mod.lstm_large_bwd(dout, dhn, dcn, wt, cseq, acts, c0, H, rev, tile, cell)
+    return hseq, cseq, acts, dg, dh0, dc0
+
+
+@pytest.mark.parametrize("cell", [0, 1])
+@pytest.mark.parametrize("B,T,ndir,rev", [(128, 9, 1, 0),    # char-LM shape: 256 workgroups, 16 rows each
+                                          (200, 5, 1, 0),    # 2 x 16 rows per workgroup, clamped last block
+                                          (40, 6, 2, 2),     # bidirectional, reverse direction 1
+                                          (7, 4, 1, 1)])     # tiny batch, reversed
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_persistent_matches_per_step(cell, B, T, ndir, rev, dt):
+    mod = _ext.require()
+    assert mod.lstm_large_persist_mt(B, H, ndir, 0 if dt == torch.bfloat16 else 1) > 0
+    torch.manual_seed(B + T + cell)
+    dev = "cuda"
+    xp = (torch.randn(T, B, ndir * 4 * H, device=dev) * 0.5).to(dt)
+    w = [(torch.randn(4 * H, H, device=dev) * 0.03).to(dt) for _ in range(ndir)]
+    wt = [(torch.randn(H, 4 * H, device=dev) * 0.03).to(dt) for _ in range(ndir)]
+    h0 = (torch.randn(ndir, B, H, device=dev) * 0.5).to(dt)
+    c0 = torch.randn(ndir, B, H, device=dev) * 0.5
+    dout = (torch.randn(T, B, ndir * H, device=dev) * 0.1).to(dt)
+    dhn = torch.randn(ndir, B, H, device=dev) * 0.1
+    dcn = torch.randn(ndir, B, H, device=dev) * 0.1
+    args = (xp, w, wt, h0, c0, dout, dhn, dcn, rev, cell)
+    got = _run(mod, -1, *args)
+    ref = _run(mod, 0, *args)
+    torch.cuda.synchronize()
+    names = ["hseq", "cseq", "acts", "dgates", "dh0", "dc0"][:6 if cell == 0 else 5]  # GRU: no dc0
+    for name, a, b in zip(names, got, ref):
+        assert torch.isfinite(a.float()).all(), name
+        assert _rel(a, b) < 1e-2, (name, _rel(a, b))
+
+
+def test_persistent_charlm_layer_matches_torch():
+    """nn.LSTM(64 -> 1024) at the char-LM batch on the persistent path vs fp32 torch."""
+    torch.manual_seed(5)
+    dt = torch.bfloat16
+    m = LSTM(64, H, 1, batch_first=True).cuda()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(p.to(dt).float())
+    ref = torch.nn.LSTM(64, H, 1, batch_first=True).cuda()
+    with torch.no_grad():
+        for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+            q.copy_(p)
+    x = torch.randn(128, 24, 64, device="cuda").to(dt)
+    x16 = x.clone().requires_grad_(True)
+    xr = x.float().clone().requires_grad_(True)
+    out, (hn, cn) = m(x16)
+    out_r, (hn_r, cn_r) = ref(xr)
+    assert _rel(out, out_r) < 2e-2 and _rel(cn, cn_r) < 2e-2
+    g = torch.randn_like(out_r)
+    (out.float() * g).sum().backward()
+    (out_r * g).sum().backward()
+    assert _rel(x16.grad, xr.grad) < 4e-2
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert _rel(p.grad, q.grad) < 4e-2, n
