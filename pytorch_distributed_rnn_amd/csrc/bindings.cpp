@@ -4,6 +4,7 @@
 // torch caching allocator, fills the POD argument structs of pdrnn/api.h and
 // launches on torch's current HIP stream.  All math lives in csrc/kernels.
 #include <torch/extension.h>
+#include <cstdio>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 
@@ -534,6 +535,16 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
   Tensor bounds = at::arange(num_embeddings + 1, flat.options());
   Tensor offsets = at::searchsorted(vals, bounds).contiguous();
   Tensor dw = at::empty({num_embeddings, dim}, dout.options().dtype(at::kFloat));
+  // small vocabulary, many contributions per row: split each row's list
+  const int64_t per_row = g.size(0) / std::max<int64_t>(num_embeddings, 1);
+  if (num_embeddings <= 4096 && per_row >= 64) {
+    const int pieces = (int)std::min<int64_t>(32, std::max<int64_t>(2, per_row / 32));
+    Tensor part = at::empty({num_embeddings, pieces, dim}, dout.options().dtype(at::kFloat));
+    HIP_LAUNCH_CHECK(pdrnn_embedding_bwd_pieces(g.data_ptr(), dt, perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(),
+                                                part.data_ptr<float>(), pieces, dw.data_ptr<float>(), num_embeddings,
+                                                dim, padding_idx, cur_stream()));
+    return dw;
+  }
   HIP_LAUNCH_CHECK(pdrnn_embedding_bwd_csr2(g.data_ptr(), dt, perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(),
                                             dw.data_ptr<float>(), num_embeddings, dim, padding_idx, cur_stream()));
   return dw;
@@ -568,12 +579,24 @@ bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int
   const int mt = pdrnn_lstm_large_persist_mt(a.B, a.H, ndir, dt, cus);
   if (mt == 0) return false;
   const int nmb = (a.B + 16 * mt - 1) / (16 * mt);
-  Tensor sync = at::zeros({ndir * nmb + 1}, opts.dtype(at::kInt));
+  // [counters | err | pad | 64 x 8 int64 stamps (diagnostic mode bit 3)]
+  const int64_t stamp_ints = (mode & 8) ? 2 + 64 * 8 * 2 : 1;
+  Tensor sync = at::zeros({ndir * nmb + 1 + stamp_ints + 2}, opts.dtype(at::kInt));
   int* cnt = sync.data_ptr<int>();
   const hipError_t e = pdrnn_lstm_large_persist(&a, ndir, backward ? 1 : 0, dt, mt, cnt, cnt + ndir * nmb, mode, st);
   if (e != hipSuccess) {
     (void)hipGetLastError();  // e.g. cooperative grid too large: per-step path
     return false;
+  }
+  if (mode & 8) {
+    // int64 stamps start at the first 8-byte boundary after err
+    Tensor st64 = sync.narrow(0, ndir * nmb + 1 + ((ndir * nmb + 1) & 1), 64 * 8 * 2).cpu();
+    const long long* v = reinterpret_cast<const long long*>(st64.data_ptr<int>());
+    for (int i = 1; i < 64; ++i) {
+      std::fprintf(stderr, "ps-stamp %s step %d:", backward ? "bwd" : "fwd", i);
+      for (int k = 1; k < 8; ++k) std::fprintf(stderr, " %lld", v[i * 8 + k] ? v[i * 8 + k] - v[i * 8] : -1);
+      std::fprintf(stderr, " | next %lld\n", v[(i + 1 < 64 ? i + 1 : i) * 8] - v[i * 8]);
+    }
   }
   if (check) {
     const int err = sync[ndir * nmb].item<int>();

@@ -178,6 +178,11 @@ hipError_t pdrnn_embedding_fwd(const float* weight, const int64_t* idx, float* o
 hipError_t pdrnn_embedding_fwd16(const float* weight, const int64_t* idx, uint16_t* out, int64_t n_idx, int64_t dim,
                                  int64_t num_embeddings, int dtype, hipStream_t stream);
 // dout_dtype: 0 bf16, 1 fp16, 2 fp32
+// Small-vocabulary form: each row's contribution list split into `pieces`
+// equal parts (partials: [V][pieces][dim] fp32 scratch), summed in order.
+hipError_t pdrnn_embedding_bwd_pieces(const void* dout, int dout_dtype, const int64_t* perm, const int64_t* offsets,
+                                     float* partials, int pieces, float* dweight, int64_t num_embeddings, int64_t dim,
+                                     int64_t padding_idx, hipStream_t stream);
 hipError_t pdrnn_embedding_bwd_csr2(const void* dout, int dout_dtype, const int64_t* perm, const int64_t* offsets,
                                    float* dweight, int64_t num_embeddings, int64_t dim, int64_t padding_idx,
                                    hipStream_t stream);

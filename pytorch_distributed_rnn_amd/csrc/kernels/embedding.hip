@@ -121,6 +121,57 @@ __global__ void __launch_bounds__(256) emb_bwd_csr8_kernel(const void* __restric
   }
 }
 
+// Small vocabularies (char-LM: V = 256 rows, 65536 contributions per step):
+// one wave per vocab row leaves only V x dim/64 waves, each walking a list of
+// hundreds to thousands of rows (frequent characters) -- latency-bound at
+// ~0.9 ms.  Here each row's list is cut into P equal pieces, one wave per
+// (row, slice, piece) writes a partial sum, and a second pass adds the P
+// partials in piece order (still bitwise deterministic).
+template <int DT>
+__global__ void __launch_bounds__(256) emb_bwd_pieces_kernel(const void* __restrict__ dout,
+                                                             const int64_t* __restrict__ perm,
+                                                             const int64_t* __restrict__ off,
+                                                             float* __restrict__ part, int64_t V, int64_t dim,
+                                                             int P) {
+  const int lane = threadIdx.x & 63;
+  const int64_t slices = (dim + 63) / 64;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = wave; w < V * slices * P; w += nwaves) {
+    const int64_t vp = w / slices;  // v * P + piece
+    const int64_t v = vp / P;
+    const int piece = (int)(vp - v * P);
+    const int64_t c = (w - vp * slices) * 64 + lane;
+    const int64_t cc = c < dim ? c : dim - 1;
+    const int64_t a = off[v], n = off[v + 1] - a;
+    const int64_t j0 = a + n * piece / P, j1 = a + n * (piece + 1) / P;
+    float acc = 0.f;
+    for (int64_t j = j0; j < j1; j += 8) {
+      int64_t p[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p[k] = perm[min(j + k, j1 - 1)];
+      float x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = ld_as_f<DT>(dout, p[k] * dim + cc);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += (j + k < j1) ? x[k] : 0.f;
+    }
+    if (c < dim) part[vp * dim + c] = acc;
+  }
+}
+
+__global__ void __launch_bounds__(256) emb_bwd_pieces_sum_kernel(const float* __restrict__ part,
+                                                                 float* __restrict__ dw, int64_t V, int64_t dim,
+                                                                 int P, int64_t padding_idx) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= V * dim) return;
+  const int64_t v = e / dim, c = e - v * dim;
+  float acc = 0.f;
+  if (v != padding_idx)
+    for (int p = 0; p < P; ++p) acc += part[(v * P + p) * dim + c];
+  dw[e] = acc;
+}
+
 int blocks_for(int64_t rows) {
   int64_t b = (rows + 3) / 4;  // 4 waves per block, one row per wave
   if (b < 1) b = 1;
@@ -167,6 +218,29 @@ hipError_t pdrnn_embedding_bwd_csr2(const void* dout, int dout_dtype, const int6
   else
     hipLaunchKernelGGL(pdrnn::emb_bwd_csr8_kernel<2>, grid, block, 0, stream, dout, perm, offsets, dweight,
                        num_embeddings, dim, padding_idx);
+  return hipGetLastError();
+}
+
+hipError_t pdrnn_embedding_bwd_pieces(const void* dout, int dout_dtype, const int64_t* perm, const int64_t* offsets,
+                                     float* partials, int pieces, float* dweight, int64_t num_embeddings, int64_t dim,
+                                     int64_t padding_idx, hipStream_t stream) {
+  if (pieces < 1) return hipErrorInvalidValue;
+  const int64_t waves = num_embeddings * ((dim + 63) / 64) * pieces;
+  const dim3 grid(pdrnn::blocks_for(waves)), block(256);
+  if (dout_dtype == 0)
+    hipLaunchKernelGGL(pdrnn::emb_bwd_pieces_kernel<0>, grid, block, 0, stream, dout, perm, offsets, partials,
+                       num_embeddings, dim, pieces);
+  else if (dout_dtype == 1)
+    hipLaunchKernelGGL(pdrnn::emb_bwd_pieces_kernel<1>, grid, block, 0, stream, dout, perm, offsets, partials,
+                       num_embeddings, dim, pieces);
+  else
+    hipLaunchKernelGGL(pdrnn::emb_bwd_pieces_kernel<2>, grid, block, 0, stream, dout, perm, offsets, partials,
+                       num_embeddings, dim, pieces);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t n = num_embeddings * dim;
+  hipLaunchKernelGGL(pdrnn::emb_bwd_pieces_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     partials, dweight, num_embeddings, dim, pieces, padding_idx);
   return hipGetLastError();
 }
 

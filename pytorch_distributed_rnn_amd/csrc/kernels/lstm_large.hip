@@ -815,12 +815,16 @@ constexpr int PS_THREADS = PS_WAVES * 64;
 struct PersistSync {
   int* cnt;   // [ndir][NMB] arrival counters, zero at launch
   int* err;   // set to 1 when a spin timed out
-  int mode;   // diagnostics (wrong results): bit 0 no waits, bit 1 no step GEMM
+  int mode;   // diagnostics (wrong results): bit 0 no waits, bit 1 no step GEMM, bit 2 no store drain
+  long long* stamps;  // mode bit 3: workgroup 0 records s_memtime at 8 points of steps 0..63
 };
+#define PS_STAMP(k)                                                                          \
+  if ((sync.mode & 8) && blockIdx.x == 0 && threadIdx.x == 0 && s < 64)                      \
+    sync.stamps[s * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime();
 
-__device__ __forceinline__ void ps_arrive(int* c) {
+__device__ __forceinline__ void ps_arrive(int* c, int mode = 0) {
   // every wave's device-coherent stores are complete before the count moves
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!(mode & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -928,7 +932,9 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
     uint2 xcur[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) xcur[mt] = xpn[mt];
+    PS_STAMP(0)
     if (!first && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err);
+    PS_STAMP(1)
 
     f32x4 acc[MT][CT];
 #pragma unroll
@@ -954,6 +960,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
 #pragma unroll
           for (int j = 0; j < CT; ++j) acc[mt][j] = DT::mfma(af[mt][ks], wf[ks][j], acc[mt][j]);
     }
+    PS_STAMP(2)
     // partial tiles -> LDS
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -963,6 +970,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
         for (int i = 0; i < 4; ++i)
           red[((wid * MT + mt) * 16 + fq * 4 + i) * LDR + j * 16 + fr] = acc[mt][j][i];
     __syncthreads();
+    PS_STAMP(3)
     float gs[MT][4];
     const __amdgpu_buffer_rsrc_t rh = ps_rsrc(static_cast<S*>(d.hseq) + (int64_t)t * d.hseq_st);
 #pragma unroll
@@ -991,8 +999,10 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
       const int b = mb * 16 * MT + mt * 16 + er;
       if (b < B) ps_st2(rh, (uint32_t)((b * d.hseq_sb + u) * sizeof(S)), DT::from_f(hv));
     }
-    if (s + 1 < T) ps_arrive(cnt);
+    PS_STAMP(4)
+    if (s + 1 < T) ps_arrive(cnt, sync.mode);
     else __syncthreads();  // (LDS reuse only; nothing waits for the last step)
+    PS_STAMP(5)
     if (s + 1 < T) load_xp(rev ? t - 1 : t + 1);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -1005,6 +1015,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
       *reinterpret_cast<uint2*>(static_cast<S*>(d.acts) + (int64_t)t * B * 4 * H + 4 * bu) = make_uint2(lo, hi);
       d.cseq[(int64_t)t * B * H + bu] = cst[mt];
     }
+    PS_STAMP(6)
   }
 }
 
@@ -1162,7 +1173,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
       ps_st2(rg, o + 3 * H * sizeof(S), DT::from_f(g3));
     }
     if (s + 1 < T) {
-      ps_arrive(cnt);
+      ps_arrive(cnt, sync.mode);
       const int tn2 = rev ? tn + 1 : tn - 1;  // cell-backward step of s + 1
       if (rev ? tn2 < T : tn2 >= 0) load_ops(tn2);
     }
@@ -1254,7 +1265,7 @@ hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, i
                                     int* counters, int* err, int mode, hipStream_t stream) {
   if (a->H != 1024 || (mt != 1 && mt != 2) || (dtype != 0 && dtype != 1)) return hipErrorInvalidValue;
   if (a->cell != 0 && a->cell != 1) return hipErrorInvalidValue;
-  const pdrnn::PersistSync sy{counters, err, mode};
+  const pdrnn::PersistSync sy{counters, err, mode, reinterpret_cast<long long*>((reinterpret_cast<uintptr_t>(err + 1) + 7) & ~(uintptr_t)7)};
   const bool bw = backward != 0;
   if (dtype == 0)
     return a->cell ? pdrnn::persist_dispatch<pdrnn::BF16, 1>(a, ndir, bw, mt, sy, stream)

@@ -141,6 +141,24 @@ def test_embedding_bwd_csr8(dt):
     assert out.dtype == torch.bfloat16 and torch.equal(out, w[idx].to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("V,D,N", [(256, 256, 65536), (100, 200, 30000)])
+def test_embedding_bwd_pieces(dt, V, D, N):
+    """Small vocabulary, many contributions per row (char-LM): each row's list
+    is split into pieces summed in order -- matches index_add, bitwise
+    reproducible, padding row zero, heavily skewed rows included."""
+    mod = _ext.require()
+    torch.manual_seed(6)
+    idx = torch.randint(0, V, (N,), device="cuda")
+    idx[: N // 3] = 7  # one very hot row
+    g = torch.randn(N, D, device="cuda").to(dt)
+    dw = mod.embedding_bwd(g, idx, V, 3)
+    ref = torch.zeros(V, D, device="cuda", dtype=torch.float64).index_add_(0, idx, g.double()).float()
+    ref[3] = 0
+    torch.testing.assert_close(dw, ref, rtol=1e-4, atol=2e-3)
+    assert torch.equal(dw, mod.embedding_bwd(g, idx, V, 3))
+
+
 def test_shadow_weights_follow_optimizer_steps():
     """16-bit shadow weights (ops/lstm_large.shadow) are rebuilt whenever the
     fp32 master changes -- FusedAdam's native step bumps the version counters
