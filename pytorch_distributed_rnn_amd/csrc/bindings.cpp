@@ -555,8 +555,11 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 // Persistent recurrence (one cooperative launch per layer direction set,
 // W_hh register-resident; lstm_large.hip) when the shape is covered and
 // PDRNN_LSTM_PERSIST != 0; false -> the caller runs the per-step kernels.
-// PDRNN_LSTM_PERSIST_CHECK=1 synchronises and fails loudly if a grid-sync
-// spin timed out (tests).
+// A grid-sync spin that times out (bounded at 2 s in the kernel) sets a
+// sticky per-device flag; it is copied to pinned host memory after every
+// launch and checked at the next one, so a timeout fails loudly one call
+// later without a synchronisation.  PDRNN_LSTM_PERSIST_CHECK=1 synchronises
+// and checks right away (tests).
 bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int dt, int64_t tile,
                    const at::TensorOptions& opts, hipStream_t st) {
   static const int env = [] {
@@ -579,11 +582,22 @@ bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int
   const int mt = pdrnn_lstm_large_persist_mt(a.B, a.H, ndir, dt, cus);
   if (mt == 0) return false;
   const int nmb = (a.B + 16 * mt - 1) / (16 * mt);
+  // leaked on purpose: no tensor destructor runs after the HIP runtime is gone
+  static std::vector<Tensor>& sticky = *new std::vector<Tensor>(64);
+  static std::vector<Tensor>& sticky_host = *new std::vector<Tensor>(64);
+  TORCH_CHECK(dev >= 0 && dev < 64, "device index");
+  if (!sticky[dev].defined()) {
+    sticky[dev] = at::zeros({1}, opts.dtype(at::kInt));
+    sticky_host[dev] = at::zeros({1}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
+  }
+  TORCH_CHECK(sticky_host[dev].data_ptr<int>()[0] == 0,
+              "persistent LSTM recurrence: a grid-sync wait timed out in an earlier launch (results invalid)");
   // [counters | err | pad | 64 x 8 int64 stamps (diagnostic mode bit 3)]
   const int64_t stamp_ints = (mode & 8) ? 2 + 64 * 8 * 2 : 1;
   Tensor sync = at::zeros({ndir * nmb + 1 + stamp_ints + 2}, opts.dtype(at::kInt));
   int* cnt = sync.data_ptr<int>();
-  const hipError_t e = pdrnn_lstm_large_persist(&a, ndir, backward ? 1 : 0, dt, mt, cnt, cnt + ndir * nmb, mode, st);
+  const hipError_t e = pdrnn_lstm_large_persist(&a, ndir, backward ? 1 : 0, dt, mt, cnt, cnt + ndir * nmb,
+                                                sticky[dev].data_ptr<int>(), mode, st);
   if (e != hipSuccess) {
     (void)hipGetLastError();  // e.g. cooperative grid too large: per-step path
     return false;
@@ -598,6 +612,7 @@ bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int
       std::fprintf(stderr, " | next %lld\n", v[(i + 1 < 64 ? i + 1 : i) * 8] - v[i * 8]);
     }
   }
+  sticky_host[dev].copy_(sticky[dev], /*non_blocking=*/true);
   if (check) {
     const int err = sync[ndir * nmb].item<int>();
     TORCH_CHECK(err == 0, "persistent LSTM grid sync timed out");

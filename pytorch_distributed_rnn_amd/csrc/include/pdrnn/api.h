@@ -236,10 +236,11 @@ hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir,
 // Persistent recurrence: all T steps of a layer in one cooperative launch with
 // W_hh register-resident.  persist_mt: rows-per-workgroup / 16 for this shape
 // (0 = not covered); counters: ndir * ceil(B / (16 mt)) zeroed ints; err: an
-// int set to 1 if a grid-sync spin timed out; mode: 0 (diagnostic bits, see the kernel).
+// int set to 1 if a grid-sync spin timed out (sticky, if not null: also set,
+// never cleared); mode: 0 (diagnostic bits, see the kernel).
 int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus);
 hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int mt,
-                                    int* counters, int* err, int mode, hipStream_t stream);
+                                    int* counters, int* err, int* sticky, int mode, hipStream_t stream);
 // tile: -1 auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_gemm_nt(const void* A, int64_t lda, const void* Bt, int64_t ldb, float* C, int64_t ldc,
                          int M, int N, int K, int dtype, int tile, hipStream_t stream);

@@ -814,7 +814,8 @@ constexpr int PS_THREADS = PS_WAVES * 64;
 
 struct PersistSync {
   int* cnt;   // [ndir][NMB] arrival counters, zero at launch
-  int* err;   // set to 1 when a spin timed out
+  int* err;   // set to 1 when a spin timed out (this launch: releases every waiter)
+  int* sticky;  // also set on a timeout; never cleared (the host checks it)
   int mode;   // diagnostics (wrong results): bit 0 no waits, bit 1 no step GEMM, bit 2 no store drain
   long long* stamps;  // mode bit 3: workgroup 0 records s_memtime at 8 points of steps 0..63
 };
@@ -829,7 +830,7 @@ __device__ __forceinline__ void ps_arrive(int* c, int mode = 0) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void ps_wait(int* c, int target, int* err) {
+__device__ __forceinline__ void ps_wait(int* c, int target, int* err, int* sticky) {
   if (threadIdx.x == 0) {
     const uint64_t t0 = wall_clock64();
     while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -839,6 +840,7 @@ __device__ __forceinline__ void ps_wait(int* c, int target, int* err) {
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
       if (wall_clock64() - t0 > 200000000ull) {  // 100 MHz constant clock: 2 s
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (sticky) __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -933,7 +935,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) xcur[mt] = xpn[mt];
     PS_STAMP(0)
-    if (!first && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err);
+    if (!first && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err, sync.sticky);
     PS_STAMP(1)
 
     f32x4 acc[MT][CT];
@@ -1093,7 +1095,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
     for (int mt = 0; mt < MT; ++mt) { od[mt] = nd[mt]; ocur[mt] = ncur[mt]; osp[mt] = nsp[mt]; oact[mt] = nact[mt]; }
     // dgates_t of the whole batch block: written by every column block (the
     // first one by the separate first-step kernel, ordered by the launch)
-    if (s > 0 && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err);
+    if (s > 0 && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err, sync.sticky);
     f32x4 acc[MT][CT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -1262,10 +1264,10 @@ int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus) {
 }
 
 hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int mt,
-                                    int* counters, int* err, int mode, hipStream_t stream) {
+                                    int* counters, int* err, int* sticky, int mode, hipStream_t stream) {
   if (a->H != 1024 || (mt != 1 && mt != 2) || (dtype != 0 && dtype != 1)) return hipErrorInvalidValue;
   if (a->cell != 0 && a->cell != 1) return hipErrorInvalidValue;
-  const pdrnn::PersistSync sy{counters, err, mode, reinterpret_cast<long long*>((reinterpret_cast<uintptr_t>(err + 1) + 7) & ~(uintptr_t)7)};
+  const pdrnn::PersistSync sy{counters, err, sticky, mode, reinterpret_cast<long long*>((reinterpret_cast<uintptr_t>(err + 1) + 7) & ~(uintptr_t)7)};
   const bool bw = backward != 0;
   if (dtype == 0)
     return a->cell ? pdrnn::persist_dispatch<pdrnn::BF16, 1>(a, ndir, bw, mt, sy, stream)
