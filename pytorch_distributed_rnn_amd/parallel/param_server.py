@@ -12,12 +12,22 @@ its gradients immediately (asynchronous, Hogwild-style -- no averaging).
 MI355X-native differences:
 
 * the server keeps the model (and the fused HIP LSTM kernels) on its GPU.
-  The RPC tensor payloads (batch in, logits out, the logits' gradient of
-  ``dist_autograd.backward``) are host-staged: TensorPipe in torch-ROCm 2.10
-  has no device channel -- a CUDA tensor in an RPC fails with "Attempting to
-  send a Tensor with unexpected device type cuda:0"
-  (profiles/r2_ps_device_payload_tried.md) -- so there is no GPU-to-GPU
-  path under RPC semantics on this stack;
+  Two payload paths (``--ps-payload``):
+
+  - ``collective`` (default when every rank owns a GPU): RPC is only the
+    control plane.  The batch, the logits and the logits' gradient travel by
+    send/recv on a 2-rank process group {server, trainer} -- RCCL, GPU to
+    GPU over xGMI, one communicator per trainer so the server's RPC threads
+    never interleave two trainers on one communicator (gloo on CPU or
+    shared-GPU runs).  The server back-propagates with ``autograd.grad``
+    (per-trainer gradients, never summed into a shared ``.grad``) and steps
+    that trainer's own Adam, the state the reference's DistributedOptimizer
+    keeps per trainer on the parameters' owner;
+  - ``rpc`` (the reference's path): payloads inside the RPC messages plus
+    distributed autograd.  They are host-staged: TensorPipe in torch-ROCm 2.10
+    has no device channel -- a CUDA tensor in an RPC fails with "Attempting
+    to send a Tensor with unexpected device type cuda:0"
+    (profiles/r2_ps_device_payload_tried.md);
 * fixes of reference quirks, each behind a flag: trainers
   shard the data over the W-1 trainers (``--ps-legacy-sharding`` restores the
   reference's ``num_replicas=W`` sharding that never trains on shard 0);
@@ -43,6 +53,60 @@ RPC_TIMEOUT_S = float(os.environ.get("PDRNN_RPC_TIMEOUT", 60))
 
 _server_model = None
 _server_lock = threading.Lock()
+# trainer rank -> 2-rank payload group {0, rank} (collective payload mode)
+_PAYLOAD_GROUPS = {}
+_PAYLOAD_BACKEND = None
+
+
+def payload_mode(requested: str, world_size: int) -> str:
+    """``auto``: collective payloads when every rank can own a GPU (RCCL
+    refuses two ranks on one device), otherwise the RPC-carried payloads."""
+    if requested != "auto":
+        return requested
+    if torch.cuda.is_available() and torch.cuda.device_count() >= world_size:
+        return "collective"
+    return "rpc"
+
+
+def init_payload_groups(rank: int, world_size: int, address: str, port: str) -> None:
+    """Process group for the tensor payloads, next to the RPC agent (port + 1).
+
+    Backend: RCCL when every rank owns a GPU (device payloads, GPU<->GPU over
+    xGMI), gloo otherwise (host payloads).  Every rank creates every pair
+    group {0, r} in the same order (``new_group`` is collective); one
+    communicator per trainer lets the server serve trainers from concurrent
+    RPC threads without interleaving their send/recv on one communicator."""
+    import torch.distributed as dist
+    global _PAYLOAD_BACKEND
+    use_gpu = torch.cuda.is_available() and torch.cuda.device_count() >= world_size
+    _PAYLOAD_BACKEND = "nccl" if use_gpu else "gloo"
+    if use_gpu:
+        torch.cuda.set_device(rank)
+    dist.init_process_group(_PAYLOAD_BACKEND, init_method=f"tcp://{address}:{int(port) + 1}", rank=rank,
+                            world_size=world_size, timeout=timedelta(seconds=max(RPC_TIMEOUT_S, 60.0)))
+    for r in range(1, world_size):
+        _PAYLOAD_GROUPS[r] = dist.new_group([0, r])
+
+
+def shutdown_payload_groups() -> None:
+    import torch.distributed as dist
+    _PAYLOAD_GROUPS.clear()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def _payload_device(compute_device: torch.device) -> torch.device:
+    return compute_device if _PAYLOAD_BACKEND == "nccl" else torch.device("cpu")
+
+
+def _to_payload(t: torch.Tensor) -> torch.Tensor:
+    return t.contiguous() if _PAYLOAD_BACKEND == "nccl" else t.cpu().contiguous()
+
+
+def _on_device(device: torch.device):
+    """RPC handler threads start on the default device: pin the server's."""
+    import contextlib
+    return torch.cuda.device(device) if device.type == "cuda" else contextlib.nullcontext()
 
 
 # --------------------------------------------------------------------------- helpers
@@ -68,6 +132,8 @@ class ServerModel:
         self.model = MotionModel(input_dim, hidden_dim, layer_dim, output_dim, cell=cell).to(self.device)
         self.lock = threading.Lock()
         self.step_lock = threading.Lock()
+        self._pending = {}  # trainer rank -> logits of its in-flight step (collective payloads)
+        self._optims = {}   # trainer rank -> that trainer's Adam over the server's parameters
 
     def begin_step(self) -> bool:
         """Serialise one trainer's forward/backward/step transaction.
@@ -93,6 +159,45 @@ class ServerModel:
     def get_param_rrefs(self):
         import torch.distributed.rpc as rpc
         return [rpc.RRef(p) for p in self.model.parameters()]
+
+    # ---------------------------------------------------- collective payloads
+    # RPC carries only the control message; the batch, the logits and the
+    # logits' gradient move over a 2-rank process group {server, trainer}
+    # (RCCL send/recv GPU<->GPU on a node with one GPU per rank, gloo on the
+    # CPU).  Forward and backward still run on the server, each trainer keeps
+    # its own Adam state there (as the reference's DistributedOptimizer does:
+    # one local optimizer per trainer on the parameters' owner), and the
+    # gradients never leave the server.
+    def forward_p2p(self, rank: int, shape, dtype: str) -> None:
+        import torch.distributed as dist
+        g = _PAYLOAD_GROUPS[rank]
+        with _on_device(self.device):
+            x = torch.empty(tuple(shape), dtype=getattr(torch, dtype), device=_payload_device(self.device))
+            dist.recv(x, src=rank, group=g)
+            out = self.model(x.to(self.device, non_blocking=True))
+            self._pending[rank] = out
+            dist.send(_to_payload(out.detach()), dst=rank, group=g)
+
+    def backward_p2p(self, rank: int, lr: float) -> None:
+        import torch.distributed as dist
+        g = _PAYLOAD_GROUPS[rank]
+        with _on_device(self.device):
+            out = self._pending.pop(rank)
+            dout = torch.empty(out.shape, dtype=out.dtype, device=_payload_device(self.device))
+            dist.recv(dout, src=rank, group=g)
+            params = [p for p in self.model.parameters() if p.requires_grad]
+            # per-trainer gradients, never accumulated into the shared .grad
+            # (a hogwild peer's backward may be running at the same time)
+            grads = torch.autograd.grad(out, params, dout.to(self.device, non_blocking=True))
+            with self.lock:  # one optimizer update at a time (torch's _LocalOptimizer.global_lock)
+                opt = self._optims.get(rank)
+                if opt is None:
+                    opt = self._optims[rank] = torch.optim.Adam(params, lr=lr)
+                for p, gr in zip(params, grads):
+                    p.grad = gr
+                opt.step()
+                for p in params:
+                    p.grad = None
 
     def save(self, path: str, epoch: int, loss: float) -> str:
         from ..train.checkpoint import save_checkpoint
@@ -120,15 +225,20 @@ def _rpc_options(address: str, port: str):
 
 
 def run_parameter_server(rank: int, world_size: int, address: str = "127.0.0.1",
-                         port: str = "29500") -> None:
+                         port: str = "29500", payload: str = "rpc") -> None:
     import torch.distributed.rpc as rpc
     if torch.cuda.is_available():
         torch.cuda.set_device(0)
     logging.info("PS master initializing RPC")
     rpc.init_rpc(name=PS_NAME, rank=rank, world_size=world_size,
                  rpc_backend_options=_rpc_options(address, port))
+    if payload == "collective":
+        init_payload_groups(rank, world_size, address, port)
+        logging.info(f"Payload groups initialized ({_PAYLOAD_BACKEND})")
     logging.info("RPC initialized! Running parameter server...")
     rpc.shutdown(graceful=True)  # returns when every trainer has finished
+    if payload == "collective":
+        shutdown_payload_groups()
     logging.info("RPC shutdown on parameter server.")
 
 
@@ -136,11 +246,18 @@ def run_parameter_server(rank: int, world_size: int, address: str = "127.0.0.1",
 class RemoteModel(nn.Module):
     """Trainer-side proxy: forward runs on the parameter server."""
 
-    def __init__(self, input_dim, hidden_dim, layer_dim, output_dim, cell="lstm"):
+    def __init__(self, input_dim, hidden_dim, layer_dim, output_dim, cell="lstm", payload: str = "rpc",
+                 rank: Optional[int] = None):
         super().__init__()
         import torch.distributed.rpc as rpc
         self.param_server_rref = rpc.remote(PS_NAME, get_parameter_network,
                                             args=(input_dim, hidden_dim, layer_dim, output_dim, cell))
+        self.payload = payload
+        self.rank = rank
+        self.output_dim = output_dim
+        # collective payloads live on this trainer's GPU when the group is RCCL
+        self.payload_device = torch.device("cuda", torch.cuda.current_device()) \
+            if payload == "collective" and _PAYLOAD_BACKEND == "nccl" else torch.device("cpu")
 
     def get_global_param_rrefs(self):
         return remote_method(ServerModel.get_param_rrefs, self.param_server_rref)
@@ -148,7 +265,37 @@ class RemoteModel(nn.Module):
     def forward(self, x, idx=None):
         if idx is not None:
             x = x.index_select(0, idx)
+        if self.payload == "collective":
+            return self._forward_p2p(x)
         return remote_method(ServerModel.forward, self.param_server_rref, x)
+
+    def _forward_p2p(self, x):
+        """Control message over RPC, batch and logits over the payload group.
+        Returns the logits as a leaf: their gradient goes back with
+        :meth:`backward_p2p`."""
+        import torch.distributed as dist
+        import torch.distributed.rpc as rpc
+        g = _PAYLOAD_GROUPS[self.rank]
+        x = x.to(self.payload_device).contiguous()
+        fut = rpc.rpc_async(self.param_server_rref.owner(), call_method,
+                            args=[ServerModel.forward_p2p, self.param_server_rref, self.rank, tuple(x.shape),
+                                  str(x.dtype).rsplit(".", 1)[-1]], timeout=RPC_TIMEOUT_S)
+        dist.send(x, dst=0, group=g)
+        out = torch.empty(x.shape[0], self.output_dim, dtype=torch.float32, device=self.payload_device)
+        dist.recv(out, src=0, group=g)
+        fut.wait()
+        return out.requires_grad_()
+
+    def backward_p2p(self, dlogits: torch.Tensor, lr: float) -> None:
+        """Send the logits' gradient; the server back-propagates it and steps
+        this trainer's Adam on its parameters."""
+        import torch.distributed as dist
+        import torch.distributed.rpc as rpc
+        fut = rpc.rpc_async(self.param_server_rref.owner(), call_method,
+                            args=[ServerModel.backward_p2p, self.param_server_rref, self.rank, lr],
+                            timeout=RPC_TIMEOUT_S)
+        dist.send(dlogits.contiguous(), dst=0, group=_PAYLOAD_GROUPS[self.rank])
+        fut.wait()
 
 
 def _make_worker_trainer_cls():
@@ -181,6 +328,9 @@ def _make_worker_trainer_cls():
             return TrainingMessageFormatter(epochs, self.rank)
 
         def _get_optimizer(self, model, lr):
+            self._lr = lr
+            if model.payload == "collective":
+                return None  # this trainer's Adam lives on the server (ServerModel.backward_p2p)
             from torch.distributed.optim import DistributedOptimizer
             return DistributedOptimizer(torch.optim.Adam, model.get_global_param_rrefs(), lr=lr)
 
@@ -208,6 +358,13 @@ def _make_worker_trainer_cls():
             return total_loss / n, total_correct / n
 
         def _one_step(self, data, target):
+            if self.model.payload == "collective":
+                output = self.model(data)
+                target = target.to(output.device).long().reshape(-1)
+                loss = F.cross_entropy(output, target)
+                loss.backward()
+                self.model.backward_p2p(output.grad, self._lr)
+                return loss.item(), int((output.detach().argmax(dim=1) == target).sum())
             import torch.distributed.autograd as dist_autograd
             with dist_autograd.context() as cid:
                 output = self.model(data)
@@ -230,13 +387,15 @@ def _make_worker_trainer_cls():
 def run_worker(rank, world_size, epochs, batch_size, learning_rate, input_dim, hidden_dim, layer_dim,
                output_dim, train_set, validation_set, test_set, address="127.0.0.1", port="29500",
                legacy_sharding=False, checkpoint_dir: Optional[Path] = None, cell="lstm",
-               hogwild: bool = False):
+               hogwild: bool = False, payload: str = "rpc"):
     import torch.distributed.rpc as rpc
     logging.info(f"Worker rank {rank} initializing RPC")
     rpc.init_rpc(name=f"trainer_{rank}", rank=rank, world_size=world_size,
                  rpc_backend_options=_rpc_options(address, port))
+    if payload == "collective":
+        init_payload_groups(rank, world_size, address, port)
     logging.info(f"Worker {rank} done initializing RPC")
-    model = RemoteModel(input_dim, hidden_dim, layer_dim, output_dim, cell)
+    model = RemoteModel(input_dim, hidden_dim, layer_dim, output_dim, cell, payload=payload, rank=rank)
     cls = _make_worker_trainer_cls()
     trainer = cls(rank, world_size, model, train_set, batch_size, learning_rate, validation_set,
                   test_set, legacy_sharding=legacy_sharding, hogwild=hogwild)
@@ -246,6 +405,8 @@ def run_worker(rank, world_size, epochs, batch_size, learning_rate, input_dim, h
         remote_method(ServerModel.save, model.param_server_rref, str(path), epochs - 1, float("nan"))
         logging.info(f"Worker {rank} asked the parameter server to save {path}")
     rpc.shutdown()
+    if payload == "collective":
+        shutdown_payload_groups()
     return trainer, result
 
 
@@ -263,6 +424,11 @@ def add_sub_command(parent_parser):
     p.add_argument("--ps-hogwild", action="store_true",
                    help="let trainers' forward/backward/step interleave on the server (reference "
                         "behaviour; races on in-place parameter updates)")
+    p.add_argument("--ps-payload", choices=("auto", "rpc", "collective"), default="auto",
+                   help="tensor payloads (batch, logits, logits' gradient): 'rpc' = inside the RPC "
+                        "messages + distributed autograd (reference); 'collective' = RPC for control, "
+                        "send/recv on a {server, trainer} process group (RCCL GPU<->GPU when every "
+                        "rank owns a GPU, else gloo); 'auto' = collective iff every rank owns a GPU")
     p.set_defaults(func=execute)
 
 
@@ -271,8 +437,9 @@ def execute(args):
     os.environ["MASTER_ADDR"] = args.master_address
     os.environ["MASTER_PORT"] = args.master_port
     address = "127.0.0.1" if args.master_address == "localhost" else args.master_address
+    payload = payload_mode(getattr(args, "ps_payload", "auto"), args.world_size)
     if args.rank == 0:
-        run_parameter_server(0, args.world_size, address, args.master_port)
+        run_parameter_server(0, args.world_size, address, args.master_port, payload=payload)
         return None
     torch.set_num_threads(args.num_threads)
     from ..cli import _load_datasets
@@ -284,4 +451,4 @@ def execute(args):
                       address=address, port=args.master_port,
                       legacy_sharding=args.ps_legacy_sharding,
                       checkpoint_dir=args.checkpoint_directory if not args.no_validation else None,
-                      cell=getattr(args, "cell", "lstm"), hogwild=args.ps_hogwild)
+                      cell=getattr(args, "cell", "lstm"), hogwild=args.ps_hogwild, payload=payload)

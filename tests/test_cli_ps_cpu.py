@@ -64,3 +64,33 @@ def test_parameter_server_liveness(tmp_path):
     per = batch_losses(log)
     assert set(per) == {1, 2}  # both trainers stepped
     assert all(x == x and x < 10 for v in per.values() for x in v)  # finite losses
+
+
+def test_parameter_server_collective_payloads(tmp_path):
+    """RPC as control plane, batch/logits/logit-gradient over {server, trainer}
+    send/recv groups (gloo here; RCCL when every rank owns a GPU): both
+    trainers step the server's model and its loss goes down."""
+    port = str(free_port())
+    common = ["--seed", "1", "--epochs", "4", "--batch-size", "96", "--no-validation", "--synthetic",
+              "--synthetic-size", "384", "--device", "cpu", "--hidden-units", "8", "--log-interval", "1",
+              "parameter-server", "--world-size", "3", "--master-address", "127.0.0.1", "--master-port", port,
+              "--ps-payload", "collective"]
+    procs = [subprocess.Popen([sys.executable, MAIN] + common + ["--rank", str(r)], cwd=str(tmp_path),
+                              env=cpu_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(3)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in procs), "\n".join(o[-2000:] for o in outs)
+    assert "Payload groups initialized (gloo)" in outs[0]
+    per = batch_losses("\n".join(outs))
+    assert set(per) == {1, 2}, per
+    for r, losses in per.items():
+        assert all(x == x for x in losses)
+        k = max(1, len(losses) // 4)
+        assert sum(losses[-k:]) / k < sum(losses[:k]) / k, (r, losses)

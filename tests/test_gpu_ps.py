@@ -16,11 +16,14 @@ pytestmark = pytest.mark.gpu
 MAIN = os.path.join(ROOT, "src", "motion", "main.py")
 
 
-def test_parameter_server_gpu_loss_decreases(tmp_path):
+@pytest.mark.parametrize("payload", ["rpc", "collective"])
+def test_parameter_server_gpu_loss_decreases(tmp_path, payload):
+    # collective on a one-GPU box: the {server, trainer} groups are gloo
+    # (RCCL needs one GPU per rank), the server's model is on the GPU
     port = str(free_port())
     common = ["--seed", "1", "--epochs", "4", "--batch-size", "96", "--no-validation", "--synthetic",
               "--synthetic-size", "384", "--log-interval", "1", "parameter-server", "--world-size", "3",
-              "--master-address", "127.0.0.1", "--master-port", port]
+              "--master-address", "127.0.0.1", "--master-port", port, "--ps-payload", payload]
     env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
