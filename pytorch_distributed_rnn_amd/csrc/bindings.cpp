@@ -372,7 +372,12 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     st_b = at::zeros({gridb, 4}, opts.dtype(at::kLong));
     f.stamps = reinterpret_cast<uint64_t*>(st_f.data_ptr<int64_t>());
   }
-  HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
+  // latency regime (one sequence per workgroup in both passes): forward,
+  // head/CE and BPTT in one launch; otherwise the forward launches here
+  const bool one_launch = !tp && !st_f.defined() &&
+      pdrnn_lstm_small_step_ok((int)H, (int)NL, (int)B, (int)nb_fwd, (int)split_fwd, (int)nb_bwd, (int)split_bwd,
+                               gridb) == 1;
+  if (!one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
 
   PdrnnLstmSmallBwdArgs bk{};
   bk.x = f.x; bk.x_bf16 = f.x_bf16; bk.idx = f.idx; bk.x_sb = f.x_sb; bk.x_st = f.x_st;
@@ -386,7 +391,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.slab = slab.data_ptr<float>(); bk.P = L.P;
   bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL; bk.cell = (int)cell;
   if (st_b.defined()) bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
-  if (tp) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_tp(&bk, (int)H, (int)nb_bwd, gridb, st));
+  if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
+  else if (tp) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_tp(&bk, (int)H, (int)nb_bwd, gridb, st));
   else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
   if (st_f.defined()) {
     report_stamps("fwd(head step)", st_f, (int)(T + NL - 1));
@@ -781,6 +787,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_small_bwd_tp_ok", [](int64_t H, int64_t NL, int64_t T, int64_t I, int64_t B, int64_t nb) {
     return pdrnn_lstm_small_bwd_tp_ok((int)H, (int)NL, (int)T, (int)I, (int)B, (int)nb) != 0;
   }, "the throughput (multi-sequence) fused-step backward covers this shape");
+  m.def("lstm_small_step_one_launch", [](int64_t H, int64_t NL, int64_t T, int64_t B, int64_t nb_fwd,
+                                         int64_t split_fwd, int64_t nb_bwd, int64_t split_bwd) {
+    if (split_fwd <= 0) split_fwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 0);
+    if (split_bwd <= 0) split_bwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 1);
+    if (nb_fwd <= 0) nb_fwd = 1;
+    if (nb_bwd <= 0) nb_bwd = 1;
+    const int gridb = pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb_bwd, (int)split_bwd);
+    return pdrnn_lstm_small_step_ok((int)H, (int)NL, (int)B, (int)nb_fwd, (int)split_fwd, (int)nb_bwd,
+                                    (int)split_bwd, gridb) != 0;
+  }, "the fused training step runs forward + head/CE + BPTT as one launch for this shape");
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });

@@ -96,6 +96,12 @@ hipError_t pdrnn_lstm_small_fwd(const PdrnnLstmSmallFwdArgs* a, int H, int nb, i
 hipError_t pdrnn_lstm_small_bwd(const PdrnnLstmSmallBwdArgs* a, int H, int nb, int split, int grid,
                                 hipStream_t stream);
 int pdrnn_lstm_small_bwd_grid(int H, int NL, int T, int B, int nb, int split);
+// One-launch training step of the latency regime: forward + head/CE epilogue
+// + BPTT of sequence b in workgroup b (lean backward contract, gridb == B).
+int pdrnn_lstm_small_step_ok(int H, int NL, int B, int nb_fwd, int split_fwd, int nb_bwd, int split_bwd,
+                             int gridb);
+hipError_t pdrnn_lstm_small_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBwdArgs* b, int H,
+                                 hipStream_t stream);
 // Throughput backward for the fused training step (lean contract: zero initial
 // state, loss through the top layer's h_T only; H in {16, 32}, NL <= 2,
 // nb in 2..4 sequences per workgroup; lstm_small_tp.hip).

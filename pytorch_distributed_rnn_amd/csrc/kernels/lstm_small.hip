@@ -319,7 +319,7 @@ constexpr float kNegLog2e = -1.4426950408889634f;
 // [W_hr; W_hz; 0; W_hn]); n = tanh(n_x + r n_h), h = n + z (h_prev - n).  The
 // saved activation slots hold r, z, n_x, n_h and n (in the cell-state slot).
 template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
-__global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFwdArgs a) {
+__device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdArgs& a) {
   constexpr int K = 2 * H;
   constexpr int LANES = 4 * H;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -500,6 +500,11 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFw
     }
   }
   if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase);
+}
+
+template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
+__global__ void __launch_bounds__(512) lstm_small_fwd_gs_kernel(PdrnnLstmSmallFwdArgs a) {
+  lstm_small_fwd_gs_body<H, NB, SAVE, XLDS, HEAD, CELL>(a);
 }
 
 template <int H, int S2, int NB, bool XLDS>
@@ -780,7 +785,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
 // so the column phase (W^T g, dW += g h^T / g x^T) is the LSTM's unchanged;
 // the direct path dh_{t-1} += dh_t z rides in the dc register.
 template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0>
-__global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBwdArgs a) {
+__device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdArgs& a) {
   constexpr int R = 4 * H;
   constexpr int RS = R / L;          // rows per lane
   constexpr int LANES = H * L;
@@ -1105,6 +1110,36 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
     if (a.off_bih[layer] >= 0) slab[a.off_bih[layer] + q * H + u] = db;
     if (a.off_bhh[layer] >= 0) slab[a.off_bhh[layer] + q * H + u] = db;
   }
+}
+
+template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0>
+__global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBwdArgs a) {
+  lstm_small_bwd_gs_body<H, L, NB, XLDS, LEAN, CELL>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Whole training step of the latency regime in ONE launch: when the backward
+// grid is one sequence per workgroup (B <= resident workgroups) and both maps
+// use the same NL*4H lanes (gate-split forward, L = 4 unit-group backward),
+// workgroup b runs sequence b's forward + head/CE epilogue and then its own
+// BPTT.  Every operand the backward reads (saved activations, h sequence,
+// dh_T) was written by this workgroup, so no grid-wide dependency exists: the
+// kernel boundary between the two launches (tail of the slowest forward
+// workgroup + the backward's launch and wave start) disappears, and each
+// workgroup goes straight from its forward into its backward.
+// ---------------------------------------------------------------------------
+template <int H, bool XLDS, int CELL>
+__global__ void __launch_bounds__(512) lstm_small_step_gs_kernel(PdrnnLstmSmallFwdArgs f, PdrnnLstmSmallBwdArgs b) {
+  lstm_small_fwd_gs_body<H, 1, true, XLDS, true, CELL>(f);
+  // this workgroup's global stores (activations, h, dh_T) before its own
+  // backward loads them: a workgroup-scope release/acquire (the barrier's
+  // own fences) is enough -- every wave of the workgroup shares the CU's
+  // L1, which holds no line of these buffers (the forward never loads them,
+  // and the L1 is invalidated at kernel start).  An agent-scope fence here
+  // would write back the XCD's L2 (measured: +6 us/step at B = 180).  The
+  // LDS operand buffers are reused by the backward.
+  __syncthreads();
+  lstm_small_bwd_gs_body<H, 4, 1, XLDS, true, CELL>(b);
 }
 
 // Column-sum of a [rows, P] slab: pass 1 sums row chunks into work[split, P].
@@ -1450,10 +1485,59 @@ hipError_t dispatch_bwd(const PdrnnLstmSmallBwdArgs* a, int nb, int split, hipSt
   }
 }
 
+template <int H>
+hipError_t launch_step_gs(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBwdArgs* b, hipStream_t st) {
+  if (f->NL * 4 * H > 512 || f->B != b->B || f->T != b->T || f->NL != b->NL) return hipErrorInvalidConfiguration;
+  if (!f->head_w || f->C > 16 || !bwd_lean(b)) return hipErrorInvalidValue;
+  const int grid = f->B;
+  const int block = f->NL * 4 * H;  // = NL * H * L with L = 4
+  const size_t lds_f = sizeof(float) * f->NL * 2 * (2 * H);
+  const size_t lds_b = bwd_gs_lds<H, 1>(f->NL);
+  const size_t lds = lds_f > lds_b ? lds_f : lds_b;
+  const size_t xbytes = sizeof(float) * (size_t)f->T * H;
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  if (f->cell == 1) {
+    if (xl) hipLaunchKernelGGL((lstm_small_step_gs_kernel<H, true, 1>), dim3(grid), dim3(block), lds + xbytes, st, *f, *b);
+    else hipLaunchKernelGGL((lstm_small_step_gs_kernel<H, false, 1>), dim3(grid), dim3(block), lds, st, *f, *b);
+  } else {
+    if (xl) hipLaunchKernelGGL((lstm_small_step_gs_kernel<H, true, 0>), dim3(grid), dim3(block), lds + xbytes, st, *f, *b);
+    else hipLaunchKernelGGL((lstm_small_step_gs_kernel<H, false, 0>), dim3(grid), dim3(block), lds, st, *f, *b);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 }  // namespace pdrnn
 
 extern "C" {
+
+// 1 when the fused one-launch step covers (H, NL, B, launch config): the
+// gate-split forward with one sequence per workgroup, the L = 4 unit-group
+// backward, and a backward grid of one sequence per workgroup (gridb == B).
+// PDRNN_STEP_ONE_LAUNCH=0 disables it (A/B measurements).
+int pdrnn_lstm_small_step_ok(int H, int NL, int B, int nb_fwd, int split_fwd, int nb_bwd, int split_bwd,
+                             int gridb) {
+  static const bool off = [] {
+    const char* e = getenv("PDRNN_STEP_ONE_LAUNCH");
+    return e && e[0] == '0';
+  }();
+  if (off || (H != 16 && H != 32) || nb_fwd != 1 || split_fwd != 1 || nb_bwd != 1 || split_bwd != 1) return 0;
+  if (NL * 4 * H > 512 || gridb != B) return 0;
+  const int lanes = H == 16 ? pdrnn::bwd_gs_lanes<16>(NL) : pdrnn::bwd_gs_lanes<32>(NL);
+  return lanes == 4 ? 1 : 0;
+}
+
+// Fused forward + head/CE + BPTT launch of the latency regime (see
+// lstm_small_step_gs_kernel); H in {16, 32}.
+hipError_t pdrnn_lstm_small_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBwdArgs* b, int H,
+                                 hipStream_t stream) {
+  if (f->x_bf16 && (size_t)f->T * H * sizeof(float) > (size_t)pdrnn::kXldsBytes) return hipErrorInvalidConfiguration;
+  switch (H) {
+    case 16: return pdrnn::launch_step_gs<16>(f, b, stream);
+    case 32: return pdrnn::launch_step_gs<32>(f, b, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 int pdrnn_lstm_small_supported(int H, int I, int NL) {
   const bool h_ok = H == 16 || H == 32 || H == 64;

@@ -36,6 +36,19 @@ def test_fused_step_matches_autograd(cell):
         assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
 
 
+def test_one_launch_step_selected_in_latency_regime():
+    """B <= one resident round: forward + head/CE + BPTT run as one launch
+    (the B=96 runs of test_fused_step_matches_autograd go through it); the
+    headline B=1440 keeps the separate launches."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.ops.lstm import fused_bwd_nb, small_launch_config
+    mod = _ext.native(torch.device("cuda", 0))
+    for b, expect in ((96, True), (180, True), (1440, False)):
+        nb_f, sp_f, _, sp_b = small_launch_config(b, 32, 2)
+        got = mod.lstm_small_step_one_launch(32, 2, 128, b, nb_f, sp_f, fused_bwd_nb(b, 32, 2), sp_b)
+        assert got == expect, (b, got)
+
+
 @pytest.mark.parametrize("cell", ["lstm", "gru"])
 @pytest.mark.parametrize("nb", [2, 3])
 def test_fused_throughput_backward_matches_autograd(cell, nb, monkeypatch):
