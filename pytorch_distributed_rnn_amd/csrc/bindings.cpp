@@ -399,8 +399,13 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     report_stamps("bwd(head step, lean)", st_b, (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)gridb * nb_bwd - 1) / ((int64_t)gridb * nb_bwd)));
   }
 
+  // PDRNN_ONE_PASS_REDUCE=0: the two-pass reduction (A/B measurements)
+  static const bool one_pass = [] {
+    const char* e = getenv("PDRNN_ONE_PASS_REDUCE");
+    return !(e && e[0] == '0');
+  }();
   const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, gridb / 16));
-  Tensor work = at::empty({split, P_rnn + PH}, opts);
+  Tensor work = one_pass ? Tensor() : at::empty({split, P_rnn + PH}, opts);
   if (adam_state.has_value() && adam_hp.has_value()) {
     // single-process step: the second reduction pass runs inside Adam
     const auto& as = *adam_state;
@@ -408,8 +413,6 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     TORCH_CHECK(as.size() == 3 && hp.size() == 7, "adam_state = [param, exp_avg, exp_avg_sq], 7 hyper-parameters");
     for (const auto& t : as)
       TORCH_CHECK(t.is_contiguous() && t.numel() == P_params && t.scalar_type() == at::kFloat, "flat fp32 Adam buffers");
-    HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,
-                                              work.data_ptr<float>(), split, colmap, L.P, st));
     PdrnnAdamArgs ad{};
     ad.param = as[0].data_ptr<float>(); ad.exp_avg = as[1].data_ptr<float>(); ad.exp_avg_sq = as[2].data_ptr<float>();
     ad.n = P_params;
@@ -418,8 +421,22 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     ad.bias_correction1 = (float)(1.0 - std::pow(hp[1], hp[5]));
     ad.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(hp[2], hp[5]));
     ad.grad_scale = 1.f; ad.decoupled = hp[6] != 0.0 ? 1 : 0; ad.maximize = 0;
+    if (one_pass) {
+      HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(&ad, slab.data_ptr<float>(), gridb, P_rnn, L.P, colmap,
+                                              head_slab.data_ptr<float>(), B, PH, P_params, flat_grad.data_ptr<float>(),
+                                              stats.data_ptr<float>(), st));
+      return;
+    }
+    HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,
+                                              work.data_ptr<float>(), split, colmap, L.P, st));
     HIP_LAUNCH_CHECK(pdrnn_adam_partials(&ad, work.data_ptr<float>(), split, P_rnn + PH, flat_grad.data_ptr<float>(),
                                          stats.data_ptr<float>(), 3, st));
+    return;
+  }
+  if (one_pass) {
+    HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(nullptr, slab.data_ptr<float>(), gridb, P_rnn, L.P, colmap,
+                                            head_slab.data_ptr<float>(), B, PH, P_params, flat_grad.data_ptr<float>(),
+                                            stats.data_ptr<float>(), st));
     return;
   }
   HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,

@@ -255,6 +255,12 @@ hipError_t pdrnn_gemm_nt(const void* A, int64_t lda, const void* Bt, int64_t ldb
 // (columns [0, a->n)); grad_out receives it, columns [n, n + n_stats) -> stats_out.
 hipError_t pdrnn_adam_partials(const PdrnnAdamArgs* a, const float* work, int split, int64_t P_total,
                                float* grad_out, float* stats_out, int n_stats, hipStream_t stream);
+// One-pass reduction of the fused step's [rowsA, ldA] (through colmap) and
+// [rowsB, PB] gradient slabs into grad_out[0:n_out] (+ tail_out for the
+// columns past n_out), with the Adam step of each element when a != nullptr.
+hipError_t pdrnn_slab_reduce_adam(const PdrnnAdamArgs* a, const float* A, int64_t rowsA, int64_t PA, int64_t ldA,
+                                  const int* colmap, const float* Bs, int64_t rowsB, int64_t PB, int64_t n_out,
+                                  float* grad_out, float* tail_out, hipStream_t stream);
 
 // Diagnostics: a single wave that spins for `microseconds` (bounded, <= 60 s).
 // Communicator-watchdog tests only.

@@ -136,8 +136,82 @@ __global__ void __launch_bounds__(256) adam_partials_kernel(PdrnnAdamArgs a, con
   }
 }
 
+// One-pass column reduction of the fused step's two gradient slabs into the
+// flat gradient, with the Adam update folded in (a.param != nullptr; the
+// single-process step) -- replaces the two-pass reduction (slab2_reduce_pass1
+// + adam_partials / slab_reduce_pass2_split) and one launch.
+//   A: [rowsA, ldA] recurrent dW rows, one per backward workgroup, read
+//      through colmap (GRU packed layout) when given;
+//   B: [rowsB, PB] per-sequence head rows (head dW, db, [loss, n, correct]).
+// A 1024-thread workgroup owns CW consecutive columns (one wave reads 64
+// consecutive floats of a row: coalesced) and splits the rows over 1024 / CW
+// row groups (A: 64 x 16, B: 16 x 64 -- the head slab has B rows over ~200
+// columns), each thread keeps 8 loads in flight, and the row-group partials
+// are summed in a fixed order through LDS (deterministic).
+__global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
+    PdrnnAdamArgs a, const float* __restrict__ A, int64_t rowsA, int64_t PA, int64_t ldA,
+    const int* __restrict__ colmap, const float* __restrict__ Bs, int64_t rowsB, int64_t PB, int64_t n_out,
+    float* __restrict__ grad_out, float* __restrict__ tail_out, int nblkA) {
+  __shared__ float red[1024];
+  const int tid = threadIdx.x;
+  const bool inA = (int)blockIdx.x < nblkA;
+  const int cw = inA ? 64 : 16;
+  const int nrg = 1024 / cw;
+  const int ci = tid % cw, rg = tid / cw;
+  const int64_t col = inA ? (int64_t)blockIdx.x * 64 + ci : (int64_t)(blockIdx.x - nblkA) * 16 + ci;
+  const bool live = col < (inA ? PA : PB);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    const float* src = inA ? A + (colmap ? colmap[col] : col) : Bs + col;
+    const int64_t ld = inA ? ldA : PB;
+    const int64_t rows = inA ? rowsA : rowsB;
+    const int64_t r0 = rows * rg / nrg, r1 = rows * (rg + 1) / nrg;
+    int64_t r = r0;
+    for (; r + 8 <= r1; r += 8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += src[(r + k) * ld];
+    }
+    for (int k = 0; r < r1; ++r, ++k) acc[k] += src[r * ld];
+  }
+  red[tid] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (tid >= cw || !live) return;
+  float g = 0.f;
+  for (int k = 0; k < nrg; ++k) g += red[k * cw + tid];
+  const int64_t p = inA ? col : PA + col;  // flat index: [A columns | B columns]
+  if (p < n_out) {
+    grad_out[p] = g;
+    if (a.param) {
+      AdamScalars s;
+      s.lr = a.lr; s.b1 = a.beta1; s.b2 = a.beta2; s.eps = a.eps; s.wd = a.weight_decay;
+      s.bc1 = a.bias_correction1; s.bc2_sqrt = a.bias_correction2_sqrt;
+      s.gscale = a.grad_scale; s.decoupled = a.decoupled; s.maximize = a.maximize;
+      s.amsgrad = 0;
+      float pv = a.param[p], m = a.exp_avg[p], v = a.exp_avg_sq[p];
+      adam_elem(pv, g, m, v, nullptr, s);
+      a.param[p] = pv; a.exp_avg[p] = m; a.exp_avg_sq[p] = v;
+    }
+  } else {
+    tail_out[p - n_out] = g;
+  }
+}
+
 }  // namespace
 }  // namespace pdrnn
+
+extern "C" hipError_t pdrnn_slab_reduce_adam(const PdrnnAdamArgs* a, const float* A, int64_t rowsA, int64_t PA,
+                                            int64_t ldA, const int* colmap, const float* Bs, int64_t rowsB,
+                                            int64_t PB, int64_t n_out, float* grad_out, float* tail_out,
+                                            hipStream_t stream) {
+  if (PA + PB <= 0) return hipSuccess;
+  if (PA + PB > n_out && tail_out == nullptr) return hipErrorInvalidValue;
+  PdrnnAdamArgs none{};
+  const int nblkA = (int)((PA + 63) / 64);
+  const int nblkB = (int)((PB + 15) / 16);
+  hipLaunchKernelGGL(pdrnn::slab_reduce_adam_kernel, dim3((unsigned)(nblkA + nblkB)), dim3(1024), 0, stream,
+                     a ? *a : none, A, rowsA, PA, ldA, colmap, Bs, rowsB, PB, n_out, grad_out, tail_out, nblkA);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t pdrnn_adam_partials(const PdrnnAdamArgs* a, const float* work, int split, int64_t P_total,
                                           float* grad_out, float* stats_out, int n_stats, hipStream_t stream) {
