@@ -319,7 +319,9 @@ constexpr float kNegLog2e = -1.4426950408889634f;
 // [W_hr; W_hz; 0; W_hn]); n = tanh(n_x + r n_h), h = n + z (h_prev - n).  The
 // saved activation slots hold r, z, n_x, n_h and n (in the cell-state slot).
 template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
-__device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdArgs& a) {
+// xs_off >= 0: x is staged at smem + xs_off (the one-launch step puts it
+// where its backward half expects it, so the backward does not stage it again)
+__device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdArgs& a, int xs_off = -1) {
   constexpr int K = 2 * H;
   constexpr int LANES = 4 * H;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -334,7 +336,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
   const int bbase = blockIdx.x * NB;
   const int Iin = layer == 0 ? I : H;
 
-  float* xs = smem + NB * NL * 2 * K;
+  float* xs = smem + (xs_off >= 0 ? xs_off : NB * NL * 2 * K);
   auto vin = [&](int n, int l, int p) -> float* { return smem + ((n * NL + l) * 2 + p) * K; };
 
   // activation: sigma(z) with z pre-scaled, then a = sigma * am + ab
@@ -785,7 +787,9 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
 // so the column phase (W^T g, dW += g h^T / g x^T) is the LSTM's unchanged;
 // the direct path dh_{t-1} += dh_t z rides in the dc register.
 template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0>
-__device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdArgs& a) {
+// xs_off >= 0: x already staged at smem + xs_off by the forward half of the
+// one-launch step (same layout, same workgroup): not loaded again
+__device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdArgs& a, int xs_off = -1) {
   constexpr int R = 4 * H;
   constexpr int RS = R / L;          // rows per lane
   constexpr int LANES = H * L;
@@ -820,7 +824,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
   constexpr int RP = R + L * 4;
   float* dg_s = smem;
   float* dha_s = dg_s + NB * NL * 2 * RP;
-  float* xs = dha_s + NB * NL * 2 * H;
+  float* xs = xs_off >= 0 ? smem + xs_off : dha_s + NB * NL * 2 * H;
   auto dgbuf = [&](int n, int l, int p) { return dg_s + ((n * NL + l) * 2 + p) * RP; };
   auto dhabuf = [&](int n, int l, int p) { return dha_s + ((n * NL + l) * 2 + p) * H; };
 
@@ -874,9 +878,11 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
       }
     }
     if constexpr (XLDS) {
+      if (xs_off < 0) {
 #pragma unroll
-      for (int n = 0; n < NB; ++n)
-        stage_x<H>(xs + (int64_t)n * T * H, a.x, (int64_t)bsrc[n] * a.x_sb, a.x_st, T, I, a.x_bf16, true);
+        for (int n = 0; n < NB; ++n)
+          stage_x<H>(xs + (int64_t)n * T * H, a.x, (int64_t)bsrc[n] * a.x_sb, a.x_st, T, I, a.x_bf16, true);
+      }
     }
 
     // ---- raw per-timestep operands (prefetched 2 steps ahead, masked at use)
@@ -1130,7 +1136,10 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
 // ---------------------------------------------------------------------------
 template <int H, bool XLDS, int CELL>
 __global__ void __launch_bounds__(512) lstm_small_step_gs_kernel(PdrnnLstmSmallFwdArgs f, PdrnnLstmSmallBwdArgs b) {
-  lstm_small_fwd_gs_body<H, 1, true, XLDS, true, CELL>(f);
+  // x staged once, past the backward's gate-gradient / dh buffers (the larger
+  // of the two halves' operand areas, bwd_gs_lds<H, 1> with L = 4 lanes)
+  const int xs_off = XLDS ? f.NL * 2 * (4 * H + 4 * 4 + H) : -1;
+  lstm_small_fwd_gs_body<H, 1, true, XLDS, true, CELL>(f, xs_off);
   // this workgroup's global stores (activations, h, dh_T) before its own
   // backward loads them: a workgroup-scope release/acquire (the barrier's
   // own fences) is enough -- every wave of the workgroup shares the CU's
@@ -1139,7 +1148,7 @@ __global__ void __launch_bounds__(512) lstm_small_step_gs_kernel(PdrnnLstmSmallF
   // would write back the XCD's L2 (measured: +6 us/step at B = 180).  The
   // LDS operand buffers are reused by the backward.
   __syncthreads();
-  lstm_small_bwd_gs_body<H, 4, 1, XLDS, true, CELL>(b);
+  lstm_small_bwd_gs_body<H, 4, 1, XLDS, true, CELL>(b, xs_off);
 }
 
 // Column-sum of a [rows, P] slab: pass 1 sums row chunks into work[split, P].
