@@ -96,8 +96,29 @@ __device__ __forceinline__ void preload_x(float* xs, const PdrnnLstmSmallFwdArgs
 // training step), shared by the gate-split and K-split forward kernels: both
 // leave h_T in the top layer's hidden slot of the LDS operand buffers
 // ([NB][NL][2][2H], parity T & 1).  Wave n handles sequence n of the tile.
+// Label and head-weight column of this lane, loaded before the recurrence
+// (the one-launch step): the epilogue's idx -> label -> logits chain then
+// starts from registers instead of two dependent global round trips.
+struct HeadPre {
+  int64_t lab;
+  float w[16];
+};
 template <int H, int NB>
-__device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a, const float* smem, int bbase) {
+__device__ __forceinline__ HeadPre head_prefetch(const PdrnnLstmSmallFwdArgs& a, int bbase) {
+  HeadPre pre{};
+  const int n = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = bbase + n;
+  if (n < NB && b < a.B) {
+    pre.lab = a.labels[a.idx ? a.idx[b] : b];
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) pre.w[cc] = (cc < a.C && lane < H) ? a.head_w[cc * H + lane] : 0.f;
+  }
+  return pre;
+}
+
+template <int H, int NB>
+__device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a, const float* smem, int bbase,
+                                                  const HeadPre* pre = nullptr) {
   constexpr int K = 2 * H;
   const int NL = a.NL, B = a.B, T = a.T;
   const int tid = threadIdx.x;
@@ -109,7 +130,7 @@ __device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a
     const int lane = tid & 63;
     const float* hT = vin(n, NL - 1, T & 1) + H;
     const float hv = lane < H ? hT[lane] : 0.f;
-    const int64_t lab = a.labels[a.idx ? a.idx[b] : b];
+    const int64_t lab = pre ? pre->lab : a.labels[a.idx ? a.idx[b] : b];
     const int C = a.C;
     float m = -INFINITY, logit_y = 0.f;
     int amax = 0;
@@ -117,7 +138,7 @@ __device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc) {
       if (cc < C) {
-        const float wv = lane < H ? a.head_w[cc * H + lane] : 0.f;
+        const float wv = pre ? pre->w[cc] : (lane < H ? a.head_w[cc * H + lane] : 0.f);
         float z = wave_sum(wv * hv) + (a.head_b ? a.head_b[cc] : 0.f);
         lg_c[cc] = z;
         if (z > m) { m = z; amax = cc; }
@@ -137,7 +158,7 @@ __device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a
       if (cc < C) {
         const float d = (expf(lg_c[cc] - m) * inv_se - (cc == lab ? 1.f : 0.f)) * a.inv_batch;
         if (lane < H) {
-          dh = fmaf(a.head_w[cc * H + lane], d, dh);
+          dh = fmaf(pre ? pre->w[cc] : a.head_w[cc * H + lane], d, dh);
           srow[a.head_off_w + cc * H + lane] = d * hv;
         }
         if (lane == 0 && a.head_b) srow[a.head_off_b + cc] = d;
@@ -321,7 +342,8 @@ constexpr float kNegLog2e = -1.4426950408889634f;
 template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
 // xs_off >= 0: x is staged at smem + xs_off (the one-launch step puts it
 // where its backward half expects it, so the backward does not stage it again)
-__device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdArgs& a, int xs_off = -1) {
+__device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdArgs& a, int xs_off = -1,
+                                                       bool head_pre = false) {
   constexpr int K = 2 * H;
   constexpr int LANES = 4 * H;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -338,6 +360,10 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
 
   float* xs = smem + (xs_off >= 0 ? xs_off : NB * NL * 2 * K);
   auto vin = [&](int n, int l, int p) -> float* { return smem + ((n * NL + l) * 2 + p) * K; };
+  HeadPre hpre{};
+  if constexpr (HEAD) {
+    if (head_pre) hpre = head_prefetch<H, NB>(a, bbase);
+  }
 
   // activation: sigma(z) with z pre-scaled, then a = sigma * am + ab
   // (GRU n_x / n_h rows stay linear: unscaled weights, activation skipped)
@@ -501,7 +527,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
       if (CELL == 0) a.cn[((int64_t)layer * B + b) * H + u] = c[n];
     }
   }
-  if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase);
+  if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase, head_pre ? &hpre : nullptr);
 }
 
 template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
@@ -786,10 +812,42 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
 // [dr*r(1-r) | dz*z(1-z) | dpre_n | dpre_n*r] with dpre_n = dh (1-z) (1-n^2),
 // so the column phase (W^T g, dW += g h^T / g x^T) is the LSTM's unchanged;
 // the direct path dh_{t-1} += dh_t z rides in the dc register.
+// W columns (u) of this lane's rows j*RS.. as float2 pairs along rows
+// (W_hh and W_ih; W_ih columns past the layer input are zero).
+template <int H, int L>
+struct BwdCols {
+  pdrnn_f2 whh[4 * H / L / 2], wih[4 * H / L / 2];
+};
+template <int H, int L>
+__device__ __forceinline__ BwdCols<H, L> bwd_load_cols(const PdrnnLstmSmallBwdArgs& a) {
+  constexpr int RS = 4 * H / L;
+  constexpr int LANES = H * L;
+  const int tid = threadIdx.x;
+  const int layer = __builtin_amdgcn_readfirstlane(tid / LANES);
+  const int lg = tid - layer * LANES;
+  const int u = lg / L, j = lg % L;
+  const int Iin = layer == 0 ? a.I : H;
+  const int r0 = j * RS;
+  const bool ih_live = u < Iin;
+  BwdCols<H, L> w;
+  const float* ph = a.w_hh[layer] + (int64_t)r0 * H + u;
+  const float* pi = a.w_ih[layer] + (int64_t)r0 * Iin + min(u, Iin - 1);
+#pragma unroll
+  for (int rr = 0; rr < RS / 2; ++rr) {
+    w.whh[rr] = pdrnn_f2{ph[(2 * rr) * H], ph[(2 * rr + 1) * H]};
+    const float x0 = pi[(int64_t)(2 * rr) * Iin], x1 = pi[(int64_t)(2 * rr + 1) * Iin];
+    w.wih[rr] = ih_live ? pdrnn_f2{x0, x1} : pdrnn_f2{0.f, 0.f};
+  }
+  return w;
+}
+
 template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0>
 // xs_off >= 0: x already staged at smem + xs_off by the forward half of the
-// one-launch step (same layout, same workgroup): not loaded again
-__device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdArgs& a, int xs_off = -1) {
+// one-launch step (same layout, same workgroup): not loaded again.
+// wpre: the W columns, loaded by the caller ahead of time (one-launch step:
+// issued before the forward so their latency hides behind it).
+__device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdArgs& a, int xs_off = -1,
+                                                       const BwdCols<H, L>* wpre = nullptr) {
   constexpr int R = 4 * H;
   constexpr int RS = R / L;          // rows per lane
   constexpr int LANES = H * L;
@@ -839,17 +897,24 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
 #pragma unroll
   for (int g = 0; g < 4; ++g) gm[g] = q == g ? 1.f : 0.f;
   pdrnn_f2 whh[RS / 2], wih[RS / 2], dwhh[RS / 2], dwih[RS / 2];
-  {
-    const float* ph = a.w_hh[layer] + (int64_t)r0 * H + u;
-    const float* pi = a.w_ih[layer] + (int64_t)r0 * Iin + min(u, Iin - 1);
+  if (wpre) {
 #pragma unroll
     for (int rr = 0; rr < RS / 2; ++rr) {
-      whh[rr] = pdrnn_f2{ph[(2 * rr) * H], ph[(2 * rr + 1) * H]};
-      const float x0 = pi[(int64_t)(2 * rr) * Iin], x1 = pi[(int64_t)(2 * rr + 1) * Iin];
-      wih[rr] = ih_live ? pdrnn_f2{x0, x1} : pdrnn_f2{0.f, 0.f};
-      dwhh[rr] = pdrnn_f2{0.f, 0.f};
-      dwih[rr] = pdrnn_f2{0.f, 0.f};
+      whh[rr] = wpre->whh[rr];
+      wih[rr] = wpre->wih[rr];
     }
+  } else {
+    const BwdCols<H, L> w = bwd_load_cols<H, L>(a);
+#pragma unroll
+    for (int rr = 0; rr < RS / 2; ++rr) {
+      whh[rr] = w.whh[rr];
+      wih[rr] = w.wih[rr];
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < RS / 2; ++rr) {
+    dwhh[rr] = pdrnn_f2{0.f, 0.f};
+    dwih[rr] = pdrnn_f2{0.f, 0.f};
   }
   float db = 0.f;
   uint64_t st0 = 0, sr0 = 0;
@@ -1139,7 +1204,11 @@ __global__ void __launch_bounds__(512) lstm_small_step_gs_kernel(PdrnnLstmSmallF
   // x staged once, past the backward's gate-gradient / dh buffers (the larger
   // of the two halves' operand areas, bwd_gs_lds<H, 1> with L = 4 lanes)
   const int xs_off = XLDS ? f.NL * 2 * (4 * H + 4 * 4 + H) : -1;
-  lstm_small_fwd_gs_body<H, 1, true, XLDS, true, CELL>(f, xs_off);
+  // the backward's W columns and the head's label / weights are issued now:
+  // their latency hides behind the forward recurrence (registers are free --
+  // the backward half sets the kernel's VGPR budget)
+  const BwdCols<H, 4> wcols = bwd_load_cols<H, 4>(b);
+  lstm_small_fwd_gs_body<H, 1, true, XLDS, true, CELL>(f, xs_off, true);
   // this workgroup's global stores (activations, h, dh_T) before its own
   // backward loads them: a workgroup-scope release/acquire (the barrier's
   // own fences) is enough -- every wave of the workgroup shares the CU's
@@ -1148,7 +1217,7 @@ __global__ void __launch_bounds__(512) lstm_small_step_gs_kernel(PdrnnLstmSmallF
   // would write back the XCD's L2 (measured: +6 us/step at B = 180).  The
   // LDS operand buffers are reused by the backward.
   __syncthreads();
-  lstm_small_bwd_gs_body<H, 4, 1, XLDS, true, CELL>(b, xs_off);
+  lstm_small_bwd_gs_body<H, 4, 1, XLDS, true, CELL>(b, xs_off, &wcols);
 }
 
 // Column-sum of a [rows, P] slab: pass 1 sums row chunks into work[split, P].
