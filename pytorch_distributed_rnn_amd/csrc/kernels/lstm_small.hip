@@ -118,7 +118,7 @@ __device__ __forceinline__ HeadPre head_prefetch(const PdrnnLstmSmallFwdArgs& a,
 
 template <int H, int NB>
 __device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a, const float* smem, int bbase,
-                                                  const HeadPre* pre = nullptr) {
+                                                  const HeadPre* pre = nullptr, float* dh_lds = nullptr) {
   constexpr int K = 2 * H;
   const int NL = a.NL, B = a.B, T = a.T;
   const int tid = threadIdx.x;
@@ -164,7 +164,10 @@ __device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a
         if (lane == 0 && a.head_b) srow[a.head_off_b + cc] = d;
       }
     }
-    if (lane < H) a.dh_top[(int64_t)b * H + lane] = dh;
+    if (lane < H) {
+      a.dh_top[(int64_t)b * H + lane] = dh;
+      if (dh_lds) dh_lds[lane] = dh;  // one-launch step: handed to the backward half through LDS
+    }
     if (lane == 0) {  // [mean-loss contribution, count, correct] -> column sums are the batch stats
       srow[a.stat_off + 0] = (lse - logit_y) * a.inv_batch;
       srow[a.stat_off + 1] = 1.f;
@@ -343,7 +346,7 @@ template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
 // xs_off >= 0: x is staged at smem + xs_off (the one-launch step puts it
 // where its backward half expects it, so the backward does not stage it again)
 __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdArgs& a, int xs_off = -1,
-                                                       bool head_pre = false) {
+                                                       bool head_pre = false, float* dh_lds = nullptr) {
   constexpr int K = 2 * H;
   constexpr int LANES = 4 * H;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -527,7 +530,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
       if (CELL == 0) a.cn[((int64_t)layer * B + b) * H + u] = c[n];
     }
   }
-  if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase, head_pre ? &hpre : nullptr);
+  if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase, head_pre ? &hpre : nullptr, dh_lds);
 }
 
 template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
@@ -846,8 +849,10 @@ template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0>
 // one-launch step (same layout, same workgroup): not loaded again.
 // wpre: the W columns, loaded by the caller ahead of time (one-launch step:
 // issued before the forward so their latency hides behind it).
+// dh_lds: the top layer's dh_T of this workgroup's (single) sequence in LDS.
 __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdArgs& a, int xs_off = -1,
-                                                       const BwdCols<H, L>* wpre = nullptr) {
+                                                       const BwdCols<H, L>* wpre = nullptr,
+                                                       const float* dh_lds = nullptr) {
   constexpr int R = 4 * H;
   constexpr int RS = R / L;          // rows per lane
   constexpr int LANES = H * L;
@@ -932,7 +937,9 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
       bsrc[n] = a.idx ? (int)a.idx[bs[n]] : bs[n];
       dh[n] = 0.f;
       dha_r[n] = 0.f;
-      if (a.dhn) {
+      if (dh_lds) {
+        dh[n] = top ? dh_lds[u] : 0.f;
+      } else if (a.dhn) {
         if (top_only) dh[n] = top ? a.dhn[(int64_t)bs[n] * H + u] : 0.f;
         else dh[n] = a.dhn[((int64_t)layer * B + bs[n]) * H + u];
       }
@@ -1201,6 +1208,8 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
 // ---------------------------------------------------------------------------
 template <int H, bool XLDS, int CELL>
 __global__ void __launch_bounds__(512) lstm_small_step_gs_kernel(PdrnnLstmSmallFwdArgs f, PdrnnLstmSmallBwdArgs b) {
+  extern __shared__ __attribute__((aligned(16))) float smem_step[];
+  static_assert(H <= 32, "dh_T slot must fit the L = 8 padding slack (NL * 2 * 16 floats >= H)");
   // x staged once, past the backward's gate-gradient / dh buffers (the larger
   // of the two halves' operand areas, bwd_gs_lds<H, 1> with L = 4 lanes)
   const int xs_off = XLDS ? f.NL * 2 * (4 * H + 4 * 4 + H) : -1;
@@ -1208,7 +1217,9 @@ __global__ void __launch_bounds__(512) lstm_small_step_gs_kernel(PdrnnLstmSmallF
   // their latency hides behind the forward recurrence (registers are free --
   // the backward half sets the kernel's VGPR budget)
   const BwdCols<H, 4> wcols = bwd_load_cols<H, 4>(b);
-  lstm_small_fwd_gs_body<H, 1, true, XLDS, true, CELL>(f, xs_off, true);
+  // dh_T slot: the launch's LDS slack past x (bwd_gs_lds pads for L = 8)
+  float* dh_lds = XLDS ? smem_step + xs_off + f.T * H : nullptr;
+  lstm_small_fwd_gs_body<H, 1, true, XLDS, true, CELL>(f, xs_off, true, dh_lds);
   // this workgroup's global stores (activations, h, dh_T) before its own
   // backward loads them: a workgroup-scope release/acquire (the barrier's
   // own fences) is enough -- every wave of the workgroup shares the CU's
@@ -1217,7 +1228,7 @@ __global__ void __launch_bounds__(512) lstm_small_step_gs_kernel(PdrnnLstmSmallF
   // would write back the XCD's L2 (measured: +6 us/step at B = 180).  The
   // LDS operand buffers are reused by the backward.
   __syncthreads();
-  lstm_small_bwd_gs_body<H, 4, 1, XLDS, true, CELL>(b, xs_off, &wcols);
+  lstm_small_bwd_gs_body<H, 4, 1, XLDS, true, CELL>(b, xs_off, &wcols, dh_lds);
 }
 
 // Column-sum of a [rows, P] slab: pass 1 sums row chunks into work[split, P].
