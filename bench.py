@@ -60,6 +60,26 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def _max_over_ranks(x: float, dev) -> float:
+    """MAX of a host scalar over ranks: on the native RCCL communicator when
+    there is one (the gradient path's), else torch.distributed."""
+    import torch
+    import torch.distributed as dist
+    from pytorch_distributed_rnn_amd.parallel.comm import native_world_comm
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return x
+    c = native_world_comm()
+    if c is not None:
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        c.all_reduce(t, "max")
+        c.wait()
+        torch.cuda.synchronize(dev)
+        return float(t.item())
+    t = torch.tensor([x], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main(argv=None):
     args = parse(argv)
     logging.basicConfig(level=logging.WARNING)
@@ -122,9 +142,7 @@ def main(argv=None):
         torch.cuda.synchronize()
     env.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = _max_over_ranks(elapsed, dev)
 
     global_batch = per_rank * world
     seqs = global_batch * args.steps
@@ -145,10 +163,7 @@ def main(argv=None):
     if dev.type == "cuda":
         torch.cuda.synchronize()
     env.barrier()
-    te = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                      device=dev if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(te, op=dist.ReduceOp.MAX)
-    epoch_s = float(te.item())
+    epoch_s = _max_over_ranks(time.perf_counter() - t0, dev)
     # sanity: loss must be finite after training
     loss = float(stats[0])
     if rank == 0:

@@ -24,6 +24,42 @@ import torch.distributed as dist
 from .. import _ext
 
 _CACHE: Dict[int, object] = {}
+_NATIVE = set()   # cache keys holding an RcclComm
+_UID_SEQ = [0]    # per-process communicator creation count (same order on every rank)
+
+
+def _exchange_uid(mod, g, rank: int) -> bytes:
+    """Rank 0's ncclUniqueId to every rank of ``g`` through the rendezvous
+    TCPStore -- a key/value exchange, not a collective, so torch's own RCCL
+    communicator for the group is never created just to bootstrap ours (one
+    communicator per process on the gradient path instead of two).  Falls
+    back to a broadcast when the default store is not reachable."""
+    _UID_SEQ[0] += 1
+    try:
+        store = dist.distributed_c10d._get_default_store()
+        ranks = dist.get_process_group_ranks(g)
+    except Exception:  # pragma: no cover - private-API drift
+        store = None
+    if store is None:
+        uid = [mod.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=dist.get_global_rank(g, 0), group=g)
+        return uid[0]
+    key = "pdrnn/rccl_uid/%d/%s" % (_UID_SEQ[0], "-".join(str(r) for r in ranks))
+    if rank == 0:
+        uid = mod.rccl_unique_id()
+        store.set(key, uid)
+        return uid
+    return bytes(store.get(key))  # blocks until rank 0 has published (store timeout)
+
+
+def native_world_comm():
+    """The native RCCL communicator of the default group, if one was made
+    (barriers and the benchmark's timing reductions then use it instead of
+    waking torch's own communicator)."""
+    if not dist.is_initialized():
+        return None
+    key = id(dist.group.WORLD)
+    return _CACHE.get(key) if key in _NATIVE else None
 
 
 class _PyComm:
@@ -87,11 +123,11 @@ def get_comm(group=None, prefer_native: bool = True):
     if use_rccl:
         rank = dist.get_rank(g)
         world = dist.get_world_size(g)
-        uid = [mod.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=dist.get_global_rank(g, 0), group=g)
+        uid = _exchange_uid(mod, g, rank)
         from .env import collective_timeout_s
-        comm = mod.make_rccl_comm(uid[0], rank, world, torch.cuda.current_device(), True,
+        comm = mod.make_rccl_comm(uid, rank, world, torch.cuda.current_device(), True,
                                   collective_timeout_s())
+        _NATIVE.add(key)
     elif mod is not None:
         comm = mod.make_pg_comm(g)
     else:
@@ -102,3 +138,4 @@ def get_comm(group=None, prefer_native: bool = True):
 
 def reset_comms() -> None:
     _CACHE.clear()
+    _NATIVE.clear()

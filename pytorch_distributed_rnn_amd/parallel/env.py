@@ -150,8 +150,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] =
     _TIMEOUT_S = float(timeout_s)
     kwargs = dict(backend=be, rank=info.rank, world_size=info.world_size,
                   timeout=datetime.timedelta(seconds=timeout_s))
-    if be == "nccl" and use_gpu:
-        kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
+    # no device_id: it makes torch create its RCCL communicator eagerly.  The
+    # gradient path runs on the native communicator (parallel/comm.py, its
+    # unique id exchanged through the TCPStore), so torch's stays lazy and is
+    # only created if something issues a torch collective on the GPU group.
     try:
         dist.init_process_group(**kwargs)
     except TypeError:
@@ -174,6 +176,11 @@ def get_world_size() -> int:
 
 def barrier() -> None:
     if is_distributed():
+        from .comm import native_world_comm
+        c = native_world_comm()
+        if c is not None:  # the gradient communicator (torch's RCCL comm stays unborn)
+            c.barrier()
+            return
         if dist.get_backend() == "nccl":
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
