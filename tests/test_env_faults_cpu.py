@@ -71,7 +71,7 @@ def test_dropped_rank_fails_survivors_fast(tmp_path):
 
     from _mp import ROOT, cpu_env, free_port
 
-    world, timeout_s = 3, 20
+    world, timeout_s = 3, 45  # generous: under a loaded test runner a rank can take >20 s to start
     main = os.path.join(ROOT, "src", "motion", "main.py")
     port = str(free_port())
     procs = []
