@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--global-batch", type=int, default=180)
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--cprofile", action="store_true", help="print the host-side hot spots (cProfile, tottime)")
     args = ap.parse_args()
     import torch
 
@@ -45,10 +46,19 @@ def main():
     for b in batches[:20]:
         tr.train_batch(loader.make_batch(b))
     torch.cuda.synchronize()
+    prof = None
+    if args.cprofile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for b in batches:
         tr.train_batch(loader.make_batch(b))
     t1 = time.perf_counter()
+    if prof is not None:
+        prof.disable()
+        import pstats
+        pstats.Stats(prof).sort_stats("tottime").print_stats(25)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     out = {"global_batch": args.global_batch,
