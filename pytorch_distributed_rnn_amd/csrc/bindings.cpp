@@ -291,7 +291,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
                           int64_t split_bwd, int64_t nb_fwd, int64_t nb_bwd,
                           const optional<std::vector<Tensor>>& adam_state,
                           const optional<std::vector<double>>& adam_hp, int64_t cell,
-                          const optional<Tensor>& grad_colmap) {
+                          const optional<Tensor>& grad_colmap, const optional<Tensor>& stats_slot_step,
+                          int64_t stats_slot_offset) {
   CHECK_HIP_TENSOR(x);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be float32 or bfloat16");
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [N, T, I] with contiguous rows");
@@ -320,6 +321,16 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   TORCH_CHECK(flat_grad.numel() == P_params && flat_grad.is_contiguous() && flat_grad.scalar_type() == at::kFloat,
               "flat_grad must be the model's flat fp32 gradient buffer (", P_params, " elements)");
   TORCH_CHECK(stats.numel() >= 3 && stats.is_contiguous() && stats.scalar_type() == at::kFloat);
+  // stats_slot_step: `stats` is the whole [rows, 3] epoch ring; the row is read
+  // on the device from the step count (graph replay, see slab_reduce_adam)
+  const float* slot_step = nullptr;
+  int ring_rows = 0;
+  if (stats_slot_step.has_value() && stats_slot_step->defined()) {
+    TORCH_CHECK(stats_slot_step->is_cuda() && stats_slot_step->scalar_type() == at::kFloat &&
+                stats.dim() == 2 && stats.size(1) == 3, "stats_slot_step needs a float device step and a [rows, 3] ring");
+    slot_step = stats_slot_step->data_ptr<float>();
+    ring_rows = (int)stats.size(0);
+  }
   const int64_t P_head = P_params - P_rnn;    // head weight (+ bias)
   const int64_t PH = P_head + 3;              // + [loss, count, correct]
   auto opts = x.options().dtype(at::kFloat);
@@ -406,6 +417,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   }();
   const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, gridb / 16));
   Tensor work = one_pass ? Tensor() : at::empty({split, P_rnn + PH}, opts);
+  TORCH_CHECK(one_pass || slot_step == nullptr, "stats_slot_step needs the one-pass reduction");
   if (adam_state.has_value() && adam_hp.has_value()) {
     // single-process step: the second reduction pass runs inside Adam
     const auto& as = *adam_state;
@@ -424,7 +436,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     if (one_pass) {
       HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(&ad, slab.data_ptr<float>(), gridb, P_rnn, L.P, colmap,
                                               head_slab.data_ptr<float>(), B, PH, P_params, flat_grad.data_ptr<float>(),
-                                              stats.data_ptr<float>(), st));
+                                              stats.data_ptr<float>(), slot_step, (int)stats_slot_offset, ring_rows, st));
       return;
     }
     HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,
@@ -436,7 +448,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   if (one_pass) {
     HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(nullptr, slab.data_ptr<float>(), gridb, P_rnn, L.P, colmap,
                                             head_slab.data_ptr<float>(), B, PH, P_params, flat_grad.data_ptr<float>(),
-                                            stats.data_ptr<float>(), st));
+                                            stats.data_ptr<float>(), slot_step, (int)stats_slot_offset, ring_rows, st));
     return;
   }
   HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,
@@ -821,7 +833,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("idx"), py::arg("labels"), py::arg("w"), py::arg("head_w"), py::arg("head_b"),
         py::arg("flat_grad"), py::arg("stats"), py::arg("H"), py::arg("NL"), py::arg("split_fwd"),
         py::arg("split_bwd"), py::arg("nb_fwd"), py::arg("nb_bwd"), py::arg("adam_state") = py::none(),
-        py::arg("adam_hp") = py::none(), py::arg("cell") = 0, py::arg("grad_colmap") = py::none());
+        py::arg("adam_hp") = py::none(), py::arg("cell") = 0, py::arg("grad_colmap") = py::none(),
+        py::arg("stats_slot_step") = py::none(), py::arg("stats_slot_offset") = 0);
   m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
   m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer", py::arg("param"), py::arg("grad"),

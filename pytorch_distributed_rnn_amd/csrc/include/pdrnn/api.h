@@ -258,9 +258,12 @@ hipError_t pdrnn_adam_partials(const PdrnnAdamArgs* a, const float* work, int sp
 // One-pass reduction of the fused step's [rowsA, ldA] (through colmap) and
 // [rowsB, PB] gradient slabs into grad_out[0:n_out] (+ tail_out for the
 // columns past n_out), with the Adam step of each element when a != nullptr.
+// slot_step != NULL: tail_out is a [ring_rows, tail] ring and the tail goes to
+// row ((int)*slot_step + slot_offset) mod ring_rows (graph-replayed steps).
 hipError_t pdrnn_slab_reduce_adam(const PdrnnAdamArgs* a, const float* A, int64_t rowsA, int64_t PA, int64_t ldA,
                                   const int* colmap, const float* Bs, int64_t rowsB, int64_t PB, int64_t n_out,
-                                  float* grad_out, float* tail_out, hipStream_t stream);
+                                  float* grad_out, float* tail_out, const float* slot_step, int slot_offset,
+                                  int ring_rows, hipStream_t stream);
 
 // Diagnostics: a single wave that spins for `microseconds` (bounded, <= 60 s).
 // Communicator-watchdog tests only.

@@ -151,7 +151,8 @@ __global__ void __launch_bounds__(256) adam_partials_kernel(PdrnnAdamArgs a, con
 __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
     PdrnnAdamArgs a, const float* __restrict__ A, int64_t rowsA, int64_t PA, int64_t ldA,
     const int* __restrict__ colmap, const float* __restrict__ Bs, int64_t rowsB, int64_t PB, int64_t n_out,
-    float* __restrict__ grad_out, float* __restrict__ tail_out, int nblkA) {
+    float* __restrict__ grad_out, float* __restrict__ tail_out, int nblkA, const float* __restrict__ slot_step,
+    int slot_offset, int ring_rows) {
   __shared__ float red[1024];
   const int tid = threadIdx.x;
   const bool inA = (int)blockIdx.x < nblkA;
@@ -192,7 +193,17 @@ __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
       a.param[p] = pv; a.exp_avg[p] = m; a.exp_avg_sq[p] = v;
     }
   } else {
-    tail_out[p - n_out] = g;
+    // tail (batch statistics): row ((int)*slot_step + slot_offset) mod
+    // ring_rows of a [ring_rows, tail] ring when slot_step is given -- a
+    // graph-replayed step then writes its statistics straight into the
+    // epoch ring slot the host assigned it (no copy after the replay)
+    int64_t row = 0;
+    if (slot_step) {
+      const int64_t r = ((int64_t)(*slot_step) + slot_offset) % ring_rows;
+      row = r < 0 ? r + ring_rows : r;
+    }
+    const int64_t nt = PA + PB - n_out;
+    tail_out[row * nt + p - n_out] = g;
   }
 }
 
@@ -202,14 +213,17 @@ __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
 extern "C" hipError_t pdrnn_slab_reduce_adam(const PdrnnAdamArgs* a, const float* A, int64_t rowsA, int64_t PA,
                                             int64_t ldA, const int* colmap, const float* Bs, int64_t rowsB,
                                             int64_t PB, int64_t n_out, float* grad_out, float* tail_out,
+                                            const float* slot_step, int slot_offset, int ring_rows,
                                             hipStream_t stream) {
+  if (slot_step && ring_rows <= 0) return hipErrorInvalidValue;
   if (PA + PB <= 0) return hipSuccess;
   if (PA + PB > n_out && tail_out == nullptr) return hipErrorInvalidValue;
   PdrnnAdamArgs none{};
   const int nblkA = (int)((PA + 63) / 64);
   const int nblkB = (int)((PB + 15) / 16);
   hipLaunchKernelGGL(pdrnn::slab_reduce_adam_kernel, dim3((unsigned)(nblkA + nblkB)), dim3(1024), 0, stream,
-                     a ? *a : none, A, rowsA, PA, ldA, colmap, Bs, rowsB, PB, n_out, grad_out, tail_out, nblkA);
+                     a ? *a : none, A, rowsA, PA, ldA, colmap, Bs, rowsB, PB, n_out, grad_out, tail_out, nblkA,
+                     slot_step, slot_offset, ring_rows);
   return hipGetLastError();
 }
 

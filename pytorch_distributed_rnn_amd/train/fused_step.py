@@ -197,7 +197,8 @@ class MotionTrainStep:
         else:
             ws = self.weights
         cell = 1 if self.gru else 0
-        stats = self.ring[self._slot]
+        slot = self._slot
+        stats = self.ring[slot]
         self._slot = (self._slot + 1) % self.RING
         adam = self._flat_adam()
         if adam is not None and self.grad_sync is None:
@@ -206,7 +207,7 @@ class MotionTrainStep:
                                               self.NL, sp_fwd, 0, nb_fwd, nb_bwd, adam[0], adam[1], cell, self.colmap)
             return stats
         if self.grad_sync is not None and adam is not None and self.cuda_graph:
-            if self._graph_step(features, labels, idx, ws, (nb_fwd, sp_fwd), nb_bwd, adam, stats):
+            if self._graph_step(features, labels, idx, ws, (nb_fwd, sp_fwd), nb_bwd, adam, stats, slot):
                 return stats
         with trace_range("pdrnn.fwd_bwd"):
             self.mod.lstm_head_train_step(
@@ -257,7 +258,7 @@ class MotionTrainStep:
     _GRAPHS_MAX = 4
 
     def _graph_step(self, features: Tensor, labels: Tensor, idx: Optional[Tensor], ws, nb_fwd,
-                    nb_bwd: int, adam, stats: Tensor) -> bool:
+                    nb_bwd: int, adam, stats: Tensor, slot: int) -> bool:
         """Run the synced step as a graph replay.  False: run it eagerly --
         the bf16 model (its per-step weight cast allocates), and the first two
         steps of a configuration, so that RCCL's lazy connection setup and the
@@ -282,7 +283,7 @@ class MotionTrainStep:
             if ent["eager"] <= 2:
                 return False
             try:
-                self._capture(ent, features, labels, idx, ws, nb_fwd, nb_bwd, adam)
+                self._capture(ent, features, labels, idx, ws, nb_fwd, nb_bwd, adam, slot)
             except Exception as exc:  # capture unsupported here: stay eager for good
                 import warnings
                 warnings.warn(f"HIP graph capture of the synced step failed ({exc!r}); running eagerly")
@@ -301,15 +302,24 @@ class MotionTrainStep:
         if comm is not None and hasattr(comm, "track_current"):
             comm.track_current()  # the communicator's watchdog bounds the replay
         ent["step_host"] = step
-        stats.copy_(ent["stats"], non_blocking=True)
+        # the graph wrote the statistics into ring row (step - 1 + slot_off):
+        # the row assigned to this step whenever the host's ring slot and step
+        # count advanced together since the capture (the usual case); else
+        # one copy moves them
+        row = (int(step) - 1 + ent["slot_off"]) % self.RING
+        if row != slot:
+            stats.copy_(self.ring[row], non_blocking=True)
         return True
 
-    def _capture(self, ent: dict, features: Tensor, labels: Tensor, idx: Tensor, ws, nb_fwd, nb_bwd: int, adam):
+    def _capture(self, ent: dict, features: Tensor, labels: Tensor, idx: Tensor, ws, nb_fwd, nb_bwd: int, adam,
+                 slot: int):
         (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
         dev = self.flat.grad.device
         hw, hb = self.m.fc.weight, self.m.fc.bias
         ent["idx"] = idx.clone()
-        ent["stats"] = torch.zeros(3, dtype=torch.float32, device=dev)
+        # statistics go straight into the epoch ring: row = device step count
+        # (before this step's Adam advances it) + slot_off
+        ent["slot_off"] = (slot - (int(step) - 1)) % self.RING
         ent["step"] = torch.zeros(1, dtype=torch.float32, device=dev)
         ent["ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
         ent["step_host"] = None
@@ -317,8 +327,9 @@ class MotionTrainStep:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             nb, sp = nb_fwd  # (sequences per forward workgroup, forward lanes per unit)
-            self.mod.lstm_head_train_step(features, ent["idx"], labels, ws, hw, hb, self.flat.grad, ent["stats"],
-                                          self.H, self.NL, sp, 0, nb, nb_bwd)
+            self.mod.lstm_head_train_step(features, ent["idx"], labels, ws, hw, hb, self.flat.grad, self.ring,
+                                          self.H, self.NL, sp, 0, nb, nb_bwd, None, None, 0, None, ent["step"],
+                                          ent["slot_off"])
             self.grad_sync()
             self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step, 1.0, bool(dec), False,
                                None, ent["step"], ent["ticket"])

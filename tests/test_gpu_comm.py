@@ -138,7 +138,9 @@ def test_graph_replayed_rccl_step_matches_local(rccl_group):
     """The synced step captured into a HIP graph (fwd/BPTT/reductions + inline
     RCCL all-reduce + Adam with a device step count) and replayed with fresh
     batch indices reproduces the eager local step, step for step, including
-    after an eager step in between (device step count re-seeded)."""
+    after an eager step in between (device step count re-seeded); the batch
+    statistics land in the step's epoch-ring row (written in-graph, or copied
+    when the host's ring slot moved off the captured mapping)."""
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
@@ -164,6 +166,8 @@ def test_graph_replayed_rccl_step_matches_local(rccl_group):
         if i == 5:  # a host-gathered batch in between runs eagerly
             a = s1(feats.index_select(0, idx), labels.index_select(0, idx), None)
         else:
+            if i == 6:  # ring slot out of step with the captured mapping: the copy fallback
+                s1._slot = (s1._slot + 3) % s1.RING
             a = s1(feats, labels, idx)
         b = s2(feats, labels, idx)
         outs.append((a.clone(), b.clone()))
