@@ -36,6 +36,35 @@ def test_fused_step_matches_autograd(cell):
         assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
 
 
+@pytest.mark.parametrize("cell,hidden,layers", [("lstm", 16, 1), ("lstm", 32, 3), ("lstm", 16, 4),
+                                                 ("gru", 16, 2), ("gru", 32, 1)])
+def test_one_launch_step_shapes_match_autograd(cell, hidden, layers):
+    """The one-launch step (B = 64: one sequence per workgroup) at other
+    hidden sizes / depths equals the autograd step."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.train.trainer import Trainer
+    torch.manual_seed(1)
+    train, _, _ = synthetic_motion(n_train=128, n_validation=2, n_test=2, seed=5)
+    m1 = MotionModel(9, hidden, layers, 6, cell=cell)
+    m2 = copy.deepcopy(m1)
+    t1 = Trainer(m1, train, batch_size=64, learning_rate=2.5e-3, device=torch.device("cuda"))
+    t2 = Trainer(m2, train, batch_size=64, learning_rate=2.5e-3, device=torch.device("cuda"))
+    t2._fused = None
+    if t1._fused_step() is None:
+        pytest.skip("fused step does not cover this shape")
+    mod = _ext.native(torch.device("cuda", 0))
+    assert mod.lstm_small_step_one_launch(hidden, layers, 128, 64, 1, 0, 1, 0)
+    for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
+        s1, _ = t1.train_batch(x1)
+        s2, _ = t2.train_batch(x2)
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+        assert int(s1[2]) == int(s2[2])
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
+
+
 def test_one_launch_step_selected_in_latency_regime():
     """B <= one resident round: forward + head/CE + BPTT run as one launch
     (the B=96 runs of test_fused_step_matches_autograd go through it); the
