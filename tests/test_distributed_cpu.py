@@ -82,3 +82,31 @@ def test_ddp_checkpoint_has_module_prefix(tmp_path):
     assert files, "rank 0 must checkpoint"
     ck = torch.load(files[0], weights_only=True)
     assert all(k.startswith("module.") for k in ck["model_state"])
+
+
+def test_rccl_uid_exchange_through_store(tmp_path):
+    """The native communicator's unique id goes rank 0 -> every rank through
+    the rendezvous TCPStore (no torch collective, so torch's own RCCL
+    communicator is never created for it): every rank of a 3-rank group ends
+    with rank 0's bytes, and a second communicator gets a fresh key."""
+    script = tmp_path / "uid.py"
+    script.write_text(
+        "import os, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch.distributed as dist\n"
+        "from pytorch_distributed_rnn_amd.parallel import comm\n"
+        "dist.init_process_group('gloo')\n"
+        "r = dist.get_rank()\n"
+        "class M:\n"
+        "    n = 0\n"
+        "    @staticmethod\n"
+        "    def rccl_unique_id():\n"
+        "        M.n += 1\n"
+        "        return bytes([M.n, 7, 0, 255]) * 32\n"
+        "a = comm._exchange_uid(M, dist.group.WORLD, r)\n"
+        "b = comm._exchange_uid(M, dist.group.WORLD, r)\n"
+        "assert a == bytes([1, 7, 0, 255]) * 32 and b == bytes([2, 7, 0, 255]) * 32, (r, a[:4], b[:4])\n"
+        "print('uid-ok', r, flush=True)\n"
+        "dist.destroy_process_group()\n")
+    out = torchrun([str(script)], nproc=3, cwd=str(tmp_path))
+    assert sorted(int(ln.split()[-1]) for ln in out.splitlines() if ln.startswith("uid-ok")) == [0, 1, 2]
