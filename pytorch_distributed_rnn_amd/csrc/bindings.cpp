@@ -334,8 +334,10 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const int64_t P_head = P_params - P_rnn;    // head weight (+ bias)
   const int64_t PH = P_head + 3;              // + [loss, count, correct]
   auto opts = x.options().dtype(at::kFloat);
-  Tensor hseq = at::empty({NL, B, T, H}, opts);
-  Tensor act = at::empty({NL, B, T, 5, H}, opts);
+  // hseq / act with the deferred-dW kernel's padding (one h row in front,
+  // 16 rows behind: it streams whole 16-row stages without clamps)
+  Tensor hseq_buf = at::empty({H + NL * B * T * H + 16 * H}, opts);
+  Tensor act = at::empty({NL * B * T * 5 * H + 16 * 5 * H}, opts);
   Tensor hn = at::empty({NL, B, H}, opts), cn = at::empty({NL, B, H}, opts);
   Tensor dh_top = at::empty({B, H}, opts);
   Tensor head_slab = at::empty({B, PH}, opts);
@@ -353,7 +355,15 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const int gridb = tp ? pdrnn_lstm_small_bwd_tp_grid((int)H, (int)NL, (int)T, (int)I, (int)B, (int)nb_bwd, (int)cell)
                        : pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb_bwd, (int)split_bwd);
   TORCH_CHECK(gridb > 0, "unsupported backward tile nb=", nb_bwd);
-  Tensor slab = at::empty({gridb, L.P}, opts);
+  // Above one residency round the BPTT defers its weight gradients: the
+  // recurrence writes the gate gradients (into `act`, in place) and the
+  // matrix-core kernel lstm_small_dw forms dW / db over all B*T rows, one slab
+  // row per K chunk (see pdrnn_lstm_small_bwd_dwout).  One round or less keeps
+  // the one-launch step (register-resident dW, no extra launch).
+  const int dw_mode = pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T);
+  const bool dwout = !tp && nb_bwd == 1 && split_bwd == 1 && ((gridb < B && dw_mode == 1) || dw_mode == 2);
+  const int slab_rows = dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
+  Tensor slab = at::empty({slab_rows, L.P}, opts);
 
   PdrnnLstmSmallFwdArgs f{};
   f.x = reinterpret_cast<const float*>(x.data_ptr());
@@ -366,7 +376,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     f.b_ih[l] = w[l * 4 + 2].data_ptr<float>();
     f.b_hh[l] = w[l * 4 + 3].data_ptr<float>();
   }
-  f.hseq = hseq.data_ptr<float>(); f.act = act.data_ptr<float>();
+  f.hseq = hseq_buf.data_ptr<float>() + H; f.act = act.data_ptr<float>();
   f.hn = hn.data_ptr<float>(); f.cn = cn.data_ptr<float>();
   f.head_w = head_w.data_ptr<float>();
   f.head_b = (head_b.has_value() && head_b->defined()) ? head_b->data_ptr<float>() : nullptr;
@@ -385,7 +395,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   }
   // latency regime (one sequence per workgroup in both passes): forward,
   // head/CE and BPTT in one launch; otherwise the forward launches here
-  const bool one_launch = !tp && !st_f.defined() &&
+  const bool one_launch = !tp && !dwout && !st_f.defined() &&
       pdrnn_lstm_small_step_ok((int)H, (int)NL, (int)B, (int)nb_fwd, (int)split_fwd, (int)nb_bwd, (int)split_bwd,
                                gridb) == 1;
   if (!one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
@@ -401,13 +411,43 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.dhn = dh_top.data_ptr<float>(); bk.dhn_top_only = 1;
   bk.slab = slab.data_ptr<float>(); bk.P = L.P;
   bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL; bk.cell = (int)cell;
+  int grid_dw = gridb;
+  Tensor xg;
+  if (dwout) {
+    grid_dw = pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B);
+    TORCH_CHECK(grid_dw > 0, "deferred-dW backward: no resident grid");
+    if (st_f.defined()) {
+      st_b = at::zeros({grid_dw, 4}, opts.dtype(at::kLong));
+      bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
+    }
+    bk.dg_out = f.act;  // in place: each row lane overwrites the activation it has consumed
+    bk.dg_st = 5 * H;
+    const int64_t xg_ld = (I + 3) / 4 * 4;
+    xg = at::empty({(B * T + 16) * xg_ld + 256}, opts);  // + one DMA job past the last 16-row stage
+    bk.xg_out = xg.data_ptr<float>();
+    bk.xg_ld = (int)xg_ld;
+  }
   if (st_b.defined()) bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
   if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
   else if (tp) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_tp(&bk, (int)H, (int)nb_bwd, gridb, st));
+  else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, st));
   else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
+  if (dwout) {
+    PdrnnLstmSmallDwArgs dw{};
+    dw.xg = xg.data_ptr<float>(); dw.xg_ld = bk.xg_ld;
+    dw.hseq = f.hseq; dw.dg = f.act; dw.dg_st = 5 * H;
+    dw.slab = slab.data_ptr<float>(); dw.P = L.P;
+    for (int64_t l = 0; l < NL; ++l) {
+      dw.off_wih[l] = L.off_wih[l]; dw.off_whh[l] = L.off_whh[l];
+      dw.off_bih[l] = L.off_bih[l]; dw.off_bhh[l] = L.off_bhh[l];
+    }
+    dw.B = (int)B; dw.T = (int)T; dw.I = (int)I; dw.NL = (int)NL; dw.chunks = slab_rows;
+    HIP_LAUNCH_CHECK(pdrnn_lstm_small_dw(&dw, (int)H, st));
+  }
   if (st_f.defined()) {
     report_stamps("fwd(head step)", st_f, (int)(T + NL - 1));
-    report_stamps("bwd(head step, lean)", st_b, (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)gridb * nb_bwd - 1) / ((int64_t)gridb * nb_bwd)));
+    report_stamps(dwout ? "bwd(head step, lean, deferred dW)" : "bwd(head step, lean)", st_b,
+                  (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_bwd - 1) / ((int64_t)grid_dw * nb_bwd)));
   }
 
   // PDRNN_ONE_PASS_REDUCE=0: the two-pass reduction (A/B measurements)
@@ -415,7 +455,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     const char* e = getenv("PDRNN_ONE_PASS_REDUCE");
     return !(e && e[0] == '0');
   }();
-  const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, gridb / 16));
+  const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, slab_rows / 16));
   Tensor work = one_pass ? Tensor() : at::empty({split, P_rnn + PH}, opts);
   TORCH_CHECK(one_pass || slot_step == nullptr, "stats_slot_step needs the one-pass reduction");
   if (adam_state.has_value() && adam_hp.has_value()) {
@@ -434,24 +474,24 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     ad.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(hp[2], hp[5]));
     ad.grad_scale = 1.f; ad.decoupled = hp[6] != 0.0 ? 1 : 0; ad.maximize = 0;
     if (one_pass) {
-      HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(&ad, slab.data_ptr<float>(), gridb, P_rnn, L.P, colmap,
+      HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(&ad, slab.data_ptr<float>(), slab_rows, P_rnn, L.P, colmap,
                                               head_slab.data_ptr<float>(), B, PH, P_params, flat_grad.data_ptr<float>(),
                                               stats.data_ptr<float>(), slot_step, (int)stats_slot_offset, ring_rows, st));
       return;
     }
-    HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,
+    HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), slab_rows, P_rnn, head_slab.data_ptr<float>(), B, PH,
                                               work.data_ptr<float>(), split, colmap, L.P, st));
     HIP_LAUNCH_CHECK(pdrnn_adam_partials(&ad, work.data_ptr<float>(), split, P_rnn + PH, flat_grad.data_ptr<float>(),
                                          stats.data_ptr<float>(), 3, st));
     return;
   }
   if (one_pass) {
-    HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(nullptr, slab.data_ptr<float>(), gridb, P_rnn, L.P, colmap,
+    HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(nullptr, slab.data_ptr<float>(), slab_rows, P_rnn, L.P, colmap,
                                             head_slab.data_ptr<float>(), B, PH, P_params, flat_grad.data_ptr<float>(),
                                             stats.data_ptr<float>(), slot_step, (int)stats_slot_offset, ring_rows, st));
     return;
   }
-  HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), gridb, P_rnn, head_slab.data_ptr<float>(), B, PH,
+  HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), slab_rows, P_rnn, head_slab.data_ptr<float>(), B, PH,
                                       P_params, flat_grad.data_ptr<float>(), stats.data_ptr<float>(),
                                       work.data_ptr<float>(), split, colmap, L.P, st));
 }
@@ -826,6 +866,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return pdrnn_lstm_small_step_ok((int)H, (int)NL, (int)B, (int)nb_fwd, (int)split_fwd, (int)nb_bwd,
                                     (int)split_bwd, gridb) != 0;
   }, "the fused training step runs forward + head/CE + BPTT as one launch for this shape");
+  m.def("lstm_small_step_deferred_dw", [](int64_t H, int64_t NL, int64_t T, int64_t B) {
+    // the fused step's default single-sequence backward (nb = 1, unit-group map)
+    const int split_bwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 1);
+    const int gridb = pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, 1, split_bwd);
+    const int mode = pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T);
+    return split_bwd == 1 && ((gridb < B && mode == 1) || mode == 2);
+  }, "the fused training step defers the weight gradients to the matrix-core dW kernel for this shape");
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });

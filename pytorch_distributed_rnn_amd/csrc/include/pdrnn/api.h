@@ -83,7 +83,51 @@ typedef struct {
   int B, T, I, NL;
   int cell;                  // 0 = LSTM, 1 = GRU (packed as a 4-row-block stack, see ops/gru.py)
   int x_bf16;                // x holds bf16 values (read once into LDS; requires the LDS-resident x path)
+  // Deferred weight gradients (pdrnn_lstm_small_bwd_dwout): the recurrence
+  // keeps no dW accumulators and writes the pre-activation gate gradients of
+  // (layer l, row b, step t) to dg_out + ((l*B + b)*T + t)*dg_st + [0, 4H)
+  // instead (dg_out may be `act` itself, dg_st = 5H: each lane overwrites the
+  // activation slot it has just consumed); pdrnn_lstm_small_dw then forms
+  // dW_ih, dW_hh and the biases on the matrix cores.
+  float* dg_out;
+  int64_t dg_st;
+  float* xg_out;             // DWOUT: [B*T][xg_ld] fp32 copy of the (gathered, widened) layer-0 input
+  int xg_ld;
 } PdrnnLstmSmallBwdArgs;
+
+// Weight gradients of the small-H stack from saved gate gradients, on the
+// fp32 matrix cores (lstm_small_dw.hip): for every layer l,
+//   dW_ih[l] = sum_{b,t} dg[l,b,t]^T in[l,b,t]     (in = x for l = 0, else h^{l-1}_t)
+//   dW_hh[l] = sum_{b,t} dg[l,b,t]^T h^l_{t-1}      (h_{-1} = 0)
+//   db[l]    = sum_{b,t} dg[l,b,t]                  (written to both bias slots)
+// split over `chunks` contiguous (b, t) row ranges: chunk c writes slab row c
+// (columns in the stack's flat parameter layout), reduced afterwards by
+// pdrnn_slab_reduce_adam.
+// Padding contract (the kernel streams whole 16-row stages without clamps):
+// hseq readable from row -1 of layer 0 (H floats before it) through 16 rows
+// past the last layer; dg and xg readable through 16 rows past their end.
+typedef struct {
+  const float* xg;           // layer-0 input rows [B*T][xg_ld] fp32 (the BPTT's xg_out), xg_ld = I rounded up to 4
+  int xg_ld;
+  const float* hseq;         // [NL, B, T, H] saved by the forward
+  const float* dg;           // gate gradients, (l,b,t) row at ((l*B+b)*T+t)*dg_st
+  int64_t dg_st;
+  float* slab;               // [chunks, P]
+  int64_t P;
+  int64_t off_wih[PDRNN_MAX_LAYERS], off_whh[PDRNN_MAX_LAYERS];
+  int64_t off_bih[PDRNN_MAX_LAYERS], off_bhh[PDRNN_MAX_LAYERS];
+  int B, T, I, NL, chunks;
+} PdrnnLstmSmallDwArgs;
+// 1 when the deferred-dW backward covers (H, NL, T) (H in {16, 32, 64}, T >= 4)
+int pdrnn_lstm_small_dwout_ok(int H, int NL, int T);
+// default chunk count (= slab rows) for a B x T batch
+int pdrnn_lstm_small_dw_chunks(int H, int NL, int B, int T);
+hipError_t pdrnn_lstm_small_dw(const PdrnnLstmSmallDwArgs* a, int H, hipStream_t stream);
+// BPTT of the lean fused-step contract with the weight gradients deferred to
+// pdrnn_lstm_small_dw (a->dg_out set, a->slab unused); grid <= 0: persistent
+// grid of the resident capacity (query with pdrnn_lstm_small_bwd_dwout_grid).
+hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int grid, hipStream_t stream);
+int pdrnn_lstm_small_bwd_dwout_grid(int H, int NL, int T, int B);
 
 // Query the launch geometry chosen for (H, B): returns grid size (number of slab rows).
 int pdrnn_lstm_small_grid(int H, int B, int nb);

@@ -29,6 +29,8 @@
 #include "pdrnn/api.h"
 #include "pdrnn/common.h"
 
+#include <cstring>
+
 namespace pdrnn {
 namespace {
 
@@ -56,9 +58,12 @@ constexpr bool kFwdBulkLds = PDRNN_FWD_BULK_LDS;
 // (columns >= I zero): only the I real columns are loaded (not H), 4 loads
 // in flight per thread, so the prologue is one memory round trip instead of
 // T*H/blockDim dependent ones.
+// xg (optional): the staged rows are also written, widened to fp32, to a
+// contiguous [T][I] image (the deferred-dW kernel's layer-0 operand: no
+// per-row gather or bf16 handling there).
 template <int H>
 __device__ __forceinline__ void stage_x(float* dst, const float* x, int64_t base, int64_t x_st, int T, int I,
-                                        int bf, bool valid) {
+                                        int bf, bool valid, float* xg = nullptr, int xg_ld = 0) {
   const int nthr = blockDim.x;
   for (int e = threadIdx.x; e < T * H; e += nthr) {
     const int k = e % H;
@@ -80,6 +85,7 @@ __device__ __forceinline__ void stage_x(float* dst, const float* x, int64_t base
       if (e < n) {
         const int t = e / I, k = e - t * I;
         dst[t * H + k] = v[r];
+        if (xg) xg[t * xg_ld + k] = v[r];
       }
     }
   }
@@ -844,12 +850,19 @@ __device__ __forceinline__ BwdCols<H, L> bwd_load_cols(const PdrnnLstmSmallBwdAr
   return w;
 }
 
-template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0>
+template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0, bool DWOUT = false>
 // xs_off >= 0: x already staged at smem + xs_off by the forward half of the
 // one-launch step (same layout, same workgroup): not loaded again.
 // wpre: the W columns, loaded by the caller ahead of time (one-launch step:
 // issued before the forward so their latency hides behind it).
 // dh_lds: the top layer's dh_T of this workgroup's (single) sequence in LDS.
+// DWOUT: no register-resident dW / db accumulators and no slab row; every
+// step's gate gradients go to a.dg_out instead (one 4-byte store per row lane,
+// overwriting the activation slot that lane has just consumed when dg_out ==
+// act) and lstm_small_dw.hip forms the weight gradients on the matrix cores.
+// The 64 accumulator VGPRs it frees raise the resident workgroups per CU
+// (B = 1440: three residency rounds become two), and the per-step rank-1
+// updates (~1/3 of a step's VALU issue) leave the recurrence's critical path.
 __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdArgs& a, int xs_off = -1,
                                                        const BwdCols<H, L>* wpre = nullptr,
                                                        const float* dh_lds = nullptr) {
@@ -953,7 +966,8 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
       if (xs_off < 0) {
 #pragma unroll
         for (int n = 0; n < NB; ++n)
-          stage_x<H>(xs + (int64_t)n * T * H, a.x, (int64_t)bsrc[n] * a.x_sb, a.x_st, T, I, a.x_bf16, true);
+          stage_x<H>(xs + (int64_t)n * T * H, a.x, (int64_t)bsrc[n] * a.x_sb, a.x_st, T, I, a.x_bf16, true,
+                     (DWOUT && valid[n]) ? a.xg_out + (int64_t)bs[n] * T * a.xg_ld : nullptr, a.xg_ld);
       }
     }
 
@@ -973,6 +987,14 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
                                       : a.hseq + ((int64_t)(layer > 0 ? layer - 1 : 0) * B + bs[n]) * T * H);
     }
     const bool has_dout = top && doutp != nullptr;
+    // deferred dW: this row's gate-gradient stream (same row layout as act)
+    __amdgpu_buffer_rsrc_t r_dg[NB];
+    uint32_t st_dg = 0;
+    if constexpr (DWOUT) {
+      st_dg = (uint32_t)a.dg_st * 4;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) r_dg[n] = uniform_rsrc(a.dg_out + ((int64_t)layer * B + bs[n]) * T * a.dg_st);
+    }
     const uint32_t vo_q = (q * H + u) * 4, vo_c = (4 * H + u) * 4, vo_u = u * 4;
     const uint32_t vo_x = (x_layer0 ? min(u, I - 1) : u) * 4;
     const uint32_t st_act = 5 * H * 4, st_h = H * 4;
@@ -1063,7 +1085,17 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
         dc[n] = active ? dcn : dc[n];
         if (L == 4 || rowlane) {
           dgbuf(n, layer, p)[q * H + u + ((q * H + u) / RS) * 4] = dgv;
-          db += valid[n] ? dgv : 0.f;
+          if constexpr (!DWOUT) db += valid[n] ? dgv : 0.f;
+        }
+        if constexpr (DWOUT) {
+          // branch-free: a step outside [0, T), an unused batch slot or a
+          // duplicate lane (L = 8) stores out of the buffer's range, which the
+          // hardware drops (a branch around it would make the loop's vmcnt
+          // waits conservative, see load_ops)
+          const bool st_ok = active && valid[n] && (L == 4 || rowlane);
+          const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)min(max(t, 0), T - 1) * st_dg);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dgv), r_dg[n],
+                                                st_ok ? vo_q : 0x80000000u, so, 0);
         }
       }
       if constexpr (PDRNN_ABLATE & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1101,7 +1133,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
           } else {
             sh[0] += g01; sx[1] += g23;
           }
-          if constexpr (!(PDRNN_ABLATE & 1)) {
+          if constexpr (!(PDRNN_ABLATE & 1) && !DWOUT) {
             dwhh[2 * r4] = __builtin_elementwise_fma(g01, hb, dwhh[2 * r4]);
             dwhh[2 * r4 + 1] = __builtin_elementwise_fma(g23, hb, dwhh[2 * r4 + 1]);
             dwih[2 * r4] = __builtin_elementwise_fma(g01, xb, dwih[2 * r4]);
@@ -1111,7 +1143,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
         // pin this step's dW updates here: they feed nothing until the
         // epilogue, and left free the scheduler sinks them into the next
         // step (keeping this step's gate-gradient slice live across it)
-        if constexpr (PDRNN_BWD_PIN_DW) {
+        if constexpr (PDRNN_BWD_PIN_DW && !DWOUT) {
 #pragma unroll
           for (int rr = 0; rr < RS / 2; ++rr) asm volatile("" : "+v"(dwhh[rr]), "+v"(dwih[rr]));
         }
@@ -1167,6 +1199,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
   }
 
   // ---------------- epilogue: this workgroup's partial dW / db ----------
+  if constexpr (DWOUT) return;
   float* slab = a.slab + (int64_t)blockIdx.x * a.P;
   {
     float* dst = slab + a.off_whh[layer] + (int64_t)r0 * H + u;
@@ -1193,6 +1226,12 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
 template <int H, int L, int NB, bool XLDS, bool LEAN, int CELL = 0>
 __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBwdArgs a) {
   lstm_small_bwd_gs_body<H, L, NB, XLDS, LEAN, CELL>(a);
+}
+
+// Lean BPTT with the weight gradients deferred to lstm_small_dw.hip.
+template <int H, int L, bool XLDS, int CELL>
+__global__ void __launch_bounds__(512) lstm_small_bwd_dwout_kernel(PdrnnLstmSmallBwdArgs a) {
+  lstm_small_bwd_gs_body<H, L, 1, XLDS, true, CELL, true>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1595,10 +1634,95 @@ hipError_t launch_step_gs(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBw
   return hipGetLastError();
 }
 
+// ---- deferred-dW backward (DWOUT) ----------------------------------------
+template <int H>
+constexpr int dwout_lanes() { return H >= 64 ? 8 : 4; }
+
+template <int H, bool XLDS, int CELL>
+int bwd_dwout_resident(int NL, size_t lds) {
+  constexpr int L = dwout_lanes<H>();
+  static thread_local int c_dev = -1, c_nl = -1, c_val = 0;
+  static thread_local size_t c_lds = 0;
+  int per_cu = 0, cus = 0, dev = 0;
+  hipGetDevice(&dev);
+  if (dev == c_dev && NL == c_nl && lds == c_lds) return c_val;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_small_bwd_dwout_kernel<H, L, XLDS, CELL>, NL * H * L, lds);
+  if (per_cu < 1) per_cu = 1;
+  if (cus < 1) cus = 1;
+  c_dev = dev; c_nl = NL; c_lds = lds; c_val = per_cu * cus;
+  return c_val;
+}
+
+template <int H>
+int bwd_dwout_grid(int NL, int T, int B, int cell) {
+  const size_t lds = bwd_gs_lds<H, 1>(NL), xbytes = bwd_gs_xbytes<H, 1>(T);
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  const int cap = cell == 1 ? (xl ? bwd_dwout_resident<H, true, 1>(NL, lds + xbytes)
+                                  : bwd_dwout_resident<H, false, 1>(NL, lds))
+                            : (xl ? bwd_dwout_resident<H, true, 0>(NL, lds + xbytes)
+                                  : bwd_dwout_resident<H, false, 0>(NL, lds));
+  return B < cap ? B : cap;
+}
+
+template <int H>
+hipError_t launch_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid) {
+  constexpr int L = dwout_lanes<H>();
+  if (a->NL * H * L > 512) return hipErrorInvalidConfiguration;
+  if (!bwd_lean(a) || !a->dg_out || a->dg_st < 4 * H) return hipErrorInvalidValue;
+  const int block = a->NL * H * L;
+  const size_t lds = bwd_gs_lds<H, 1>(a->NL), xbytes = bwd_gs_xbytes<H, 1>(a->T);
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  if (!xl || !a->xg_out) return hipErrorInvalidConfiguration;  // x staged once per sequence (writes xg_out)
+  if (grid <= 0) grid = bwd_dwout_grid<H>(a->NL, a->T, a->B, a->cell);
+  if (a->cell == 1) {
+    if (xl) hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, true, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+    else hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, false, 1>), dim3(grid), dim3(block), lds, st, *a);
+  } else {
+    if (xl) hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, true, 0>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+    else hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, false, 0>), dim3(grid), dim3(block), lds, st, *a);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 }  // namespace pdrnn
 
 extern "C" {
+
+// PDRNN_LSTM_DWOUT=0 disables the deferred-dW backward, =force selects it at
+// every batch size (tests: the one-launch step would otherwise take B <= one
+// residency round).  Returns 0 (not covered), 1 (covered), 2 (covered, forced).
+int pdrnn_lstm_small_dwout_ok(int H, int NL, int T) {
+  // read per call (one host query per training step): tests flip it in-process
+  const char* e = getenv("PDRNN_LSTM_DWOUT");
+  const int mode = !e ? 1 : (e[0] == '0' ? 0 : (strcmp(e, "force") == 0 ? 2 : 1));
+  if (mode == 0 || T < 4 || NL < 1 || NL > PDRNN_MAX_LAYERS) return 0;
+  if (H != 16 && H != 32 && H != 64) return 0;
+  if ((size_t)T * H * sizeof(float) > (size_t)pdrnn::kXldsBytes) return 0;  // LDS-resident x only
+  return NL * H * (H >= 64 ? 8 : 4) <= 512 ? mode : 0;
+}
+
+int pdrnn_lstm_small_bwd_dwout_grid(int H, int NL, int T, int B) {
+  // LSTM and GRU instantiations share the register budget (same VGPR class);
+  // the LSTM's is the one queried
+  switch (H) {
+    case 16: return pdrnn::bwd_dwout_grid<16>(NL, T, B, 0);
+    case 32: return pdrnn::bwd_dwout_grid<32>(NL, T, B, 0);
+    case 64: return pdrnn::bwd_dwout_grid<64>(NL, T, B, 0);
+    default: return -1;
+  }
+}
+
+hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int grid, hipStream_t stream) {
+  if (a->x_bf16 && (size_t)a->T * H * sizeof(float) > (size_t)pdrnn::kXldsBytes) return hipErrorInvalidConfiguration;
+  switch (H) {
+    case 16: return pdrnn::launch_bwd_dwout<16>(a, stream, grid);
+    case 32: return pdrnn::launch_bwd_dwout<32>(a, stream, grid);
+    case 64: return pdrnn::launch_bwd_dwout<64>(a, stream, grid);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 // 1 when the fused one-launch step covers (H, NL, B, launch config): the
 // gate-split forward with one sequence per workgroup, the L = 4 unit-group

@@ -129,8 +129,20 @@ class RcclComm final : public Comm {
     cv_.notify_all();
     if (watchdog_.joinable()) watchdog_.join();
     if (comm_ && !aborted_.load()) {
-      hipStreamSynchronize(stream_);
-      ncclCommDestroy(comm_);
+      // Teardown is where a dead peer usually shows up (an exception unwinds,
+      // reset_comms(), interpreter exit): a collective still pending would
+      // block hipStreamSynchronize / ncclCommDestroy for ever.  Drain with a
+      // deadline instead and abort the communicator if it passes.
+      const double limit = std::min(timeout_s_, env_double("PDRNN_COMM_TEARDOWN_S", 30.0));
+      std::string why;
+      if (drain(limit, why)) {
+        ncclCommDestroy(comm_);
+      } else {
+        std::fprintf(stderr, "[pdrnn] RCCL communicator (rank %d/%d) teardown: %s -- aborting instead of destroying\n",
+                     rank_, world_, why.c_str());
+        std::fflush(stderr);
+        ncclCommAbort(comm_);
+      }
     }
     for (auto& w : works_) hipEventDestroy(w.ev);
     for (auto ev : free_events_) hipEventDestroy(ev);
@@ -351,6 +363,41 @@ class RcclComm final : public Comm {
     }
     tracked_.fetch_add(1);
   }
+  // Destructor helper (watchdog already stopped): poll the comm stream and
+  // every still-tracked collective (inline ones run on compute streams) until
+  // all completed, an error shows up, or `limit_s` passes.
+  bool drain(double limit_s, std::string& why) {
+    const auto until = Clock::now() + std::chrono::duration<double>(limit_s);
+    for (int spins = 0;; ++spins) {
+      bool done = true;
+      const hipError_t qs = hipStreamQuery(stream_);
+      if (qs == hipErrorNotReady) done = false;
+      else if (qs != hipSuccess) { why = std::string("comm stream error: ") + hipGetErrorString(qs); return false; }
+      while (done && !works_.empty()) {
+        const hipError_t q = hipEventQuery(works_.front().ev);
+        if (q == hipErrorNotReady) { done = false; break; }
+        if (q != hipSuccess) { why = std::string("error on ") + works_.front().what + ": " + hipGetErrorString(q); return false; }
+        free_events_.push_back(works_.front().ev);
+        works_.pop_front();
+      }
+      if (done) return true;
+      if (comm_ != nullptr) {
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+          why = std::string("asynchronous RCCL error: ") + ncclGetErrorString(ae);
+          return false;
+        }
+      }
+      if (Clock::now() > until) {
+        char buf[160];
+        std::snprintf(buf, sizeof(buf), "collectives still pending after %.1f s", limit_s);
+        why = buf;
+        return false;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(spins < 64 ? 50 : 1000));
+    }
+  }
+
   // host-side wait that raises (instead of hanging) once the watchdog aborts
   void host_wait(hipStream_t st, const char* what) {
     hipEvent_t ev;

@@ -47,20 +47,27 @@ class ShardedSampler(torch.utils.data.Sampler):
     def set_epoch(self, epoch: int) -> None:
         self.epoch = epoch
 
-    def indices(self) -> List[int]:
+    def index_tensor(self) -> Tensor:
+        """This rank's indices of the current epoch as an int64 CPU tensor
+        (the same values as :meth:`indices`, built with tensor ops: no Python
+        list of N ints on the per-epoch path)."""
         if self.shuffle:
             g = torch.Generator()
             g.manual_seed(self.seed + self.epoch)
-            idx = torch.randperm(self.n, generator=g).tolist()
+            idx = torch.randperm(self.n, generator=g)
         else:
-            idx = list(range(self.n))
+            idx = torch.arange(self.n)
         if not self.drop_last:
-            pad = self.total_size - len(idx)
+            pad = self.total_size - idx.numel()
             if pad > 0:
-                idx += (idx * math.ceil(pad / len(idx)))[:pad]
+                reps = math.ceil(pad / idx.numel())
+                idx = torch.cat([idx, idx.repeat(reps)[:pad]])
         else:
             idx = idx[:self.total_size]
         return idx[self.rank:self.total_size:self.num_replicas]
+
+    def indices(self) -> List[int]:
+        return self.index_tensor().tolist()
 
     def __iter__(self) -> Iterator[int]:
         return iter(self.indices())
@@ -98,11 +105,27 @@ class DeviceBatchLoader:
         return math.ceil(self.num_items / self.batch_size)
 
     def batch_indices(self) -> List[Tensor]:
+        """This epoch's per-batch row indices, on the device.  The host
+        permutation goes through a persistent pinned staging buffer with an
+        asynchronous copy (a pageable-memory copy would be synchronous)."""
         if self.sampler is not None:
-            idx = torch.tensor(self.sampler.indices(), dtype=torch.long)
+            idx = self.sampler.index_tensor()
         else:
             idx = torch.arange(self.num_items)
-        idx = idx.to(self.device, non_blocking=True)
+        if self.device.type == "cuda":
+            stage = getattr(self, "_pinned", None)
+            if stage is None or stage.numel() < idx.numel():
+                stage = self._pinned = torch.empty(idx.numel(), dtype=torch.long, pin_memory=True)
+                self._pinned_ev = None
+            if self._pinned_ev is not None:
+                self._pinned_ev.synchronize()  # the previous epoch's copy out of the buffer is done
+            stage = stage[:idx.numel()]
+            stage.copy_(idx)
+            idx = stage.to(self.device, non_blocking=True)
+            self._pinned_ev = torch.cuda.Event()
+            self._pinned_ev.record()
+        else:
+            idx = idx.to(self.device)
         return list(torch.split(idx, self.batch_size))
 
     def make_batch(self, bidx: Tensor):

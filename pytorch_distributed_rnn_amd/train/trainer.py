@@ -196,6 +196,10 @@ class Trainer:
 
         for b in sizes:
             one_pass(b)
+        # the per-epoch index path (host permutation, pinned staging buffer,
+        # host->device copy): its first use allocates the staging buffer
+        if self.sampler is not None:
+            loader.batch_indices()
         # the epoch-end statistics read-back (first use of the copy / stack
         # kernels costs ~10 ms of code-object loading on a fresh process)
         ring = getattr(fused, "ring", None)

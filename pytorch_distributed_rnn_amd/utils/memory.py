@@ -51,9 +51,56 @@ class PeakRSSMonitor:
         return False
 
 
+def _read_hwm_mib() -> float:
+    with open("/proc/self/status", "rb") as f:
+        for line in f:
+            if line.startswith(b"VmHWM:"):
+                return int(line.split()[1]) / 1024.0
+    raise OSError("no VmHWM in /proc/self/status")
+
+
+class KernelPeakRSS:
+    """Peak RSS of a region from the kernel's own high-water mark: writing
+    ``5`` to ``/proc/self/clear_refs`` resets ``VmHWM`` to the current RSS, and
+    ``VmHWM`` read at the end is the exact peak in between -- no sampler
+    thread competing for the GIL with the training loop (a polling thread
+    also misses peaks shorter than its interval).  ``available()`` is False
+    where procfs does not allow it; ``measure_peak_rss`` then samples."""
+
+    @staticmethod
+    def available() -> bool:
+        try:
+            with open("/proc/self/clear_refs", "wb") as f:
+                f.write(b"5")
+            _read_hwm_mib()
+            return True
+        except OSError:
+            return False
+
+    def __enter__(self):
+        with open("/proc/self/clear_refs", "wb") as f:
+            f.write(b"5")
+        return self
+
+    def __exit__(self, *exc):
+        self.peak = _read_hwm_mib()
+        return False
+
+
+_HWM_OK = None
+
+
+def peak_rss_monitor(interval: float = 0.01):
+    """Context manager whose ``.peak`` (MiB) is the region's peak RSS."""
+    global _HWM_OK
+    if _HWM_OK is None:
+        _HWM_OK = os.environ.get("PDRNN_RSS_SAMPLER", "0") != "1" and KernelPeakRSS.available()
+    return KernelPeakRSS() if _HWM_OK else PeakRSSMonitor(interval)
+
+
 def measure_peak_rss(fn: Callable[[], Any], interval: float = 0.01) -> Tuple[float, Any]:
     """Run ``fn`` and return (peak RSS in MiB during the run, fn's result)."""
-    with PeakRSSMonitor(interval) as mon:
+    with peak_rss_monitor(interval) as mon:
         result = fn()
     return mon.peak, result
 

@@ -125,6 +125,113 @@ def test_fused_step_headline_batch_matches_autograd(nb, monkeypatch):
         assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
 
 
+@pytest.mark.parametrize("cell,hidden,layers,seq,features", [
+    ("lstm", 32, 2, 128, 9), ("lstm", 16, 1, 37, 9), ("lstm", 32, 3, 21, 5),
+    ("lstm", 16, 2, 6, 16), ("gru", 32, 2, 128, 9), ("gru", 16, 2, 9, 3)])
+def test_deferred_dw_backward_matches_autograd(cell, hidden, layers, seq, features, monkeypatch):
+    """The BPTT with the weight gradients deferred to the matrix-core kernel
+    (lstm_small_dw.hip) -- forced at B = 96 so that every shape runs it; 382
+    samples leave a last batch of 94 (with odd T: B*T not a multiple of the
+    4-row MFMA step), T from 6 to 128, chunks straddling sequences, 3..16
+    input features (x tiles masked)."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.setenv("PDRNN_LSTM_DWOUT", "force")
+    assert _ext.native(torch.device("cuda")).lstm_small_step_deferred_dw(hidden, layers, seq, 96)
+    torch.manual_seed(3)
+    train, _, _ = synthetic_motion(n_train=382, n_validation=2, n_test=2, seq_length=seq, num_features=features,
+                                   seed=6)
+    m1 = MotionModel(features, hidden, layers, 6, cell=cell)
+    m2 = copy.deepcopy(m1)
+    t1, t2 = _trainer(m1, train, True), _trainer(m2, train, False)
+    if t1._fused_step() is None:
+        pytest.skip("fused step does not cover this shape")
+    for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
+        s1, _ = t1.train_batch(x1)
+        s2, _ = t2.train_batch(x2)
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+        assert int(s1[2]) == int(s2[2])
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
+
+
+def _fused_grads(model, train, B):
+    """Gradients of one fused step (no optimizer update) on the first batch."""
+    from pytorch_distributed_rnn_amd.ops.lstm import fused_bwd_nb, small_launch_config
+    from pytorch_distributed_rnn_amd.train.trainer import Trainer
+    t = Trainer(model, train, batch_size=B, learning_rate=2.5e-3, device=torch.device("cuda"))
+    f = t._fused_step()
+    assert f is not None
+    feats, labels, idx = t.train_loader.make_batch(t.train_loader.batch_indices()[0])
+    nb_f, sp_f, _, _ = small_launch_config(idx.numel(), f.H, f.NL)
+    ws = f.weights
+    if f.gru:
+        from pytorch_distributed_rnn_amd.ops.gru_fused import _pack
+        ws = _pack(f.weights, f.NL, f.H, f.flat.data)
+        nb_f, sp_f = 1, 1
+    f.flat.attach_grads()
+    stats = torch.zeros(3, device="cuda")
+    f.mod.lstm_head_train_step(feats, idx, labels, ws, f.m.fc.weight, f.m.fc.bias, f.flat.grad, stats, f.H, f.NL,
+                               sp_f, 0, nb_f, fused_bwd_nb(idx.numel(), f.H, f.NL), None, None,
+                               1 if f.gru else 0, f.colmap)
+    return [p.grad.detach().double() for p in f.m.parameters()], feats.index_select(0, idx), \
+        labels.index_select(0, idx).reshape(-1)
+
+
+@pytest.mark.parametrize("cell,hidden,layers,seq", [("lstm", 64, 1, 16), ("lstm", 32, 2, 128), ("gru", 64, 1, 12)])
+def test_deferred_dw_gradients_match_fp64(cell, hidden, layers, seq, monkeypatch):
+    """Gradients of the deferred-dW step (before Adam) against fp64 autograd:
+    max error <= 2e-6 of each parameter's largest gradient (the Adam-trajectory
+    test above cannot take H = 64 at T = 16: Adam's first step is sign(g) * lr,
+    so elements whose gradient is at rounding level flip either way)."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.setenv("PDRNN_LSTM_DWOUT", "force")
+    torch.manual_seed(3)
+    train, _, _ = synthetic_motion(n_train=190, n_validation=2, n_test=2, seq_length=seq, seed=6)
+    m0 = MotionModel(9, hidden, layers, 6, cell=cell)
+    grads, x, y = _fused_grads(copy.deepcopy(m0), train, 95)
+    ref = copy.deepcopy(m0).cuda().double()
+    torch.nn.functional.cross_entropy(ref(x.double()), y).backward()
+    for (k, r), g in zip(ref.named_parameters(), grads):
+        scale = r.grad.abs().max().item()
+        assert (g - r.grad).abs().max().item() <= 2e-6 * scale + 1e-12, k
+
+
+def test_deferred_dw_selected_above_one_round(monkeypatch):
+    """Default selection: the headline B = 1440 (three residency rounds of the
+    register-dW backward) takes the deferred-dW path, the 8-GPU per-rank batch
+    (180, one round) keeps the one-launch step."""
+    from pytorch_distributed_rnn_amd import _ext
+    monkeypatch.delenv("PDRNN_LSTM_DWOUT", raising=False)
+    mod = _ext.native(torch.device("cuda", 0))
+    assert mod.lstm_small_step_deferred_dw(32, 2, 128, 1440)
+    assert not mod.lstm_small_step_deferred_dw(32, 2, 128, 180)
+    monkeypatch.setenv("PDRNN_LSTM_DWOUT", "0")
+    assert not mod.lstm_small_step_deferred_dw(32, 2, 128, 1440)
+
+
+def test_deferred_dw_bf16_inputs_match_autograd(monkeypatch):
+    """bf16 inputs (BASELINE config 2) through the deferred-dW backward: the dW
+    kernel widens the gathered bf16 x rows itself."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.setenv("PDRNN_LSTM_DWOUT", "force")
+    torch.manual_seed(0)
+    train, _, _ = synthetic_motion(n_train=384, n_validation=2, n_test=2, seed=3)
+    m1 = MotionModel(9, 32, 1, 6, compute_dtype=torch.bfloat16)
+    m2 = copy.deepcopy(m1)
+    t1, t2 = _trainer(m1, train, True), _trainer(m2, train, False)
+    assert t1._fused_step() is not None and t1.train_loader.features.dtype == torch.bfloat16
+    for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
+        s1, _ = t1.train_batch(x1)
+        s2, _ = t2.train_batch(x2)
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
+
+
 def test_local_trainer_epoch_on_gpu(tmp_path):
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
