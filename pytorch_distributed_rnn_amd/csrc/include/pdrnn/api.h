@@ -88,7 +88,8 @@ typedef struct {
   // (layer l, row b, step t) to dg_out + ((l*B + b)*T + t)*dg_st + [0, 4H)
   // instead (dg_out may be `act` itself, dg_st = 5H: each lane overwrites the
   // activation slot it has just consumed); pdrnn_lstm_small_dw then forms
-  // dW_ih, dW_hh and the biases on the matrix cores.
+  // dW_ih, dW_hh and the biases on the matrix cores.  dg_out must have 16
+  // padding rows behind the last layer (the kernel zeroes them).
   float* dg_out;
   int64_t dg_st;
   float* xg_out;             // DWOUT: [B*T][xg_ld] fp32 copy of the (gathered, widened) layer-0 input

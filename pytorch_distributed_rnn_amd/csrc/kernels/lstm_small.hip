@@ -1199,7 +1199,16 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
   }
 
   // ---------------- epilogue: this workgroup's partial dW / db ----------
-  if constexpr (DWOUT) return;
+  if constexpr (DWOUT) {
+    // the dW kernel streams whole 16-row stages: the 16 padding rows behind
+    // the last layer's gate gradients must hold finite values (masked
+    // operands are multiplied by zero there, and NaN * 0 = NaN)
+    if (blockIdx.x == 0) {
+      float* pad = a.dg_out + (int64_t)NL * B * T * a.dg_st;
+      for (int e = threadIdx.x; e < 16 * a.dg_st; e += blockDim.x) pad[e] = 0.f;
+    }
+    return;
+  }
   float* slab = a.slab + (int64_t)blockIdx.x * a.P;
   {
     float* dst = slab + a.off_whh[layer] + (int64_t)r0 * H + u;

@@ -64,6 +64,18 @@ def _comm():
     return get_comm(None)
 
 
+def comm():
+    """The native communicator Horovod mode runs on (the default group's)."""
+    return _comm()
+
+
+def _skip_world1() -> bool:
+    # one rank: an in-place reduction is the identity -- unless
+    # PDRNN_FORCE_COLLECTIVE=1 keeps it (the communicator then really issues
+    # it: tests of the comm-stream hop and its graph capture on one GPU)
+    return size() == 1 and os.environ.get("PDRNN_FORCE_COLLECTIVE", "0") != "1"
+
+
 def _tensors_of(params) -> List[Tuple[str, torch.Tensor]]:
     if isinstance(params, dict):
         return list(params.items())
@@ -116,7 +128,7 @@ def allreduce_(tensor: torch.Tensor, average: Optional[bool] = None, name: Optio
                op: Optional[str] = None) -> torch.Tensor:
     if op is None:
         op = Average if average in (None, True) else Sum
-    if size() == 1:
+    if _skip_world1():
         return tensor
     comm = _comm()
     if op == Average and not comm.native_avg:

@@ -96,6 +96,9 @@ class DDPTrainer(DistributedTrainer):
             return None
         return reducer.all_reduce_inline
 
+    def _grad_comm(self):
+        return self.model.comm
+
     @staticmethod
     def _device() -> torch.device:
         if torch.cuda.is_available() and torch.distributed.get_backend() == "nccl":
@@ -125,12 +128,15 @@ class HorovodTrainer(DistributedTrainer):
         return hvd.DistributedOptimizer(optimizer, named_parameters=model.named_parameters())
 
     def _grad_sync(self):
-        if self._world_size == 1:
+        if self._world_size == 1 and os.environ.get("PDRNN_FORCE_GRAD_SYNC", "0") != "1":
             return None
         flat = next(iter(getattr(self.model, "_pdrnn_flat").values()))
         # the fused step bypasses the per-tensor hooks: one fused all-reduce of
         # the whole flat gradient (= Horovod's fusion buffer holding every tensor)
         return lambda: hvd.allreduce_(flat.grad, average=True)
+
+    def _grad_comm(self):
+        return hvd.comm() if self._world_size > 1 or os.environ.get("PDRNN_FORCE_GRAD_SYNC", "0") == "1" else None
 
     def train(self, epochs: int):
         hvd.broadcast_parameters(self.model.state_dict(), root_rank=0)

@@ -92,11 +92,15 @@ class MotionTrainStep:
     RING = 16384
 
     def __init__(self, model: nn.Module, optimizer, grad_sync: Optional[Callable[[], None]] = None,
-                 cuda_graph: Optional[bool] = None):
+                 cuda_graph: Optional[bool] = None, comm=None):
         self.model = model
         self.m = _inner(model)
         self.optimizer = optimizer
         self.grad_sync = grad_sync
+        # the communicator grad_sync runs on: a graph replay (whose captured
+        # collectives carry no completion event) is registered with ITS
+        # watchdog as one unit.  Default: the DDP wrapper's communicator.
+        self.comm = comm if comm is not None else getattr(model, "comm", None)
         self.mod = _ext.native(next(self.m.parameters()).device)
         lstm = self.m.lstm
         self.H, self.NL = lstm.hidden_size, lstm.num_layers
@@ -298,9 +302,8 @@ class MotionTrainStep:
         ent["idx"].copy_(idx, non_blocking=True)
         with trace_range("pdrnn.graph_step"):
             ent["graph"].replay()
-        comm = getattr(self.model, "comm", None)
-        if comm is not None and hasattr(comm, "track_current"):
-            comm.track_current()  # the communicator's watchdog bounds the replay
+        if self.comm is not None and hasattr(self.comm, "track_current"):
+            self.comm.track_current()  # the communicator's watchdog bounds the replay
         ent["step_host"] = step
         # the graph wrote the statistics into ring row (step - 1 + slot_off):
         # the row assigned to this step whenever the host's ring slot and step

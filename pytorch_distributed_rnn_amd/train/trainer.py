@@ -230,6 +230,11 @@ class Trainer:
         """Gradient synchronisation used by the fused step (None: local)."""
         return None
 
+    def _grad_comm(self):
+        """The communicator ``_grad_sync`` runs on (its watchdog bounds the
+        fused step's graph replays); None: local."""
+        return None
+
     def _fused_step(self):
         if getattr(self, "_fused", False) is not False:
             return self._fused
@@ -238,7 +243,7 @@ class Trainer:
             from . import fused_step
             if fused_step.supported(self.model, self.optimizer, self.device):
                 self._fused = fused_step.MotionTrainStep(self.model, self.optimizer, self._grad_sync(),
-                                                         cuda_graph=self.cuda_graph)
+                                                         cuda_graph=self.cuda_graph, comm=self._grad_comm())
         return self._fused
 
     def train_batch(self, batch) -> Tuple[Tensor, int]:

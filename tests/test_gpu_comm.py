@@ -182,6 +182,49 @@ def test_graph_replayed_rccl_step_matches_local(rccl_group):
     assert o1.state_dict()["state"][0]["step"] == o2.state_dict()["state"][0]["step"]
 
 
+def test_graph_replayed_horovod_step_matches_local(rccl_group):
+    """Horovod mode on the graph path: the synced step's gradient sync is
+    ``hvd.allreduce_`` -- a hop to the communicator's own stream (event
+    record/wait, recordStream) -- and that hop is captured INSIDE the HIP
+    graph with the fused kernels and the Adam launch.  Replays with fresh
+    batch indices must equal the eager local step, and every replay is
+    registered with the Horovod communicator's watchdog (not a DDP wrapper's:
+    the Horovod model is unwrapped)."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    from pytorch_distributed_rnn_amd.parallel import horovod as hvd
+    from pytorch_distributed_rnn_amd.train.fused_step import MotionTrainStep
+    from pytorch_distributed_rnn_amd.utils.flat import flatten_module
+    torch.manual_seed(4)
+    train, _, _ = synthetic_motion(n_train=512, n_validation=1, n_test=1, seed=4)
+    feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
+    m1 = MotionModel(9, 32, 2, 6).cuda()
+    m2 = copy.deepcopy(m1)
+    flatten_module(m1)
+    flatten_module(m2)
+    o1 = hvd.DistributedOptimizer(FusedAdam(m1.parameters(), lr=2.5e-3), named_parameters=m1.named_parameters())
+    o2 = FusedAdam(m2.parameters(), lr=2.5e-3)
+    flat1 = next(iter(m1._pdrnn_flat.values()))
+    comm = hvd.comm()
+    s1 = MotionTrainStep(m1, o1, lambda: hvd.allreduce_(flat1.grad, average=True), cuda_graph=True, comm=comm)
+    s2 = MotionTrainStep(m2, o2, None)
+    assert s1.comm is comm
+    g = torch.Generator().manual_seed(1)
+    n0 = comm.tracked
+    outs = []
+    for _ in range(6):
+        idx = torch.randperm(512, generator=g)[:64].cuda()
+        outs.append((s1(feats, labels, idx).clone(), s2(feats, labels, idx).clone()))
+    assert s1._graph is not None, "the Horovod synced step was never captured"
+    # 2 eager steps (their all-reduce tracked) + 4 replays (tracked as a whole)
+    assert comm.tracked - n0 == 6
+    for a, b in outs:
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+
+
 def test_ddp_autograd_hooks_rccl(rccl_group):
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
