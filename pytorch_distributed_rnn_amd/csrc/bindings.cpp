@@ -5,6 +5,7 @@
 // launches on torch's current HIP stream.  All math lives in csrc/kernels.
 #include <torch/extension.h>
 #include <cstdio>
+#include <map>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 
@@ -22,18 +23,39 @@ bool stamps_enabled() {
   return on;
 }
 void report_stamps(const char* what, const Tensor& st, int iters) {
+  // [grid, 8]: loop start / end shader cycles, loop start / end real time,
+  // workgroup entry / exit real time (100 MHz; entry/exit 0 when not stamped)
   auto h = st.cpu();
   const int64_t g = h.size(0);
   auto p = h.data_ptr<int64_t>();
-  double cyc = 0, real = 0;
+  double cyc = 0, real = 0, pro = 0, epi = 0;
+  int64_t in_min = INT64_MAX, in_max = 0, out_min = INT64_MAX, out_max = 0;
   for (int64_t i = 0; i < g; ++i) {
-    cyc += (double)(p[i * 4 + 1] - p[i * 4 + 0]);
-    real += (double)(p[i * 4 + 3] - p[i * 4 + 2]);
+    const int64_t* r = p + i * 8;
+    cyc += (double)(r[1] - r[0]);
+    real += (double)(r[3] - r[2]);
+    if (r[4] && r[5]) {
+      pro += (double)(r[2] - r[4]);
+      epi += (double)(r[5] - r[3]);
+      in_min = std::min(in_min, r[4]); in_max = std::max(in_max, r[4]);
+      out_min = std::min(out_min, r[5]); out_max = std::max(out_max, r[5]);
+    }
   }
-  cyc /= g; real /= g;
+  cyc /= g; real /= g; pro /= g; epi /= g;
   const double us = real / 100.0;  // s_memrealtime ticks at 100 MHz
-  fprintf(stderr, "[stamps] %s grid=%lld iters=%d loop=%.1f us cycles=%.0f clock=%.2f GHz cyc/iter=%.0f\n", what,
+  fprintf(stderr, "[stamps] %s grid=%lld iters=%d loop=%.1f us cycles=%.0f clock=%.2f GHz cyc/iter=%.0f", what,
           (long long)g, iters, us, cyc, cyc / (us * 1e3), cyc / iters);
+  if (in_max) {
+    fprintf(stderr, " | prologue=%.1f us epilogue=%.1f us entry spread=%.1f us exit spread=%.1f us span=%.1f us",
+            pro / 100.0, epi / 100.0, (in_max - in_min) / 100.0, (out_max - out_min) / 100.0,
+            (out_max - in_min) / 100.0);
+    std::map<int64_t, int> per_cu;  // placement census: workgroups per CU
+    for (int64_t i = 0; i < g; ++i) per_cu[p[i * 8 + 6]]++;
+    int lo = INT32_MAX, hi = 0;
+    for (auto& kv : per_cu) { lo = std::min(lo, kv.second); hi = std::max(hi, kv.second); }
+    fprintf(stderr, " | CUs used=%zu workgroups/CU min=%d max=%d", per_cu.size(), lo, hi);
+  }
+  fprintf(stderr, "\n");
 }
 using c10::optional;
 
@@ -175,7 +197,7 @@ std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx,
   if (split <= 0) split = pdrnn_lstm_small_max_split((int)H, (int)NL, 0);
   Tensor stamps;
   if (stamps_enabled()) {
-    stamps = at::zeros({(B + nb - 1) / nb, 4}, opts.dtype(at::kLong));
+    stamps = at::zeros({(B + nb - 1) / nb, 8}, opts.dtype(at::kLong));
     a.stamps = reinterpret_cast<uint64_t*>(stamps.data_ptr<int64_t>());
   }
   if (B > 0 && T > 0)
@@ -263,7 +285,7 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
   if (B > 0 && T > 0) {
     Tensor stamps;
     if (stamps_enabled()) {
-      stamps = at::zeros({grid, 4}, opts.dtype(at::kLong));
+      stamps = at::zeros({grid, 8}, opts.dtype(at::kLong));
       a.stamps = reinterpret_cast<uint64_t*>(stamps.data_ptr<int64_t>());
     }
     HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&a, (int)H, (int)nb, (int)split, grid, cur_stream()));
@@ -347,13 +369,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   TORCH_CHECK((split_fwd == 1 || split_fwd == 2) && split_bwd == 1,
               "fused train step runs on the gate-split or 2-lane K-split forward and the unit-group backward");
   if (nb_fwd <= 0) nb_fwd = 1;
-  if (nb_bwd <= 0) nb_bwd = 1;
-  // nb_bwd >= 2: the throughput backward (several sequences per workgroup,
-  // operands DMA-staged through LDS; lstm_small_tp.hip) when it covers the shape
-  const bool tp = nb_bwd >= 2 && pdrnn_lstm_small_bwd_tp_ok((int)H, (int)NL, (int)T, (int)I, (int)B, (int)nb_bwd);
-  if (!tp && cell == 1) nb_bwd = 1;  // the GRU latency backward is single-sequence
-  const int gridb = tp ? pdrnn_lstm_small_bwd_tp_grid((int)H, (int)NL, (int)T, (int)I, (int)B, (int)nb_bwd, (int)cell)
-                       : pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb_bwd, (int)split_bwd);
+  if (nb_bwd <= 0 || cell == 1) nb_bwd = 1;  // the GRU backward is single-sequence
+  const int gridb = pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb_bwd, (int)split_bwd);
   TORCH_CHECK(gridb > 0, "unsupported backward tile nb=", nb_bwd);
   // Above one residency round the BPTT defers its weight gradients: the
   // recurrence writes the gate gradients (into `act`, in place) and the
@@ -361,7 +378,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   // row per K chunk (see pdrnn_lstm_small_bwd_dwout).  One round or less keeps
   // the one-launch step (register-resident dW, no extra launch).
   const int dw_mode = pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T);
-  const bool dwout = !tp && nb_bwd == 1 && split_bwd == 1 && ((gridb < B && dw_mode == 1) || dw_mode == 2);
+  const bool dwout = nb_bwd == 1 && split_bwd == 1 && ((gridb < B && dw_mode == 1) || dw_mode == 2);
   const int slab_rows = dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
   Tensor slab = at::empty({slab_rows, L.P}, opts);
 
@@ -389,13 +406,13 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   hipStream_t st = cur_stream();
   Tensor st_f, st_b;
   if (stamps_enabled()) {
-    st_f = at::zeros({(B + nb_fwd - 1) / nb_fwd, 4}, opts.dtype(at::kLong));
-    st_b = at::zeros({gridb, 4}, opts.dtype(at::kLong));
+    st_f = at::zeros({(B + nb_fwd - 1) / nb_fwd, 8}, opts.dtype(at::kLong));
+    st_b = at::zeros({gridb, 8}, opts.dtype(at::kLong));
     f.stamps = reinterpret_cast<uint64_t*>(st_f.data_ptr<int64_t>());
   }
   // latency regime (one sequence per workgroup in both passes): forward,
   // head/CE and BPTT in one launch; otherwise the forward launches here
-  const bool one_launch = !tp && !dwout && !st_f.defined() &&
+  const bool one_launch = !dwout && !st_f.defined() &&
       pdrnn_lstm_small_step_ok((int)H, (int)NL, (int)B, (int)nb_fwd, (int)split_fwd, (int)nb_bwd, (int)split_bwd,
                                gridb) == 1;
   if (!one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
@@ -417,7 +434,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     grid_dw = pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B);
     TORCH_CHECK(grid_dw > 0, "deferred-dW backward: no resident grid");
     if (st_f.defined()) {
-      st_b = at::zeros({grid_dw, 4}, opts.dtype(at::kLong));
+      st_b = at::zeros({grid_dw, 8}, opts.dtype(at::kLong));
       bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
     }
     bk.dg_out = f.act;  // in place: each row lane overwrites the activation it has consumed
@@ -429,7 +446,6 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   }
   if (st_b.defined()) bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
   if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
-  else if (tp) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_tp(&bk, (int)H, (int)nb_bwd, gridb, st));
   else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, st));
   else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
   if (dwout) {
@@ -853,9 +869,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_small_max_split", [](int64_t H, int64_t NL, bool backward) {
     return pdrnn_lstm_small_max_split((int)H, (int)NL, backward ? 1 : 0);
   });
-  m.def("lstm_small_bwd_tp_ok", [](int64_t H, int64_t NL, int64_t T, int64_t I, int64_t B, int64_t nb) {
-    return pdrnn_lstm_small_bwd_tp_ok((int)H, (int)NL, (int)T, (int)I, (int)B, (int)nb) != 0;
-  }, "the throughput (multi-sequence) fused-step backward covers this shape");
   m.def("lstm_small_step_one_launch", [](int64_t H, int64_t NL, int64_t T, int64_t B, int64_t nb_fwd,
                                          int64_t split_fwd, int64_t nb_bwd, int64_t split_bwd) {
     if (split_fwd <= 0) split_fwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 0);

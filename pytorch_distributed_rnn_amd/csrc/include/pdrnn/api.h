@@ -147,12 +147,6 @@ int pdrnn_lstm_small_step_ok(int H, int NL, int B, int nb_fwd, int split_fwd, in
                              int gridb);
 hipError_t pdrnn_lstm_small_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBwdArgs* b, int H,
                                  hipStream_t stream);
-// Throughput backward for the fused training step (lean contract: zero initial
-// state, loss through the top layer's h_T only; H in {16, 32}, NL <= 2,
-// nb in 2..4 sequences per workgroup; lstm_small_tp.hip).
-int pdrnn_lstm_small_bwd_tp_ok(int H, int NL, int T, int I, int B, int nb);
-int pdrnn_lstm_small_bwd_tp_grid(int H, int NL, int T, int I, int B, int nb, int cell);
-hipError_t pdrnn_lstm_small_bwd_tp(const PdrnnLstmSmallBwdArgs* a, int H, int nb, int grid, hipStream_t stream);
 
 // Column sums of a [rows, P] fp32 slab into out[P] (out = beta*out + sum).
 // Two deterministic passes through `work` ([split, P] floats, split <= 64).

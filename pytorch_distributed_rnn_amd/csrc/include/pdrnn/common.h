@@ -108,6 +108,13 @@ PDRNN_DEVICE float opaque_copy(float v) {
 // Diagnostic cycle stamps (shader clock and 100 MHz real-time clock).
 PDRNN_DEVICE uint64_t stamp_cycles() { return __builtin_amdgcn_s_memtime(); }
 PDRNN_DEVICE uint64_t stamp_real() { return __builtin_amdgcn_s_memrealtime(); }
+// Which CU runs this wave (diagnostics: workgroup placement census): XCC id
+// << 16 | the SE / SH / CU fields of HW_ID (bits 8..14).
+PDRNN_DEVICE uint32_t stamp_cu() {
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+  return ((xcc & 0xF) << 16) | ((hw >> 8) & 0x7F);
+}
 
 // bf16 <-> f32 (round to nearest even; NaN preserved by the hardware cvt).
 PDRNN_DEVICE float bf16_to_f32(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
@@ -119,7 +126,7 @@ PDRNN_DEVICE uint16_t f32_to_bf16(float f) {
 }
 
 // ---------------------------------------------------------------------------
-// Shared by the small-H recurrent kernels (lstm_small.hip, lstm_small_tp.hip)
+// Shared by the small-H recurrent kernels (lstm_small.hip, lstm_small_dw.hip)
 // ---------------------------------------------------------------------------
 // Buffer descriptor for a wave-uniform base pointer: the halves go through
 // readfirstlane so the compiler can keep the descriptor in SGPRs (no

@@ -161,34 +161,43 @@ __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
   const int ci = tid % cw, rg = tid / cw;
   const int64_t col = inA ? (int64_t)blockIdx.x * 64 + ci : (int64_t)(blockIdx.x - nblkA) * 16 + ci;
   const bool live = col < (inA ? PA : PB);
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t p = inA ? col : PA + col;  // flat index: [A columns | B columns]
+  // the Adam operands of this column first: their latency hides behind the
+  // slab reads instead of adding a dependent round trip after the reduction
+  const bool adam = a.param && tid < cw && live && p < n_out;
+  float pv = 0.f, m = 0.f, v = 0.f;
+  if (adam) { pv = a.param[p]; m = a.exp_avg[p]; v = a.exp_avg_sq[p]; }
+  // 16 loads in flight per thread (a column's rows split over nrg groups)
+  float acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
   if (live) {
     const float* src = inA ? A + (colmap ? colmap[col] : col) : Bs + col;
     const int64_t ld = inA ? ldA : PB;
     const int64_t rows = inA ? rowsA : rowsB;
     const int64_t r0 = rows * rg / nrg, r1 = rows * (rg + 1) / nrg;
     int64_t r = r0;
-    for (; r + 8 <= r1; r += 8) {
+    for (; r + 16 <= r1; r += 16) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += src[(r + k) * ld];
+      for (int k = 0; k < 16; ++k) acc[k] += src[(r + k) * ld];
     }
     for (int k = 0; r < r1; ++r, ++k) acc[k] += src[r * ld];
   }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] += acc[k + 8];
   red[tid] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (tid >= cw || !live) return;
   float g = 0.f;
   for (int k = 0; k < nrg; ++k) g += red[k * cw + tid];
-  const int64_t p = inA ? col : PA + col;  // flat index: [A columns | B columns]
   if (p < n_out) {
     grad_out[p] = g;
-    if (a.param) {
+    if (adam) {
       AdamScalars s;
       s.lr = a.lr; s.b1 = a.beta1; s.b2 = a.beta2; s.eps = a.eps; s.wd = a.weight_decay;
       s.bc1 = a.bias_correction1; s.bc2_sqrt = a.bias_correction2_sqrt;
       s.gscale = a.grad_scale; s.decoupled = a.decoupled; s.maximize = a.maximize;
       s.amsgrad = 0;
-      float pv = a.param[p], m = a.exp_avg[p], v = a.exp_avg_sq[p];
       adam_elem(pv, g, m, v, nullptr, s);
       a.param[p] = pv; a.exp_avg[p] = m; a.exp_avg_sq[p] = v;
     }

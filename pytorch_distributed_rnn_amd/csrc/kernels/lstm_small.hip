@@ -182,6 +182,8 @@ __device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a
   }
 }
 
+constexpr float kNegLog2eK = -1.4426950408889634f;
+
 template <int H, int S, int NB, bool SAVE, bool XLDS, bool HEAD = false>
 __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   constexpr int K = 2 * H;
@@ -192,6 +194,7 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
 
   const int NL = a.NL, B = a.B, T = a.T, I = a.I;
   const int tid = threadIdx.x;
+  const uint64_t sr_in = (a.stamps && tid == 0) ? stamp_real() : 0;
   const int layer = __builtin_amdgcn_readfirstlane(tid / LANES);
   const int lg = tid - layer * LANES;
   const int u = lg / S;
@@ -212,17 +215,43 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
     const float* src = in_part ? a.w_ih[layer] : a.w_hh[layer];
     const int ld = in_part ? Iin : H;
     const int c0 = in_part ? k0 : k0 - H;
+    // float4 row loads where the slice is aligned (every h part, the input
+    // part of layers >= 1): each lane reads a different row, so every load
+    // instruction touches 64 cache lines -- 4x fewer instructions matter at
+    // B = 1440, where all workgroups load the weights at once (the prologue
+    // was ~27 us with scalar loads)
+    const bool vec = (ld % 4) == 0 && (!in_part || Iin == H);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = q * H + u;
+      if (vec) {
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int c = c0 + kk;
-        const bool live = !in_part || c < Iin;
-        const float v = src[r * ld + (live ? c : 0)];
-        w[q][kk] = live ? v : 0.f;
+        for (int k4 = 0; k4 < KS / 4; ++k4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + r * ld + c0 + 4 * k4);
+          w[q][4 * k4 + 0] = v.x; w[q][4 * k4 + 1] = v.y; w[q][4 * k4 + 2] = v.z; w[q][4 * k4 + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const int c = c0 + kk;
+          const bool live = !in_part || c < Iin;
+          const float v = src[r * ld + (live ? c : 0)];
+          w[q][kk] = live ? v : 0.f;
+        }
       }
       bias[q] = (a.b_ih[layer] ? a.b_ih[layer][r] : 0.f) + (a.b_hh[layer] ? a.b_hh[layer][r] : 0.f);
+    }
+    if constexpr (S == 2) {
+      // pre-scaled rows (as in the gate-split map): the pre-activation comes
+      // out as -log2(e) z (x2 for the g gate), so sigmoid = 1 / (1 + 2^acc)
+      // and tanh(g) = 2 sigmoid(2g) - 1 with no scaling in the recurrence
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float sc = kNegLog2eK * (q == 2 ? 2.f : 1.f);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) w[q][kk] *= sc;
+        bias[q] *= sc;
+      }
     }
   }
 
@@ -281,6 +310,35 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = group_sum<S>(acc[q]) + bias[q];
+        if constexpr (S == 2 && NB == 1 && SAVE) {
+          // the unit's two lanes split the activations (lane 0: i, g; lane
+          // 1: f, o; one DPP swap exchanges them) and the stores: every lane
+          // writes one LDS slot and three global words, no branches
+          const float z0 = s == 0 ? acc[0] : acc[1];
+          const float z1 = s == 0 ? acc[2] : acc[3];
+          const float a0 = fast_rcp(1.f + __builtin_amdgcn_exp2f(z0));               // i | f
+          const float s1 = fast_rcp(1.f + __builtin_amdgcn_exp2f(z1));
+          const float a1 = s == 0 ? fmaf(s1, 2.f, -1.f) : s1;                         // g | o
+          const float b0 = dpp_swap1(a0), b1 = dpp_swap1(a1);
+          const float ig = s == 0 ? a0 : b0, fg = s == 0 ? b0 : a0;
+          const float gg = s == 0 ? a1 : b1, og = s == 0 ? b1 : a1;
+          const float cn = fmaf(fg, c[n], ig * gg);
+          const float th = fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(cn * (2.f * kNegLog2eK))), 2.f, -1.f);
+          const float h = og * th;
+          c[n] = cn;
+          hl[n] = h;
+          // lane 0: own-h slot of the next step; lane 1: the next layer's
+          // input slot (top layer: its own slot again, same value)
+          float* hslot = (s == 0 || layer == NL - 1) ? vin(n, layer, p ^ 1) + H + u : vin(n, layer + 1, p) + u;
+          *hslot = h;
+          const int64_t row = ((int64_t)layer * B + bbase + n) * T + t;
+          float* act = a.act + row * 5 * H + u;
+          act[(s == 0 ? 0 : 1) * H] = s == 0 ? ig : fg;
+          act[(s == 0 ? 2 : 3) * H] = s == 0 ? gg : og;
+          float* w3 = s == 0 ? act + 4 * H : a.hseq + row * H + u;
+          *w3 = s == 0 ? cn : h;
+          continue;
+        }
         const float ig = sigmoidf_fast(acc[0]);
         const float fg = sigmoidf_fast(acc[1]);
         const float gg = tanhf_fast(acc[2]);
@@ -314,7 +372,7 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
     lds_barrier();
   }
   if (a.stamps && tid == 0) {
-    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
     st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
   }
 
@@ -327,6 +385,10 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
     }
   }
   if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase);
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
+    st[4] = sr_in; st[5] = stamp_real(); st[6] = stamp_cu();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -359,6 +421,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
 
   const int NL = a.NL, B = a.B, T = a.T, I = a.I;
   const int tid = threadIdx.x;
+  const uint64_t sr_in = (a.stamps && tid == 0) ? stamp_real() : 0;
   const int layer = __builtin_amdgcn_readfirstlane(tid / LANES);
   const int lg = tid - layer * LANES;
   const int u = lg >> 2;
@@ -525,7 +588,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
     else lds_barrier();
   }
   if (a.stamps && tid == 0) {
-    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
     st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
   }
 #pragma unroll
@@ -537,6 +600,10 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
     }
   }
   if constexpr (HEAD) fwd_head_epilogue<H, NB>(a, smem, bbase, head_pre ? &hpre : nullptr, dh_lds);
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
+    st[4] = sr_in; st[5] = stamp_real(); st[6] = stamp_cu();
+  }
 }
 
 template <int H, int NB, bool SAVE, bool XLDS, bool HEAD, int CELL = 0>
@@ -772,7 +839,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
   }
   if (it < iters) step(it, ropA, inA);
   if (a.stamps && tid == 0) {
-    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
     st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
   }
 
@@ -874,6 +941,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
 
   const int NL = a.NL, B = a.B, T = a.T, I = a.I;
   const int tid = threadIdx.x;
+  const uint64_t sr_in = (a.stamps && tid == 0) ? stamp_real() : 0;
   const int layer = __builtin_amdgcn_readfirstlane(tid / LANES);
   const int lg = tid - layer * LANES;
   const int u = lg / L;
@@ -1044,6 +1112,10 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
     // join makes the waitcnt pass conservative, and every conservative
     // vmcnt here would wait for the prefetches of the next two steps.
     const int dha_tgt = layer > 0 ? layer - 1 : NL - 1;  // top layer's dha slots are never read
+    // the lean contract wants no input gradient: layer 0 skips W_ih^T g (a
+    // quarter to a half of its column-phase FMAs) -- unless the dW updates
+    // still need the column loop's operands (they do not depend on it)
+    const bool need_dx = !LEAN || layer > 0;
     auto step = [&](int it, Ops* op) {
       const int t = t_first - it;
       const bool active = t >= 0 && t < T;
@@ -1128,8 +1200,10 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
           if constexpr (!(PDRNN_ABLATE & 2)) {
             sh[0] = __builtin_elementwise_fma(whh[2 * r4], g01, sh[0]);
             sh[1] = __builtin_elementwise_fma(whh[2 * r4 + 1], g23, sh[1]);
-            sx[0] = __builtin_elementwise_fma(wih[2 * r4], g01, sx[0]);
-            sx[1] = __builtin_elementwise_fma(wih[2 * r4 + 1], g23, sx[1]);
+            if (need_dx) {  // wave-uniform (one layer per wave); no loads inside
+              sx[0] = __builtin_elementwise_fma(wih[2 * r4], g01, sx[0]);
+              sx[1] = __builtin_elementwise_fma(wih[2 * r4 + 1], g23, sx[1]);
+            }
           } else {
             sh[0] += g01; sx[1] += g23;
           }
@@ -1151,12 +1225,14 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
         float dhn_ = group_sum<L>(shs.x + shs.y);  // dh_{t-1}[u] on every lane of the unit
         if constexpr (CELL == 1) dhn_ += dc[n];
         dh[n] = active ? dhn_ : dh[n];
-        const float dx = group_sum<L>(sxs.x + sxs.y);
-        // every lane of the unit holds dx: all write the same value (no branch);
-        // consumed by layer-1 at it+2 (same parity)
-        dhabuf(n, dha_tgt, p)[u] = dx;
-        if (!LEAN && layer == 0 && dxp && active && j == 0 && u < I && valid[n])
-          dxp[bs[n] * a.dx_sb + (int64_t)t * a.dx_st + u] = dx;
+        if (need_dx) {
+          const float dx = group_sum<L>(sxs.x + sxs.y);
+          // every lane of the unit holds dx: all write the same value (no
+          // branch); consumed by layer-1 at it+2 (same parity)
+          dhabuf(n, dha_tgt, p)[u] = dx;
+          if (!LEAN && layer == 0 && dxp && active && j == 0 && u < I && valid[n])
+            dxp[bs[n] * a.dx_sb + (int64_t)t * a.dx_st + u] = dx;
+        }
       }
       // dh the layer above wrote for the NEXT iteration (its column phase of
       // it-1, published by this iteration's barrier): read now, off the next
@@ -1194,8 +1270,9 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
     __syncthreads();  // LDS is reused by the next tile
   }
   if (a.stamps && tid == 0) {
-    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 4;
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
     st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+    st[4] = sr_in; st[5] = st[3]; st[6] = stamp_cu();
   }
 
   // ---------------- epilogue: this workgroup's partial dW / db ----------
@@ -1663,6 +1740,11 @@ int bwd_dwout_resident(int NL, size_t lds) {
   return c_val;
 }
 
+// Balanced persistent grid: the fewest residency rounds, then the fewest
+// workgroups that still finish in that many rounds -- every workgroup walks
+// the same number of sequences (B = 1440 at 768 resident: 720 x 2, not a
+// second round of 672 behind a first of 768), and fewer co-resident waves
+// make each recurrence step cheaper.
 template <int H>
 int bwd_dwout_grid(int NL, int T, int B, int cell) {
   const size_t lds = bwd_gs_lds<H, 1>(NL), xbytes = bwd_gs_xbytes<H, 1>(T);
@@ -1671,7 +1753,9 @@ int bwd_dwout_grid(int NL, int T, int B, int cell) {
                                   : bwd_dwout_resident<H, false, 1>(NL, lds))
                             : (xl ? bwd_dwout_resident<H, true, 0>(NL, lds + xbytes)
                                   : bwd_dwout_resident<H, false, 0>(NL, lds));
-  return B < cap ? B : cap;
+  if (B <= cap) return B;
+  const int rounds = (B + cap - 1) / cap;
+  return (B + rounds - 1) / rounds;
 }
 
 template <int H>

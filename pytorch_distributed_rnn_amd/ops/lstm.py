@@ -60,17 +60,14 @@ def small_launch_config(batch: int, hidden: int, num_layers: int = 2) -> Tuple[i
 def fused_bwd_nb(batch: int, hidden: int, num_layers: int) -> int:
     """Sequences per workgroup of the fused training step's backward.
 
-    1 = the latency kernel (lstm_small.hip: one sequence per workgroup, two
-    resident per CU).  2..3 = the throughput kernel (lstm_small_tp.hip:
-    several sequences share the register-resident W / dW, operands DMA-staged
-    through LDS; B = 1440 runs in one residency round instead of three).  The
-    throughput kernel is correct but measured SLOWER at every motion batch
-    size (profiles/r2_tp_backward_tried.md: the backward is VALU-issue bound,
-    so interleaving sequences in a wave buys no latency hiding and the LDS
-    operand reads cost more than register prefetch); it stays opt-in for
-    sweeps via PDRNN_LSTM_NB_BWD."""
+    1 = one sequence per workgroup (the default: above one residency round
+    the deferred-dW backward, lstm_small.hip DWOUT + lstm_small_dw.hip).
+    2..3 interleave sequences in one workgroup of the register-dW backward
+    (sweeps via PDRNN_LSTM_NB_BWD); a multi-sequence variant with LDS-DMA
+    staged operands was measured slower at every motion batch and removed
+    (profiles/r2_tp_backward_tried.md)."""
     env = _env_int("PDRNN_LSTM_NB_BWD", 0)
-    if env in (1, 2, 3, 4):
+    if env in (1, 2, 3):
         return env
     return 1
 

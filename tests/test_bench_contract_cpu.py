@@ -4,18 +4,22 @@ JSON line from rank 0 with the whole-job value and the dp degree."""
 import json
 import os
 
+import pytest
+
 from _mp import ROOT, torchrun
 
 
-def test_bench_two_ranks_json_contract(tmp_path):
-    out = torchrun([os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"], 2,
-                   str(tmp_path), timeout=300)
+@pytest.mark.parametrize("world,baseline", [(2, 85.9), (8, 213.3)])
+def test_bench_multi_rank_json_contract(tmp_path, world, baseline):
+    """world 8: the driver's N=8 scaling launch, rehearsed on gloo."""
+    out = torchrun([os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1"], world,
+                   str(tmp_path), timeout=600)
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out[-3000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
-    assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 1440
-    assert d["config"]["per_gpu_batch"] == 720 and d["scaling"] == "strong"
+    assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["parallelism"] == f"dp{world}" and d["config"]["global_batch"] == 1440
+    assert d["config"]["per_gpu_batch"] == 1440 // world and d["scaling"] == "strong"
     assert d["value"] > 0 and abs(d["value"] - 1440 * 2 / (d["ms_per_step"] * 2e-3)) / d["value"] < 1e-2
-    assert d["vs_baseline"] == round(d["value"] / 85.9, 2)
+    assert d["vs_baseline"] == round(d["value"] / baseline, 2)
     assert d["final_loss"] == d["final_loss"]

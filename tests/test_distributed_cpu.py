@@ -37,8 +37,10 @@ def _rank_mean(log, world):
 
 
 @pytest.mark.parametrize("mode", ["distributed", "horovod"])
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_world_size_invariance(tmp_path, local_losses, mode, world):
+    # world 8 = the driver's scaling node: the same torch.distributed.run
+    # launch, rendezvous and per-rank batch split (1440 / 8 = 180 there)
     out = torchrun([MAIN] + COMMON + [mode], nproc=world, cwd=str(tmp_path))
     mean = _rank_mean(out, world)
     assert len(mean) == len(local_losses)

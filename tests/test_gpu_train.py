@@ -80,15 +80,14 @@ def test_one_launch_step_selected_in_latency_regime():
 
 @pytest.mark.parametrize("cell", ["lstm", "gru"])
 @pytest.mark.parametrize("nb", [2, 3])
-def test_fused_throughput_backward_matches_autograd(cell, nb, monkeypatch):
-    """The multi-sequence (LDS-DMA staged) backward of the fused step
-    (csrc/kernels/lstm_small_tp.hip) against the autograd path; 380 samples in
-    batches of 96 leave a last batch of 92, so tiles with unused slots run."""
-    from pytorch_distributed_rnn_amd import _ext
+def test_fused_multi_sequence_backward_matches_autograd(cell, nb, monkeypatch):
+    """Sequences interleaved in one workgroup of the fused step's register-dW
+    backward (PDRNN_LSTM_NB_BWD; the GRU stays single-sequence) against the
+    autograd path; 380 samples in batches of 96 leave a last batch of 92, so
+    tiles with unused slots run."""
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     monkeypatch.setenv("PDRNN_LSTM_NB_BWD", str(nb))
-    assert _ext.native(torch.device("cuda")).lstm_small_bwd_tp_ok(32, 2, 128, 9, 96, nb)
     torch.manual_seed(1)
     train, _, _ = synthetic_motion(n_train=380, n_validation=2, n_test=2, seed=4)
     m1 = MotionModel(9, 32, 2, 6, cell=cell)
@@ -105,7 +104,8 @@ def test_fused_throughput_backward_matches_autograd(cell, nb, monkeypatch):
 
 @pytest.mark.parametrize("nb", [1, 3])
 def test_fused_step_headline_batch_matches_autograd(nb, monkeypatch):
-    """B = 1440 (the headline per-GPU batch), latency and throughput backward."""
+    """B = 1440 (the headline per-GPU batch): the deferred-dW backward (nb 1)
+    and the register-dW backward with 3 sequences per workgroup."""
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     from pytorch_distributed_rnn_amd.train.trainer import Trainer
