@@ -50,12 +50,94 @@ void report_stamps(const char* what, const Tensor& st, int iters) {
             pro / 100.0, epi / 100.0, (in_max - in_min) / 100.0, (out_max - out_min) / 100.0,
             (out_max - in_min) / 100.0);
     std::map<int64_t, int> per_cu;  // placement census: workgroups per CU
-    for (int64_t i = 0; i < g; ++i) per_cu[p[i * 8 + 6]]++;
+    for (int64_t i = 0; i < g; ++i) per_cu[p[i * 8 + 6] & 0xFFFFFF]++;
     int lo = INT32_MAX, hi = 0;
     for (auto& kv : per_cu) { lo = std::min(lo, kv.second); hi = std::max(hi, kv.second); }
     fprintf(stderr, " | CUs used=%zu workgroups/CU min=%d max=%d", per_cu.size(), lo, hi);
+    // loop time by the load of the workgroup's CU (mean / max us): is the
+    // exit spread placement (more co-resident waves) or something else
+    std::map<int, std::pair<double, double>> by_load;
+    std::map<int, int> n_load;
+    for (int64_t i = 0; i < g; ++i) {
+      const int64_t* r = p + i * 8;
+      const int k = per_cu[r[6] & 0xFFFFFF];
+      const double t = (double)(r[3] - r[2]) / 100.0;
+      auto& e = by_load[k];
+      e.first += t; e.second = std::max(e.second, t); n_load[k]++;
+    }
+    for (auto& kv : by_load)
+      fprintf(stderr, " | %d/CU: n=%d loop mean=%.1f max=%.1f", kv.first, n_load[kv.first],
+              kv.second.first / n_load[kv.first], kv.second.second);
+    // waves per SIMD (wave 0 always, wave 1 where stamped): loop time by the
+    // busiest SIMD the workgroup's waves sit on, and by XCC
+    std::map<int64_t, int> per_simd;
+    for (int64_t i = 0; i < g; ++i) {
+      const int64_t* r = p + i * 8;
+      per_simd[r[6] & 0xFFFFFFFF]++;
+      if (r[7] >> 32) per_simd[r[7] & 0xFFFFFFFF]++;
+    }
+    std::map<int, std::pair<double, double>> by_simd, by_xcc;
+    std::map<int, int> n_simd, n_xcc;
+    for (int64_t i = 0; i < g; ++i) {
+      const int64_t* r = p + i * 8;
+      int k = per_simd[r[6] & 0xFFFFFFFF];
+      if (r[7] >> 32) k = std::max(k, per_simd[r[7] & 0xFFFFFFFF]);
+      const int x = (int)((r[6] >> 16) & 0xF);
+      const double t = (double)(r[3] - r[2]) / 100.0;
+      auto& e = by_simd[k]; e.first += t; e.second = std::max(e.second, t); n_simd[k]++;
+      auto& f = by_xcc[x]; f.first += t; f.second = std::max(f.second, t); n_xcc[x]++;
+    }
+    fprintf(stderr, "\n[stamps]   by busiest SIMD:");
+    for (auto& kv : by_simd)
+      fprintf(stderr, " %d waves: n=%d mean=%.1f max=%.1f |", kv.first, n_simd[kv.first],
+              kv.second.first / n_simd[kv.first], kv.second.second);
+    {  // are a workgroup's two waves on one SIMD (they then serialise the step)?
+      double ts[2] = {0, 0}, tm[2] = {0, 0};
+      int tn[2] = {0, 0};
+      for (int64_t i = 0; i < g; ++i) {
+        const int64_t* r = p + i * 8;
+        if (!(r[7] >> 32)) continue;
+        const int same = (r[6] & 0xFFFFFFFF) == (r[7] & 0xFFFFFFFF);
+        const double t = (double)(r[3] - r[2]) / 100.0;
+        ts[same] += t; tm[same] = std::max(tm[same], t); tn[same]++;
+      }
+      if (tn[0] + tn[1])
+        fprintf(stderr, "\n[stamps]   waves on distinct SIMDs: n=%d mean=%.1f max=%.1f | same SIMD: n=%d mean=%.1f max=%.1f",
+                tn[0], tn[0] ? ts[0] / tn[0] : 0., tm[0], tn[1], tn[1] ? ts[1] / tn[1] : 0., tm[1]);
+    }
+    {  // by launch order (blockIdx deciles): dispatch-age effects
+      double ds[10] = {0}, dm[10] = {0};
+      int dn[10] = {0};
+      for (int64_t i = 0; i < g; ++i) {
+        const int64_t* r = p + i * 8;
+        const int d = (int)(i * 10 / g);
+        const double t = (double)(r[3] - r[2]) / 100.0;
+        ds[d] += t; dm[d] = std::max(dm[d], t); dn[d]++;
+      }
+      fprintf(stderr, "\n[stamps]   by blockIdx decile (mean/max):");
+      for (int d = 0; d < 10; ++d)
+        if (dn[d]) fprintf(stderr, " %.1f/%.1f", ds[d] / dn[d], dm[d]);
+    }
+    fprintf(stderr, "\n[stamps]   by XCC:");
+    for (auto& kv : by_xcc)
+      fprintf(stderr, " %d: mean=%.1f max=%.1f |", kv.first, kv.second.first / n_xcc[kv.first], kv.second.second);
   }
   fprintf(stderr, "\n");
+}
+// progress-ordered wave priority in the small-H recurrences (PDRNN_PRIO=0 off)
+int prio_env() {
+  const char* e = std::getenv("PDRNN_PRIO");
+  const char* p = std::getenv("PDRNN_PRIO_SHIFT");
+  const int mode = e ? std::atoi(e) : 1;
+  const int sh = p ? std::atoi(p) : 4;
+  static int cus = 0;  // one GPU model per process
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  return mode | (sh << 4) | (cus << 8);
 }
 using c10::optional;
 
@@ -167,6 +249,7 @@ std::vector<Tensor> lstm_small_fwd(const Tensor& x, const optional<Tensor>& idx,
   Tensor hn = at::empty({NL, B, H}, opts), cn = at::empty({NL, B, H}, opts);
   Tensor hseq, act, out;
   PdrnnLstmSmallFwdArgs a{};
+  a.prio = prio_env();
   a.x = reinterpret_cast<const float*>(x.data_ptr());
   a.x_bf16 = x.scalar_type() == at::kBFloat16;
   a.idx = (idx.has_value() && idx->defined()) ? idx->data_ptr<int64_t>() : nullptr;
@@ -236,6 +319,7 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
   Tensor slab = at::empty({std::max(grid, 1), L.P}, opts);
   Tensor dx, dh0, dc0;
   PdrnnLstmSmallBwdArgs a{};
+  a.prio = prio_env();
   a.x = reinterpret_cast<const float*>(x.data_ptr());
   a.x_bf16 = x.scalar_type() == at::kBFloat16;
   a.idx = gathered ? idx->data_ptr<int64_t>() : nullptr;
@@ -383,6 +467,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   Tensor slab = at::empty({slab_rows, L.P}, opts);
 
   PdrnnLstmSmallFwdArgs f{};
+  f.prio = prio_env();
   f.x = reinterpret_cast<const float*>(x.data_ptr());
   f.x_bf16 = x.scalar_type() == at::kBFloat16;
   f.idx = gathered ? idx->data_ptr<int64_t>() : nullptr;
@@ -418,6 +503,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   if (!one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
 
   PdrnnLstmSmallBwdArgs bk{};
+  bk.prio = prio_env();
   bk.x = f.x; bk.x_bf16 = f.x_bf16; bk.idx = f.idx; bk.x_sb = f.x_sb; bk.x_st = f.x_st;
   for (int64_t l = 0; l < NL; ++l) {
     bk.w_ih[l] = f.w_ih[l]; bk.w_hh[l] = f.w_hh[l];

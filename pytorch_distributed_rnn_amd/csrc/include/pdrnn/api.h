@@ -54,6 +54,7 @@ typedef struct {
   int B, T, I, NL;
   int cell;                  // 0 = LSTM, 1 = GRU (packed as a 4-row-block stack, see ops/gru.py)
   int x_bf16;                // x holds bf16 values (read once into LDS; requires the LDS-resident x path)
+  int prio;                  // lower the waves' issue priority as the recurrence progresses (see prio_by_progress)
 } PdrnnLstmSmallFwdArgs;
 
 typedef struct {
@@ -94,6 +95,7 @@ typedef struct {
   int64_t dg_st;
   float* xg_out;             // DWOUT: [B*T][xg_ld] fp32 copy of the (gathered, widened) layer-0 input
   int xg_ld;
+  int prio;                  // see the forward
 } PdrnnLstmSmallBwdArgs;
 
 // Weight gradients of the small-H stack from saved gate gradients, on the

@@ -90,6 +90,41 @@ PDRNN_DEVICE float tanhf_fast(float x) {
 // behind the HBM write latency of the previous one.  Cross-wave hand-offs in
 // the recurrent kernels go exclusively through LDS, so waiting for lgkmcnt is
 // sufficient; global prefetches and output stores stay in flight.
+// Wave issue priority in the long small-H recurrences.  Co-resident
+// workgroups start together and the SIMD's arbiter otherwise favours the
+// oldest wave, so the workgroups dispatched last on a CU finish last and set
+// the kernel's end (stamps: loop time rises with blockIdx in tiers of one
+// workgroup per CU).  `prio` = mode | log2(period) << 4 | CUs << 8:
+//   mode 1: priority falls with the wave's own progress (4 levels);
+//   mode 2: priority rotates every `period` steps over the dispatch tiers
+//           (tier = blockIdx / CUs, 3 levels), every tier leads a third of
+//           the time.
+// `it` is wave-uniform (scalar compares only).
+PDRNN_DEVICE void set_prio_level(int lvl) {
+  switch (lvl) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+}
+PDRNN_DEVICE void prio_by_progress(int it, int iters, int prio) {
+  const int mode = prio & 15;
+  if (mode == 1) {
+    if (it == 0) set_prio_level(3);
+    else if (it == iters / 4) set_prio_level(2);
+    else if (it == iters / 2) set_prio_level(1);
+    else if (it == 3 * iters / 4) set_prio_level(0);
+  } else if (mode == 2) {
+    const int sh = (prio >> 4) & 15;
+    if ((it & ((1 << sh) - 1)) == 0) {
+      const int ncu = max(prio >> 8, 1);
+      const int tier = (int)blockIdx.x / ncu;
+      set_prio_level(((it >> sh) + tier) % 3);
+    }
+  }
+}
+
 PDRNN_DEVICE void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -108,12 +143,12 @@ PDRNN_DEVICE float opaque_copy(float v) {
 // Diagnostic cycle stamps (shader clock and 100 MHz real-time clock).
 PDRNN_DEVICE uint64_t stamp_cycles() { return __builtin_amdgcn_s_memtime(); }
 PDRNN_DEVICE uint64_t stamp_real() { return __builtin_amdgcn_s_memrealtime(); }
-// Which CU runs this wave (diagnostics: workgroup placement census): XCC id
-// << 16 | the SE / SH / CU fields of HW_ID (bits 8..14).
+// Which CU runs this wave (diagnostics: workgroup placement census): SIMD id
+// << 24 | XCC id << 16 | the SE / SH / CU fields of HW_ID (bits 8..14).
 PDRNN_DEVICE uint32_t stamp_cu() {
   const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
   const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-  return ((xcc & 0xF) << 16) | ((hw >> 8) & 0x7F);
+  return (((hw >> 4) & 3) << 24) | ((xcc & 0xF) << 16) | ((hw >> 8) & 0x7F);
 }
 
 // bf16 <-> f32 (round to nearest even; NaN preserved by the hardware cvt).

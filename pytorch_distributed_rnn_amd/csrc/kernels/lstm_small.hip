@@ -231,12 +231,16 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
           w[q][4 * k4 + 0] = v.x; w[q][4 * k4 + 1] = v.y; w[q][4 * k4 + 2] = v.z; w[q][4 * k4 + 3] = v.w;
         }
       } else {
+        // only the live columns are loaded: for the layer-0 input slice
+        // (I << KS) the guard is uniform over the slice's lanes, so the
+        // zero-padded tail issues no loads at all (128 -> 4 I per lane)
+        const int lim = in_part ? Iin : H;
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
           const int c = c0 + kk;
-          const bool live = !in_part || c < Iin;
-          const float v = src[r * ld + (live ? c : 0)];
-          w[q][kk] = live ? v : 0.f;
+          float v = 0.f;
+          if (c < lim) v = src[r * ld + c];
+          w[q][kk] = v;
         }
       }
       bias[q] = (a.b_ih[layer] ? a.b_ih[layer][r] : 0.f) + (a.b_hh[layer] ? a.b_hh[layer][r] : 0.f);
@@ -278,6 +282,7 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
   if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
   const int iters = T + NL - 1;
   for (int it = 0; it < iters; ++it) {
+    prio_by_progress(it, iters, a.prio);
     const int t = it - layer;
     if (t >= 0 && t < T) {
       const int p = t & 1;
@@ -389,6 +394,8 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
     uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
     st[4] = sr_in; st[5] = stamp_real(); st[6] = stamp_cu();
   }
+  // the second wave's SIMD (bit 32 marks the slot as written)
+  if (a.stamps && tid == 64) a.stamps[(uint64_t)blockIdx.x * 8 + 7] = stamp_cu() | (1ull << 32);
 }
 
 // ---------------------------------------------------------------------------
@@ -516,6 +523,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
   if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
   const int iters = T + NL - 1;
   for (int it = 0; it < iters; ++it) {
+    prio_by_progress(it, iters, a.prio);
     const int t = it - layer;
     if (t >= 0 && t < T) {
       const int p = t & 1;
@@ -834,6 +842,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
   const int iters = T + NL - 1;
   int it = 0;
   for (; it + 1 < iters; it += 2) {
+    prio_by_progress(it / 2, iters / 2, a.prio);
     step(it, ropA, inA);
     step(it + 1, ropB, inB);
   }
@@ -1252,8 +1261,13 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
     };
 
     const int iters = T + 2 * (NL - 1);
+    // progress over all of this workgroup's tiles, in step pairs
+    const int tiles = (B - (int)blockIdx.x * NB + (int)gridDim.x * NB - 1) / ((int)gridDim.x * NB);
+    const int tile = (b0 - (int)blockIdx.x * NB) / ((int)gridDim.x * NB);
+    const int hp = (iters + 1) / 2;
     int it = 0;
     for (; it + 1 < iters; it += 2) {
+      prio_by_progress(tile * hp + it / 2, tiles * hp, a.prio);
       step(it, opA);
       step(it + 1, opB);
     }

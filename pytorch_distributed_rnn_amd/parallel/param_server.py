@@ -58,30 +58,87 @@ _PAYLOAD_GROUPS = {}
 _PAYLOAD_BACKEND = None
 
 
-def payload_mode(requested: str, world_size: int) -> str:
-    """``auto``: collective payloads when every rank can own a GPU (RCCL
-    refuses two ranks on one device), otherwise the RPC-carried payloads."""
+def _local_gpu_ok(rank: int, world_size: int) -> bool:
+    """Can this rank own a GPU of its host?  From LOCAL_RANK / LOCAL_WORLD_SIZE
+    when a launcher set them (multi-host jobs: the per-host count matters, not
+    the global world size), else every rank of the job on this host."""
+    if not torch.cuda.is_available():
+        return False
+    n = torch.cuda.device_count()
+    lws = os.environ.get("LOCAL_WORLD_SIZE")
+    if lws is not None:
+        return n >= int(lws)
+    lr = os.environ.get("LOCAL_RANK")
+    if lr is not None:
+        return n > int(lr)
+    return n >= world_size
+
+
+def _local_device_index(rank: int) -> int:
+    return int(os.environ.get("LOCAL_RANK", rank))
+
+
+def payload_mode(requested: str, world_size: int, rank: int = 0) -> str:
+    """Local guess only (no agreement): ``auto`` -> collective iff this rank
+    could own a GPU.  The job-wide decision is :func:`agree_payload`."""
     if requested != "auto":
         return requested
-    if torch.cuda.is_available() and torch.cuda.device_count() >= world_size:
-        return "collective"
-    return "rpc"
+    return "collective" if _local_gpu_ok(rank, world_size) else "rpc"
 
 
-def init_payload_groups(rank: int, world_size: int, address: str, port: str) -> None:
+_AGREE_STORE = None
+
+
+def agree_payload(requested: str, rank: int, world_size: int, address: str, port: str,
+                  timeout_s: Optional[float] = None):
+    """Job-wide payload mode and backend: every rank publishes whether it can
+    own a GPU on a TCPStore (rank 0 hosts it, port + 2) and all ranks apply
+    the same rule to the same answers, so hosts with different GPU counts
+    cannot disagree (a split decision would leave some ranks in the payload
+    group rendezvous until it times out).  Returns (mode, backend): mode
+    ``collective`` iff requested so, or ``auto`` and every rank owns a GPU;
+    backend ``nccl`` (RCCL) iff every rank owns a GPU, else ``gloo``."""
+    global _AGREE_STORE
+    if requested == "rpc":
+        return "rpc", None
+    from torch.distributed import TCPStore
+    import time
+    t = timedelta(seconds=timeout_s if timeout_s is not None else max(RPC_TIMEOUT_S, 60.0))
+    store = TCPStore(address, int(port) + 2, world_size, rank == 0, t)
+    store.set(f"pdrnn_ps_gpu/{rank}", "1" if _local_gpu_ok(rank, world_size) else "0")
+    keys = [f"pdrnn_ps_gpu/{r}" for r in range(world_size)]
+    store.wait(keys, t)
+    all_gpu = all(store.get(k) == b"1" for k in keys)
+    # the store lives in rank 0: it may only go away once everyone has read
+    store.add("pdrnn_ps_gpu_read", 1)
+    if rank == 0:
+        deadline = time.monotonic() + t.total_seconds()
+        while store.add("pdrnn_ps_gpu_read", 0) < world_size:
+            if time.monotonic() > deadline:
+                raise TimeoutError("payload-mode agreement: not every rank read the decision")
+            time.sleep(0.005)
+    _AGREE_STORE = store if rank == 0 else None
+    mode = requested if requested != "auto" else ("collective" if all_gpu else "rpc")
+    return mode, ("nccl" if all_gpu else "gloo")
+
+
+def init_payload_groups(rank: int, world_size: int, address: str, port: str,
+                        backend: Optional[str] = None) -> None:
     """Process group for the tensor payloads, next to the RPC agent (port + 1).
 
     Backend: RCCL when every rank owns a GPU (device payloads, GPU<->GPU over
-    xGMI), gloo otherwise (host payloads).  Every rank creates every pair
+    xGMI), gloo otherwise (host payloads) -- as agreed by :func:`agree_payload`
+    (every rank must pass the same one).  Every rank creates every pair
     group {0, r} in the same order (``new_group`` is collective); one
     communicator per trainer lets the server serve trainers from concurrent
     RPC threads without interleaving their send/recv on one communicator."""
     import torch.distributed as dist
     global _PAYLOAD_BACKEND
-    use_gpu = torch.cuda.is_available() and torch.cuda.device_count() >= world_size
-    _PAYLOAD_BACKEND = "nccl" if use_gpu else "gloo"
-    if use_gpu:
-        torch.cuda.set_device(rank)
+    if backend is None:
+        backend = "nccl" if _local_gpu_ok(rank, world_size) else "gloo"
+    _PAYLOAD_BACKEND = backend
+    if backend == "nccl":
+        torch.cuda.set_device(_local_device_index(rank) % torch.cuda.device_count())
     dist.init_process_group(_PAYLOAD_BACKEND, init_method=f"tcp://{address}:{int(port) + 1}", rank=rank,
                             world_size=world_size, timeout=timedelta(seconds=max(RPC_TIMEOUT_S, 60.0)))
     for r in range(1, world_size):
@@ -232,8 +289,9 @@ def run_parameter_server(rank: int, world_size: int, address: str = "127.0.0.1",
     logging.info("PS master initializing RPC")
     rpc.init_rpc(name=PS_NAME, rank=rank, world_size=world_size,
                  rpc_backend_options=_rpc_options(address, port))
+    payload, backend = agree_payload(payload, rank, world_size, address, port)
     if payload == "collective":
-        init_payload_groups(rank, world_size, address, port)
+        init_payload_groups(rank, world_size, address, port, backend)
         logging.info(f"Payload groups initialized ({_PAYLOAD_BACKEND})")
     logging.info("RPC initialized! Running parameter server...")
     rpc.shutdown(graceful=True)  # returns when every trainer has finished
@@ -392,8 +450,9 @@ def run_worker(rank, world_size, epochs, batch_size, learning_rate, input_dim, h
     logging.info(f"Worker rank {rank} initializing RPC")
     rpc.init_rpc(name=f"trainer_{rank}", rank=rank, world_size=world_size,
                  rpc_backend_options=_rpc_options(address, port))
+    payload, backend = agree_payload(payload, rank, world_size, address, port)
     if payload == "collective":
-        init_payload_groups(rank, world_size, address, port)
+        init_payload_groups(rank, world_size, address, port, backend)
     logging.info(f"Worker {rank} done initializing RPC")
     model = RemoteModel(input_dim, hidden_dim, layer_dim, output_dim, cell, payload=payload, rank=rank)
     cls = _make_worker_trainer_cls()
@@ -437,7 +496,7 @@ def execute(args):
     os.environ["MASTER_ADDR"] = args.master_address
     os.environ["MASTER_PORT"] = args.master_port
     address = "127.0.0.1" if args.master_address == "localhost" else args.master_address
-    payload = payload_mode(getattr(args, "ps_payload", "auto"), args.world_size)
+    payload = getattr(args, "ps_payload", "auto")  # agreed across ranks in run_* (agree_payload)
     if args.rank == 0:
         run_parameter_server(0, args.world_size, address, args.master_port, payload=payload)
         return None

@@ -112,3 +112,26 @@ def test_rccl_uid_exchange_through_store(tmp_path):
         "dist.destroy_process_group()\n")
     out = torchrun([str(script)], nproc=3, cwd=str(tmp_path))
     assert sorted(int(ln.split()[-1]) for ln in out.splitlines() if ln.startswith("uid-ok")) == [0, 1, 2]
+
+
+def test_parameter_server_payload_mode_is_agreed(tmp_path):
+    """each rank used to pick the PS payload mode from its own GPU
+    count.  agree_payload exchanges every rank's answer through a TCPStore,
+    so a job whose ranks differ (here rank 2 claims a GPU, the others do not)
+    still gets ONE mode and backend everywhere: 'auto' -> rpc, an explicit
+    'collective' -> gloo payloads."""
+    from _mp import free_port
+    script = tmp_path / "agree.py"
+    script.write_text(
+        "import os, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "from pytorch_distributed_rnn_amd.parallel import param_server as ps\n"
+        "r, w, port = int(os.environ['RANK']), int(os.environ['WORLD_SIZE']), sys.argv[1]\n"
+        "ps._local_gpu_ok = lambda rank, world: rank == 2\n"
+        "a = ps.agree_payload('auto', r, w, '127.0.0.1', port, timeout_s=60)\n"
+        "b = ps.agree_payload('collective', r, w, '127.0.0.1', str(int(port) + 10), timeout_s=60)\n"
+        "c = ps.agree_payload('rpc', r, w, '127.0.0.1', port)\n"
+        "open(f'agree{r}.txt', 'w').write(' '.join([a[0], a[1], b[0], b[1], c[0]]))\n")
+    torchrun([str(script), str(free_port())], nproc=3, cwd=str(tmp_path))
+    for r in range(3):  # one file per rank: stdout lines of the ranks interleave
+        assert (tmp_path / f"agree{r}.txt").read_text().split() == ["rpc", "gloo", "collective", "gloo", "rpc"]
