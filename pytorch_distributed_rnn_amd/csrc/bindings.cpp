@@ -5,6 +5,7 @@
 // launches on torch's current HIP stream.  All math lives in csrc/kernels.
 #include <torch/extension.h>
 #include <cstdio>
+#include <atomic>
 #include <map>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
@@ -128,8 +129,8 @@ void report_stamps(const char* what, const Tensor& st, int iters) {
 int prio_env() {
   const char* e = std::getenv("PDRNN_PRIO");
   const char* p = std::getenv("PDRNN_PRIO_SHIFT");
-  const int mode = e ? std::atoi(e) : 1;
-  const int sh = p ? std::atoi(p) : 4;
+  const int mode = e ? std::atoi(e) : 2;  // B = 1440: 0.403 -> 0.387 ms/step (profiles/r3p_prio.md)
+  const int sh = p ? std::atoi(p) : 3;
   static int cus = 0;  // one GPU model per process
   if (!cus) {
     int dev = 0;
@@ -731,14 +732,38 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 // ---------------------------------------------------------------------------
 // Persistent recurrence (one cooperative launch per layer direction set,
 // W_hh register-resident; lstm_large.hip) when the shape is covered and
-// PDRNN_LSTM_PERSIST != 0; false -> the caller runs the per-step kernels.
-// A grid-sync spin that times out (bounded at 2 s in the kernel) sets a
-// sticky per-device flag; it is copied to pinned host memory after every
-// launch and checked at the next one, so a timeout fails loudly one call
-// later without a synchronisation.  PDRNN_LSTM_PERSIST_CHECK=1 synchronises
-// and checks right away (tests).
-bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int dt, int64_t tile,
-                   const at::TensorOptions& opts, hipStream_t st) {
+// PDRNN_LSTM_PERSIST != 0.  A grid-sync spin that times out (bounded at 2 s
+// in the kernel: co-residency lost, e.g. to RCCL kernels on the comm stream)
+// leaves that launch's outputs invalid.
+//   * verify on (set_persist_verify(true) -- the multi-rank trainers do it --
+//     or PDRNN_LSTM_PERSIST_VERIFY=1): the host synchronises after the launch
+//     and reads its error flag; on a timeout it warns, clears the sticky flag
+//     and returns kPersistFailed, and the caller re-runs the layer on the
+//     per-step kernels -- before anything (the next layer, the optimizer)
+//     consumes the result.
+//   * verify off (single rank: nothing else runs on the GPU): no
+//     synchronisation; a sticky per-device flag is copied to pinned memory
+//     after every launch and checked at the next one (fails loudly one call
+//     later), and by persist_check() at epoch end.
+enum PersistResult { kPersistNotRun = 0, kPersistOk = 1, kPersistFailed = 2 };
+std::atomic<int> g_persist_verify{-1};     // -1: PDRNN_LSTM_PERSIST_VERIFY (default off)
+std::atomic<int> g_persist_inject{0};      // tests: flag the next N launches as timed out
+std::atomic<long long> g_persist_fallbacks{0};
+bool persist_verify_on() {
+  const int v = g_persist_verify.load();
+  if (v >= 0) return v != 0;
+  static const bool env = [] {
+    const char* e = std::getenv("PDRNN_LSTM_PERSIST_VERIFY");
+    return e && std::atoi(e) != 0;
+  }();
+  return env;
+}
+// leaked on purpose: no tensor destructor runs after the HIP runtime is gone
+std::vector<Tensor>& persist_sticky() { static auto& v = *new std::vector<Tensor>(64); return v; }
+std::vector<Tensor>& persist_sticky_host() { static auto& v = *new std::vector<Tensor>(64); return v; }
+
+int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int dt, int64_t tile,
+                  const at::TensorOptions& opts, hipStream_t st) {
   static const int env = [] {
     const char* e = std::getenv("PDRNN_LSTM_PERSIST");
     return e ? std::atoi(e) : 1;
@@ -751,17 +776,16 @@ bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int
     const char* e = std::getenv("PDRNN_PS_MODE");
     return e ? std::atoi(e) : 0;
   }();
-  if (env == 0 || tile >= 0) return false;
+  if (env == 0 || tile >= 0) return kPersistNotRun;
   int dev = 0;
   TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
   int cus = 0;
   TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
   const int mt = pdrnn_lstm_large_persist_mt(a.B, a.H, ndir, dt, cus);
-  if (mt == 0) return false;
+  if (mt == 0) return kPersistNotRun;
   const int nmb = (a.B + 16 * mt - 1) / (16 * mt);
-  // leaked on purpose: no tensor destructor runs after the HIP runtime is gone
-  static std::vector<Tensor>& sticky = *new std::vector<Tensor>(64);
-  static std::vector<Tensor>& sticky_host = *new std::vector<Tensor>(64);
+  std::vector<Tensor>& sticky = persist_sticky();
+  std::vector<Tensor>& sticky_host = persist_sticky_host();
   TORCH_CHECK(dev >= 0 && dev < 64, "device index");
   if (!sticky[dev].defined()) {
     sticky[dev] = at::zeros({1}, opts.dtype(at::kInt));
@@ -773,11 +797,29 @@ bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int
   const int64_t stamp_ints = (mode & 8) ? 2 + 64 * 8 * 2 : 1;
   Tensor sync = at::zeros({ndir * nmb + 1 + stamp_ints + 2}, opts.dtype(at::kInt));
   int* cnt = sync.data_ptr<int>();
+  int m = mode;
+  for (int k = g_persist_inject.load(); k > 0; k = g_persist_inject.load())
+    if (g_persist_inject.compare_exchange_weak(k, k - 1)) { m |= 16; break; }
   const hipError_t e = pdrnn_lstm_large_persist(&a, ndir, backward ? 1 : 0, dt, mt, cnt, cnt + ndir * nmb,
-                                                sticky[dev].data_ptr<int>(), mode, st);
+                                                sticky[dev].data_ptr<int>(), m, st);
   if (e != hipSuccess) {
     (void)hipGetLastError();  // e.g. cooperative grid too large: per-step path
-    return false;
+    return kPersistNotRun;
+  }
+  if (persist_verify_on()) {
+    static std::vector<Tensor>& flag = *new std::vector<Tensor>(64);
+    if (!flag[dev].defined()) flag[dev] = at::zeros({1}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
+    int* hf = flag[dev].data_ptr<int>();
+    hf[0] = 0;
+    TORCH_CHECK(hipMemcpyAsync(hf, cnt + ndir * nmb, sizeof(int), hipMemcpyDeviceToHost, st) == hipSuccess, "flag copy");
+    TORCH_CHECK(hipStreamSynchronize(st) == hipSuccess, "persistent LSTM: stream synchronisation failed");
+    if (hf[0] != 0) {
+      g_persist_fallbacks++;
+      TORCH_WARN("persistent LSTM recurrence (", backward ? "backward" : "forward",
+                 "): a grid-sync wait timed out (co-residency lost); re-running the layer on the per-step kernels");
+      TORCH_CHECK(hipMemsetAsync(sticky[dev].data_ptr<int>(), 0, sizeof(int), st) == hipSuccess, "sticky reset");
+      return kPersistFailed;
+    }
   }
   if (mode & 8) {
     // int64 stamps start at the first 8-byte boundary after err
@@ -794,7 +836,17 @@ bool large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int
     const int err = sync[ndir * nmb].item<int>();
     TORCH_CHECK(err == 0, "persistent LSTM grid sync timed out");
   }
-  return true;
+  return kPersistOk;
+}
+
+// End-of-epoch check of the deferred (verify-off) path: raises if any
+// persistent launch on this device timed out since the last check.
+void persist_check() {
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
+  if (dev < 0 || dev >= 64 || !persist_sticky()[dev].defined()) return;
+  const int v = persist_sticky()[dev].item<int>();  // synchronises
+  TORCH_CHECK(v == 0, "persistent LSTM recurrence: a grid-sync wait timed out (results of that step invalid)");
 }
 
 // Large-H LSTM layer (both directions in one launch per step).
@@ -844,7 +896,7 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
     dd.acts = eptrm(acts, d * T * B * 4 * H);
   }
   hipStream_t st = cur_stream();
-  if (!large_persist(a, ndir, false, dt, tile, o32, st)) {
+  if (large_persist(a, ndir, false, dt, tile, o32, st) != kPersistOk) {
     for (int64_t s = 0; s < T; ++s) {
       a.step = (int)s;
       HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 0, dt, (int)tile, st));
@@ -920,7 +972,10 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   }
   hipStream_t st = cur_stream();
   HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, ndir, dt, st));
-  if (!large_persist(a, ndir, true, dt, tile, o32, st)) {
+  const int pr = large_persist(a, ndir, true, dt, tile, o32, st);
+  if (pr != kPersistOk) {
+    // a failed launch may have advanced the dc carry: start the layer over
+    if (pr == kPersistFailed) HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, ndir, dt, st));
     for (int64_t s = 0; s < T; ++s) {
       a.step = (int)s;
       HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 1, dt, (int)tile, st));
@@ -991,6 +1046,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
   m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
   m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });
+  m.def("set_persist_verify", [](bool on) { g_persist_verify = on ? 1 : 0; },
+        "synchronise after every persistent-recurrence launch and re-run a timed-out layer on the per-step kernels");
+  m.def("persist_inject_timeouts", [](int64_t n) { g_persist_inject = (int)n; },
+        "tests: flag the next n persistent launches as timed out");
+  m.def("persist_fallbacks", []() { return (int64_t)g_persist_fallbacks.load(); },
+        "persistent launches re-run on the per-step kernels after a timeout");
+  m.def("debug_spin_cus", [](double ms, int64_t workgroups, int64_t threads, int64_t lds_bytes) {
+    HIP_LAUNCH_CHECK(pdrnn_debug_spin_cus((uint64_t)(ms * 1e3), (int)workgroups, (int)threads, (int)lds_bytes,
+                                          cur_stream()));
+  }, "diagnostics: fill CUs with bounded spinning workgroups on the current stream");
+  m.def("persist_check", &persist_check, "raise if a persistent launch on this device timed out (synchronises)");
   m.def("lstm_large_persist_mt", [](int64_t B, int64_t H, int64_t ndir, int64_t dtype) {
     int dev = 0, cus = 0;
     TORCH_CHECK(hipGetDevice(&dev) == hipSuccess &&

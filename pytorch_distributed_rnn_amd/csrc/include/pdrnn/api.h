@@ -309,6 +309,10 @@ hipError_t pdrnn_slab_reduce_adam(const PdrnnAdamArgs* a, const float* A, int64_
 // Diagnostics: a single wave that spins for `microseconds` (bounded, <= 60 s).
 // Communicator-watchdog tests only.
 hipError_t pdrnn_debug_spin(uint64_t microseconds, hipStream_t stream);
+// Diagnostics: `workgroups` x `threads` spinning for `microseconds` each
+// (bounded, <= 10 s), `lds_bytes` of LDS apiece (CU occupancy).
+hipError_t pdrnn_debug_spin_cus(uint64_t microseconds, int workgroups, int threads, int lds_bytes,
+                                hipStream_t stream);
 
 #ifdef __cplusplus
 }

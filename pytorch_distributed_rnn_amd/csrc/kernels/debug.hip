@@ -16,8 +16,30 @@ __global__ void __launch_bounds__(64) debug_spin_kernel(uint64_t ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
+// pdrnn_debug_spin_cus: a grid of workgroups (threads, dynamic LDS as
+// given) that spin for a bounded time each -- fills the CUs so that a
+// cooperative launch issued meanwhile on another stream cannot become
+// co-resident (test of the persistent recurrence's timeout recovery).
+__global__ void __launch_bounds__(1024) debug_spin_cus_kernel(uint64_t ticks) {
+  extern __shared__ float hold[];  // occupancy only
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+  if (ticks == 0) hold[threadIdx.x] = 0.f;  // keep the allocation referenced
+}
+
 }  // namespace
 }  // namespace pdrnn
+
+extern "C" hipError_t pdrnn_debug_spin_cus(uint64_t microseconds, int workgroups, int threads, int lds_bytes,
+                                           hipStream_t stream) {
+  if (microseconds > 10ull * 1000 * 1000) microseconds = 10ull * 1000 * 1000;  // bounded: 10 s
+  if (workgroups < 1 || threads < 64 || threads > 1024 || threads % 64 || lds_bytes < 4 * threads ||
+      lds_bytes > 160 * 1024)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pdrnn::debug_spin_cus_kernel, dim3(workgroups), dim3(threads), (size_t)lds_bytes, stream,
+                     microseconds * 100ull);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t pdrnn_debug_spin(uint64_t microseconds, hipStream_t stream) {
   // bounded: at most 60 s

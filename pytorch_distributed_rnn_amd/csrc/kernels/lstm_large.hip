@@ -816,7 +816,8 @@ struct PersistSync {
   int* cnt;   // [ndir][NMB] arrival counters, zero at launch
   int* err;   // set to 1 when a spin timed out (this launch: releases every waiter)
   int* sticky;  // also set on a timeout; never cleared (the host checks it)
-  int mode;   // diagnostics (wrong results): bit 0 no waits, bit 1 no step GEMM, bit 2 no store drain
+  int mode;   // diagnostics (wrong results): bit 0 no waits, bit 1 no step GEMM, bit 2 no store drain,
+              // bit 4 flag the launch as timed out (tests of the host's recovery)
   long long* stamps;  // mode bit 3: workgroup 0 records s_memtime at 8 points of steps 0..63
 };
 #define PS_STAMP(k)                                                                          \
@@ -887,6 +888,8 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   float* red = reinterpret_cast<float*>(smem_raw);  // [wave][MT][16][LDR]
   const int B = args.B, H = args.H, T = args.T;
+  if ((sync.mode & 16) && blockIdx.x == 0 && threadIdx.x == 0)  // test hook: this launch "timed out"
+    __hip_atomic_store(sync.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int NCB = H / PS_NU, NMB = (B + 16 * MT - 1) / (16 * MT);
   int dir, cb, mb;
   ps_coords(NCB, NMB, dir, cb, mb);
@@ -1034,6 +1037,8 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   float* red = reinterpret_cast<float*>(smem_raw);  // [wave][MT][16][LDR]
   const int B = args.B, H = args.H, T = args.T;
+  if ((sync.mode & 16) && blockIdx.x == 0 && threadIdx.x == 0)  // test hook: this launch "timed out"
+    __hip_atomic_store(sync.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int NCB = H / PS_NU, NMB = (B + 16 * MT - 1) / (16 * MT);
   int dir, cb, mb;
   ps_coords(NCB, NMB, dir, cb, mb);

@@ -133,6 +133,12 @@ def get_comm(group=None, prefer_native: bool = True):
     else:
         comm = _PyComm(g)
     _CACHE[key] = comm
+    if mod is not None and torch.cuda.is_available() and dist.get_world_size(g) > 1 \
+            and hasattr(mod, "set_persist_verify"):
+        # collectives now run beside the compute stream: a persistent
+        # recurrence can lose co-residency to them, so its launches are
+        # verified and a timed-out layer is re-run (bindings.cpp large_persist)
+        mod.set_persist_verify(True)
     return comm
 
 

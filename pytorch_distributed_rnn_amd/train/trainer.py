@@ -68,6 +68,16 @@ def stats_to_host(rows: List[Tensor]) -> Tensor:
     return torch.stack(rows).detach().cpu()
 
 
+
+def _persist_check() -> None:
+    """A persistent-recurrence launch that timed out without per-launch
+    verification (single rank) fails the run here at the latest."""
+    if torch.cuda.is_available():
+        from .. import _ext
+        mod = _ext.extension()
+        if mod is not None and hasattr(mod, "persist_check"):
+            mod.persist_check()
+
 class Trainer:
     loss_fn = CrossEntropyLoss()
 
@@ -154,6 +164,7 @@ class Trainer:
         memory, _ = mem.measure_peak_rss(train_inner)
         mem.synchronize()
         duration = time.perf_counter() - start
+        _persist_check()
         logging.info(formatter.performance_message(memory, duration))
         logging.info(formatter.throughput_message(self.sequences_seen, duration,
                                                   mem.device_peak_mib(), self.world_size()))
