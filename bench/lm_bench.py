@@ -32,7 +32,7 @@ from pytorch_distributed_rnn_amd.models.charlm import BiLSTMEncoder, CharLM  # n
 from pytorch_distributed_rnn_amd.ops.adam import FusedAdam  # noqa: E402
 from pytorch_distributed_rnn_amd.ops.xent import cross_entropy  # noqa: E402
 from pytorch_distributed_rnn_amd.parallel import env  # noqa: E402
-from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel  # noqa: E402
+from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel, format_bucket_layout  # noqa: E402
 from pytorch_distributed_rnn_amd.train.lm import LMTrainer  # noqa: E402
 from pytorch_distributed_rnn_amd.utils.flat import flatten_module  # noqa: E402
 from pytorch_distributed_rnn_amd.utils.memory import device_peak_mib  # noqa: E402
@@ -50,7 +50,7 @@ def parse(argv=None):
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--input-dim", type=int, default=1024, help="bilstm input features")
     ap.add_argument("--ddp", action="store_true",
-                    help="charlm: bucketed DDP reducer even at one rank (overlap traces with "
+                    help="bucketed DDP reducer even at one rank (overlap traces with "
                          "PDRNN_FORCE_COLLECTIVE=1)")
     ap.add_argument("--bucket-mb", type=float, default=None)
     return ap.parse_args(argv)
@@ -79,7 +79,10 @@ def main(argv=None):
         B, T, H = a.batch or 4096, a.seq_len or 64, a.hidden or 4096
         model = BiLSTMEncoder(a.input_dim, H, a.layers, 32, torch.float16).to(dev)
         flatten_module(model)
-        net = DistributedDataParallel(model) if world > 1 else model
+        net = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb) if world > 1 or a.ddp else model
+        if isinstance(net, DistributedDataParallel) and rank == 0:
+            print("bucket layout (launch order): " + format_bucket_layout(net.bucket_layout()), file=sys.stderr,
+                  flush=True)
         opt = FusedAdam(model.parameters(), lr=1e-4)
         g = torch.Generator(device=dev).manual_seed(rank)
         xs = torch.randn(T, B, a.input_dim, device=dev, generator=g).half()
@@ -117,7 +120,8 @@ def main(argv=None):
             "data": "synthetic", "config": {"model": model_name, "global_batch": B * world, "seq_len": T,
                                             "parallelism": f"dp{world}"},
             "final_loss": round(float(loss), 5), "device_peak_mib": round(device_peak_mib(dev), 1),
-            "ddp_reducer": a.config == "charlm" and isinstance(tr.model, DistributedDataParallel)}), flush=True)
+            "ddp_reducer": isinstance(tr.model if a.config == "charlm" else net, DistributedDataParallel),
+            "force_collective": os.environ.get("PDRNN_FORCE_COLLECTIVE", "0") == "1"}), flush=True)
     env.shutdown()
 
 

@@ -52,6 +52,12 @@ class Comm {
   }
   // ---- failure detection (RcclComm: watchdog thread; others: their
   // backend's own timeouts) ----
+  // Release the communicator now (watchdog joined, collectives drained with
+  // a deadline, then destroyed or aborted); idempotent, later calls raise.
+  // Called for every cached communicator at interpreter exit (parallel/comm.py)
+  // so no watchdog thread is still polling the HIP runtime while the
+  // process's exit handlers tear it down.
+  virtual void close() {}
   virtual bool aborted() const { return false; }
   virtual double timeout_s() const { return 0.0; }
   virtual int64_t tracked() const { return 0; }  // collectives the watchdog has followed

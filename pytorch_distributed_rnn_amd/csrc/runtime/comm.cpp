@@ -121,7 +121,10 @@ class RcclComm final : public Comm {
     poll_ms_ = std::max(1.0, env_double("PDRNN_COMM_WATCHDOG_POLL_MS", 100.0));
     watchdog_ = std::thread([this] { watchdog_loop(); });
   }
-  ~RcclComm() override {
+  ~RcclComm() override { close(); }
+  void close() override {
+    // no api_mu_ here: the watchdog may be waiting for it to abort
+    if (closed_.exchange(true)) return;
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
@@ -144,11 +147,16 @@ class RcclComm final : public Comm {
         ncclCommAbort(comm_);
       }
     }
+    comm_ = nullptr;
     for (auto& w : works_) hipEventDestroy(w.ev);
+    works_.clear();
     for (auto ev : free_events_) hipEventDestroy(ev);
+    free_events_.clear();
     if (ev_in_) hipEventDestroy(ev_in_);
     if (ev_out_) hipEventDestroy(ev_out_);
     if (stream_) hipStreamDestroy(stream_);
+    ev_in_ = ev_out_ = nullptr;
+    stream_ = nullptr;
   }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
@@ -318,6 +326,7 @@ class RcclComm final : public Comm {
   }
   // raise once the watchdog has aborted the communicator
   void live() const {
+    TORCH_CHECK(!closed_.load(), "RCCL communicator (rank ", rank_, "/", world_, ") was closed");
     if (aborted_.load()) {
       std::lock_guard<std::mutex> lk(mu_);
       TORCH_CHECK(false, "RCCL communicator (rank ", rank_, "/", world_, ") was aborted by the watchdog: ",
@@ -510,6 +519,7 @@ class RcclComm final : public Comm {
   bool stop_ = false;
   std::string abort_reason_;
   std::atomic<bool> aborted_{false};
+  std::atomic<bool> closed_{false};
   std::atomic<int64_t> tracked_{0};
   std::thread watchdog_;
 };

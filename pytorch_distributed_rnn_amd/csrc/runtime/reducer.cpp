@@ -34,9 +34,16 @@ class GradReducer {
   // flat_grad (optional): an existing flat gradient buffer in which the
   // params' gradients are laid out back to back in registration order (see
   // utils/flat.py).  Buckets then are plain slices of it -- zero copies.
+  // groups (optional, one id per param): a bucket never spans two groups --
+  // the DDP wrapper gives every (RNN layer, direction) its own id, so a
+  // layer's buckets launch as soon as that layer's weight gradients exist
+  // instead of waiting for the first parameters of the layer below; a group
+  // larger than the cap is subdivided.
   GradReducer(std::vector<at::Tensor> params, std::shared_ptr<Comm> comm, int64_t bucket_cap_bytes,
-              int64_t first_bucket_cap_bytes, bool average, c10::optional<at::Tensor> flat_grad)
+              int64_t first_bucket_cap_bytes, bool average, c10::optional<at::Tensor> flat_grad,
+              std::vector<int64_t> groups = {})
       : params_(std::move(params)), comm_(std::move(comm)), average_(average) {
+    TORCH_CHECK(groups.empty() || groups.size() == params_.size(), "groups: one id per parameter");
     const bool use_flat = flat_grad.has_value() && flat_grad->defined();
     std::vector<int64_t> flat_off;
     if (use_flat) {
@@ -56,6 +63,7 @@ class GradReducer {
     int64_t cur_bytes = 0;
     at::ScalarType cur_dtype = at::kFloat;
     c10::Device cur_dev = at::kCPU;
+    int64_t cur_group = 0;
     auto close = [&]() {
       if (cur.empty()) return;
       buckets_idx_.push_back(cur);
@@ -66,8 +74,11 @@ class GradReducer {
       const auto& p = params_[i];
       const int64_t cap = buckets_idx_.empty() ? first_bucket_cap_bytes : bucket_cap_bytes;
       const int64_t bytes = p.numel() * p.element_size();
-      if (!cur.empty() && (p.scalar_type() != cur_dtype || p.device() != cur_dev || cur_bytes + bytes > cap)) close();
-      if (cur.empty()) { cur_dtype = p.scalar_type(); cur_dev = p.device(); }
+      const int64_t grp = groups.empty() ? 0 : groups[i];
+      if (!cur.empty() && (p.scalar_type() != cur_dtype || p.device() != cur_dev || grp != cur_group ||
+                           cur_bytes + bytes > cap))
+        close();
+      if (cur.empty()) { cur_dtype = p.scalar_type(); cur_dev = p.device(); cur_group = grp; }
       cur.push_back(i);
       cur_bytes += bytes;
     }
@@ -327,7 +338,8 @@ void register_runtime(py::module_& m) {
       .def_property_readonly("aborted", &Comm::aborted)
       .def_property_readonly("timeout_s", &Comm::timeout_s)
       .def_property_readonly("tracked", &Comm::tracked)
-      .def("track_current", &Comm::track_current);
+      .def("track_current", &Comm::track_current)
+      .def("close", &Comm::close, py::call_guard<py::gil_scoped_release>());
   m.attr("WATCHDOG_EXIT") = kWatchdogExit;
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("make_rccl_comm", [](py::bytes uid, int rank, int world, int device, bool high_priority, double timeout_s) {
@@ -337,9 +349,10 @@ void register_runtime(py::module_& m) {
   m.def("make_pg_comm", &make_pg_comm, py::arg("process_group"));
 
   py::class_<GradReducer, std::shared_ptr<GradReducer>>(m, "GradReducer")
-      .def(py::init<std::vector<at::Tensor>, std::shared_ptr<Comm>, int64_t, int64_t, bool, c10::optional<at::Tensor>>(),
+      .def(py::init<std::vector<at::Tensor>, std::shared_ptr<Comm>, int64_t, int64_t, bool, c10::optional<at::Tensor>,
+                    std::vector<int64_t>>(),
            py::arg("params"), py::arg("comm"), py::arg("bucket_cap_bytes"), py::arg("first_bucket_cap_bytes"),
-           py::arg("average") = true, py::arg("flat_grad") = py::none())
+           py::arg("average") = true, py::arg("flat_grad") = py::none(), py::arg("groups") = std::vector<int64_t>{})
       .def("grad_views", &GradReducer::grad_views)
       .def("buckets", &GradReducer::buckets)
       .def("bucket_indices", &GradReducer::bucket_indices)

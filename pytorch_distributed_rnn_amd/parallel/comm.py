@@ -15,6 +15,8 @@ Communicators are cached per group.
 """
 from __future__ import annotations
 
+import atexit
+import logging
 import os
 from typing import Dict, Optional
 
@@ -140,6 +142,26 @@ def get_comm(group=None, prefer_native: bool = True):
         # verified and a timed-out layer is re-run (bindings.cpp large_persist)
         mod.set_persist_verify(True)
     return comm
+
+
+def close_comms() -> None:
+    """Release every cached communicator now (native: watchdog joined,
+    pending collectives drained with a deadline, RCCL communicator destroyed
+    or aborted).  Registered with atexit: the interpreter otherwise may never
+    drop the last reference, leaving a watchdog thread polling the HIP runtime
+    while the process's exit handlers tear it down (seen as a SIGSEGV in
+    exit() under rocprofv3)."""
+    for c in list(_CACHE.values()):
+        close = getattr(c, "close", None)
+        if close is not None:
+            try:
+                close()
+            except Exception as e:  # teardown must not mask the run's own outcome
+                logging.warning(f"communicator close failed: {e}")
+    reset_comms()
+
+
+atexit.register(close_comms)
 
 
 def reset_comms() -> None:

@@ -23,8 +23,10 @@ past the latency-bound regime (see docs/DESIGN.md, "Bucket sizing").
 from __future__ import annotations
 
 import contextlib
+import logging
 import os
-from typing import List, Optional
+import re
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -37,6 +39,33 @@ from .comm import get_comm
 
 DEFAULT_BUCKET_MB = float(os.environ.get("PDRNN_BUCKET_MB", 32))
 DEFAULT_FIRST_BUCKET_MB = float(os.environ.get("PDRNN_FIRST_BUCKET_MB", 1))
+
+
+_RNN_PARAM = re.compile(r"^(?P<base>.*_l\d+)(?P<rev>_reverse)?$")
+
+
+def param_group_ids(module: nn.Module, params) -> List[int]:
+    """One id per (RNN layer, direction) -- ``weight_ih_l1_reverse`` and
+    ``bias_hh_l1_reverse`` share one, ``*_l1`` another -- and per owning
+    module for everything else (head, embedding).  Ids are consecutive in
+    registration order, so a bucket boundary falls on every layer-direction
+    boundary (buckets aligned to the weights a BPTT layer
+    finishes together)."""
+    names = {id(p): n for n, p in module.named_parameters()}
+    keys: Dict[str, int] = {}
+    out = []
+    for p in params:
+        n = names.get(id(p), f"<unnamed {len(out)}>")
+        mod_path, _, leaf = n.rpartition(".")
+        m = _RNN_PARAM.match(leaf)
+        key = f"{mod_path}:{m.group('base').split('_')[-1]}{m.group('rev') or ''}" if m else mod_path
+        out.append(keys.setdefault(key, len(keys)))
+    return out
+
+
+def format_bucket_layout(layout) -> str:
+    return "; ".join(f"#{b['bucket']} {b['mib']:.2f} MiB {b['params']} params [{', '.join(b['names'])}]"
+                     for b in layout)
 
 
 class _PyReducer:
@@ -109,17 +138,35 @@ class DistributedDataParallel(nn.Module):
         first = int((first_bucket_cap_mb if first_bucket_cap_mb is not None
                      else DEFAULT_FIRST_BUCKET_MB) * 2 ** 20)
         mod = _ext.extension()
+        self.param_groups_ids = param_group_ids(module, self.flat.params)
         if mod is not None:
             self.reducer = mod.GradReducer(self.flat.params, self.comm, cap, first, average,
-                                           self.flat.grad)
+                                           self.flat.grad, self.param_groups_ids)
         else:
             self.reducer = _PyReducer(self.flat.params, self.comm, self.flat.grad)
+        if self.rank == 0:
+            logging.info("DDP buckets (launch order): " + format_bucket_layout(self.bucket_layout()))
         self._views = list(self.reducer.grad_views())
         for p, v in zip(self.flat.params, self._views):
             p.grad = v
         self._finalize_queued = False
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i))
                        for i, p in enumerate(self.flat.params)]
+
+    def bucket_layout(self) -> List[Dict]:
+        """Buckets in launch order: size, parameter count and names."""
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        if not hasattr(self.reducer, "bucket_indices"):  # python twin: one flat bucket
+            idx = [list(range(len(self.flat.params) - 1, -1, -1))]
+        else:
+            idx = [list(b) for b in self.reducer.bucket_indices()]
+        out = []
+        for b, ids in enumerate(idx):
+            ps = [self.flat.params[i] for i in ids]
+            out.append({"bucket": b, "params": len(ps),
+                        "mib": sum(p.numel() * p.element_size() for p in ps) / 2 ** 20,
+                        "names": [names.get(id(p), "?") for p in ps]})
+        return out
 
     # -------------------------------------------------------------- sync
     @torch.no_grad()
@@ -162,5 +209,3 @@ class DistributedDataParallel(nn.Module):
         finally:
             self.require_backward_grad_sync = old
 
-    def bucket_layout(self) -> List[List[int]]:
-        return [list(b) for b in getattr(self.reducer, "bucket_indices", lambda: [])()]

@@ -135,3 +135,50 @@ def test_parameter_server_payload_mode_is_agreed(tmp_path):
     torchrun([str(script), str(free_port())], nproc=3, cwd=str(tmp_path))
     for r in range(3):  # one file per rank: stdout lines of the ranks interleave
         assert (tmp_path / f"agree{r}.txt").read_text().split() == ["rpc", "gloo", "collective", "gloo", "rpc"]
+
+
+def test_ddp_buckets_align_to_layer_direction(tmp_path):
+    """GradReducer closes a bucket at every (layer,
+    direction) boundary and subdivides a group only above the cap -- no bucket
+    mixes two groups; the layout is logged (rank 0) and returned by
+    bucket_layout().  Stacked bi-LSTM 2 x 16 + head, world 2 (gloo)."""
+    script = tmp_path / "buckets.py"
+    script.write_text(
+        "import json, logging, os, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch\n"
+        "from pytorch_distributed_rnn_amd.parallel import env\n"
+        "from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel\n"
+        "from pytorch_distributed_rnn_amd.models.charlm import BiLSTMEncoder\n"
+        "from pytorch_distributed_rnn_amd.utils.flat import flatten_module\n"
+        "logging.basicConfig(level=logging.INFO)\n"
+        "env.init_distributed('gloo')\n"
+        "torch.manual_seed(0)\n"
+        "out = {}\n"
+        "for cap in (64.0, 0.004):\n"
+        "    m = BiLSTMEncoder(8, 16, 2, 4, torch.float32)\n"
+        "    flatten_module(m)\n"
+        "    d = DistributedDataParallel(m, bucket_cap_mb=cap, first_bucket_cap_mb=cap)\n"
+        "    out[str(cap)] = [b['names'] for b in d.bucket_layout()]\n"
+        "    x = torch.randn(5, 3, 8)\n"
+        "    d(x).sum().backward()\n"
+        "    d.finalize() if hasattr(d, 'finalize') else None\n"
+        "if env.get_rank() == 0:\n"
+        "    open('layout.json', 'w').write(json.dumps(out))\n"
+        "env.shutdown()\n")
+    log = torchrun([str(script)], nproc=2, cwd=str(tmp_path))
+    assert "DDP buckets (launch order)" in log
+    layout = json.loads((tmp_path / "layout.json").read_text())
+
+    def key(n):
+        leaf = n.rsplit(".", 1)[-1]
+        if "_l" in leaf:
+            return n.rsplit(".", 1)[0] + leaf[leaf.index("_l"):]
+        return n.rsplit(".", 1)[0]
+    big = layout["64.0"]
+    # one bucket per group, launch order = reverse registration: head, l1_reverse, l1, l0_reverse, l0
+    assert [sorted({key(n) for n in b}) for b in big] == [["fc"], ["lstm_l1_reverse"], ["lstm_l1"],
+                                                          ["lstm_l0_reverse"], ["lstm_l0"]], big
+    small = layout["0.004"]  # 4 KiB cap: groups are split, never mixed
+    assert len(small) > len(big)
+    assert all(len({key(n) for n in b}) == 1 for b in small), small
