@@ -47,13 +47,13 @@ class ShardedSampler(torch.utils.data.Sampler):
     def set_epoch(self, epoch: int) -> None:
         self.epoch = epoch
 
-    def index_tensor(self) -> Tensor:
-        """This rank's indices of the current epoch as an int64 CPU tensor
-        (the same values as :meth:`indices`, built with tensor ops: no Python
-        list of N ints on the per-epoch path)."""
+    def index_tensor(self, epoch: Optional[int] = None) -> Tensor:
+        """This rank's indices of the current epoch (or of ``epoch``) as an
+        int64 CPU tensor (the same values as :meth:`indices`, built with
+        tensor ops: no Python list of N ints on the per-epoch path)."""
         if self.shuffle:
             g = torch.Generator()
-            g.manual_seed(self.seed + self.epoch)
+            g.manual_seed(self.seed + (self.epoch if epoch is None else epoch))
             idx = torch.randperm(self.n, generator=g)
         else:
             idx = torch.arange(self.n)
@@ -104,14 +104,32 @@ class DeviceBatchLoader:
     def __len__(self) -> int:
         return math.ceil(self.num_items / self.batch_size)
 
+    def prefetch(self, epoch: Optional[int] = None) -> None:
+        """Build the batch indices of sampler epoch ``epoch`` (default: the
+        sampler's current one) now -- the trainer calls it while the GPU still
+        runs the previous epoch's steps, so the next epoch's first launch does
+        not wait for the host permutation and its copy (a DataLoader
+        prefetch).  Consumed by the next :meth:`batch_indices` of that epoch."""
+        if self.sampler is None:
+            return
+        e = self.sampler.epoch if epoch is None else epoch
+        self._prefetched = (e, self._build_indices(self.sampler.index_tensor(e)))
+
     def batch_indices(self) -> List[Tensor]:
         """This epoch's per-batch row indices, on the device.  The host
         permutation goes through a persistent pinned staging buffer with an
         asynchronous copy (a pageable-memory copy would be synchronous)."""
+        pre = getattr(self, "_prefetched", None)
+        if pre is not None and self.sampler is not None and pre[0] == self.sampler.epoch:
+            self._prefetched = None
+            return pre[1]
         if self.sampler is not None:
             idx = self.sampler.index_tensor()
         else:
             idx = torch.arange(self.num_items)
+        return self._build_indices(idx)
+
+    def _build_indices(self, idx: Tensor) -> List[Tensor]:
         if self.device.type == "cuda":
             stage = getattr(self, "_pinned", None)
             if stage is None or stage.numel() < idx.numel():

@@ -36,6 +36,13 @@ class FusedAdam(torch.optim.Adam):
         self._flat_state = {}
 
     # -- flat state -------------------------------------------------------
+    def materialize_state(self) -> None:
+        """Allocate (zero) the flat moment buffers of every group now instead
+        of inside the first step; no parameter or step count changes."""
+        with torch.no_grad():
+            for gi, g in enumerate(self.param_groups):
+                self._group_flat(gi, g)
+
     def _group_flat(self, gi: int, group) -> Optional[dict]:
         params: List[Tensor] = [p for p in group["params"]]
         if not params:

@@ -251,10 +251,31 @@ class MotionTrainStep:
         else:
             ws = self.weights
         stats = torch.zeros(3, dtype=torch.float32, device=self.flat.grad.device)
+        # the single-process step folds Adam into its reduction: warm THAT
+        # kernel variant too (its first launch pays the code-object load), on
+        # scratch copies of the parameters and moments -- nothing real moves
+        adam_bufs = adam_hp = None
+        if self.grad_sync is None:
+            st = self._flat_adam_peek()
+            if st is not None:
+                (p, m, v), adam_hp = st
+                adam_bufs = [p.clone(), m.clone(), v.clone()]
         self.mod.lstm_head_train_step(features, idx, labels, ws, self.m.fc.weight, self.m.fc.bias, self.flat.grad,
-                                      stats, self.H, self.NL, sp_fwd, 0, nb_fwd, nb_bwd, None, None,
+                                      stats, self.H, self.NL, sp_fwd, 0, nb_fwd, nb_bwd, adam_bufs, adam_hp,
                                       1 if self.gru else 0, self.colmap)
         self.flat.grad.zero_()
+
+    def _flat_adam_peek(self):
+        """_flat_adam's operands without advancing the step count."""
+        opt = self.optimizer
+        g = opt.param_groups[0] if len(opt.param_groups) == 1 else None
+        fs = opt._group_flat(0, g) if g is not None and hasattr(opt, "_group_flat") else None
+        if fs is None:
+            return None
+        res = self._flat_adam()
+        if res is not None:
+            fs["step"] -= 1.0  # undo the advance
+        return res
 
     # ------------------------------------------------------------ HIP graph
     # captured steps are kept per configuration (full and short last batch of
