@@ -184,8 +184,12 @@ __device__ __forceinline__ void fwd_head_epilogue(const PdrnnLstmSmallFwdArgs& a
 
 constexpr float kNegLog2eK = -1.4426950408889634f;
 
+// H <= 32: at most 168 VGPRs, three waves per SIMD -- the B = 1440 forward
+// (2880 waves on 1024 SIMDs) must stay one residency round (170 VGPRs with
+// the packed K loop would drop it to two: 135 -> 184 us)
 template <int H, int S, int NB, bool SAVE, bool XLDS, bool HEAD = false>
-__global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(H <= 32 ? 3 : 1)))
+lstm_small_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   constexpr int K = 2 * H;
   constexpr int KS = K / S;
   constexpr int LANES = H * S;
@@ -259,6 +263,12 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
     }
   }
 
+  pdrnn_f2 w2[4][KS / 2];  // k pairs of the slice (packed FMA operands)
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < KS / 2; ++j) w2[q][j] = pdrnn_f2{w[q][2 * j], w[q][2 * j + 1]};
+
   int bsrc[NB];
   bool valid[NB];
   float c[NB], hl[NB];
@@ -301,20 +311,22 @@ __global__ void __launch_bounds__(512) lstm_small_fwd_kernel(PdrnnLstmSmallFwdAr
         const float* src = vin(n, layer, p) + k0;
         if (XLDS && layer == 0 && k0 < H) src = xs + ((int64_t)n * T + t) * H + k0;
         const float4* v4 = reinterpret_cast<const float4*>(src);
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        // packed fp32 FMAs over k pairs (v_pk_fma_f32: 2 MACs per lane and
+        // instruction, 64 instead of 128 per step), halves summed at the end
+        pdrnn_f2 acc2[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
         for (int k4 = 0; k4 < KS / 4; ++k4) {
           const float4 v = v4[k4];
+          const pdrnn_f2 vlo = {v.x, v.y}, vhi = {v.z, v.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            acc[q] = fmaf(w[q][4 * k4 + 0], v.x, acc[q]);
-            acc[q] = fmaf(w[q][4 * k4 + 1], v.y, acc[q]);
-            acc[q] = fmaf(w[q][4 * k4 + 2], v.z, acc[q]);
-            acc[q] = fmaf(w[q][4 * k4 + 3], v.w, acc[q]);
+            acc2[q] = __builtin_elementwise_fma(w2[q][2 * k4], vlo, acc2[q]);
+            acc2[q] = __builtin_elementwise_fma(w2[q][2 * k4 + 1], vhi, acc2[q]);
           }
         }
+        float acc[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = group_sum<S>(acc[q]) + bias[q];
+        for (int q = 0; q < 4; ++q) acc[q] = group_sum<S>(acc2[q].x + acc2[q].y) + bias[q];
         if constexpr (S == 2 && NB == 1 && SAVE) {
           // the unit's two lanes split the activations (lane 0: i, g; lane
           // 1: f, o; one DPP swap exchanges them) and the stores: every lane
