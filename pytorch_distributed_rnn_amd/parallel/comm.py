@@ -27,7 +27,7 @@ from .. import _ext
 
 _CACHE: Dict[int, object] = {}
 _NATIVE = set()   # cache keys holding an RcclComm
-_UID_SEQ = [0]    # per-process communicator creation count (same order on every rank)
+_UID_SEQ: Dict[tuple, int] = {}  # communicators made so far per member-rank tuple
 
 
 def _exchange_uid(mod, g, rank: int) -> bytes:
@@ -36,17 +36,19 @@ def _exchange_uid(mod, g, rank: int) -> bytes:
     communicator for the group is never created just to bootstrap ours (one
     communicator per process on the gradient path instead of two).  Falls
     back to a broadcast when the default store is not reachable."""
-    _UID_SEQ[0] += 1
     try:
         store = dist.distributed_c10d._get_default_store()
-        ranks = dist.get_process_group_ranks(g)
+        ranks = tuple(sorted(dist.get_process_group_ranks(g)))
     except Exception:  # pragma: no cover - private-API drift
         store = None
     if store is None:
         uid = [mod.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=dist.get_global_rank(g, 0), group=g)
         return uid[0]
-    key = "pdrnn/rccl_uid/%d/%s" % (_UID_SEQ[0], "-".join(str(r) for r in ranks))
+    # the sequence number counts communicators per member set, which only the
+    # members themselves advance: ranks outside a subgroup never skew it
+    seq = _UID_SEQ[ranks] = _UID_SEQ.get(ranks, 0) + 1
+    key = "pdrnn/rccl_uid/%d/%s" % (seq, "-".join(str(r) for r in ranks))
     if rank == 0:
         uid = mod.rccl_unique_id()
         store.set(key, uid)

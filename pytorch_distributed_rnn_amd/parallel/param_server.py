@@ -48,6 +48,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .. import _ext
+
 PS_NAME = "parameter_server"
 RPC_TIMEOUT_S = float(os.environ.get("PDRNN_RPC_TIMEOUT", 60))
 
@@ -187,6 +189,10 @@ class ServerModel:
         self.device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
             else torch.device("cpu")
         self.model = MotionModel(input_dim, hidden_dim, layer_dim, output_dim, cell=cell).to(self.device)
+        if self.device.type == "cuda":
+            from ..utils.flat import flatten_module
+            flatten_module(self.model)  # one flat span: a trainer's Adam step is one adam_flat launch
+        self.native_adam_steps = 0
         self.lock = threading.Lock()
         self.step_lock = threading.Lock()
         self._pending = {}  # trainer rank -> logits of its in-flight step (collective payloads)
@@ -249,12 +255,17 @@ class ServerModel:
             with self.lock:  # one optimizer update at a time (torch's _LocalOptimizer.global_lock)
                 opt = self._optims.get(rank)
                 if opt is None:
-                    opt = self._optims[rank] = torch.optim.Adam(params, lr=lr)
+                    # per-trainer flat moments over the server's flat parameter span:
+                    # one adam_flat_kernel launch per step (torch.optim.Adam on the CPU)
+                    from ..ops.adam import FusedAdam
+                    opt = self._optims[rank] = FusedAdam(params, lr=lr)
                 for p, gr in zip(params, grads):
                     p.grad = gr
                 opt.step()
                 for p in params:
                     p.grad = None
+                if self.device.type == "cuda" and _ext.native(self.device) is not None:
+                    self.native_adam_steps += 1
 
     def save(self, path: str, epoch: int, loss: float) -> str:
         from ..train.checkpoint import save_checkpoint
@@ -295,6 +306,8 @@ def run_parameter_server(rank: int, world_size: int, address: str = "127.0.0.1",
         logging.info(f"Payload groups initialized ({_PAYLOAD_BACKEND})")
     logging.info("RPC initialized! Running parameter server...")
     rpc.shutdown(graceful=True)  # returns when every trainer has finished
+    if _server_model is not None:
+        logging.info(f"Server optimizer steps on the native flat Adam: {_server_model.native_adam_steps}")
     if payload == "collective":
         shutdown_payload_groups()
     logging.info("RPC shutdown on parameter server.")
@@ -417,12 +430,16 @@ def _make_worker_trainer_cls():
 
         def _one_step(self, data, target):
             if self.model.payload == "collective":
+                from ..ops.xent import cross_entropy_with_stats
                 output = self.model(data)
                 target = target.to(output.device).long().reshape(-1)
-                loss = F.cross_entropy(output, target)
+                # fused softmax-CE + argmax counts (one xent launch when the
+                # logits arrive on this trainer's GPU over RCCL)
+                loss, stats = cross_entropy_with_stats(output, target)
                 loss.backward()
                 self.model.backward_p2p(output.grad, self._lr)
-                return loss.item(), int((output.detach().argmax(dim=1) == target).sum())
+                loss_v, _, correct = stats.tolist()
+                return loss_v, int(correct)
             import torch.distributed.autograd as dist_autograd
             with dist_autograd.context() as cid:
                 output = self.model(data)

@@ -53,3 +53,9 @@ def test_parameter_server_gpu_loss_decreases(tmp_path, payload):
         assert all(x == x for x in losses)
         k = max(1, len(losses) // 4)
         assert sum(losses[-k:]) / k < sum(losses[:k]) / k, (r, losses)  # learning on the server
+    if payload == "collective":
+        # the server stepped every trainer's update on the native flat Adam
+        # (adam_flat_kernel over the flattened server model)
+        import re
+        m = re.search(r"Server optimizer steps on the native flat Adam: (\d+)", outs[0])
+        assert m and int(m.group(1)) == sum(len(v) for v in per.values()), outs[0][-2000:]
