@@ -984,6 +984,87 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   return {dgates, dh0, dc0};
 }
 
+// Time-batched GEMM (kernels/gemm.hip).  A: a_kmajor ? [K, M] : [M, K];
+// B: b_kmajor ? [K, N] : [N, K] (unit stride along the last dim, any row
+// stride); optional second K segment A2 / B2 of the same layouts; output
+// fp32 [M, N] (out16: the inputs' dtype, + fp32 bias[N]); `out` is written (or
+// accumulated into, fp32) in place when given.
+Tensor gemm16(const Tensor& A, bool a_kmajor, const Tensor& B, bool b_kmajor, const optional<Tensor>& A2,
+              const optional<Tensor>& B2, const optional<Tensor>& bias, bool out16, const optional<Tensor>& out,
+              bool accumulate, int64_t splitk, int64_t variant) {
+  CHECK_HIP_TENSOR(A);
+  CHECK_HIP_TENSOR(B);
+  const c10::DeviceGuard guard(A.device());
+  const int dt = dtype_code(A);
+  TORCH_CHECK(dtype_code(B) == dt && A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1,
+              "gemm16: 2-D 16-bit operands of one dtype with unit inner stride");
+  const int64_t M = a_kmajor ? A.size(1) : A.size(0), K = a_kmajor ? A.size(0) : A.size(1);
+  const int64_t N = b_kmajor ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == K, "gemm16: K mismatch");
+  PdrnnGemmArgs a{};
+  a.A = A.data_ptr();
+  a.B = B.data_ptr();
+  a.lda = A.stride(0);
+  a.ldb = B.stride(0);
+  if (A2.has_value() || B2.has_value()) {
+    TORCH_CHECK(A2.has_value() && B2.has_value(), "gemm16: A2 and B2 together");
+    const Tensor& a2 = *A2;
+    const Tensor& b2 = *B2;
+    TORCH_CHECK(dtype_code(a2) == dt && dtype_code(b2) == dt && a2.stride(1) == 1 && b2.stride(1) == 1);
+    const int64_t K2 = a_kmajor ? a2.size(0) : a2.size(1);
+    TORCH_CHECK((a_kmajor ? a2.size(1) : a2.size(0)) == M && (b_kmajor ? b2.size(1) : b2.size(0)) == N &&
+                (b_kmajor ? b2.size(0) : b2.size(1)) == K2, "gemm16: segment-2 shapes");
+    a.A2 = a2.data_ptr();
+    a.B2 = b2.data_ptr();
+    a.lda2 = a2.stride(0);
+    a.ldb2 = b2.stride(0);
+    a.K2 = (int)K2;
+  }
+  Tensor C;
+  if (splitk > 1) {
+    // fp32 partials [splitk, M, N], summed in fixed order
+    TORCH_CHECK(!out16, "gemm16: split-K gives fp32 partials");
+    C = at::empty({splitk, M, N}, A.options().dtype(at::kFloat));
+    a.splitk = (int)splitk;
+    a.c_split_stride = M * N;
+  } else if (out.has_value()) {
+    C = *out;
+    TORCH_CHECK(C.size(0) == M && C.size(1) == N && C.stride(1) == 1 &&
+                (out16 ? C.scalar_type() == A.scalar_type() : C.scalar_type() == at::kFloat), "gemm16: out");
+  } else {
+    C = at::empty({M, N}, A.options().dtype(out16 ? A.scalar_type() : at::kFloat));
+  }
+  if (bias.has_value()) {
+    TORCH_CHECK(out16 && bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N,
+                "gemm16: fp32 bias[N] with 16-bit output");
+    a.bias = bias->data_ptr<float>();
+  }
+  a.C = C.data_ptr();
+  a.ldc = splitk > 1 ? N : C.stride(0);
+  a.variant = (int)variant;
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.dtype = dt;
+  a.a_kmajor = a_kmajor;
+  a.b_kmajor = b_kmajor;
+  a.c_16bit = out16;
+  a.accumulate = splitk > 1 ? 0 : accumulate;
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && pdrnn_gemm_supported(&a),
+              "gemm16: shape not covered (K % 64, k-major M/N % 8, 16-bit output N % 8)");
+  HIP_LAUNCH_CHECK(pdrnn_gemm(&a, cur_stream()));
+  if (splitk > 1) {
+    Tensor r = C.sum(0);
+    if (out.has_value()) {
+      if (accumulate) out->add_(r);
+      else out->copy_(r);
+      return *out;
+    }
+    return r;
+  }
+  return C;
+}
+
 // C[M, N] f32 = A[M, K] Bt[N, K]^T on the MFMA core (tests).
 Tensor gemm_nt(const Tensor& A, const Tensor& Bt, int64_t tile) {
   CHECK_HIP_TENSOR(A);
@@ -1065,6 +1146,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "persistent large-H recurrence: rows-per-workgroup / 16 for this shape on the current device (0 = not covered)");
   m.def("gemm_nt", &gemm_nt, "C = A Bt^T (bf16/fp16 in, f32 out) on the MFMA tile core", py::arg("A"),
         py::arg("Bt"), py::arg("tile") = -1);
+  m.def("gemm16", &gemm16, "time-batched MFMA GEMM (kernels/gemm.hip): C = op(A) op(B) [+ A2 B2] [+ bias]",
+        py::arg("A"), py::arg("a_kmajor"), py::arg("B"), py::arg("b_kmajor"), py::arg("A2") = py::none(),
+        py::arg("B2") = py::none(), py::arg("bias") = py::none(), py::arg("out16") = false,
+        py::arg("out") = py::none(), py::arg("accumulate") = false, py::arg("splitk") = 1,
+        py::arg("variant") = 0);
+  m.def("gemm16_supported", [](int64_t M, int64_t N, int64_t K, int64_t K2, bool akm, bool bkm, bool out16) {
+    PdrnnGemmArgs a{};
+    a.M = (int)M; a.N = (int)N; a.K = (int)K; a.K2 = (int)K2; a.a_kmajor = akm; a.b_kmajor = bkm;
+    a.c_16bit = out16; a.ldc = N; a.A2 = a.B2 = K2 ? (const void*)1 : nullptr;
+    return M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && pdrnn_gemm_supported(&a) != 0;
+  });
   m.def("embedding_fwd", &embedding_fwd, py::arg("weight"), py::arg("idx"), py::arg("out_dtype") = py::none());
   m.def("embedding_bwd", &embedding_bwd);
   m.attr("offload_arch") = "gfx950";

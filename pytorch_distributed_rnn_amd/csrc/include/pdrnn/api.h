@@ -288,6 +288,29 @@ hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir,
 int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus);
 hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int mt,
                                     int* counters, int* err, int* sticky, int mode, hipStream_t stream);
+// Time-batched GEMM of the large-H layers (kernels/gemm.hip), 16-bit inputs:
+//   C[M, N] (= or +=) sum over the K segments of op(A) op(B) (+ bias[n])
+// A: a_kmajor ? element (m, k) at A[k * lda + m] : A[m * lda + k]
+// B: b_kmajor ? element (n, k) at B[k * ldb + n] : B[n * ldb + k]
+// segment 2 (K2 > 0): A2 / B2 with lda2 / ldb2, same layouts.
+// C: fp32 (accumulate: C += ...) or, with c_16bit, the input dtype (+ fp32 bias).
+typedef struct {
+  const void* A;
+  const void* B;
+  const void* A2;
+  const void* B2;
+  void* C;
+  const float* bias;
+  int64_t lda, ldb, lda2, ldb2, ldc;
+  int M, N, K, K2;
+  int dtype;  // 0 bf16, 1 fp16
+  int a_kmajor, b_kmajor, c_16bit, accumulate;
+  int splitk;              // > 1: K split over blockIdx.y, partial s at C + s * c_split_stride (fp32)
+  int64_t c_split_stride;
+  int variant;             // schedule variant (tuning)
+} PdrnnGemmArgs;
+int pdrnn_gemm_supported(const PdrnnGemmArgs* a);
+hipError_t pdrnn_gemm(const PdrnnGemmArgs* a, hipStream_t stream);
 // tile: -1 auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_gemm_nt(const void* A, int64_t lda, const void* Bt, int64_t ldb, float* C, int64_t ldc,
                          int M, int N, int K, int dtype, int tile, hipStream_t stream);

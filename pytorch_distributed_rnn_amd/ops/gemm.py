@@ -1,0 +1,118 @@
+"""Time-batched GEMMs of the large-H layers on the in-tree MFMA kernel
+(``csrc/kernels/gemm.hip``), with the library (hipBLASLt through torch) as the
+fallback for shapes the kernel does not cover, CPU tensors and fp32.
+
+* :func:`linear16`  -- ``Xp = x W^T + b`` (input projection, 16-bit out, fp32 bias);
+* :func:`mm_kk`     -- ``sum_s A_s^T B_s`` over K-major pairs, fp32 out (weight
+  gradients; a second pair folds the initial-state term of dW_hh into the same
+  launch); split-K when the output has too few 256 x 256 tiles to fill the GPU;
+* :func:`mm_nk16`   -- ``sum_s G_s W_s`` with W stored [K, N] (input gradient
+  of both directions in one launch), 16-bit out.
+
+``PDRNN_GEMM=torch`` forces the library path (A/B comparisons).
+SURVEY N1: input projection and dW/dX on the matrix cores; the reference
+trains the same cell through torch.nn.LSTM (reference: src/motion/model.py:9).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Sequence, Tuple
+
+import torch
+from torch import Tensor
+
+from .. import _ext
+
+_CUS = {}
+
+
+def _native(t: Tensor):
+    if os.environ.get("PDRNN_GEMM", "mfma") == "torch":
+        return None
+    if t.device.type != "cuda" or t.dtype not in (torch.bfloat16, torch.float16):
+        return None
+    mod = _ext.native(t.device)
+    return mod if mod is not None and hasattr(mod, "gemm16") else None
+
+
+def _variant() -> int:
+    return int(os.environ.get("PDRNN_GEMM_VARIANT", "3"))
+
+
+def _cus(dev) -> int:
+    n = _CUS.get(dev)
+    if n is None:
+        n = _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return n
+
+
+def _splitk(dev, M: int, N: int, K: int) -> int:
+    """K splits that bring the launch to >= 1.5 workgroups per CU (fp32 partials
+    summed in fixed order), at least 16 K-tiles per split."""
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    cus = _cus(dev)
+    if tiles >= cus:
+        return 1
+    s = min((3 * cus // 2 + tiles - 1) // tiles, max(1, K // (64 * 16)), 16)
+    return max(1, s)
+
+
+def _rowmajor(t: Tensor) -> bool:
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]
+
+
+def linear16(x: Tensor, w: Tensor, bias: Optional[Tensor]) -> Tensor:
+    """x [M, K] @ w[N, K]^T + bias[N] in x's dtype (fp32 bias and accumulation)."""
+    mod = _native(x)
+    M, K = x.shape
+    N = w.shape[0]
+    if mod is not None and _rowmajor(x) and _rowmajor(w) and w.dtype == x.dtype and \
+            mod.gemm16_supported(M, N, K, 0, False, False, True):
+        b = bias.float().contiguous() if bias is not None else None
+        return mod.gemm16(x, False, w, False, bias=b, out16=True, variant=_variant())
+    if bias is None:
+        return torch.mm(x, w.t())
+    return torch.addmm(bias.to(x.dtype), x, w.t())
+
+
+def mm_kk(pairs: Sequence[Tuple[Tensor, Tensor]]) -> Tensor:
+    """sum over (a [K_s, M], b [K_s, N]) of a^T b, fp32 [M, N] (1 or 2 pairs)."""
+    a, b = pairs[0]
+    mod = _native(a)
+    M, N = a.shape[1], b.shape[1]
+    K1 = a.shape[0]
+    K2 = pairs[1][0].shape[0] if len(pairs) > 1 else 0
+    ok = mod is not None and all(_rowmajor(p) and p.dtype == a.dtype for pr in pairs for p in pr) and \
+        len(pairs) <= 2 and mod.gemm16_supported(M, N, K1, K2, True, True, False)
+    if ok:
+        sk = _splitk(a.device, M, N, K1 + K2)
+        if len(pairs) == 2:
+            return mod.gemm16(a, True, b, True, A2=pairs[1][0], B2=pairs[1][1], splitk=sk, variant=_variant())
+        return mod.gemm16(a, True, b, True, splitk=sk, variant=_variant())
+    out = None
+    for a_, b_ in pairs:
+        try:
+            r = torch.mm(a_.t(), b_, out_dtype=torch.float32)
+        except (RuntimeError, TypeError):
+            r = torch.mm(a_.t().float(), b_.float())
+        out = r if out is None else out.add_(r)
+    return out
+
+
+def mm_nk16(pairs: Sequence[Tuple[Tensor, Tensor]]) -> Tensor:
+    """sum over (g [M, K_s], w [K_s, N]) of g w in g's dtype (1 or 2 pairs)."""
+    g, w = pairs[0]
+    mod = _native(g)
+    M, N = g.shape[0], w.shape[1]
+    K1 = g.shape[1]
+    K2 = pairs[1][0].shape[1] if len(pairs) > 1 else 0
+    ok = mod is not None and all(_rowmajor(p) and p.dtype == g.dtype for pr in pairs for p in pr) and \
+        len(pairs) <= 2 and mod.gemm16_supported(M, N, K1, K2, False, True, True)
+    if ok:
+        if len(pairs) == 2:
+            return mod.gemm16(g, False, w, True, A2=pairs[1][0], B2=pairs[1][1], out16=True, variant=_variant())
+        return mod.gemm16(g, False, w, True, out16=True, variant=_variant())
+    out = torch.mm(g, w)
+    for g_, w_ in pairs[1:]:
+        out.addmm_(g_, w_)
+    return out

@@ -35,6 +35,7 @@ from torch import Tensor
 
 from .. import _ext
 from .lstm_large import _interleave, _mm_f32, _mm_tn_f32, _perm, _tile
+from .gemm import linear16, mm_kk, mm_nk16
 
 
 def supported(x: Tensor, hidden: int) -> bool:
@@ -76,7 +77,7 @@ class _LargeGRULayer(torch.autograd.Function):
                 b[:2 * H] += b_hh[:2 * H].float()
                 b[3 * H:] += b_hh[2 * H:].float()
             b4.append(b[perm])
-        xp = torch.addmm(torch.cat(b4).to(cdt), x.reshape(T * B, I), torch.cat(wih4).t())
+        xp = linear16(x.reshape(T * B, I), torch.cat(wih4), torch.cat(b4))  # in-tree MFMA GEMM (16-bit)
         xp = xp.view(T, B, ndir * 4 * H)
         whh_p = [_interleave(w, H).contiguous() for w in whh4]
         h0c = h0.to(cdt).contiguous() if h0 is not None else None
@@ -104,25 +105,34 @@ class _LargeGRULayer(torch.autograd.Function):
         dgates, dh0, _ = mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1)
         grads: List[Optional[Tensor]] = []
         dx = None
+        dx_pairs = []
         need_dx = ctx.needs_input_grad[0]
         x2 = x.reshape(T * B, I)
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # [r | z | dpre_n | dpre_n r]
             hprev = _hprev(hseq[:, :, d * H:(d + 1) * H], h0c[d:d + 1] if h0c is not None else None, d)
-            dw4 = _mm_tn_f32(G, hprev.reshape(T * B, H), T)
-            dwhh = torch.cat([dw4[:2 * H], dw4[3 * H:]])
             Gx = G[:, :3 * H]                                        # x side: [r | z | dpre_n]
-            dwih = _mm_tn_f32(Gx, x2, T)
+            if cdt == torch.float32:
+                dw4 = _mm_tn_f32(G, hprev.reshape(T * B, H), T)
+                dwih = _mm_tn_f32(Gx, x2, T)
+            else:  # in-tree MFMA GEMM (ops/gemm.py)
+                dw4 = mm_kk([(G, hprev.reshape(T * B, H))])
+                dwih = mm_kk([(Gx, x2)])
+            dwhh = torch.cat([dw4[:2 * H], dw4[3 * H:]])
             cs = G.sum(0, dtype=torch.float32)
             dbih = cs[:3 * H]
             dbhh = torch.cat([cs[:2 * H], cs[3 * H:]])
             if not need_dx:
                 pass  # layer input without grad (e.g. the data): no dX GEMM
+            elif cdt != torch.float32:
+                dx_pairs.append((Gx, wih[d]))
             elif dx is None:
                 dx = torch.mm(Gx, wih[d])
             else:
                 dx.addmm_(Gx, wih[d])
             grads += [dwih, dwhh, dbih if has_w[4 * d + 2] else None, dbhh if has_w[4 * d + 3] else None]
+        if dx_pairs:
+            dx = mm_nk16(dx_pairs)  # both directions in one launch
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         return (dx.view(T, B, I) if dx is not None else None, dh0_out, None, *grads)
 

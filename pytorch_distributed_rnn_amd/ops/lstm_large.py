@@ -29,6 +29,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
+from .gemm import linear16, mm_kk, mm_nk16
 
 _PERM_CACHE = {}
 
@@ -187,7 +188,10 @@ class _LargeLSTMLayer(torch.autograd.Function):
             bias.append(b[perm])
         wih_p = _shadow_cat(w_ih, cdt, H)                                  # [ndir*4H, I]
         bias_p = torch.cat(bias, 0).to(cdt)
-        xp = torch.addmm(bias_p, x.reshape(T * B, I), wih_p.t()).view(T, B, ndir * 4 * H)
+        if cdt == torch.float32:
+            xp = torch.addmm(bias_p, x.reshape(T * B, I), wih_p.t()).view(T, B, ndir * 4 * H)
+        else:  # in-tree MFMA GEMM, fp32 bias added before the 16-bit rounding (ops/gemm.py)
+            xp = linear16(x.reshape(T * B, I), wih_p, torch.cat(bias, 0)).view(T, B, ndir * 4 * H)
         whh_p = [shadow(w, "i", cdt, H) for w in w_hh]
         h0c = h0.to(cdt).contiguous() if h0 is not None else None
         c0c = c0.float().contiguous() if c0 is not None else None
@@ -222,6 +226,8 @@ class _LargeLSTMLayer(torch.autograd.Function):
         dx = None
         need_dx = ctx.needs_input_grad[0]
         x2 = x.reshape(T * B, I)
+        if cdt != torch.float32:
+            return _backward_gemms16(ctx, dgates, dh0, dc0, hseq, h0c, x2, wih)
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
             hd = hseq[:, :, d * H:(d + 1) * H]                       # strided view, row stride ndir*H
@@ -251,6 +257,37 @@ class _LargeLSTMLayer(torch.autograd.Function):
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         dc0_out = dc0.to(c0_dtype) if has_c0 else None
         return (dx, dh0_out, dc0_out, None, *grads)
+
+
+def _backward_gemms16(ctx, dgates, dh0, dc0, hseq, h0c, x2, wih):
+    """16-bit layers: weight and input gradients on the in-tree MFMA GEMM
+    (ops/gemm.py): dW_hh = sum_t dgates_t^T h_prev(t) with the initial-state
+    pairing folded in as a second K segment, dW_ih = dG^T X, dX of both
+    directions in one launch (K segments), fp32 accumulation throughout."""
+    H, ndir, tile, rev_mask, has_w, has_h0, has_c0, h0_dtype, c0_dtype = ctx.cfg
+    T, B, I = ctx.saved_tensors[0].shape
+    grads: List[Optional[Tensor]] = []
+    Gs = []
+    for d in range(ndir):
+        G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
+        Gs.append(G)
+        hd = hseq[:, :, d * H:(d + 1) * H]                       # strided view, row stride ndir*H
+        pairs = []
+        if T > 1:
+            if d == 0:
+                pairs.append((G[B:], hd[:-1].reshape((T - 1) * B, H)))
+            else:
+                pairs.append((G[:(T - 1) * B], hd[1:].reshape((T - 1) * B, H)))
+        if h0c is not None:
+            pairs.append((G[:B] if d == 0 else G[(T - 1) * B:], h0c[d]))
+        dwhh = mm_kk(pairs) if pairs else torch.zeros(4 * H, H, device=G.device, dtype=torch.float32)
+        dwih = mm_kk([(G, x2)])
+        db = G.sum(0, dtype=torch.float32)
+        grads += [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
+    dx = mm_nk16([(Gs[d], wih[d]) for d in range(ndir)]).view(T, B, I) if ctx.needs_input_grad[0] else None
+    dh0_out = dh0.to(h0_dtype) if has_h0 else None
+    dc0_out = dc0.to(c0_dtype) if has_c0 else None
+    return (dx, dh0_out, dc0_out, None, *grads)
 
 
 def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor],
