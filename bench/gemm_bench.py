@@ -65,9 +65,10 @@ for what, M, N, K, kind in [
         fl = 2.0 * M * N * K
     err = (ours().float() - ref().float()).abs().max().item()
     tr = bench(ref)
-    tv = [bench(lambda v=v: ours(v)) for v in range(4)]
+    VARS = (3, 16)
+    tv = [bench(lambda v=v: ours(v)) for v in VARS]
     to = min(tv)
     line = (f"{what:24s} M{M} N{N} K{K}: hipBLASLt {fl / tr / 1e12:7.1f} TF/s ({tr * 1e3:7.3f} ms) | "
             f"in-tree {fl / to / 1e12:7.1f} TF/s ({to * 1e3:7.3f} ms) | x{tr / to:5.2f} | maxerr {err:.3g} | "
-            f"variants " + " ".join(f"{fl / t / 1e12:.0f}" for t in tv))
+            "variants " + " ".join(f"v{v}:{fl / t / 1e12:.0f}" for v, t in zip(VARS, tv)))
     print(line, flush=True)

@@ -22,35 +22,41 @@ def _op(t, km):
     return t.float().t() if km else t.float()
 
 
+VARIANTS = [3, 16]  # 8-wave ping-pong form, 4-wave 128x128-per-wave form
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("akm,bkm", [(False, False), (False, True), (True, True), (True, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 264, 192), (1000, 776, 448)])
-def test_gemm16_layouts_fp32_out(dtype, akm, bkm, M, N, K):
+def test_gemm16_layouts_fp32_out(dtype, akm, bkm, M, N, K, variant):
     mod = _mod()
     torch.manual_seed(M + N + K)
     A = torch.randn(*((K, M) if akm else (M, K)), device="cuda").to(dtype)
     B = torch.randn(*((K, N) if bkm else (N, K)), device="cuda").to(dtype)
-    C = mod.gemm16(A, akm, B, bkm)
+    C = mod.gemm16(A, akm, B, bkm, variant=variant)
     ref = _op(A, akm) @ _op(B, bkm).t()
     torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-3 * K ** 0.5)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_gemm16_xp_bias_16bit_out(dtype):
+def test_gemm16_xp_bias_16bit_out(dtype, variant):
     mod = _mod()
     torch.manual_seed(1)
     M, N, K = 777, 1280, 320
     X = torch.randn(M, K, device="cuda").to(dtype)
     W = torch.randn(N, K, device="cuda").to(dtype) * 0.1
     b = torch.randn(N, device="cuda")
-    C = mod.gemm16(X, False, W, False, bias=b, out16=True)
+    C = mod.gemm16(X, False, W, False, bias=b, out16=True, variant=variant)
     assert C.dtype == dtype and C.shape == (M, N)
     ref = X.float() @ W.float().t() + b
     tol = 8e-3 if dtype == torch.bfloat16 else 1e-3
     torch.testing.assert_close(C.float(), ref, rtol=tol, atol=tol * 4)
 
 
-def test_gemm16_dx_two_segments_strided():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_gemm16_dx_two_segments_strided(variant):
     """dX = G0 W0 + G1 W1 with G the two direction slices of one [M, 2*4H] tensor."""
     mod = _mod()
     torch.manual_seed(2)
@@ -59,12 +65,13 @@ def test_gemm16_dx_two_segments_strided():
     W0 = torch.randn(G4, I, device="cuda").half()
     W1 = torch.randn(G4, I, device="cuda").half()
     g0, g1 = G[:, :G4], G[:, G4:]
-    C = mod.gemm16(g0, False, W0, True, A2=g1, B2=W1, out16=True)
+    C = mod.gemm16(g0, False, W0, True, A2=g1, B2=W1, out16=True, variant=variant)
     ref = g0.float() @ W0.float() + g1.float() @ W1.float()
     torch.testing.assert_close(C.float(), ref, rtol=2e-3, atol=0.15)
 
 
-def test_gemm16_dw_segment_and_accumulate():
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_gemm16_dw_segment_and_accumulate(variant):
     """dW_hh = G[B:]^T Hprev + G[:B]^T h0 (k-major operands, strided H view), then += into an existing grad."""
     mod = _mod()
     torch.manual_seed(3)
@@ -73,12 +80,12 @@ def test_gemm16_dw_segment_and_accumulate():
     hseq = torch.randn(T * Bsz, 2 * H, device="cuda").bfloat16()
     h = hseq[:, :H]
     h0 = torch.randn(Bsz, H, device="cuda").bfloat16()
-    C = mod.gemm16(G[Bsz:], True, h[:-Bsz], True, A2=G[:Bsz], B2=h0)
+    C = mod.gemm16(G[Bsz:], True, h[:-Bsz], True, A2=G[:Bsz], B2=h0, variant=variant)
     ref = G[Bsz:].float().t() @ h[:-Bsz].float() + G[:Bsz].float().t() @ h0.float()
     torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
     base = torch.randn(G4, H, device="cuda")
     out = base.clone()
-    mod.gemm16(G, True, h, True, out=out, accumulate=True)
+    mod.gemm16(G, True, h, True, out=out, accumulate=True, variant=variant)
     torch.testing.assert_close(out, base + G.float().t() @ h.float(), rtol=1e-3, atol=1e-2)
 
 
@@ -94,23 +101,24 @@ def test_gemm16_asymmetric_identity():
     del B
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("splitk", [2, 3, 5])
-def test_gemm16_splitk_with_segment(splitk):
+def test_gemm16_splitk_with_segment(splitk, variant):
     """split-K partials (fixed-order sum) across a segment boundary, incl. accumulate into out."""
     mod = _mod()
     torch.manual_seed(4)
     K1, K2, M, N = 64 * 7, 64 * 3, 264, 520
     G, Hh = torch.randn(K1, M, device="cuda").half(), torch.randn(K1, N, device="cuda").half()
     G2, H2 = torch.randn(K2, M, device="cuda").half(), torch.randn(K2, N, device="cuda").half()
-    C = mod.gemm16(G, True, Hh, True, A2=G2, B2=H2, splitk=splitk)
+    C = mod.gemm16(G, True, Hh, True, A2=G2, B2=H2, splitk=splitk, variant=variant)
     ref = G.float().t() @ Hh.float() + G2.float().t() @ H2.float()
     torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
     out = torch.ones(M, N, device="cuda")
-    mod.gemm16(G, True, Hh, True, out=out, accumulate=True, splitk=splitk)
+    mod.gemm16(G, True, Hh, True, out=out, accumulate=True, splitk=splitk, variant=variant)
     torch.testing.assert_close(out, 1 + G.float().t() @ Hh.float(), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 16])
 def test_gemm16_schedule_variants(variant):
     mod = _mod()
     torch.manual_seed(5)
