@@ -83,7 +83,10 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void bar() { __builtin_amdgcn_s_barrier(); }
-__device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// lgkmcnt(0) through the builtin (vmcnt / expcnt fields at their maxima): the
+// compiler's waitcnt pass sees it, so it does not add its own lgkmcnt(0) in
+// front of the next MFMA for fragment reads this wait already retired
+__device__ __forceinline__ void wait_lds() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
 // k-major image swizzle (chunk units, even: chunk pairs stay together)
 __device__ __forceinline__ int kswz(int k) { return (((k & 3) | (((k >> 3) & 1) << 2)) << 1); }
