@@ -21,6 +21,7 @@ from torch import Tensor, nn
 from torch.nn import functional as F
 
 from ..ops.embedding import embedding
+from ..ops.gemm import linear
 from .rnn import LSTM
 
 
@@ -57,7 +58,7 @@ class CharLM(nn.Module):
         out, (hn, cn) = self.lstm(x, state)
         if carry:
             self._state = (hn.detach(), cn.detach())
-        return F.linear(out, self.fc.weight.to(cdt), self.fc.bias.to(cdt))
+        return linear(out, self.fc.weight, self.fc.bias)  # in-tree GEMM head (ops/gemm.py)
 
 
 class BiLSTMEncoder(nn.Module):
@@ -74,4 +75,4 @@ class BiLSTMEncoder(nn.Module):
         """x [T, B, I] -> [T, B, output_dim]."""
         cdt = self.compute_dtype if x.is_cuda else torch.float32
         out, _ = self.lstm(x.to(cdt))
-        return F.linear(out, self.fc.weight.to(cdt), self.fc.bias.to(cdt))
+        return linear(out, self.fc.weight, self.fc.bias)

@@ -116,3 +116,42 @@ def mm_nk16(pairs: Sequence[Tuple[Tensor, Tensor]]) -> Tensor:
     for g_, w_ in pairs[1:]:
         out.addmm_(g_, w_)
     return out
+
+
+class _Linear16(torch.autograd.Function):
+    """y = x W^T + b with 16-bit x, fp32 master W / b: the forward, dX and dW
+    products on the in-tree GEMM (fp32 dW / db straight into the masters'
+    gradients, no cast kernels on the backward)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        w16 = weight.detach().to(x.dtype)
+        y = linear16(x2, w16, bias.detach() if bias is not None else None)
+        ctx.save_for_backward(x2, w16)
+        ctx.has_bias = bias is not None
+        ctx.shp = shp
+        return y.view(*shp[:-1], w16.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w16 = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype).contiguous()
+        dx = mm_nk16([(dy2, w16)]).view(ctx.shp) if ctx.needs_input_grad[0] else None
+        dw = mm_kk([(dy2, x2)]) if ctx.needs_input_grad[1] else None
+        db = dy2.sum(0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
+    """F.linear(x, weight.to(x.dtype), bias.to(x.dtype)) for a 16-bit x and fp32
+    parameters; on the in-tree GEMM when the shape fits it (output width a
+    multiple of 8 and at least 128 -- a narrower head would leave most of a
+    256-wide tile idle, the library keeps those)."""
+    mod = _native(x)
+    N, K = weight.shape
+    if mod is not None and N >= 128 and N % 8 == 0 and K % 64 == 0 and x.shape[-1] == K:
+        return _Linear16.apply(x.contiguous(), weight, bias)
+    import torch.nn.functional as F
+    return F.linear(x, weight.to(x.dtype), bias.to(x.dtype) if bias is not None else None)

@@ -70,6 +70,12 @@ def test_large_gru_every_tile(tile, monkeypatch):
     _check(m, ref, x, h0)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_large_gru_pingpong_step_matches_torch(dt, monkeypatch):
+    monkeypatch.setenv("PDRNN_LSTM_LARGE_PP", "2")
+    test_large_gru_matches_torch(dt, 256, 1, True, 300, 3, 64)
+
+
 def test_large_gru_no_bias_no_state():
     m, ref = _pair(32, 128, 2, False, torch.bfloat16, bias=False, seed=6)
     x = torch.randn(6, 5, 32, device="cuda").to(torch.bfloat16)

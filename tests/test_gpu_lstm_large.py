@@ -86,6 +86,15 @@ def test_large_lstm_matches_torch(dt, H, L, bi, B, T, I):
         assert _rel(p.grad, q.grad) < 4e-2, n
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,L,bi,B,T,I", [(256, 1, True, 300, 3, 64), (512, 2, False, 520, 4, 128)])
+def test_large_lstm_pingpong_step_matches_torch(dt, H, L, bi, B, T, I, monkeypatch):
+    """The 256x256 ping-pong step kernels (two-pass cell epilogues), forced at
+    shapes below their occupancy threshold; batch not a multiple of 256."""
+    monkeypatch.setenv("PDRNN_LSTM_LARGE_PP", "2")
+    test_large_lstm_matches_torch(dt, H, L, bi, B, T, I)
+
+
 @pytest.mark.parametrize("H", [64, 128])  # 64: small fused path with bf16 inputs, 128: MFMA path
 def test_large_lstm_state_grads(H):
     torch.manual_seed(3)
