@@ -133,9 +133,11 @@ __device__ __forceinline__ uint4 frag(const uint16_t* img, int base, int ks, int
 // K-tiles [ktb, ktb + KT) of the concatenation (segment 1: K-tiles [0, KT1) of
 // A / B; segment 2: A2 / B2).  V: schedule variant bits (tuning A/B): 1 = B_n1
 // refill in Q3 instead of Q2, 2 = issue a phase's DMA after its fragment reads.
+// SEG2 = false: one K segment (the segment-switch code and the per-lane
+// values it re-derives are compiled out -- fewer registers live in the loop).
 // Returns with all LDS DMA retired and a full workgroup barrier passed: the
 // caller may reuse the 128 KiB of LDS.
-template <class DT, bool AKM, bool BKM, int V>
+template <class DT, bool AKM, bool BKM, int V, bool SEG2 = true>
 __device__ __forceinline__ void mainloop(const uint16_t* __restrict__ Ab, int64_t lda,
                                          const uint16_t* __restrict__ Bb, int64_t ldb,
                                          const uint16_t* __restrict__ A2b, int64_t lda2,
@@ -162,14 +164,14 @@ __device__ __forceinline__ void mainloop(const uint16_t* __restrict__ Ab, int64_
   auto img = [&](int s, int kind) -> uint16_t* { return smem + (s * 4 + kind) * QELEMS; };
   // tile t's quarter (kind) issue; switches to the second K segment at KT1
   auto issueA = [&](int t, int mq) {
-    if (t + ktb == KT1 && t > 0) {
+    if (SEG2 && t + ktb == KT1 && t > 0) {
       // second K segment (dW: h0 pairing, dX: second direction)
       opA.init(A2b, lda2, M, m0, true, wid, lane);
     }
     opA.issue(mq, img(t & 1, mq), wid);
   };
   auto issueB = [&](int t, int nq) {
-    if (t + ktb == KT1 && t > 0) opB.init(B2b, ldb2, N, n0, false, wid, lane);
+    if (SEG2 && t + ktb == KT1 && t > 0) opB.init(B2b, ldb2, N, n0, false, wid, lane);
     opB.issue(nq, img(t & 1, 2 + nq), wid);
   };
   // per-tile issue order: B_n0, A_m0, B_n1, A_m1 (the vmcnt counts below assume it);

@@ -727,7 +727,7 @@ __global__ void __launch_bounds__(512) lstm_large_fwd_step_pp_kernel(PdrnnLstmLa
   } else {
     const uint16_t* a16 = reinterpret_cast<const uint16_t*>(hA);
     const uint16_t* w16 = static_cast<const uint16_t*>(d.w);
-    pp::mainloop<DT, false, false, 3>(a16, lda, w16, H, a16, lda, w16, H, B, 4 * H, H / 64, 0, H / 64, m0, n0,
+    pp::mainloop<DT, false, false, 3, false>(a16, lda, w16, H, a16, lda, w16, H, B, 4 * H, H / 64, 0, H / 64, m0, n0,
                                       reinterpret_cast<uint16_t*>(smem_raw), acc);
   }
   float* cs = reinterpret_cast<float*>(smem_raw);
@@ -818,7 +818,7 @@ __global__ void __launch_bounds__(512) lstm_large_bwd_step_pp_kernel(PdrnnLstmLa
   {
     const uint16_t* g16 = static_cast<const uint16_t*>(d.dgates) + (int64_t)t * B * 4 * H;
     const uint16_t* w16 = static_cast<const uint16_t*>(d.wt);
-    pp::mainloop<DT, false, false, 3>(g16, 4 * H, w16, 4 * H, g16, 4 * H, w16, 4 * H, B, H, 4 * H / 64, 0,
+    pp::mainloop<DT, false, false, 3, false>(g16, 4 * H, w16, 4 * H, g16, 4 * H, w16, 4 * H, B, H, 4 * H / 64, 0,
                                       4 * H / 64, m0, n0, reinterpret_cast<uint16_t*>(smem_raw), acc);
   }
   float* cs = reinterpret_cast<float*>(smem_raw);
