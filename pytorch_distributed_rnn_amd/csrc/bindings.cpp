@@ -965,8 +965,10 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   const int auto_splitk = pdrnn_lstm_large_bwd_splitk((int)B, (int)H, ndir, &big);
   a.splitk = env_splitk > 0 ? env_splitk : auto_splitk;
   a.splitk_big = env_splitk > 0 ? (B >= 128 && H % 128 == 0) : big;
+  // large batch: ping-pong GEMM + cell kernel (fp32 dh through ws)
+  a.bwd_pp = (env_splitk <= 0 && a.splitk == 1) ? pdrnn_lstm_large_bwd_pp((int)B, (int)H, ndir, dt) : 0;
   Tensor ws;
-  if (a.splitk > 1) {
+  if (a.splitk > 1 || a.bwd_pp) {
     ws = at::empty({a.splitk, 2, B, H}, o32);
     a.ws = ws.data_ptr<float>();
   }

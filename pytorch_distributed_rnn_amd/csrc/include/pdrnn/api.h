@@ -270,12 +270,15 @@ typedef struct {
   int reverse_mask;        // bit d set: direction d runs time-reversed
   int splitk;              // backward: K slices (> 1 needs ws)
   int splitk_big;          // split-K tile: 0 = 32x32, 1 = 128x128
+  int bwd_pp;              // backward: ping-pong GEMM into ws, then the cell kernel (needs ws, splitk = 1)
   int cell;                // 0 = LSTM; 1 = GRU packed as [r|z|n_x|n_h] (cseq = fp32 h, acts = r,z,n,n_h)
   float* ws;               // backward split-K partials [splitk][2][B][H] fp32
 } PdrnnLstmLargeStepArgs;
 
 int pdrnn_lstm_large_supported(int H);
 int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir, int* big);
+// 1: run the backward step as the ping-pong GEMM (fp32 dh into ws) + the cell kernel
+int pdrnn_lstm_large_bwd_pp(int B, int H, int ndir, int dtype);
 // dtype 0 = bf16, 1 = fp16, 2 = fp32; tile -1 = auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
                                  hipStream_t stream);

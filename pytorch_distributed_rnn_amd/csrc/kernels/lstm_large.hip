@@ -859,6 +859,39 @@ __global__ void __launch_bounds__(512) lstm_large_bwd_step_pp_kernel(PdrnnLstmLa
   }
 }
 
+// Backward step as two launches at large batch: the ping-pong GEMM dh_t =
+// dgates_t W_hh with a plain fp32 epilogue into ws[dir][B][H] (no cell
+// epilogue registers live beside the accumulators), then
+// lstm_large_bwd_cell_kernel (S = 1).  The fused GemmPipe kernel's epilogue
+// saves the dh round trip, but its 256x128 tiles run the GEMM slower.
+template <class DT>
+__global__ void __launch_bounds__(512) lstm_large_bwd_gemm_pp_kernel(PdrnnLstmLargeStepArgs args) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int dir = blockIdx.z;
+  const PdrnnLstmLargeDir& d = args.dir[dir];
+  const int B = args.B, H = args.H, T = args.T;
+  const bool rev = args.reverse_mask & (1 << dir);
+  const int t = rev ? args.step : T - 1 - args.step;
+  const int m0 = blockIdx.y * 256, n0 = blockIdx.x * 256;
+  pp::g_f32x4 acc[8][4];
+  const uint16_t* g16 = static_cast<const uint16_t*>(d.dgates) + (int64_t)t * B * 4 * H;
+  const uint16_t* w16 = static_cast<const uint16_t*>(d.wt);
+  pp::mainloop<DT, false, false, 3, false>(g16, 4 * H, w16, 4 * H, g16, 4 * H, w16, 4 * H, B, H, 4 * H / 64, 0,
+                                           4 * H / 64, m0, n0, reinterpret_cast<uint16_t*>(smem_raw), acc);
+  float* ws = args.ws + (int64_t)dir * B * H;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = m0 + wr * 128 + i * 16 + (lane >> 4) * 4 + r;
+      if (b >= B) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ws[(int64_t)b * H + n0 + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+}
+
 // the ping-pong form: 16-bit storage, N a multiple of 256, >= one workgroup
 // per CU; forward only by default -- measured on the bi-LSTM (B 4096, H 4096,
 // fp16): forward step 1165 -> 930 us, backward 1160 -> 2353 us (its cell
@@ -916,6 +949,17 @@ inline int pick_tile(int M, int N, int ndir) {
 template <class DT, int CELL>
 hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, int tile, hipStream_t st) {
   const int N = backward ? a->H : 4 * a->H;
+  if constexpr (sizeof(typename DT::S) == 2) {
+    if (backward && a->bwd_pp && a->ws && a->splitk == 1 && a->H % 256 == 0) {
+      dim3 grid(a->H / 256, (a->B + 255) / 256, ndir);
+      hipLaunchKernelGGL((lstm_large_bwd_gemm_pp_kernel<DT>), grid, dim3(512), 131072, st, *a);
+      PDRNN_HIP_CHECK(hipGetLastError());
+      const int64_t n = (int64_t)a->B * a->H;
+      hipLaunchKernelGGL((lstm_large_bwd_cell_kernel<DT, CELL>), dim3((unsigned)((n + 255) / 256), 1, ndir), dim3(256),
+                         0, st, *a);
+      return hipGetLastError();
+    }
+  }
   if (backward && a->splitk > 1 && a->ws) {
     // S K-slices (32x32 tiles for small batches, 128x128 once the batch fills
     // them), then the fixed-order sum + cell backward
@@ -1432,6 +1476,14 @@ int pdrnn_lstm_large_supported(int H) { return H >= 64 && H % 64 == 0; }
 // fewest slices reaching one workgroup per CU (bi-LSTM h4096 B256: 2 slices,
 // -6 % step time); small batches: 32x32 tiles, slices while < 512 workgroups
 // and each slice keeps >= 8 k-tiles (char-LM h1024 B128: 4 slices).
+int pdrnn_lstm_large_bwd_pp(int B, int H, int ndir, int dtype) {
+  const char* e = getenv("PDRNN_LSTM_LARGE_PP_BWD");
+  const int env = e ? atoi(e) : 1;
+  if (!env || (dtype != 0 && dtype != 1) || H % 256) return 0;
+  if (env == 2) return 1;
+  return B >= 128 && (int64_t)(H / 256) * ((B + 255) / 256) * ndir >= 256;
+}
+
 int pdrnn_lstm_large_bwd_splitk(int B, int H, int ndir, int* big) {
   *big = 0;
   const int kt = 4 * H / 64;

@@ -71,8 +71,10 @@ def test_large_gru_every_tile(tile, monkeypatch):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_large_gru_pingpong_step_matches_torch(dt, monkeypatch):
+@pytest.mark.parametrize("bwd", ["0", "2"])
+def test_large_gru_pingpong_step_matches_torch(dt, bwd, monkeypatch):
     monkeypatch.setenv("PDRNN_LSTM_LARGE_PP", "2")
+    monkeypatch.setenv("PDRNN_LSTM_LARGE_PP_BWD", bwd)
     test_large_gru_matches_torch(dt, 256, 1, True, 300, 3, 64)
 
 
