@@ -55,6 +55,7 @@ class GradReducer {
         off += p.numel();
       }
       TORCH_CHECK(off == flat_grad->numel() && flat_grad->is_contiguous(), "flat_grad size mismatch");
+      flat_ = *flat_grad;
     }
     const int64_t n = (int64_t)params_.size();
     loc_.resize(n);
@@ -171,7 +172,16 @@ class GradReducer {
 
   // Same, each bucket reduced straight on the caller's stream (nothing to
   // overlap: the fused motion step produces every gradient in one kernel).
+  // The fused step's sync: the whole gradient is ready at once (after the
+  // BPTT), so over a flat gradient it is ONE collective -- the per-bucket
+  // split only serves the hook path that overlaps the backward, and at the
+  // 8-GPU per-rank batch each extra call is a latency-bound RCCL launch.
   void all_reduce_inline() {
+    if (flat_.defined()) {
+      comm_->all_reduce_inline(flat_, op());
+      if (average_ && !comm_->native_avg() && comm_->world() > 1) flat_.div_((double)comm_->world());
+      return;
+    }
     for (size_t b = 0; b < buckets_.size(); ++b) comm_->all_reduce_inline(buckets_[b], op());
     if (average_ && !comm_->native_avg() && comm_->world() > 1)
       for (auto& f : buckets_) f.div_((double)comm_->world());
@@ -192,6 +202,7 @@ class GradReducer {
   std::vector<at::Tensor> params_;
   std::shared_ptr<Comm> comm_;
   bool average_;
+  at::Tensor flat_;  // the flat gradient every bucket views (undefined without one)
   std::vector<std::vector<int64_t>> buckets_idx_;
   std::vector<at::Tensor> buckets_;
   std::vector<at::Tensor> views_;
