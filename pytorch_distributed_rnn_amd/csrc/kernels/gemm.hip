@@ -94,7 +94,7 @@ __device__ __forceinline__ void gemm_body(const PdrnnGemmArgs& p, const uint16_t
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  constexpr int GROUP = 8;
+  constexpr int GROUP = (V & 32) ? 4 : (V & 64) ? 16 : 8;  // tile-rows per raster group (V bits 32 / 64: tuning)
   const int per_group = GROUP * tiles_n;
   const int gidx = wg / per_group, first_m = gidx * GROUP;
   const int gsz = min(tiles_m - first_m, GROUP);
@@ -456,6 +456,8 @@ hipError_t launch(const PdrnnGemmArgs& a, hipStream_t st) {
     case 1: return launch_v<DT, AKM, BKM, 1>(a, st);
     case 2: return launch_v<DT, AKM, BKM, 2>(a, st);
     case 3: return launch_v<DT, AKM, BKM, 3>(a, st);
+    case 35: return launch_v<DT, AKM, BKM, 35>(a, st);
+    case 67: return launch_v<DT, AKM, BKM, 67>(a, st);
     default: return launch_v<DT, AKM, BKM, 0>(a, st);
   }
 }

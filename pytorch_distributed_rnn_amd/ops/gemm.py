@@ -36,7 +36,9 @@ def _native(t: Tensor):
 
 
 def _variant() -> int:
-    return int(os.environ.get("PDRNN_GEMM_VARIANT", "3"))
+    # 3: B_n1 refill in Q3 + DMA after the fragment reads; +32: raster groups of
+    # 4 tile-rows (+2-4 % over 8 on the bi-LSTM shapes, profiles/r3_gemm/raster.log)
+    return int(os.environ.get("PDRNN_GEMM_VARIANT", "35"))
 
 
 def _cus(dev) -> int:

@@ -22,7 +22,7 @@ def _op(t, km):
     return t.float().t() if km else t.float()
 
 
-VARIANTS = [3, 16]  # 8-wave ping-pong form, 4-wave 128x128-per-wave form
+VARIANTS = [3, 35, 16]  # 8-wave ping-pong form (raster groups of 8 / 4 tile-rows), 4-wave form
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
