@@ -65,7 +65,7 @@ for what, M, N, K, kind in [
         fl = 2.0 * M * N * K
     err = (ours().float() - ref().float()).abs().max().item()
     tr = bench(ref)
-    VARS = tuple(int(v) for v in os.environ.get('GEMM_VARS', '3,16').split(','))
+    VARS = tuple(int(v) for v in os.environ.get('GEMM_VARS', '3,35').split(','))
     tv = [bench(lambda v=v: ours(v)) for v in VARS]
     to = min(tv)
     line = (f"{what:24s} M{M} N{N} K{K}: hipBLASLt {fl / tr / 1e12:7.1f} TF/s ({tr * 1e3:7.3f} ms) | "

@@ -174,255 +174,6 @@ __device__ __forceinline__ void gemm_body(const PdrnnGemmArgs& p, const uint16_t
   }
 }
 
-// ---------------------------------------------------------------------------
-// Four-wave form: the same 256 x 256 tile on 4 waves (2 x 2), each wave 128 x
-// 128 outputs = 8 x 8 accumulator tiles (256 registers, one wave per SIMD).
-// Per MFMA it reads 2/3 of the LDS bytes of the 8-wave form (16 fragment
-// reads per 64 MFMAs instead of 12 per 32).  LDS is a ring of four K-half
-// images (32 k of A and of B, 16 KiB each); half-step u (= K-tile * 2 + half)
-// is DMA'd three phases ahead into ring entry u % 4, its fragments are read
-// one phase ahead into one of two register sets, and phase u issues the 64
-// MFMAs of u between them -- one barrier per half-step.
-//   NT image: [256 rows][32 k], 64-byte rows, chunk c at slot c ^ ((row >> 1) & 3)
-//   KM image: [32 k][256 rows], 512-byte rows, chunk c at slot c ^ kswz(k)
-template <bool KM>
-struct Operand4 {
-  const uint16_t* src[4];  // the wave's 4 DMA groups (1 KiB each) of a K-half image
-  int64_t hstep;           // elements to advance per K-half
-
-  __device__ __forceinline__ void init(const uint16_t* base, int64_t ld, int lim, int r0, int wid, int lane) {
-    hstep = KM ? (int64_t)32 * ld : (int64_t)32;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int g = wid * 4 + i;
-      if constexpr (!KM) {
-        const int row = g * 16 + (lane >> 2), slot = lane & 3;
-        const int c = slot ^ ((row >> 1) & 3);
-        src[i] = base + (int64_t)min(r0 + row, lim - 1) * ld + c * 8;
-      } else {
-        const int kr = g * 2 + (lane >> 5), slot = lane & 31;
-        const int c = slot ^ kswz(kr);
-        src[i] = base + (int64_t)kr * ld + min(r0 + c * 8, lim - 8);
-      }
-    }
-  }
-  __device__ __forceinline__ void skip(int halves) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) src[i] += halves * hstep;
-  }
-  __device__ __forceinline__ void issue(uint16_t* dst, int wid) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src[i],
-                                       (__attribute__((address_space(3))) void*)(dst + (wid * 4 + i) * 512), 16, 0,
-                                       0);
-      src[i] += hstep;
-    }
-  }
-};
-
-__device__ __forceinline__ uint4 frag4_row(const uint16_t* img, int row, int lane) {
-  const int r = row + (lane & 15), c = lane >> 4;
-  return *reinterpret_cast<const uint4*>(img + r * 32 + ((c ^ ((r >> 1) & 3)) << 3));
-}
-__device__ __forceinline__ uint4 frag4_tr(const uint16_t* img, int col, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int cc = col + 4 * p;
-  const int ch = cc >> 3, within = cc & 7;
-  const int k0 = 8 * g + q, k1 = k0 + 4;
-  const g_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) g_s16x4*)(img + k0 * 256 + ((ch ^ kswz(k0)) << 3) + within));
-  const g_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) g_s16x4*)(img + k1 * 256 + ((ch ^ kswz(k1)) << 3) + within));
-  uint4 r;
-  r.x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
-  r.y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
-  r.z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
-  r.w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
-  return r;
-}
-template <bool KM>
-__device__ __forceinline__ uint4 frag4(const uint16_t* img, int base, int lane) {
-  if constexpr (KM) return frag4_tr(img, base, lane);
-  else return frag4_row(img, base, lane);
-}
-
-template <class DT, bool AKM, bool BKM, bool OUT16>
-__device__ __forceinline__ void gemm4w_body(const PdrnnGemmArgs& p, const uint16_t* __restrict__ Ab,
-                                            const uint16_t* __restrict__ Bb, const uint16_t* __restrict__ A2b,
-                                            const uint16_t* __restrict__ B2b, uint16_t* smem) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-
-  const int tiles_m = (p.M + TM - 1) / TM, tiles_n = (p.N + TN - 1) / TN;
-  const int nwg = tiles_m * tiles_n;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  constexpr int GROUP = 8;
-  const int per_group = GROUP * tiles_n;
-  const int gidx = wg / per_group, first_m = gidx * GROUP;
-  const int gsz = min(tiles_m - first_m, GROUP);
-  const int tm = first_m + (wg % per_group) % gsz, tn = (wg % per_group) / gsz;
-  const int m0 = tm * TM, n0 = tn * TN;
-
-  // K-halves of the concatenated segments; split-K over blockIdx.y in whole K-tiles
-  const int KT1 = p.K / TK, KTALL = KT1 + p.K2 / TK;
-  const int ktb = (int)((int64_t)KTALL * blockIdx.y / gridDim.y);
-  const int KT = (int)((int64_t)KTALL * (blockIdx.y + 1) / gridDim.y) - ktb;
-  const int U = 2 * KT, U1 = 2 * (KT1 - ktb);  // U1: local half-step where segment 2 starts
-  Operand4<AKM> opA;
-  Operand4<BKM> opB;
-  if (ktb < KT1) {
-    opA.init(Ab, p.lda, p.M, m0, wid, lane);
-    opB.init(Bb, p.ldb, p.N, n0, wid, lane);
-    opA.skip(2 * ktb);
-    opB.skip(2 * ktb);
-  } else {
-    opA.init(A2b, p.lda2, p.M, m0, wid, lane);
-    opB.init(B2b, p.ldb2, p.N, n0, wid, lane);
-    opA.skip(2 * (ktb - KT1));
-    opB.skip(2 * (ktb - KT1));
-  }
-  auto imgA = [&](int u) -> uint16_t* { return smem + (u & 3) * 2 * QELEMS; };
-  auto imgB = [&](int u) -> uint16_t* { return smem + ((u & 3) * 2 + 1) * QELEMS; };
-  auto issue = [&](int u) {
-    if (u == U1 && u > 0) {
-      opA.init(A2b, p.lda2, p.M, m0, wid, lane);
-      opB.init(B2b, p.ldb2, p.N, n0, wid, lane);
-    }
-    opA.issue(imgA(u), wid);
-    opB.issue(imgB(u), wid);
-  };
-
-  g_f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = g_f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int arow = wr * 128, bcol = wc * 128;
-  uint4 fa0[8], fb0[8], fa1[8], fb1[8];
-  auto read = [&](int u, uint4 (&fa)[8], uint4 (&fb)[8]) {
-    const uint16_t* ia = imgA(u);
-    const uint16_t* ib = imgB(u);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = frag4<AKM>(ia, arow + i * 16, lane);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fb[j] = frag4<BKM>(ib, bcol + j * 16, lane);
-  };
-  auto mfmas = [&](const uint4 (&fa)[8], const uint4 (&fb)[8]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = DT::mfma(fa[i], fb[j], acc[i][j]);
-  };
-  // outstanding DMA half-steps issued after half-step v, at the point where u is the newest issued
-  // vmcnt = 8 glds per half-step x (newest - v)
-  auto wait_upto = [&](int ahead) {  // ahead = half-steps issued after the one waited for (0..3)
-    if (ahead >= 3) wait_vm<24>();
-    else if (ahead == 2) wait_vm<16>();
-    else if (ahead == 1) wait_vm<8>();
-    else wait_vm<0>();
-  };
-
-  // prologue: half-steps 0..3 in flight, fragments of 0 in set 0
-  const int pre = min(U, 4);
-  for (int u = 0; u < pre; ++u) issue(u);
-  wait_upto(pre - 1);
-  bar();
-  read(0, fa0, fb0);
-
-  // phase u: retire DMA(u+1), barrier, DMA(u+4) into the entry u's fragments came
-  // from, fragments of u+1 into the other set, MFMAs of u
-  for (int u = 0; u < U; u += 2) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int v = u + h;  // U is even: both halves of a K-tile always run
-      if (v + 1 < U) wait_upto(min(U - 1, v + 3) - (v + 1));
-      wait_lds();
-      bar();
-      if (v + 4 < U) issue(v + 4);
-      if (h == 0) {
-        if (v + 1 < U) read(v + 1, fa1, fb1);
-        mfmas(fa0, fb0);
-      } else {
-        if (v + 1 < U) read(v + 1, fa0, fb0);
-        mfmas(fa1, fb1);
-      }
-    }
-  }
-  wait_vm<0>();
-  wait_lds();
-  __syncthreads();
-
-  const int fr = lane & 15, fq = lane >> 4;
-  if constexpr (!OUT16) {
-    float* C = static_cast<float*>(p.C) + (int64_t)blockIdx.y * p.c_split_stride;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rb = m0 + arow + i * 16 + fq * 4;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = n0 + bcol + j * 16 + fr;
-        if (col >= p.N) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = rb + r;
-          if (row < p.M) {
-            float* dst = C + (int64_t)row * p.ldc + col;
-            *dst = p.accumulate ? *dst + acc[i][j][r] : acc[i][j][r];
-          }
-        }
-      }
-    }
-  } else {
-    uint16_t* stg = smem + wid * (128 * 128);
-    const float* bias = static_cast<const float*>(p.bias);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int lc = j * 16 + fr;
-      const float bv = bias ? bias[min(n0 + bcol + lc, p.N - 1)] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float v[4], w[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) w[r] = dpp_swap1(v[r]);
-        const bool odd = fr & 1;
-        const int c0 = lc & ~1;
-        const int rr = i * 16 + fq * 4 + (odd ? 2 : 0);
-        const float a0 = odd ? w[2] : v[0], b0 = odd ? v[2] : w[0];
-        const float a1 = odd ? w[3] : v[1], b1 = odd ? v[3] : w[1];
-        *reinterpret_cast<uint32_t*>(stg + rr * 128 + c0) =
-            (uint32_t)DT::from_f(a0) | ((uint32_t)DT::from_f(b0) << 16);
-        *reinterpret_cast<uint32_t*>(stg + (rr + 1) * 128 + c0) =
-            (uint32_t)DT::from_f(a1) | ((uint32_t)DT::from_f(b1) << 16);
-      }
-    }
-    wait_lds();
-    uint16_t* C = static_cast<uint16_t*>(p.C);
-    // 128 rows x 16 chunks of 16 B; 64 lanes -> 4 rows per pass
-#pragma unroll 4
-    for (int it = 0; it < 32; ++it) {
-      const int lr = it * 4 + (lane >> 4), ch = lane & 15;
-      const int row = m0 + arow + lr, col = n0 + bcol + ch * 8;
-      const uint4 v = *reinterpret_cast<const uint4*>(stg + lr * 128 + ch * 8);
-      if (row < p.M && col < p.N) *reinterpret_cast<uint4*>(C + (int64_t)row * p.ldc + col) = v;
-    }
-  }
-}
-
-template <class DT, bool AKM, bool BKM, bool OUT16>
-__global__ void __launch_bounds__(256) gemm4w_kernel(PdrnnGemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  gemm4w_body<DT, AKM, BKM, OUT16>(p, static_cast<const uint16_t*>(p.A), static_cast<const uint16_t*>(p.B),
-                                   static_cast<const uint16_t*>(p.A2 ? p.A2 : p.A),
-                                   static_cast<const uint16_t*>(p.B2 ? p.B2 : p.B), smem);
-}
-
 template <class DT, bool AKM, bool BKM, bool OUT16, int V>
 __global__ void __launch_bounds__(512) gemm256_kernel(PdrnnGemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -443,15 +194,6 @@ hipError_t launch_v(const PdrnnGemmArgs& a, hipStream_t st) {
 }
 template <class DT, bool AKM, bool BKM>
 hipError_t launch(const PdrnnGemmArgs& a, hipStream_t st) {
-  if (a.variant & 16) {
-    const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
-    const dim3 grid(tiles, a.splitk > 1 ? a.splitk : 1);
-    if (a.c_16bit)
-      hipLaunchKernelGGL((gemm4w_kernel<DT, AKM, BKM, true>), grid, dim3(256), LDS_BYTES, st, a);
-    else
-      hipLaunchKernelGGL((gemm4w_kernel<DT, AKM, BKM, false>), grid, dim3(256), LDS_BYTES, st, a);
-    return hipGetLastError();
-  }
   switch (a.variant) {
     case 1: return launch_v<DT, AKM, BKM, 1>(a, st);
     case 2: return launch_v<DT, AKM, BKM, 2>(a, st);

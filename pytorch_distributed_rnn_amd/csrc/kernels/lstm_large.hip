@@ -641,6 +641,29 @@ __global__ void lstm_large_bwd_cell_kernel(PdrnnLstmLargeStepArgs args) {
   cell_bwd_elem<DT, CELL>(d, B, H, T, rev, tn, cell, b, u, dh, d.dc_carry[e]);
 }
 
+// The same with 8 consecutive units per thread (16-byte loads / stores of
+// dh, acts, c, carry, dout and one store per gate block of dgates): the cell
+// half of the large-batch backward (ping-pong GEMM + cell), S = 1.
+template <class DT, int CELL>
+__global__ void __launch_bounds__(256) lstm_large_bwd_cell8_kernel(PdrnnLstmLargeStepArgs args) {
+  const int dir = blockIdx.z;
+  const PdrnnLstmLargeDir& d = args.dir[dir];
+  const int B = args.B, H = args.H, T = args.T;
+  const bool rev = args.reverse_mask & (1 << dir);
+  const int t = rev ? args.step : T - 1 - args.step;
+  const int tn = rev ? t + 1 : t - 1;
+  const bool cell = rev ? tn < T : tn >= 0;
+  const int64_t e8 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int H8 = H >> 3;
+  if (e8 >= (int64_t)B * H8) return;
+  const int b = (int)(e8 / H8), u0 = (int)(e8 - (int64_t)b * H8) * 8;
+  CellBwdOps8<DT> ops;
+  cell_bwd_load8<DT, CELL>(d, B, H, T, rev, tn, cell, b, u0, ops);
+  float dh[8];
+  ld8(args.ws + (int64_t)dir * B * H + (int64_t)b * H + u0, dh);
+  cell_bwd_compute8<DT, CELL>(d, B, H, cell, tn, b, u0, dh, ops);
+}
+
 // Cell backward of the LAST forward step (no recurrent dh yet):
 // dh = dout_T-1 + dhn, carry = dcn (LSTM) / 0 (GRU).  One thread per (b, u).
 template <class DT, int CELL>
@@ -681,7 +704,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(const typename DT
 }
 
 // ---------------------------------------------------------------------------
-// Large-batch form of the two step kernels on the ping-pong GEMM main loop
+// Large-batch form of the forward step kernel on the ping-pong GEMM main loop
 // (pdrnn/gemm_pp.h: 256 x 256 tile, 8 waves, LDS-DMA quarter ring, counted
 // vmcnt, staggered wave groups) -- the same cell epilogues as above, run in
 // two passes over the tile's row halves because a 256 x 256 fp32 C tile does
@@ -802,63 +825,6 @@ __global__ void __launch_bounds__(512) lstm_large_fwd_step_pp_kernel(PdrnnLstmLa
   }
 }
 
-template <class DT, int CELL>
-__global__ void __launch_bounds__(512) lstm_large_bwd_step_pp_kernel(PdrnnLstmLargeStepArgs args) {
-  typedef typename DT::S S;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const PdrnnLstmLargeDir& d = args.dir[blockIdx.z];
-  const int B = args.B, H = args.H, T = args.T;
-  const bool rev = args.reverse_mask & (1 << blockIdx.z);
-  const int s = args.step;
-  const int t = rev ? s : T - 1 - s;
-  const int tn = rev ? t + 1 : t - 1;
-  const bool cell = rev ? tn < T : tn >= 0;
-  const int m0 = blockIdx.y * 256, n0 = blockIdx.x * 256;
-  pp::g_f32x4 acc[8][4];
-  {
-    const uint16_t* g16 = static_cast<const uint16_t*>(d.dgates) + (int64_t)t * B * 4 * H;
-    const uint16_t* w16 = static_cast<const uint16_t*>(d.wt);
-    pp::mainloop<DT, false, false, 3, false>(g16, 4 * H, w16, 4 * H, g16, 4 * H, w16, 4 * H, B, H, 4 * H / 64, 0,
-                                      4 * H / 64, m0, n0, reinterpret_cast<uint16_t*>(smem_raw), acc);
-  }
-  float* cs = reinterpret_cast<float*>(smem_raw);
-  // the epilogue's per-thread indices derive from an opaque copy of the
-  // thread id, so the compiler cannot hoist them above the main loop (where
-  // they would hold registers the accumulators need)
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  constexpr int C8 = 32, ITEMS = 128 * C8 / 512, IB = 1;  // (register budget: see the forward)
-#pragma unroll 1
-  for (int half = 0; half < 2; ++half) {
-    pp_park<DT>(cs, acc, half);
-    __syncthreads();
-#pragma unroll 1
-    for (int i0 = 0; i0 < ITEMS; i0 += IB) {
-      CellBwdOps8<DT> ops[IB];
-#pragma unroll
-      for (int ib = 0; ib < IB; ++ib) {
-        const int e = tid + (i0 + ib) * 512;
-        const int row = e / C8, c8 = e - row * C8;
-        cell_bwd_load8<DT, CELL>(d, B, H, T, rev, tn, cell, min(m0 + half * 128 + row, B - 1), n0 + c8 * 8, ops[ib]);
-      }
-#pragma unroll
-      for (int ib = 0; ib < IB; ++ib) {
-        const int e = tid + (i0 + ib) * 512;
-        const int row = e / C8, c8 = e - row * C8;
-        const int b = m0 + half * 128 + row;
-        if (b >= B) continue;
-        float dh[8];
-        const float4 z0 = *reinterpret_cast<const float4*>(cs + row * kPpLdc + c8 * 8);
-        const float4 z1 = *reinterpret_cast<const float4*>(cs + row * kPpLdc + c8 * 8 + 4);
-        dh[0] = z0.x; dh[1] = z0.y; dh[2] = z0.z; dh[3] = z0.w;
-        dh[4] = z1.x; dh[5] = z1.y; dh[6] = z1.z; dh[7] = z1.w;
-        cell_bwd_compute8<DT, CELL>(d, B, H, cell, tn, b, n0 + c8 * 8, dh, ops[ib]);
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // Backward step as two launches at large batch: the ping-pong GEMM dh_t =
 // dgates_t W_hh with a plain fp32 epilogue into ws[dir][B][H] (no cell
 // epilogue registers live beside the accumulators), then
@@ -892,17 +858,18 @@ __global__ void __launch_bounds__(512) lstm_large_bwd_gemm_pp_kernel(PdrnnLstmLa
     }
 }
 
-// the ping-pong form: 16-bit storage, N a multiple of 256, >= one workgroup
-// per CU; forward only by default -- measured on the bi-LSTM (B 4096, H 4096,
-// fp16): forward step 1165 -> 930 us, backward 1160 -> 2353 us (its cell
-// epilogue spills in the main loop; profiles/r3_pp_step/).
-// PDRNN_LSTM_LARGE_PP=0 opts out, =2 takes both at any legal shape (tests).
+// the ping-pong forward step: 16-bit storage, 4H a multiple of 256, >= one
+// workgroup per CU (bi-LSTM B 4096, H 4096, fp16: 1165 -> 930 us per step).
+// The same fused form for the backward step measured 2353 us (its two-pass
+// cell epilogue kept too many registers live beside the accumulators and the
+// fp16 build spilled inside the main loop; profiles/r3_pp_step/) and was
+// replaced by the GEMM + cell pair below.  PDRNN_LSTM_LARGE_PP=0 opts out,
+// =2 takes it at any legal shape (tests).
 inline bool use_pp_step(int B, int N, int ndir, int dsize, bool backward) {
   const char* e = getenv("PDRNN_LSTM_LARGE_PP");
   const int env = e ? atoi(e) : 1;
-  if (!env || dsize != 2 || N % 256) return false;
+  if (!env || backward || dsize != 2 || N % 256) return false;
   if (env == 2) return true;
-  if (backward) return false;
   return B >= 128 && (int64_t)(N / 256) * ((B + 255) / 256) * ndir >= 256;
 }
 
@@ -910,10 +877,8 @@ template <class DT, int CELL>
 hipError_t launch_step_pp(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, hipStream_t st) {
   const int N = backward ? a->H : 4 * a->H;
   dim3 grid(N / 256, (a->B + 255) / 256, ndir);
-  if (backward)
-    hipLaunchKernelGGL((lstm_large_bwd_step_pp_kernel<DT, CELL>), grid, dim3(512), kPpLds, st, *a);
-  else
-    hipLaunchKernelGGL((lstm_large_fwd_step_pp_kernel<DT, CELL>), grid, dim3(512), kPpLds, st, *a);
+  if (backward) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((lstm_large_fwd_step_pp_kernel<DT, CELL>), grid, dim3(512), kPpLds, st, *a);
   return hipGetLastError();
 }
 
@@ -954,9 +919,9 @@ hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwar
       dim3 grid(a->H / 256, (a->B + 255) / 256, ndir);
       hipLaunchKernelGGL((lstm_large_bwd_gemm_pp_kernel<DT>), grid, dim3(512), 131072, st, *a);
       PDRNN_HIP_CHECK(hipGetLastError());
-      const int64_t n = (int64_t)a->B * a->H;
-      hipLaunchKernelGGL((lstm_large_bwd_cell_kernel<DT, CELL>), dim3((unsigned)((n + 255) / 256), 1, ndir), dim3(256),
-                         0, st, *a);
+      const int64_t n8 = (int64_t)a->B * a->H / 8;
+      hipLaunchKernelGGL((lstm_large_bwd_cell8_kernel<DT, CELL>), dim3((unsigned)((n8 + 255) / 256), 1, ndir),
+                         dim3(256), 0, st, *a);
       return hipGetLastError();
     }
   }

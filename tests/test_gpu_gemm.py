@@ -22,7 +22,7 @@ def _op(t, km):
     return t.float().t() if km else t.float()
 
 
-VARIANTS = [3, 35, 16]  # 8-wave ping-pong form (raster groups of 8 / 4 tile-rows), 4-wave form
+VARIANTS = [3, 35]  # ping-pong schedule with raster groups of 8 / 4 tile-rows
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -118,7 +118,7 @@ def test_gemm16_splitk_with_segment(splitk, variant):
     torch.testing.assert_close(out, 1 + G.float().t() @ Hh.float(), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 16])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 35, 67])
 def test_gemm16_schedule_variants(variant):
     mod = _mod()
     torch.manual_seed(5)

@@ -86,14 +86,14 @@ def test_large_lstm_matches_torch(dt, H, L, bi, B, T, I):
         assert _rel(p.grad, q.grad) < 4e-2, n
 
 
-@pytest.mark.parametrize("mode", ["fused", "gemm+cell"])
+@pytest.mark.parametrize("mode", ["gemmpipe", "gemm+cell"])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("H,L,bi,B,T,I", [(256, 1, True, 300, 3, 64), (512, 2, False, 520, 4, 128)])
 def test_large_lstm_pingpong_step_matches_torch(dt, H, L, bi, B, T, I, mode, monkeypatch):
     """The 256x256 ping-pong step kernels, forced at shapes below their
     occupancy threshold (batch not a multiple of 256): forward with the
-    two-pass cell epilogue, backward either fused the same way or as the
-    ping-pong GEMM into the dh workspace + the cell kernel."""
+    two-pass cell epilogue, backward either on the fused GemmPipe step kernel
+    or as the ping-pong GEMM into the dh workspace + the cell kernel."""
     monkeypatch.setenv("PDRNN_LSTM_LARGE_PP", "2")
     monkeypatch.setenv("PDRNN_LSTM_LARGE_PP_BWD", "2" if mode == "gemm+cell" else "0")
     test_large_lstm_matches_torch(dt, H, L, bi, B, T, I)
