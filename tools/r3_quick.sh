@@ -4,7 +4,7 @@ set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 tag=${1:-r3q}
-timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { tail -40 gpurun_out/${tag}_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { tail -40 gpurun_out/${tag}_tests.log; exit 1; }
 tail -1 gpurun_out/${tag}_tests.log
 for B in 1440 720 180; do
   timeout -k 10 180 python bench.py --steps 200 --warmup 20 --global-batch $B > gpurun_out/${tag}_bench$B.log 2>&1 || { tail -20 gpurun_out/${tag}_bench$B.log; exit 1; }
