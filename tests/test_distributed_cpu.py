@@ -182,3 +182,14 @@ def test_ddp_buckets_align_to_layer_direction(tmp_path):
     small = layout["0.004"]  # 4 KiB cap: groups are split, never mixed
     assert len(small) > len(big)
     assert all(len({key(n) for n in b}) == 1 for b in small), small
+
+
+def test_allreduce_sweep_tool_world2(tmp_path):
+    """bench/allreduce_sweep.py (the bucket-cap measurement) at world 2 on gloo:
+    one JSON line per message size from rank 0."""
+    import json
+    out = torchrun([os.path.join(ROOT, "bench", "allreduce_sweep.py"), "--min-kb", "4", "--max-mb", "0.02",
+                    "--iters", "2", "--warmup", "1"], nproc=2, cwd=str(tmp_path))
+    rows = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+    assert [r["bytes"] for r in rows] == [4096, 8192, 16384]
+    assert all(r["world"] == 2 and r["backend"] == "gloo" and r["us"] > 0 and r["busbw_GBs"] > 0 for r in rows)
