@@ -9,12 +9,19 @@ batch = 1440 / N, exactly like reference src/motion/trainer/distributed.py:48-49
 Data are synthetic tensors of the UCI-HAR shape ([6912, 128, 9] fp32), weights
 random-init (no network: no dataset or checkpoint download).
 
-Every timed step is the full training step of the CLI's ``distributed``
-trainer (``Trainer.train_batch``): device batch gather, fused LSTM forward,
-fused cross-entropy, fused BPTT backward, native RCCL bucketed all-reduce,
-fused Adam.  ``--warmup`` untimed steps, then ``--steps`` steps bracketed by a
-barrier + device synchronize on both sides; the MAX elapsed time over ranks
-is reported by rank 0 as ONE JSON line.
+The headline ``value`` is the reference's own metric: training sequences per
+second over whole epochs (6912 sequences / epoch time, reference
+src/motion/trainer/base.py:93-96).  The timed region is EXACTLY ``--steps``
+steps starting at an epoch boundary, in sampler order -- full batches and the
+short last batch of every epoch (1440 x 4 + 1152 at global batch 1440) -- so
+the default ``--steps 50`` is 10 whole epochs.  Every timed step is the full
+training step of the CLI's ``distributed`` trainer (``Trainer.train_batch``):
+device batch gather, fused LSTM forward, fused cross-entropy, fused BPTT
+backward, native RCCL all-reduce, fused Adam.  ``--warmup`` untimed steps
+first; the timed region is bracketed by a barrier + device synchronize on both
+sides; the MAX elapsed time over ranks is reported by rank 0 as ONE JSON line.
+``step_seq_per_s`` is a second, full-batch-only measurement (the per-step
+figure of earlier rounds).
 
     python bench.py                       # 1 GPU
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \\
@@ -111,59 +118,66 @@ def main(argv=None):
     per_rank = trainer.train_loader.batch_size
 
     loader = trainer.train_loader
+    steps_per_epoch = len(loader)
 
-    def index_stream():
-        epoch = 0
+    def epoch_batches(first_epoch):
+        """Sampler epochs first_epoch, first_epoch+1, ...: every batch of each
+        epoch in order, the short last one included (the reference's epoch)."""
+        epoch = first_epoch
         while True:
             trainer.sampler.set_epoch(epoch)
-            for bidx in loader.batch_indices():
-                if bidx.shape[0] == per_rank:  # full batches only: every timed step is global B
-                    yield bidx
+            yield from loader.batch_indices()
             epoch += 1
 
-    stream = index_stream()
+    def timed_run(batches):
+        env.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stats = None
+        for bidx in batches:
+            stats, _ = trainer.train_batch(loader.make_batch(bidx))
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        env.barrier()
+        return _max_over_ranks(time.perf_counter() - t0, dev), stats
+
     trainer.model.train()
     # one-time device setup (kernel code-object load, workspace sizing): the
     # trainer's gradient-only pre-pass, no parameter update -- the same
     # preparation the CLI runs before its timed epochs
     trainer.prepare()
+    warm = epoch_batches(0)
     for _ in range(args.warmup):
-        trainer.train_batch(loader.make_batch(next(stream)))
-    # the sampler's host-side permutations are drawn up front; the batch
-    # assembly (label gather, in-kernel feature gather) is inside the timed loop
+        trainer.train_batch(loader.make_batch(next(warm)))
+    # The timed region: EXACTLY --steps training steps starting at an epoch
+    # boundary, in the sampler's epoch order (full batches and the short last
+    # batch of every epoch).  With --steps a multiple of the steps per epoch it
+    # is E whole epochs and value = epoch_sequences * E / time: the reference's
+    # metric (6912 / Training Duration, reference src/motion/trainer/base.py:93-96,
+    # evaluation/Experiments.ipynb:49).  The host permutations are drawn up
+    # front (the CLI trainer prefetches them during the previous epoch); the
+    # batch assembly is inside the timed loop.
+    stream = epoch_batches(1000)
     timed = [next(stream) for _ in range(args.steps)]
-    env.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for bidx in timed:
-        trainer.train_batch(loader.make_batch(bidx))
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    env.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = _max_over_ranks(elapsed, dev)
-
-    global_batch = per_rank * world
-    seqs = global_batch * args.steps
+    local_seqs = sum(int(b.numel()) for b in timed)
+    elapsed, stats = timed_run(timed)
+    seqs = local_seqs * world  # every rank runs the same batch sizes (per-rank batch = global / world)
     value = seqs / elapsed
     ms = elapsed / args.steps * 1e3
+    epochs = args.steps / steps_per_epoch
+    global_batch = per_rank * world
     base = BASELINE_SEQ_PER_S.get(world)
-    # one real epoch after the timed steps (every batch of the sampler's
-    # permutation, the short last one included), timed the same way: the
-    # reference's own metric is a 1-epoch duration (fabfile.py:48-66)
-    trainer.sampler.set_epoch(10_000)
-    epoch_batches = loader.batch_indices()
-    env.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for bidx in epoch_batches:
-        stats, _ = trainer.train_batch(loader.make_batch(bidx))
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    env.barrier()
-    epoch_s = _max_over_ranks(time.perf_counter() - t0, dev)
+    # secondary: full-batch step throughput (the short last batch skipped),
+    # the per-step figure of earlier rounds
+    full = []
+    stream = epoch_batches(2000)
+    while len(full) < args.steps:
+        b = next(stream)
+        if b.numel() == per_rank:
+            full.append(b)
+    step_elapsed, _ = timed_run(full)
+    step_value = per_rank * world * args.steps / step_elapsed
     # sanity: loss must be finite after training
     loss = float(stats[0])
     if rank == 0:
@@ -188,8 +202,13 @@ def main(argv=None):
                 "trainer": args.trainer,
                 "per_gpu_batch": per_rank,
             },
-            "epoch_time_s": round(epoch_s, 6),
+            "epochs": round(epochs, 4),
+            "steps_per_epoch": steps_per_epoch,
+            "epoch_time_s": round(elapsed / epochs, 6),
             "epoch_sequences": n_train,
+            "timed_sequences": seqs,
+            "step_seq_per_s": round(step_value, 2),
+            "step_ms_full_batch": round(step_elapsed / args.steps * 1e3, 4),
             "final_loss": round(loss, 6),
             "baseline_seq_per_s": base,
         }

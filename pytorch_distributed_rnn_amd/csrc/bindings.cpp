@@ -515,10 +515,11 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.dhn = dh_top.data_ptr<float>(); bk.dhn_top_only = 1;
   bk.slab = slab.data_ptr<float>(); bk.P = L.P;
   bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL; bk.cell = (int)cell;
-  int grid_dw = gridb;
+  int grid_dw = gridb, nb_dw = (int)nb_bwd;
   Tensor xg;
   if (dwout) {
-    grid_dw = pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B);
+    nb_dw = pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B);
+    grid_dw = pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb_dw);
     TORCH_CHECK(grid_dw > 0, "deferred-dW backward: no resident grid");
     if (st_f.defined()) {
       st_b = at::zeros({grid_dw, 8}, opts.dtype(at::kLong));
@@ -533,7 +534,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   }
   if (st_b.defined()) bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
   if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
-  else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, st));
+  else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, nb_dw, st));
   else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
   if (dwout) {
     PdrnnLstmSmallDwArgs dw{};
@@ -550,7 +551,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   if (st_f.defined()) {
     report_stamps("fwd(head step)", st_f, (int)(T + NL - 1));
     report_stamps(dwout ? "bwd(head step, lean, deferred dW)" : "bwd(head step, lean)", st_b,
-                  (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_bwd - 1) / ((int64_t)grid_dw * nb_bwd)));
+                  (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_dw - 1) / ((int64_t)grid_dw * nb_dw)));
   }
 
   // PDRNN_ONE_PASS_REDUCE=0: the two-pass reduction (A/B measurements)
@@ -1110,6 +1111,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     const int mode = pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T);
     return split_bwd == 1 && ((gridb < B && mode == 1) || mode == 2);
   }, "the fused training step defers the weight gradients to the matrix-core dW kernel for this shape");
+  m.def("lstm_small_dwout_geometry", [](int64_t H, int64_t NL, int64_t T, int64_t B) {
+    const int nb = pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B);
+    return py::make_tuple(nb, pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb));
+  }, "(sequences per workgroup, grid) of the deferred-dW backward for this shape");
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });

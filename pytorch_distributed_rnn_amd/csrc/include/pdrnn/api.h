@@ -128,9 +128,11 @@ int pdrnn_lstm_small_dw_chunks(int H, int NL, int B, int T);
 hipError_t pdrnn_lstm_small_dw(const PdrnnLstmSmallDwArgs* a, int H, hipStream_t stream);
 // BPTT of the lean fused-step contract with the weight gradients deferred to
 // pdrnn_lstm_small_dw (a->dg_out set, a->slab unused); grid <= 0: persistent
-// grid of the resident capacity (query with pdrnn_lstm_small_bwd_dwout_grid).
-hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int grid, hipStream_t stream);
-int pdrnn_lstm_small_bwd_dwout_grid(int H, int NL, int T, int B);
+// grid of the resident capacity (query with pdrnn_lstm_small_bwd_dwout_grid);
+// nb = sequences per workgroup (1 or 2: pdrnn_lstm_small_bwd_dwout_nb).
+hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int grid, int nb, hipStream_t stream);
+int pdrnn_lstm_small_bwd_dwout_nb(int H, int NL, int T, int B);
+int pdrnn_lstm_small_bwd_dwout_grid(int H, int NL, int T, int B, int nb);
 
 // Query the launch geometry chosen for (H, B): returns grid size (number of slab rows).
 int pdrnn_lstm_small_grid(int H, int B, int nb);

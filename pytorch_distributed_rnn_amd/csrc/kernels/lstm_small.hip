@@ -1341,9 +1341,16 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_gs_kernel(PdrnnLstmSmallBw
 }
 
 // Lean BPTT with the weight gradients deferred to lstm_small_dw.hip.
-template <int H, int L, bool XLDS, int CELL>
-__global__ void __launch_bounds__(512) lstm_small_bwd_dwout_kernel(PdrnnLstmSmallBwdArgs a) {
-  lstm_small_bwd_gs_body<H, L, 1, XLDS, true, CELL, true>(a);
+// NB = 2: two sequences per workgroup share the register-resident W columns
+// (64 of the ~147 VGPRs of a lane), so a workgroup carries twice the batch at
+// about the same register cost: B = 1440 (1152) fits ONE residency round of
+// 720 (576) workgroups at 3 waves per SIMD instead of two rounds of one
+// sequence each -- the recurrence's 130 dependent steps are paid once, each
+// step issuing both sequences' independent chains.
+template <int H, int L, int NB, bool XLDS, int CELL>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB > 1 ? 3 : 1)))
+lstm_small_bwd_dwout_kernel(PdrnnLstmSmallBwdArgs a) {
+  lstm_small_bwd_gs_body<H, L, NB, XLDS, true, CELL, true>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1750,7 +1757,7 @@ hipError_t launch_step_gs(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBw
 template <int H>
 constexpr int dwout_lanes() { return H >= 64 ? 8 : 4; }
 
-template <int H, bool XLDS, int CELL>
+template <int H, int NB, bool XLDS, int CELL>
 int bwd_dwout_resident(int NL, size_t lds) {
   constexpr int L = dwout_lanes<H>();
   static thread_local int c_dev = -1, c_nl = -1, c_val = 0;
@@ -1759,49 +1766,76 @@ int bwd_dwout_resident(int NL, size_t lds) {
   hipGetDevice(&dev);
   if (dev == c_dev && NL == c_nl && lds == c_lds) return c_val;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_small_bwd_dwout_kernel<H, L, XLDS, CELL>, NL * H * L, lds);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_small_bwd_dwout_kernel<H, L, NB, XLDS, CELL>,
+                                               NL * H * L, lds);
   if (per_cu < 1) per_cu = 1;
   if (cus < 1) cus = 1;
   c_dev = dev; c_nl = NL; c_lds = lds; c_val = per_cu * cus;
   return c_val;
 }
 
+template <int H, int NB>
+int bwd_dwout_cap(int NL, int T, int cell) {
+  const size_t lds = bwd_gs_lds<H, NB>(NL), xbytes = bwd_gs_xbytes<H, NB>(T);
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  return cell == 1 ? (xl ? bwd_dwout_resident<H, NB, true, 1>(NL, lds + xbytes)
+                         : bwd_dwout_resident<H, NB, false, 1>(NL, lds))
+                   : (xl ? bwd_dwout_resident<H, NB, true, 0>(NL, lds + xbytes)
+                         : bwd_dwout_resident<H, NB, false, 0>(NL, lds));
+}
+
+// Sequences per workgroup of the deferred-dW backward: 2 when pairing the
+// sequences takes fewer residency rounds than one per workgroup (B = 1152 /
+// 1440 at H = 32: one round instead of two), else 1.  PDRNN_DWOUT_NB=1|2
+// forces one (A/B measurements).
+template <int H>
+int bwd_dwout_nb(int NL, int T, int B, int cell) {
+  const char* e = getenv("PDRNN_DWOUT_NB");  // per call: tests flip it in-process
+  const int env = e ? atoi(e) : 0;
+  if (env == 1 || env == 2) return env;
+  if (H > 32 || NL * H * dwout_lanes<H>() > 512) return 1;
+  const int cap1 = bwd_dwout_cap<H, 1>(NL, T, cell), cap2 = bwd_dwout_cap<H, 2>(NL, T, cell);
+  const int r1 = (B + cap1 - 1) / cap1, r2 = ((B + 1) / 2 + cap2 - 1) / cap2;
+  return r2 < r1 ? 2 : 1;
+}
+
 // Balanced persistent grid: the fewest residency rounds, then the fewest
 // workgroups that still finish in that many rounds -- every workgroup walks
-// the same number of sequences (B = 1440 at 768 resident: 720 x 2, not a
+// the same number of batch tiles (B = 1440 at 768 resident: 720 x 2, not a
 // second round of 672 behind a first of 768), and fewer co-resident waves
 // make each recurrence step cheaper.
 template <int H>
-int bwd_dwout_grid(int NL, int T, int B, int cell) {
-  const size_t lds = bwd_gs_lds<H, 1>(NL), xbytes = bwd_gs_xbytes<H, 1>(T);
+int bwd_dwout_grid(int NL, int T, int B, int cell, int nb) {
+  const int cap = nb == 2 ? bwd_dwout_cap<H, 2>(NL, T, cell) : bwd_dwout_cap<H, 1>(NL, T, cell);
+  const int tiles = (B + nb - 1) / nb;
+  if (tiles <= cap) return tiles;
+  const int rounds = (tiles + cap - 1) / cap;
+  return (tiles + rounds - 1) / rounds;
+}
+
+template <int H, int NB>
+hipError_t launch_bwd_dwout_nb(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid) {
+  constexpr int L = dwout_lanes<H>();
+  const int block = a->NL * H * L;
+  const size_t lds = bwd_gs_lds<H, NB>(a->NL), xbytes = bwd_gs_xbytes<H, NB>(a->T);
   const bool xl = xbytes <= (size_t)kXldsBytes;
-  const int cap = cell == 1 ? (xl ? bwd_dwout_resident<H, true, 1>(NL, lds + xbytes)
-                                  : bwd_dwout_resident<H, false, 1>(NL, lds))
-                            : (xl ? bwd_dwout_resident<H, true, 0>(NL, lds + xbytes)
-                                  : bwd_dwout_resident<H, false, 0>(NL, lds));
-  if (B <= cap) return B;
-  const int rounds = (B + cap - 1) / cap;
-  return (B + rounds - 1) / rounds;
+  if (!xl || !a->xg_out) return hipErrorInvalidConfiguration;  // x staged once per sequence (writes xg_out)
+  if (grid <= 0) grid = bwd_dwout_grid<H>(a->NL, a->T, a->B, a->cell, NB);
+  if (a->cell == 1) hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, NB, true, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  else hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, NB, true, 0>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  return hipGetLastError();
 }
 
 template <int H>
-hipError_t launch_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid) {
+hipError_t launch_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid, int nb) {
   constexpr int L = dwout_lanes<H>();
   if (a->NL * H * L > 512) return hipErrorInvalidConfiguration;
   if (!bwd_lean(a) || !a->dg_out || a->dg_st < 4 * H) return hipErrorInvalidValue;
-  const int block = a->NL * H * L;
-  const size_t lds = bwd_gs_lds<H, 1>(a->NL), xbytes = bwd_gs_xbytes<H, 1>(a->T);
-  const bool xl = xbytes <= (size_t)kXldsBytes;
-  if (!xl || !a->xg_out) return hipErrorInvalidConfiguration;  // x staged once per sequence (writes xg_out)
-  if (grid <= 0) grid = bwd_dwout_grid<H>(a->NL, a->T, a->B, a->cell);
-  if (a->cell == 1) {
-    if (xl) hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, true, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
-    else hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, false, 1>), dim3(grid), dim3(block), lds, st, *a);
-  } else {
-    if (xl) hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, true, 0>), dim3(grid), dim3(block), lds + xbytes, st, *a);
-    else hipLaunchKernelGGL((lstm_small_bwd_dwout_kernel<H, L, false, 0>), dim3(grid), dim3(block), lds, st, *a);
+  if (nb == 2) {
+    if constexpr (H <= 32) return launch_bwd_dwout_nb<H, 2>(a, st, grid);
+    return hipErrorInvalidConfiguration;
   }
-  return hipGetLastError();
+  return launch_bwd_dwout_nb<H, 1>(a, st, grid);
 }
 
 }  // namespace
@@ -1822,23 +1856,34 @@ int pdrnn_lstm_small_dwout_ok(int H, int NL, int T) {
   return NL * H * (H >= 64 ? 8 : 4) <= 512 ? mode : 0;
 }
 
-int pdrnn_lstm_small_bwd_dwout_grid(int H, int NL, int T, int B) {
+int pdrnn_lstm_small_bwd_dwout_nb(int H, int NL, int T, int B) {
   // LSTM and GRU instantiations share the register budget (same VGPR class);
   // the LSTM's is the one queried
   switch (H) {
-    case 16: return pdrnn::bwd_dwout_grid<16>(NL, T, B, 0);
-    case 32: return pdrnn::bwd_dwout_grid<32>(NL, T, B, 0);
-    case 64: return pdrnn::bwd_dwout_grid<64>(NL, T, B, 0);
+    case 16: return pdrnn::bwd_dwout_nb<16>(NL, T, B, 0);
+    case 32: return pdrnn::bwd_dwout_nb<32>(NL, T, B, 0);
+    case 64: return pdrnn::bwd_dwout_nb<64>(NL, T, B, 0);
     default: return -1;
   }
 }
 
-hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int grid, hipStream_t stream) {
-  if (a->x_bf16 && (size_t)a->T * H * sizeof(float) > (size_t)pdrnn::kXldsBytes) return hipErrorInvalidConfiguration;
+int pdrnn_lstm_small_bwd_dwout_grid(int H, int NL, int T, int B, int nb) {
   switch (H) {
-    case 16: return pdrnn::launch_bwd_dwout<16>(a, stream, grid);
-    case 32: return pdrnn::launch_bwd_dwout<32>(a, stream, grid);
-    case 64: return pdrnn::launch_bwd_dwout<64>(a, stream, grid);
+    case 16: return pdrnn::bwd_dwout_grid<16>(NL, T, B, 0, nb);
+    case 32: return pdrnn::bwd_dwout_grid<32>(NL, T, B, 0, nb);
+    case 64: return pdrnn::bwd_dwout_grid<64>(NL, T, B, 0, nb);
+    default: return -1;
+  }
+}
+
+hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int grid, int nb, hipStream_t stream) {
+  if (a->x_bf16 && (size_t)a->T * H * sizeof(float) * (nb > 1 ? nb : 1) > (size_t)pdrnn::kXldsBytes)
+    return hipErrorInvalidConfiguration;
+  if (nb != 1 && nb != 2) return hipErrorInvalidValue;
+  switch (H) {
+    case 16: return pdrnn::launch_bwd_dwout<16>(a, stream, grid, nb);
+    case 32: return pdrnn::launch_bwd_dwout<32>(a, stream, grid, nb);
+    case 64: return pdrnn::launch_bwd_dwout<64>(a, stream, grid, nb);
     default: return hipErrorInvalidValue;
   }
 }

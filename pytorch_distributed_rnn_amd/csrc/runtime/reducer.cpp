@@ -37,8 +37,11 @@ class GradReducer {
   // groups (optional, one id per param): a bucket never spans two groups --
   // the DDP wrapper gives every (RNN layer, direction) its own id, so a
   // layer's buckets launch as soon as that layer's weight gradients exist
-  // instead of waiting for the first parameters of the layer below; a group
-  // larger than the cap is subdivided.
+  // instead of waiting for the first parameters of the layer below.
+  // A parameter larger than the cap is split into ceil(bytes / cap) equal
+  // sub-tensor buckets (narrow views of its gradient, 4 KiB-aligned): a
+  // 512 MiB bi-LSTM weight becomes 16 all-reduces of 32 MiB that pipeline on
+  // the ring instead of one message whose first byte waits for the last.
   GradReducer(std::vector<at::Tensor> params, std::shared_ptr<Comm> comm, int64_t bucket_cap_bytes,
               int64_t first_bucket_cap_bytes, bool average, c10::optional<at::Tensor> flat_grad,
               std::vector<int64_t> groups = {})
@@ -58,8 +61,9 @@ class GradReducer {
       flat_ = *flat_grad;
     }
     const int64_t n = (int64_t)params_.size();
-    loc_.resize(n);
-    // Reverse order bucketing, split on dtype/device change or cap.
+    // Reverse order bucketing, split on dtype/device/group change or cap.
+    // chunk_[b] = (offset, length) in elements when bucket b is a slice of one
+    // oversized parameter, (-1, 0) for a bucket of whole parameters.
     std::vector<int64_t> cur;
     int64_t cur_bytes = 0;
     at::ScalarType cur_dtype = at::kFloat;
@@ -68,14 +72,28 @@ class GradReducer {
     auto close = [&]() {
       if (cur.empty()) return;
       buckets_idx_.push_back(cur);
+      chunk_.push_back({-1, 0});
       cur.clear();
       cur_bytes = 0;
     };
     for (int64_t i = n - 1; i >= 0; --i) {
       const auto& p = params_[i];
-      const int64_t cap = buckets_idx_.empty() ? first_bucket_cap_bytes : bucket_cap_bytes;
+      const int64_t cap = std::max<int64_t>(buckets_idx_.empty() ? first_bucket_cap_bytes : bucket_cap_bytes, 1);
       const int64_t bytes = p.numel() * p.element_size();
       const int64_t grp = groups.empty() ? 0 : groups[i];
+      if (bytes > cap && p.numel() > 1) {
+        close();
+        // equal chunks rounded up to 4 KiB, issued from the parameter's end
+        const int64_t k = (bytes + cap - 1) / cap;
+        const int64_t align = std::max<int64_t>(4096 / p.element_size(), 1);
+        const int64_t len = ((p.numel() + k - 1) / k + align - 1) / align * align;
+        for (int64_t c = (p.numel() + len - 1) / len - 1; c >= 0; --c) {
+          buckets_idx_.push_back({i});
+          chunk_.push_back({c * len, std::min(len, p.numel() - c * len)});
+        }
+        cur_dtype = p.scalar_type(); cur_dev = p.device(); cur_group = grp;
+        continue;
+      }
       if (!cur.empty() && (p.scalar_type() != cur_dtype || p.device() != cur_dev || grp != cur_group ||
                            cur_bytes + bytes > cap))
         close();
@@ -84,7 +102,26 @@ class GradReducer {
       cur_bytes += bytes;
     }
     close();
+    views_.resize(n);
+    param_buckets_.assign(n, {});
+    std::map<int64_t, at::Tensor> own;  // non-flat: the gradient buffer of a split parameter
     for (size_t b = 0; b < buckets_idx_.size(); ++b) {
+      for (int64_t i : buckets_idx_[b]) param_buckets_[i].push_back((int64_t)b);
+      if (chunk_[b].first >= 0) {
+        const int64_t i = buckets_idx_[b][0];
+        const auto& p = params_[i];
+        if (use_flat) {
+          buckets_.push_back(flat_grad->narrow(0, flat_off[i] + chunk_[b].first, chunk_[b].second));
+          views_[i] = flat_grad->narrow(0, flat_off[i], p.numel()).view(p.sizes());
+        } else {
+          auto it = own.find(i);
+          if (it == own.end())
+            it = own.emplace(i, at::zeros({p.numel()}, p.options().requires_grad(false))).first;
+          buckets_.push_back(it->second.narrow(0, chunk_[b].first, chunk_[b].second));
+          views_[i] = it->second.view(p.sizes());
+        }
+        continue;
+      }
       int64_t total = 0;
       for (int64_t i : buckets_idx_[b]) total += params_[i].numel();
       if (use_flat) {
@@ -92,21 +129,17 @@ class GradReducer {
         const int64_t lo = buckets_idx_[b].back();
         const int64_t start = flat_off[lo];
         buckets_.push_back(flat_grad->narrow(0, start, total));
-        for (int64_t i : buckets_idx_[b]) loc_[i] = {(int64_t)b, flat_off[i] - start};
+        for (int64_t i : buckets_idx_[b])
+          views_[i] = buckets_[b].narrow(0, flat_off[i] - start, params_[i].numel()).view(params_[i].sizes());
       } else {
         auto flat = at::zeros({total}, params_[buckets_idx_[b][0]].options().requires_grad(false));
         int64_t off = 0;
         for (int64_t i : buckets_idx_[b]) {
-          loc_[i] = {(int64_t)b, off};
+          views_[i] = flat.narrow(0, off, params_[i].numel()).view(params_[i].sizes());
           off += params_[i].numel();
         }
         buckets_.push_back(flat);
       }
-    }
-    views_.resize(n);
-    for (int64_t i = 0; i < n; ++i) {
-      const auto& p = params_[i];
-      views_[i] = buckets_[loc_[i].first].narrow(0, loc_[i].second, p.numel()).view(p.sizes());
     }
     pending_.resize(buckets_.size());
     ready_.assign(n, 0);
@@ -116,6 +149,7 @@ class GradReducer {
   const std::vector<at::Tensor>& grad_views() const { return views_; }
   const std::vector<at::Tensor>& buckets() const { return buckets_; }
   const std::vector<std::vector<int64_t>>& bucket_indices() const { return buckets_idx_; }
+  const std::vector<std::pair<int64_t, int64_t>>& bucket_chunks() const { return chunk_; }
 
   void reset() {
     for (size_t b = 0; b < buckets_.size(); ++b) pending_[b] = (int64_t)buckets_idx_[b].size();
@@ -135,20 +169,17 @@ class GradReducer {
     }
     if (ready_[i]) return repoint;  // grad accumulated twice in one backward (shared weight)
     ready_[i] = 1;
-    const int64_t b = loc_[i].first;
-    if (--pending_[b] == 0) launch_ready();
+    for (int64_t b : param_buckets_[i]) --pending_[b];
+    launch_ready();
     return repoint;
   }
 
   void finalize() {
     // Params that received no gradient this iteration contribute zeros.
-    for (size_t b = 0; b < buckets_.size(); ++b) {
-      for (int64_t i : buckets_idx_[b]) {
-        if (!ready_[i]) {
-          ready_[i] = 1;
-          --pending_[b];
-        }
-      }
+    for (size_t i = 0; i < params_.size(); ++i) {
+      if (ready_[i]) continue;
+      ready_[i] = 1;
+      for (int64_t b : param_buckets_[i]) --pending_[b];
     }
     launch_ready();
     comm_->wait();
@@ -206,7 +237,8 @@ class GradReducer {
   std::vector<std::vector<int64_t>> buckets_idx_;
   std::vector<at::Tensor> buckets_;
   std::vector<at::Tensor> views_;
-  std::vector<std::pair<int64_t, int64_t>> loc_;
+  std::vector<std::pair<int64_t, int64_t>> chunk_;     // per bucket: (offset, length) of a split parameter
+  std::vector<std::vector<int64_t>> param_buckets_;    // per parameter: the buckets it feeds
   std::vector<int64_t> pending_;
   std::vector<char> ready_;
   int64_t next_ = 0;
@@ -367,6 +399,7 @@ void register_runtime(py::module_& m) {
       .def("grad_views", &GradReducer::grad_views)
       .def("buckets", &GradReducer::buckets)
       .def("bucket_indices", &GradReducer::bucket_indices)
+      .def("bucket_chunks", &GradReducer::bucket_chunks)
       .def("mark_ready", &GradReducer::mark_ready)
       .def("finalize", &GradReducer::finalize)
       .def("reset", &GradReducer::reset)

@@ -64,8 +64,10 @@ def param_group_ids(module: nn.Module, params) -> List[int]:
 
 
 def format_bucket_layout(layout) -> str:
-    return "; ".join(f"#{b['bucket']} {b['mib']:.2f} MiB {b['params']} params [{', '.join(b['names'])}]"
-                     for b in layout)
+    def one(b):
+        sl = f" elements {b['slice'][0]}:{b['slice'][1]}" if "slice" in b else ""
+        return f"#{b['bucket']} {b['mib']:.2f} MiB {b['params']} params [{', '.join(b['names'])}]{sl}"
+    return "; ".join(one(b) for b in layout)
 
 
 class _PyReducer:
@@ -160,12 +162,19 @@ class DistributedDataParallel(nn.Module):
             idx = [list(range(len(self.flat.params) - 1, -1, -1))]
         else:
             idx = [list(b) for b in self.reducer.bucket_indices()]
+        # (offset, length) of a bucket that is a slice of one oversized parameter
+        chunks = list(self.reducer.bucket_chunks()) if hasattr(self.reducer, "bucket_chunks") else \
+            [(-1, 0)] * len(idx)
         out = []
         for b, ids in enumerate(idx):
             ps = [self.flat.params[i] for i in ids]
-            out.append({"bucket": b, "params": len(ps),
-                        "mib": sum(p.numel() * p.element_size() for p in ps) / 2 ** 20,
-                        "names": [names.get(id(p), "?") for p in ps]})
+            off, length = chunks[b]
+            nbytes = length * ps[0].element_size() if off >= 0 else sum(p.numel() * p.element_size() for p in ps)
+            ent = {"bucket": b, "params": len(ps), "mib": nbytes / 2 ** 20,
+                   "names": [names.get(id(p), "?") for p in ps]}
+            if off >= 0:
+                ent["slice"] = [int(off), int(off + length)]
+            out.append(ent)
         return out
 
     # -------------------------------------------------------------- sync

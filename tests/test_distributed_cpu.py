@@ -184,6 +184,54 @@ def test_ddp_buckets_align_to_layer_direction(tmp_path):
     assert all(len({key(n) for n in b}) == 1 for b in small), small
 
 
+def test_ddp_splits_oversized_parameter_across_buckets(tmp_path):
+    """a parameter larger than the bucket cap is spread
+    over several sub-tensor buckets (512 MiB weight at a 32 MiB cap: 16
+    slices) and the all-reduced gradient is still the average of the ranks'
+    gradients.  World 2, gloo."""
+    script = tmp_path / "split.py"
+    script.write_text(
+        "import json, os, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch\n"
+        "from pytorch_distributed_rnn_amd.parallel import env\n"
+        "from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel\n"
+        "from pytorch_distributed_rnn_amd.utils.flat import flatten_module\n"
+        "env.init_distributed('gloo')\n"
+        "rank, world = env.get_rank(), env.get_world_size()\n"
+        "torch.manual_seed(0)\n"
+        "m = torch.nn.Sequential(torch.nn.Linear(8192, 16384), torch.nn.Linear(16384, 4))\n"
+        "flatten_module(m)\n"
+        "d = DistributedDataParallel(m, bucket_cap_mb=32, first_bucket_cap_mb=32)\n"
+        "lay = d.bucket_layout()\n"
+        "def batch(r):\n"
+        "    g = torch.Generator().manual_seed(100 + r)\n"
+        "    return torch.randn(2, 8192, generator=g)\n"
+        "d(batch(rank)).square().sum().backward()\n"
+        "w = m[0].weight.grad.clone()\n"
+        "ref = torch.zeros_like(w)\n"
+        "for r in range(world):\n"
+        "    m2 = torch.nn.Sequential(torch.nn.Linear(8192, 16384), torch.nn.Linear(16384, 4))\n"
+        "    m2.load_state_dict(m.state_dict())\n"
+        "    m2(batch(r)).square().sum().backward()\n"
+        "    ref += m2[0].weight.grad / world\n"
+        "    del m2\n"
+        "err = float((w - ref).abs().max() / ref.abs().max())\n"
+        "if rank == 0:\n"
+        "    open('split.json', 'w').write(json.dumps({'layout': [{k: b[k] for k in ('names', 'mib') if k in b} |"
+        " {'slice': b.get('slice')} for b in lay], 'err': err}))\n"
+        "env.shutdown()\n")
+    torchrun([str(script)], nproc=2, cwd=str(tmp_path), timeout=600)
+    out = json.loads((tmp_path / "split.json").read_text())
+    w_buckets = [b for b in out["layout"] if b["names"] == ["0.weight"]]
+    assert len(w_buckets) == 16, out["layout"]
+    assert all(b["slice"] is not None and b["mib"] <= 32.0 for b in w_buckets)
+    spans = sorted(tuple(b["slice"]) for b in w_buckets)
+    assert spans[0][0] == 0 and spans[-1][1] == 8192 * 16384
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert out["err"] < 1e-6, out["err"]
+
+
 def test_allreduce_sweep_tool_world2(tmp_path):
     """bench/allreduce_sweep.py (the bucket-cap measurement) at world 2 on gloo:
     one JSON line per message size from rank 0."""

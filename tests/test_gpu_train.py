@@ -199,6 +199,42 @@ def test_deferred_dw_gradients_match_fp64(cell, hidden, layers, seq, monkeypatch
         assert (g - r.grad).abs().max().item() <= 2e-6 * scale + 1e-12, k
 
 
+@pytest.mark.parametrize("B,nb", [(1440, "2"), (1152, "2"), (1440, "1")])
+def test_headline_batch_gradients_match_fp64(B, nb, monkeypatch):
+    """The headline step at the epoch's two batch sizes (1440 and the short
+    last 1152 of a 6912-sequence epoch): gradients of the fused HIP step
+    (deferred-dW BPTT, one or two sequences per workgroup, 256 dW chunks, the
+    one-pass slab reduction) before Adam against fp64 torch autograd on the
+    same weights and batch -- an oracle independent of the HIP kernels."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.delenv("PDRNN_LSTM_DWOUT", raising=False)
+    monkeypatch.setenv("PDRNN_DWOUT_NB", nb)
+    mod = _ext.native(torch.device("cuda", 0))
+    assert mod.lstm_small_step_deferred_dw(32, 2, 128, B)
+    torch.manual_seed(11)
+    train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=12)
+    m0 = MotionModel(9, 32, 2, 6)
+    grads, x, y = _fused_grads(copy.deepcopy(m0), train, B)
+    ref = copy.deepcopy(m0).cuda().double()
+    torch.nn.functional.cross_entropy(ref(x.double()), y).backward()
+    for (k, r), g in zip(ref.named_parameters(), grads):
+        scale = r.grad.abs().max().item()
+        assert (g - r.grad).abs().max().item() <= 2e-6 * scale + 1e-12, k
+
+
+def test_deferred_dw_pairs_sequences_at_headline_batch(monkeypatch):
+    """B = 1440 / 1152: two sequences per workgroup of the deferred-dW BPTT,
+    all of them resident in one round (the grid fits the occupancy)."""
+    from pytorch_distributed_rnn_amd import _ext
+    monkeypatch.delenv("PDRNN_DWOUT_NB", raising=False)
+    mod = _ext.native(torch.device("cuda", 0))
+    for B in (1440, 1152):
+        nb, grid = mod.lstm_small_dwout_geometry(32, 2, 128, B)
+        assert (nb, grid) == (2, B // 2), (B, nb, grid)
+
+
 def test_deferred_dw_selected_above_one_round(monkeypatch):
     """Default selection: the headline B = 1440 (three residency rounds of the
     register-dW backward) takes the deferred-dW path, the 8-GPU per-rank batch

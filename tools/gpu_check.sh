@@ -1,0 +1,33 @@
+# GPU loop (one gpurun call): fused-step tests, the bench at the 1/2/4/8-GPU
+# per-rank batches, the forced-collective graph-replayed synced step, and a
+# kernel-trace window of the default bench.
+#   tools/gpu_check.sh TAG [quick|full]
+set -e
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+tag=${1:-chk}
+mode=${2:-quick}
+if [ "$mode" = full ]; then
+  timeout -k 10 1500 python -u -m pytest tests -m gpu --maxfail=10 -q --timeout 300 --timeout-method thread > gpurun_out/${tag}_gpu_tests.log 2>&1 || { tail -40 gpurun_out/${tag}_gpu_tests.log; exit 1; }
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { tail -20 gpurun_out/${tag}_smoke.log; exit 1; }
+  tail -1 gpurun_out/${tag}_smoke.log
+else
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_kernels.py tests/test_gpu_comm.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_gpu_tests.log 2>&1 || { tail -40 gpurun_out/${tag}_gpu_tests.log; exit 1; }
+fi
+tail -1 gpurun_out/${tag}_gpu_tests.log
+timeout -k 10 300 python bench.py > gpurun_out/${tag}_bench.log 2>&1 || { tail -20 gpurun_out/${tag}_bench.log; exit 1; }
+tail -1 gpurun_out/${tag}_bench.log | cut -c1-400
+for B in 1440 720 360 180; do
+  timeout -k 10 180 python bench.py --steps 200 --warmup 20 --global-batch $B > gpurun_out/${tag}_bench$B.log 2>&1 || { tail -20 gpurun_out/${tag}_bench$B.log; exit 1; }
+  tail -1 gpurun_out/${tag}_bench$B.log | python tools/bench_line.py "B=$B eager"
+done
+for B in 720 360 180; do
+  PDRNN_FORCE_GRAD_SYNC=1 PDRNN_FORCE_COLLECTIVE=1 timeout -k 10 180 python bench.py --steps 200 --warmup 20 --global-batch $B --cuda-graph > gpurun_out/${tag}_synced$B.log 2>&1 || { tail -20 gpurun_out/${tag}_synced$B.log; exit 1; }
+  tail -1 gpurun_out/${tag}_synced$B.log | python tools/bench_line.py "B=$B synced-graph"
+done
+cd /tmp
+timeout -k 10 240 rocprofv3 --kernel-trace -d /tmp/prof_${tag} -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 10 > $GRAFT_REPO_ROOT/gpurun_out/${tag}_prof.log 2>&1
+cd $GRAFT_REPO_ROOT
+db=$(find /tmp/prof_${tag} -name '*.db' | head -1)
+python tools/prof_window.py "$db" --anchor lstm_small_fwd --last 50 --out gpurun_out/${tag}_b1440_window.md
+cat gpurun_out/${tag}_b1440_window.md | head -30
