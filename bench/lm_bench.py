@@ -27,6 +27,7 @@ if ROOT not in sys.path:
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from pytorch_distributed_rnn_amd import _ext  # noqa: E402
 from pytorch_distributed_rnn_amd.data.charlm import CharCorpus  # noqa: E402
 from pytorch_distributed_rnn_amd.models.charlm import BiLSTMEncoder, CharLM  # noqa: E402
 from pytorch_distributed_rnn_amd.ops.adam import FusedAdam  # noqa: E402
@@ -121,7 +122,8 @@ def main(argv=None):
                                             "parallelism": f"dp{world}"},
             "final_loss": round(float(loss), 5), "device_peak_mib": round(device_peak_mib(dev), 1),
             "ddp_reducer": isinstance(tr.model if a.config == "charlm" else net, DistributedDataParallel),
-            "force_collective": os.environ.get("PDRNN_FORCE_COLLECTIVE", "0") == "1"}), flush=True)
+            "force_collective": os.environ.get("PDRNN_FORCE_COLLECTIVE", "0") == "1",
+            **_ext.persist_stats()}), flush=True)
     env.shutdown()
 
 

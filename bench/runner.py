@@ -6,8 +6,9 @@ builder, 240-290 resumable runner, 125-191 netem sweep).
 * Matrix: batch {480, 960, 1440} x GPUs {1, 2, 4, 8} x trainer {local,
   distributed, horovod}; ``local`` only at 1 GPU; ``--epochs 1 --seed
   123456789 --no-validation`` like the reference.  ``--fault`` adds the
-  network-fault sweep (host-side delay per step, the netem stand-in: xGMI
-  cannot be netem'd; see pytorch_distributed_rnn_amd/utils/faults.py).
+  network-fault sweep (host-side delay per step and retransmission stalls on
+  a share of the syncs, the netem delay / loss stand-ins: xGMI cannot be
+  netem'd; see pytorch_distributed_rnn_amd/utils/faults.py).
 * Launcher: one process per GPU via ``torch.distributed.run`` on 127.0.0.1
   (replaces mpirun/horovodrun over ssh); ``--launcher mpirun`` emits
   ``mpirun -np N`` lines instead (ranks come from OMPI_* variables).
@@ -46,20 +47,25 @@ def free_port() -> int:
 
 
 def matrix(batches: Iterable[int], gpus: Iterable[int], trainers: Iterable[str],
-           delays: Iterable[float]) -> List[Dict]:
+           delays: Iterable[float], losses: Iterable[float] = (0,)) -> List[Dict]:
+    """Configurations; the fault sweeps vary one knob at a time like the
+    reference's (delay rules with no loss, loss rules with no delay)."""
+    faults = [(d, 0) for d in delays] + [(0, l) for l in losses if l]
     out = []
     for b in batches:
         for n in gpus:
             for tr in trainers:
                 if tr == "local" and n != 1:
                     continue
-                for d in delays:
-                    if tr == "local" and d:
+                for d, l in faults:
+                    if tr == "local" and (d or l):
                         continue
-                    out.append({"trainer": tr, "hosts": 1, "gpus": n, "slots": n,
-                                "fault_delay_ms": d,
-                                "parameters": {"--batch-size": b, "--epochs": 1, "--seed": 123456789,
-                                               "--no-validation": ""}})
+                    cfg = {"trainer": tr, "hosts": 1, "gpus": n, "slots": n, "fault_delay_ms": d,
+                           "parameters": {"--batch-size": b, "--epochs": 1, "--seed": 123456789,
+                                          "--no-validation": ""}}
+                    if l:
+                        cfg["fault_loss_pct"] = l
+                    out.append(cfg)
     return out
 
 
@@ -69,6 +75,8 @@ def command(cfg: Dict, launcher: str, extra: List[str]) -> List[str]:
         params += [k] + ([str(v)] if v != "" else [])
     if cfg.get("fault_delay_ms"):
         params += ["--fault-delay-ms", str(cfg["fault_delay_ms"])]
+    if cfg.get("fault_loss_pct"):
+        params += ["--fault-loss", str(cfg["fault_loss_pct"])]
     params += extra
     if cfg["trainer"] == "local":
         return [sys.executable, str(MAIN)] + params + ["local"]
@@ -82,7 +90,8 @@ def command(cfg: Dict, launcher: str, extra: List[str]) -> List[str]:
 
 
 def key(cfg: Dict) -> str:
-    return json.dumps({k: cfg[k] for k in ("trainer", "gpus", "fault_delay_ms", "parameters")}, sort_keys=True)
+    return json.dumps({k: cfg.get(k) for k in ("trainer", "gpus", "fault_delay_ms", "fault_loss_pct", "parameters")},
+                      sort_keys=True)
 
 
 def done_keys(path: Path) -> set:
@@ -102,8 +111,11 @@ def main(argv=None):
     ap.add_argument("--batches", type=int, nargs="+", default=[480, 960, 1440])
     ap.add_argument("--gpus", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--trainers", nargs="+", default=list(TRAINERS), choices=TRAINERS)
-    ap.add_argument("--fault", action="store_true", help="add the delay sweep 0/50/100/200/400 ms")
+    ap.add_argument("--fault", action="store_true",
+                    help="the reference's network sweep: delay 0/1/2/5/10/25/50/100/200/300/400 ms, "
+                         "loss 0.1/0.5/1/2/5/10/15 %% (reference fabfile.py:125-183)")
     ap.add_argument("--delays", type=float, nargs="+", default=None)
+    ap.add_argument("--losses", type=float, nargs="+", default=None)
     ap.add_argument("--launcher", choices=("torchrun", "mpirun"), default="torchrun")
     ap.add_argument("--device", default=None, help="cpu: gloo plumbing run")
     ap.add_argument("--synthetic", action="store_true", default=True)
@@ -112,8 +124,10 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--dry-run", action="store_true")
     a = ap.parse_args(argv)
-    delays = a.delays if a.delays is not None else ([0, 50, 100, 200, 400] if a.fault else [0])
-    cfgs = matrix(a.batches, a.gpus, a.trainers, delays)
+    delays = a.delays if a.delays is not None else \
+        ([0, 1, 2, 5, 10, 25, 50, 100, 200, 300, 400] if a.fault else [0])
+    losses = a.losses if a.losses is not None else ([0.1, 0.5, 1, 2, 5, 10, 15] if a.fault else [])
+    cfgs = matrix(a.batches, a.gpus, a.trainers, delays, losses)
     random.Random(a.seed).shuffle(cfgs)
     extra = shlex.split(a.extra)
     if a.synthetic:

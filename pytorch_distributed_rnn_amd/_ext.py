@@ -102,3 +102,15 @@ def require():
     if mod is None:
         raise RuntimeError(f"native extension not importable: {_IMPORT_ERROR!r}")
     return mod
+
+
+def persist_stats() -> dict:
+    """Persistent large-H recurrence health of this process: per-launch
+    verification on/off, launches re-run on the per-step kernels after a
+    grid-sync timeout, and whether the persistent path is off for good
+    (bindings.cpp large_persist)."""
+    mod = extension()
+    if mod is None or not hasattr(mod, "persist_fallbacks"):
+        return {"persist_verify": False, "persist_fallbacks": 0, "persist_disabled": False}
+    return {"persist_verify": bool(mod.persist_verify_on()), "persist_fallbacks": int(mod.persist_fallbacks()),
+            "persist_disabled": bool(mod.persist_disabled())}

@@ -82,6 +82,10 @@ def build_parser(script_dir: Optional[Path] = None) -> argparse.ArgumentParser:
                    help="--batch-size is per rank instead of global")
     p.add_argument("--fault-delay-ms", default=0.0, type=float,
                    help="inject a host delay before every gradient sync (netem stand-in)")
+    p.add_argument("--fault-loss", default=0.0, type=float,
+                   help="percent of gradient syncs hit by a retransmission stall (netem loss stand-in)")
+    p.add_argument("--fault-retransmit-ms", default=200.0, type=float,
+                   help="stall of one lost sync (Linux TCP's minimum retransmission timeout)")
     p.add_argument("--fault-rank", default=-1, type=int, help="only this rank is delayed / dropped (-1: all)")
     p.add_argument("--fault-drop-step", default=-1, type=int,
                    help="the --fault-rank rank(s) exit abruptly at this training step (failure-detection test)")
@@ -123,11 +127,15 @@ def _apply_common(args) -> None:
         os.environ["PDRNN_KERNELS"] = "hip-strict"
     if args.device == "cpu":
         os.environ["PDRNN_FORCE_CPU"] = "1"
-    if args.fault_delay_ms > 0 or args.fault_drop_step >= 0:
+    if args.fault_delay_ms > 0 or args.fault_drop_step >= 0 or args.fault_loss > 0:
         from .utils import faults
         kw = {"rank": args.fault_rank}
         if args.fault_delay_ms > 0:
             kw["delay_ms"] = args.fault_delay_ms
+        if args.fault_loss > 0:
+            kw["loss_prob"] = args.fault_loss / 100.0
+            kw["retransmit_ms"] = args.fault_retransmit_ms
+            kw["seed"] = args.seed or 0
         if args.fault_drop_step >= 0:
             kw["drop_step"] = args.fault_drop_step
         faults.configure(**kw)

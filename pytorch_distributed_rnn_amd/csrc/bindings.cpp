@@ -750,6 +750,10 @@ enum PersistResult { kPersistNotRun = 0, kPersistOk = 1, kPersistFailed = 2 };
 std::atomic<int> g_persist_verify{-1};     // -1: PDRNN_LSTM_PERSIST_VERIFY (default off)
 std::atomic<int> g_persist_inject{0};      // tests: flag the next N launches as timed out
 std::atomic<long long> g_persist_fallbacks{0};
+// after the first timed-out launch in a process the persistent path is off for
+// good: a lost co-residency (RCCL kernels beside it) tends to recur every step,
+// and each occurrence costs the 2 s spin bound plus the per-step re-run
+std::atomic<int> g_persist_disabled{0};
 bool persist_verify_on() {
   const int v = g_persist_verify.load();
   if (v >= 0) return v != 0;
@@ -777,7 +781,7 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     const char* e = std::getenv("PDRNN_PS_MODE");
     return e ? std::atoi(e) : 0;
   }();
-  if (env == 0 || tile >= 0) return kPersistNotRun;
+  if (env == 0 || tile >= 0 || g_persist_disabled.load()) return kPersistNotRun;
   int dev = 0;
   TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
   int cus = 0;
@@ -816,8 +820,12 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     TORCH_CHECK(hipStreamSynchronize(st) == hipSuccess, "persistent LSTM: stream synchronisation failed");
     if (hf[0] != 0) {
       g_persist_fallbacks++;
-      TORCH_WARN("persistent LSTM recurrence (", backward ? "backward" : "forward",
-                 "): a grid-sync wait timed out (co-residency lost); re-running the layer on the per-step kernels");
+      const bool keep = std::getenv("PDRNN_LSTM_PERSIST_RETRY") != nullptr;  // tests: keep retrying
+      if (!keep) g_persist_disabled = 1;
+      std::fprintf(stderr, "[pdrnn] persistent LSTM recurrence (%s): a grid-sync wait timed out (co-residency "
+                   "lost, fallback #%lld); re-running the layer on the per-step kernels%s\n",
+                   backward ? "backward" : "forward", (long long)g_persist_fallbacks.load(),
+                   keep ? "" : " and using them for the rest of the process");
       TORCH_CHECK(hipMemsetAsync(sticky[dev].data_ptr<int>(), 0, sizeof(int), st) == hipSuccess, "sticky reset");
       return kPersistFailed;
     }
@@ -1140,6 +1148,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "tests: flag the next n persistent launches as timed out");
   m.def("persist_fallbacks", []() { return (int64_t)g_persist_fallbacks.load(); },
         "persistent launches re-run on the per-step kernels after a timeout");
+  m.def("persist_verify_on", []() { return persist_verify_on(); },
+        "every persistent launch is verified (host sync + flag read) before its result is used");
+  m.def("persist_disabled", []() { return g_persist_disabled.load() != 0; },
+        "the persistent recurrence is off for this process (after a timed-out launch)");
+  m.def("persist_reset", []() { g_persist_disabled = 0; g_persist_fallbacks = 0; },
+        "tests: re-enable the persistent recurrence and clear the fallback count");
   m.def("debug_spin_cus", [](double ms, int64_t workgroups, int64_t threads, int64_t lds_bytes) {
     HIP_LAUNCH_CHECK(pdrnn_debug_spin_cus((uint64_t)(ms * 1e3), (int)workgroups, (int)threads, (int)lds_bytes,
                                           cur_stream()));

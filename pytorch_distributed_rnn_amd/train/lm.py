@@ -18,6 +18,7 @@ from typing import Dict, List, Optional
 import torch
 from torch import Tensor, nn
 
+from .. import _ext
 from ..data.charlm import CharCorpus
 from .checkpoint import adapt_state_dict_keys, save_checkpoint
 from ..ops.adam import FusedAdam
@@ -99,8 +100,11 @@ class LMTrainer:
         mean = float(torch.stack(losses).mean()) if losses else float("nan")
         out = {"loss": mean, "tokens": tokens, "duration": dt, "tokens_per_sec": tokens / dt if dt else 0.0,
                "steps": len(losses), "device_peak_mib": device_peak_mib(self.device)}
+        ps = _ext.persist_stats()
+        out.update(ps)
         logging.info(f"{self.rank}: Epoch {epoch} loss {mean:.6f} tokens/s {out['tokens_per_sec']:.1f} "
-                     f"(x{self.world} ranks) device_peak_mib={out['device_peak_mib']:.1f}")
+                     f"(x{self.world} ranks) device_peak_mib={out['device_peak_mib']:.1f} "
+                     f"persist_verify={int(ps['persist_verify'])} persist_fallbacks={ps['persist_fallbacks']}")
         return out
 
     # ------------------------------------------------------------ checkpoints
