@@ -129,14 +129,20 @@ def main(argv=None):
             yield from loader.batch_indices()
             epoch += 1
 
-    def timed_run(batches):
+    def timed_run(batches, per_step=False):
         env.barrier()
         if dev.type == "cuda":
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         stats = None
-        for bidx in batches:
-            stats, _ = trainer.train_batch(loader.make_batch(bidx))
+        # one trainer call per epoch's worth of steps (the multi-GPU fused
+        # step replays them from one HIP graph, like the CLI's epoch loop)
+        if per_step:
+            for b in batches:
+                stats, _ = trainer.train_batch(loader.make_batch(b))
+        for k in range(0, 0 if per_step else len(batches), steps_per_epoch):
+            res = trainer.train_batches([loader.make_batch(b) for b in batches[k:k + steps_per_epoch]])
+            stats = res[-1][0]
         if dev.type == "cuda":
             torch.cuda.synchronize()
         env.barrier()
@@ -148,8 +154,9 @@ def main(argv=None):
     # preparation the CLI runs before its timed epochs
     trainer.prepare()
     warm = epoch_batches(0)
-    for _ in range(args.warmup):
-        trainer.train_batch(loader.make_batch(next(warm)))
+    warm_steps = [next(warm) for _ in range(args.warmup)]
+    for k in range(0, len(warm_steps), steps_per_epoch):
+        trainer.train_batches([loader.make_batch(b) for b in warm_steps[k:k + steps_per_epoch]])
     # The timed region: EXACTLY --steps training steps starting at an epoch
     # boundary, in the sampler's epoch order (full batches and the short last
     # batch of every epoch).  With --steps a multiple of the steps per epoch it
@@ -172,11 +179,13 @@ def main(argv=None):
     # the per-step figure of earlier rounds
     full = []
     stream = epoch_batches(2000)
-    while len(full) < args.steps:
+    while len(full) < args.steps + 3:
         b = next(stream)
         if b.numel() == per_rank:
             full.append(b)
-    step_elapsed, _ = timed_run(full)
+    for b in full[:3]:  # per-step graph capture of the synced step (N > 1) outside the clock
+        trainer.train_batch(loader.make_batch(b))
+    step_elapsed, _ = timed_run(full[3:], per_step=True)
     step_value = per_rank * world * args.steps / step_elapsed
     # sanity: loss must be finite after training
     loss = float(stats[0])

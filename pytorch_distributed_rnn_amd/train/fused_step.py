@@ -152,6 +152,154 @@ class MotionTrainStep:
         r = self.flat.data.to(torch.bfloat16).float()
         return [r[o:o + int(torch.Size(s).numel())].view(s) for o, s in self._offs]
 
+    def run_steps(self, features: Tensor, labels: Tensor, idx_list) -> Optional[list]:
+        """Consecutive training steps (an epoch's batches, the short last one
+        included) as ONE HIP-graph replay of the synced step -- forward/BPTT,
+        inline RCCL all-reduce and Adam for every batch, the device step
+        count advancing from one captured step to the next (adam_flat's
+        arrival ticket) -- so neither a per-step graph boundary nor a per-step
+        host copy sits between the steps: the batch indices of all steps reach
+        the graph's static buffer in one copy before the replay.  Returns each
+        step's statistics row, or None when this configuration runs per step
+        (no gradient sync / no graph replay, bf16 or GRU packing, host-gathered
+        batches, the first two calls of a configuration)."""
+        if self.grad_sync is None or not self.cuda_graph or self.bf16 or self.gru:
+            return None
+        if not idx_list or any(i is None for i in idx_list):
+            return None
+        adam = self._flat_adam_peek()
+        if adam is None:
+            return None
+        (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
+        sizes = tuple(int(i.numel()) for i in idx_list)
+        key, cfgs = self._epoch_key(features, labels, sizes, idx_list[0].dtype, adam)
+        graphs = self.__dict__.setdefault("_graphs", {})
+        ent = graphs.get(key)
+        if ent is None:
+            ent = {"graph": None, "eager": 0}
+            if len(graphs) >= self._GRAPHS_MAX:
+                graphs.pop(next(iter(graphs)))
+            graphs[key] = ent
+        n = len(sizes)
+        slots = [(self._slot + k) % self.RING for k in range(n)]
+        if ent["graph"] is None:
+            ent["eager"] += 1
+            if ent["eager"] <= 2:
+                return None  # RCCL's lazy setup and first-use allocations outside the capture
+            self.flat.attach_grads()
+            try:
+                self._capture_epoch(ent, features, labels, idx_list, cfgs, adam, slots[0])
+            except Exception as exc:  # capture unsupported here: stay eager for good
+                import warnings
+                warnings.warn(f"HIP graph capture of the synced epoch failed ({exc!r}); running per step")
+                torch.cuda.synchronize(self.flat.grad.device)
+                graphs.clear()
+                self.cuda_graph = False
+                return None
+        self.flat.attach_grads()
+        # host-side optimizer state advances by n steps (the graph advances the device count)
+        for _ in range(n):
+            self._flat_adam()
+        c0 = step - 1.0  # optimizer step count before this call's first step
+        if ent["step_host"] != c0:
+            ent["step"].fill_(c0)
+        # one copy of every step's indices: a single slice when the batches are
+        # consecutive views of one index tensor (DeviceBatchLoader's split)
+        total = sum(sizes)
+        b0 = idx_list[0]._base
+        esz = idx_list[0].element_size()
+        if b0 is not None and b0.is_contiguous() and all(i._base is b0 for i in idx_list) and \
+                all(idx_list[k].data_ptr() == idx_list[0].data_ptr() + esz * sum(sizes[:k]) for k in range(n)):
+            first = (idx_list[0].data_ptr() - b0.data_ptr()) // esz
+            ent["idx_all"].copy_(b0.view(-1).narrow(0, first, total), non_blocking=True)
+        else:
+            torch.cat(list(idx_list), out=ent["idx_all"])
+        with trace_range("pdrnn.graph_epoch"):
+            ent["graph"].replay()
+        if self.comm is not None and hasattr(self.comm, "track_current"):
+            self.comm.track_current()  # the communicator's watchdog bounds the replay
+        ent["step_host"] = c0 + n
+        self._slot = (self._slot + n) % self.RING
+        rows = [(int(c0) + k + ent["slot_off"]) % self.RING for k in range(n)]
+        out = []
+        for row, slot in zip(rows, slots):
+            if row != slot:
+                self.ring[slot].copy_(self.ring[row], non_blocking=True)
+            out.append(self.ring[slot])
+        return out
+
+    def _epoch_key(self, features: Tensor, labels: Tensor, sizes, idx_dtype, adam):
+        from ..ops.lstm import fused_bwd_nb, small_launch_config
+        (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
+        cfgs = []
+        for b in sizes:
+            nb_fwd, sp_fwd, _, _ = small_launch_config(b, self.H, self.NL)
+            cfgs.append(((nb_fwd, sp_fwd), fused_bwd_nb(b, self.H, self.NL)))
+        key = ("epoch", features.data_ptr(), tuple(features.shape), features.dtype, labels.data_ptr(),
+               labels.numel(), tuple(sizes), idx_dtype, tuple(cfgs), lr, b1, b2, eps, wd, dec,
+               p.data_ptr(), m.data_ptr(), v.data_ptr(), self.flat.grad.data_ptr())
+        return key, cfgs
+
+    def prepare_epoch(self, features: Tensor, labels: Tensor, sizes) -> bool:
+        """Capture the epoch graph of ``run_steps`` for these batch sizes ahead
+        of time (Trainer.prepare, before the timed epochs): one eager gradient
+        all-reduce first -- RCCL's lazy connection setup cannot happen inside a
+        capture -- then the capture itself, which runs nothing.  Parameters
+        and optimizer state are untouched; the flat gradient (rewritten by
+        every step) is left zeroed.  True when the graph is ready."""
+        if self.grad_sync is None or not self.cuda_graph or self.bf16 or self.gru or not sizes:
+            return False
+        adam = self._flat_adam_peek()
+        if adam is None:
+            return False
+        dev = self.flat.grad.device
+        idx_list = list(torch.split(torch.zeros(sum(sizes), dtype=torch.long, device=dev), list(sizes)))
+        key, cfgs = self._epoch_key(features, labels, tuple(sizes), torch.long, adam)
+        graphs = self.__dict__.setdefault("_graphs", {})
+        if key in graphs and graphs[key]["graph"] is not None:
+            return True
+        self.flat.attach_grads()
+        self.grad_sync()
+        self.flat.grad.zero_()
+        ent = {"graph": None, "eager": 0}
+        try:
+            self._capture_epoch(ent, features, labels, idx_list, cfgs, adam, self._slot)
+        except Exception as exc:
+            import warnings
+            warnings.warn(f"HIP graph capture of the synced epoch failed ({exc!r}); running per step")
+            torch.cuda.synchronize(dev)
+            return False
+        if len(graphs) >= self._GRAPHS_MAX:
+            graphs.pop(next(iter(graphs)))
+        graphs[key] = ent
+        return True
+
+    def _capture_epoch(self, ent: dict, features: Tensor, labels: Tensor, idx_list, cfgs, adam, slot: int):
+        (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
+        dev = self.flat.grad.device
+        hw, hb = self.m.fc.weight, self.m.fc.bias
+        sizes = [int(i.numel()) for i in idx_list]
+        ent["idx_all"] = torch.cat(list(idx_list)).clone()
+        offs = [sum(sizes[:k]) for k in range(len(sizes))]
+        views = [ent["idx_all"][o:o + b] for o, b in zip(offs, sizes)]
+        # the statistics of captured step k go to ring row (device step count
+        # before that step's Adam) + slot_off = the host slot of step k
+        ent["slot_off"] = (slot - (int(step) - 1)) % self.RING
+        ent["step"] = torch.zeros(1, dtype=torch.float32, device=dev)
+        ent["ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
+        ent["step_host"] = None
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            for view, ((nb, sp), nb_bwd) in zip(views, cfgs):
+                self.mod.lstm_head_train_step(features, view, labels, self.weights, hw, hb, self.flat.grad, self.ring,
+                                              self.H, self.NL, sp, 0, nb, nb_bwd, None, None, 0, None, ent["step"],
+                                              ent["slot_off"])
+                self.grad_sync()
+                self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step + 1.0, 1.0, bool(dec),
+                                   False, None, ent["step"], ent["ticket"])
+        ent["graph"] = g
+
     def _flat_adam(self):
         """(state, hyper-parameters) when the optimizer is a plain single-group
         FusedAdam over exactly the model's flat buffer: the step then runs as

@@ -271,6 +271,11 @@ class Trainer:
                 break
             one_pass(max(sizes))
             mem.synchronize()
+        # the multi-GPU step replays whole epochs from one HIP graph: captured
+        # here, for the epoch's batch sizes (the full ones and the short last)
+        if hasattr(fused, "prepare_epoch") and loader.gather_in_kernel:
+            bs = loader.batch_size
+            fused.prepare_epoch(loader.features, loader.labels, [min(bs, n - k) for k in range(0, n, bs)])
         # the first timed epoch's indices (DataLoader-style prefetch)
         if self.sampler is not None and hasattr(loader, "prefetch"):
             self.sampler.set_epoch(self.start_epoch)
@@ -329,6 +334,23 @@ class Trainer:
             self.optimizer.step()
         return stats, labels.shape[0]
 
+    def train_batches(self, batches) -> List[Tuple[Tensor, int]]:
+        """Several optimizer steps on consecutive batches (an epoch); returns
+        ``train_batch``'s (stats, batch size) per batch.  The multi-GPU fused
+        step replays all of them from ONE HIP graph
+        (``MotionTrainStep.run_steps``); otherwise -- or when ``train_batch``
+        is wrapped (fault injection) -- one ``train_batch`` per batch."""
+        batches = list(batches)
+        fused = self._fused_step()
+        if fused is not None and self.model.training and "train_batch" not in self.__dict__ and batches and \
+                all(len(b) == 3 for b in batches):
+            feats, labels = batches[0][0], batches[0][1]
+            if all(b[0] is feats and b[1] is labels for b in batches):
+                res = fused.run_steps(feats, labels, [b[2] for b in batches])
+                if res is not None:
+                    return [(st, b[2].numel()) for st, b in zip(res, batches)]
+        return [self.train_batch(b) for b in batches]
+
     def _train_step(self, formatter: TrainingMessageFormatter):
         self.model.train()
         loader = self.train_loader
@@ -352,14 +374,21 @@ class Trainer:
             pending.clear()
             _TL.mark("logged")
 
-        for batch_idx, batch in enumerate(loader):
-            _TL.mark(f"batch{batch_idx}_ready")
-            stats, n = self.train_batch(batch)
-            _TL.mark(f"batch{batch_idx}_issued")
-            self.sequences_seen += n
-            pending.append((batch_idx, n, stats))
-            if self.log_interval and len(pending) >= self.log_interval:
-                flush()
+        if self.log_interval:
+            for batch_idx, batch in enumerate(loader):
+                _TL.mark(f"batch{batch_idx}_ready")
+                stats, n = self.train_batch(batch)
+                _TL.mark(f"batch{batch_idx}_issued")
+                self.sequences_seen += n
+                pending.append((batch_idx, n, stats))
+                if len(pending) >= self.log_interval:
+                    flush()
+        else:
+            # the whole epoch at once (one graph replay on the multi-GPU fused path)
+            for batch_idx, (stats, n) in enumerate(self.train_batches(loader)):
+                self.sequences_seen += n
+                pending.append((batch_idx, n, stats))
+            _TL.mark("epoch_issued")
         # next epoch's indices while the GPU drains this one's steps
         nxt = getattr(self, "_prefetch_epoch", None)
         if nxt is not None and self.sampler is not None and hasattr(loader, "prefetch"):

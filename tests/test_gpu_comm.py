@@ -225,6 +225,71 @@ def test_graph_replayed_horovod_step_matches_local(rccl_group):
         torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
 
 
+def _epoch_of(step, feats, labels, idx_list):
+    res = step.run_steps(feats, labels, idx_list)
+    replayed = res is not None
+    if res is None:
+        res = [step(feats, labels, i) for i in idx_list]
+    return [r.clone() for r in res], replayed
+
+
+@pytest.mark.parametrize("mode", ["ddp", "horovod"])
+def test_epoch_graph_replay_matches_local(rccl_group, mode):
+    """every step of an epoch (4 full batches + the short
+    last one, indices as consecutive views of one tensor like the loader's)
+    replayed as ONE HIP graph -- fused step, inline all-reduce and Adam per
+    batch, the device step count advancing inside the graph -- equals the
+    eager local steps, statistics and parameters; one watchdog registration
+    per replayed epoch."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    from pytorch_distributed_rnn_amd.parallel import horovod as hvd
+    from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_rnn_amd.train.fused_step import MotionTrainStep
+    from pytorch_distributed_rnn_amd.utils.flat import flatten_module
+    torch.manual_seed(5)
+    train, _, _ = synthetic_motion(n_train=448, n_validation=1, n_test=1, seed=5)
+    feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
+    m1 = MotionModel(9, 32, 2, 6).cuda()
+    m2 = copy.deepcopy(m1)
+    flatten_module(m2)
+    o2 = FusedAdam(m2.parameters(), lr=2.5e-3)
+    if mode == "ddp":
+        ddp = DistributedDataParallel(m1)
+        o1 = FusedAdam(m1.parameters(), lr=2.5e-3)
+        s1 = MotionTrainStep(ddp, o1, ddp.reducer.all_reduce_inline, cuda_graph=True)
+        comm = ddp.comm
+    else:
+        flatten_module(m1)
+        o1 = hvd.DistributedOptimizer(FusedAdam(m1.parameters(), lr=2.5e-3), named_parameters=m1.named_parameters())
+        flat1 = next(iter(m1._pdrnn_flat.values()))
+        comm = hvd.comm()
+        s1 = MotionTrainStep(m1, o1, lambda: hvd.allreduce_(flat1.grad, average=True), cuda_graph=True, comm=comm)
+    s2 = MotionTrainStep(m2, o2, None)
+    g = torch.Generator().manual_seed(2)
+    outs, replays = [], 0
+    for e in range(5):
+        idx_list = list(torch.split(torch.randperm(448, generator=g).cuda(), 96))
+        assert [i.numel() for i in idx_list] == [96, 96, 96, 96, 64]
+        if e == 4:  # ring slots out of step with the captured mapping: the copy fallback
+            s1._slot = (s1._slot + 5) % s1.RING
+        n0 = comm.tracked
+        a, replayed = _epoch_of(s1, feats, labels, idx_list)
+        if replayed:
+            replays += 1
+            assert comm.tracked - n0 == 1
+        b = [s2(feats, labels, i).clone() for i in idx_list]
+        outs.append((a, b))
+    assert replays == 3, "the epoch was never replayed from a graph"
+    for a, b in outs:
+        for x, y in zip(a, b):
+            torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+    assert o1.state_dict()["state"][0]["step"] == o2.state_dict()["state"][0]["step"] == 25
+
+
 def test_ddp_autograd_hooks_rccl(rccl_group):
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
