@@ -464,7 +464,15 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   // the one-launch step (register-resident dW, no extra launch).
   const int dw_mode = pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T);
   const bool dwout = nb_bwd == 1 && split_bwd == 1 && ((gridb < B && dw_mode == 1) || dw_mode == 2);
-  const int slab_rows = dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
+  // deferred dW: sequences per BPTT workgroup, and whether those workgroups
+  // form the dW of their own tile (one slab row per tile) or a separate
+  // matrix-core launch does it over fixed K chunks
+  const int nb_dw = dwout ? pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B) : (int)nb_bwd;
+  // (one slab row per tile: above ~1k tiles the reduction's slab read outweighs the saved dW pass)
+  const bool dw_fused = dwout && (B + nb_dw - 1) / nb_dw <= 1024 &&
+                        pdrnn_lstm_small_bwd_dw_ok((int)H, (int)NL, (int)T, (int)B, (int)I, nb_dw) == 1;
+  const int slab_rows = dw_fused ? (int)((B + nb_dw - 1) / nb_dw)
+                                 : dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
   Tensor slab = at::empty({slab_rows, L.P}, opts);
 
   PdrnnLstmSmallFwdArgs f{};
@@ -515,11 +523,10 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.dhn = dh_top.data_ptr<float>(); bk.dhn_top_only = 1;
   bk.slab = slab.data_ptr<float>(); bk.P = L.P;
   bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL; bk.cell = (int)cell;
-  int grid_dw = gridb, nb_dw = (int)nb_bwd;
+  int grid_dw = gridb;
   Tensor xg;
   if (dwout) {
-    nb_dw = pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B);
-    grid_dw = pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb_dw);
+    grid_dw = dw_fused ? slab_rows : pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb_dw);
     TORCH_CHECK(grid_dw > 0, "deferred-dW backward: no resident grid");
     if (st_f.defined()) {
       st_b = at::zeros({grid_dw, 8}, opts.dtype(at::kLong));
@@ -533,11 +540,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     bk.xg_ld = (int)xg_ld;
   }
   if (st_b.defined()) bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
-  if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
-  else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, nb_dw, st));
-  else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
+  PdrnnLstmSmallDwArgs dw{};
   if (dwout) {
-    PdrnnLstmSmallDwArgs dw{};
     dw.xg = xg.data_ptr<float>(); dw.xg_ld = bk.xg_ld;
     dw.hseq = f.hseq; dw.dg = f.act; dw.dg_st = 5 * H;
     dw.slab = slab.data_ptr<float>(); dw.P = L.P;
@@ -546,11 +550,16 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
       dw.off_bih[l] = L.off_bih[l]; dw.off_bhh[l] = L.off_bhh[l];
     }
     dw.B = (int)B; dw.T = (int)T; dw.I = (int)I; dw.NL = (int)NL; dw.chunks = slab_rows;
-    HIP_LAUNCH_CHECK(pdrnn_lstm_small_dw(&dw, (int)H, st));
   }
+  if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
+  else if (dw_fused) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dw(&bk, &dw, (int)H, nb_dw, st));
+  else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, nb_dw, st));
+  else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
+  if (dwout && !dw_fused) HIP_LAUNCH_CHECK(pdrnn_lstm_small_dw(&dw, (int)H, st));
   if (st_f.defined()) {
     report_stamps("fwd(head step)", st_f, (int)(T + NL - 1));
-    report_stamps(dwout ? "bwd(head step, lean, deferred dW)" : "bwd(head step, lean)", st_b,
+    report_stamps(dw_fused ? "bwd(head step, lean, own-tile dW)" : dwout ? "bwd(head step, lean, deferred dW)"
+                                                                    : "bwd(head step, lean)", st_b,
                   (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_dw - 1) / ((int64_t)grid_dw * nb_dw)));
   }
 
@@ -1031,6 +1040,13 @@ Tensor gemm16(const Tensor& A, bool a_kmajor, const Tensor& B, bool b_kmajor, co
     a.ldb2 = b2.stride(0);
     a.K2 = (int)K2;
   }
+  // the operand DMA issues 16-byte loads from base + row * ld + 8 * chunk:
+  // row strides a multiple of 8 elements, 16-byte aligned bases (else the
+  // caller's torch fallback, ops/gemm.py:_rowmajor)
+  for (const int64_t ld : {a.lda, a.ldb, a.A2 ? a.lda2 : (int64_t)8, a.B2 ? a.ldb2 : (int64_t)8})
+    TORCH_CHECK(ld % 8 == 0, "gemm16: row strides must be multiples of 8 elements");
+  for (const void* ptr : {a.A, a.B, a.A2, a.B2})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(ptr) % 16 == 0, "gemm16: operand bases must be 16-byte aligned");
   Tensor C;
   if (splitk > 1) {
     // fp32 partials [splitk, M, N], summed in fixed order
@@ -1121,8 +1137,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "the fused training step defers the weight gradients to the matrix-core dW kernel for this shape");
   m.def("lstm_small_dwout_geometry", [](int64_t H, int64_t NL, int64_t T, int64_t B) {
     const int nb = pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B);
-    return py::make_tuple(nb, pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb));
-  }, "(sequences per workgroup, grid) of the deferred-dW backward for this shape");
+    return py::make_tuple(nb, pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb),
+                          pdrnn_lstm_small_bwd_dw_ok((int)H, (int)NL, (int)T, (int)B, 9, nb) == 1);
+  }, "(sequences per workgroup, grid, own-tile dW) of the deferred-dW backward for this shape (9 inputs)");
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });

@@ -132,6 +132,11 @@ hipError_t pdrnn_lstm_small_dw(const PdrnnLstmSmallDwArgs* a, int H, hipStream_t
 // nb = sequences per workgroup (1 or 2: pdrnn_lstm_small_bwd_dwout_nb).
 hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int grid, int nb, hipStream_t stream);
 int pdrnn_lstm_small_bwd_dwout_nb(int H, int NL, int T, int B);
+// Deferred-dW BPTT whose workgroups (one per nb-sequence tile, grid = tiles)
+// then form the weight gradients of their own rows: d->chunks = tiles slab rows.
+int pdrnn_lstm_small_bwd_dw_ok(int H, int NL, int T, int B, int I, int nb);
+hipError_t pdrnn_lstm_small_bwd_dw(const PdrnnLstmSmallBwdArgs* a, const PdrnnLstmSmallDwArgs* d, int H, int nb,
+                                   hipStream_t stream);
 int pdrnn_lstm_small_bwd_dwout_grid(int H, int NL, int T, int B, int nb);
 
 // Query the launch geometry chosen for (H, B): returns grid size (number of slab rows).

@@ -123,7 +123,7 @@ class RcclComm final : public Comm {
   }
   ~RcclComm() override { close(); }
   void close() override {
-    // no api_mu_ here: the watchdog may be waiting for it to abort
+    // api_mu_ only after the watchdog is joined: it may be waiting for it to abort
     if (closed_.exchange(true)) return;
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -131,6 +131,19 @@ class RcclComm final : public Comm {
     }
     cv_.notify_all();
     if (watchdog_.joinable()) watchdog_.join();
+    // The watchdog is gone: now wait (bounded) for an API call another thread
+    // may still be inside (daemon threads survive to atexit) -- closed_ makes
+    // every later call raise in live(), so once api_mu_ is ours no enqueue can
+    // touch the stream / works_ being torn down below.
+    std::unique_lock<std::mutex> api(api_mu_, std::defer_lock);
+    for (const auto until = Clock::now() + std::chrono::seconds(10); !api.try_lock();) {
+      if (Clock::now() > until) {
+        std::fprintf(stderr, "[pdrnn] RCCL communicator (rank %d/%d) teardown: an API call still holds the "
+                     "communicator after 10 s; tearing down anyway\n", rank_, world_);
+        break;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
     if (comm_ && !aborted_.load()) {
       // Teardown is where a dead peer usually shows up (an exception unwinds,
       // reset_comms(), interpreter exit): a collective still pending would

@@ -113,6 +113,7 @@ class FusedAdam(torch.optim.Adam):
                           float(group["lr"]), beta1, beta2, group["eps"], group["weight_decay"],
                           step, self._pdrnn_grad_scale, bool(group.get("decoupled_weight_decay", False)),
                           bool(group.get("maximize", False)), None, None)
+            self.native_steps = getattr(self, "native_steps", 0) + 1  # groups stepped by the native kernel
             # the native kernel wrote the parameters through raw pointers: move
             # their version counters like any in-place torch update would, so
             # derived copies keyed on versions (16-bit shadow weights of the

@@ -60,7 +60,11 @@ def _splitk(dev, M: int, N: int, K: int) -> int:
 
 
 def _rowmajor(t: Tensor) -> bool:
-    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]
+    """Row-major 2-D operand the in-tree GEMM can stream: unit column stride,
+    row stride a multiple of 8 elements and a 16-byte aligned base (its LDS
+    DMA issues 16-byte loads from base + row * ld + 8 * chunk)."""
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1] and t.stride(0) % 8 == 0 and \
+        t.data_ptr() % 16 == 0
 
 
 def linear16(x: Tensor, w: Tensor, bias: Optional[Tensor]) -> Tensor:

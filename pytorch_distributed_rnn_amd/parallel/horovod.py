@@ -71,9 +71,11 @@ def comm():
 
 def _skip_world1() -> bool:
     # one rank: an in-place reduction is the identity -- unless
-    # PDRNN_FORCE_COLLECTIVE=1 keeps it (the communicator then really issues
-    # it: tests of the comm-stream hop and its graph capture on one GPU)
-    return size() == 1 and os.environ.get("PDRNN_FORCE_COLLECTIVE", "0") != "1"
+    # PDRNN_FORCE_COLLECTIVE=1 or PDRNN_FORCE_GRAD_SYNC=1 keeps it (the
+    # communicator then really issues it: tests of the comm-stream hop and its
+    # graph capture on one GPU; the multi-GPU step's launch sequence at world 1)
+    return size() == 1 and os.environ.get("PDRNN_FORCE_COLLECTIVE", "0") != "1" and \
+        os.environ.get("PDRNN_FORCE_GRAD_SYNC", "0") != "1"
 
 
 def _tensors_of(params) -> List[Tuple[str, torch.Tensor]]:

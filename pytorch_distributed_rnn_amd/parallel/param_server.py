@@ -261,10 +261,13 @@ class ServerModel:
                     opt = self._optims[rank] = FusedAdam(params, lr=lr)
                 for p, gr in zip(params, grads):
                     p.grad = gr
+                before = getattr(opt, "native_steps", 0)
                 opt.step()
                 for p in params:
                     p.grad = None
-                if self.device.type == "cuda" and _ext.native(self.device) is not None:
+                # counted only when FusedAdam really ran the flat native kernel
+                # (not its per-group reference fallback)
+                if getattr(opt, "native_steps", 0) > before:
                     self.native_adam_steps += 1
 
     def save(self, path: str, epoch: int, loss: float) -> str:
