@@ -107,7 +107,7 @@ def build(verbose: bool = False, clean: bool = False, jobs: int | None = None) -
     hip_flags = [
         "-c", *hip_opt, "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
         "-munsafe-fp-atomics", "-Wno-unused-result", *common_inc,
-        # diagnostics only (e.g. -DPDRNN_ABLATE=N timing ablations); part of the build signature
+        # diagnostic / A-B builds only (e.g. -DPDRNN_GEMM_AB=3); part of the build signature
         *os.environ.get("PDRNN_HIP_EXTRA_FLAGS", "").split(),
     ]
     host_flags = [

@@ -125,12 +125,12 @@ void report_stamps(const char* what, const Tensor& st, int iters) {
   }
   fprintf(stderr, "\n");
 }
-// progress-ordered wave priority in the small-H recurrences (PDRNN_PRIO=0 off)
+// progress-ordered wave priority in the small-H recurrences (PDRNN_PRIO=0 off):
+// B = 1440: 0.403 -> 0.387 ms/step (profiles/r3p_prio.md); rotation every 2^3 step pairs
 int prio_env() {
   const char* e = std::getenv("PDRNN_PRIO");
-  const char* p = std::getenv("PDRNN_PRIO_SHIFT");
-  const int mode = e ? std::atoi(e) : 2;  // B = 1440: 0.403 -> 0.387 ms/step (profiles/r3p_prio.md)
-  const int sh = p ? std::atoi(p) : 3;
+  const int mode = e ? std::atoi(e) : 2;
+  const int sh = 3;
   static int cus = 0;  // one GPU model per process
   if (!cus) {
     int dev = 0;
@@ -563,22 +563,16 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
                   (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_dw - 1) / ((int64_t)grid_dw * nb_dw)));
   }
 
-  // PDRNN_ONE_PASS_REDUCE=0: the two-pass reduction (A/B measurements)
-  static const bool one_pass = [] {
-    const char* e = getenv("PDRNN_ONE_PASS_REDUCE");
-    return !(e && e[0] == '0');
-  }();
-  const int split = (int)std::min<int64_t>(32, std::max<int64_t>(1, slab_rows / 16));
-  Tensor work = one_pass ? Tensor() : at::empty({split, P_rnn + PH}, opts);
-  TORCH_CHECK(one_pass || slot_step == nullptr, "stats_slot_step needs the one-pass reduction");
-  if (adam_state.has_value() && adam_hp.has_value()) {
-    // single-process step: the second reduction pass runs inside Adam
+  // one-pass reduction of the slabs into the flat gradient (+ batch statistics),
+  // with Adam folded in for a single process (slab_reduce_adam_kernel)
+  PdrnnAdamArgs ad{};
+  const bool fold_adam = adam_state.has_value() && adam_hp.has_value();
+  if (fold_adam) {
     const auto& as = *adam_state;
     const auto& hp = *adam_hp;  // lr, beta1, beta2, eps, weight_decay, step, decoupled
     TORCH_CHECK(as.size() == 3 && hp.size() == 7, "adam_state = [param, exp_avg, exp_avg_sq], 7 hyper-parameters");
     for (const auto& t : as)
       TORCH_CHECK(t.is_contiguous() && t.numel() == P_params && t.scalar_type() == at::kFloat, "flat fp32 Adam buffers");
-    PdrnnAdamArgs ad{};
     ad.param = as[0].data_ptr<float>(); ad.exp_avg = as[1].data_ptr<float>(); ad.exp_avg_sq = as[2].data_ptr<float>();
     ad.n = P_params;
     ad.lr = (float)hp[0]; ad.beta1 = (float)hp[1]; ad.beta2 = (float)hp[2]; ad.eps = (float)hp[3];
@@ -586,27 +580,11 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     ad.bias_correction1 = (float)(1.0 - std::pow(hp[1], hp[5]));
     ad.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(hp[2], hp[5]));
     ad.grad_scale = 1.f; ad.decoupled = hp[6] != 0.0 ? 1 : 0; ad.maximize = 0;
-    if (one_pass) {
-      HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(&ad, slab.data_ptr<float>(), slab_rows, P_rnn, L.P, colmap,
-                                              head_slab.data_ptr<float>(), B, PH, P_params, flat_grad.data_ptr<float>(),
-                                              stats.data_ptr<float>(), slot_step, (int)stats_slot_offset, ring_rows, st));
-      return;
-    }
-    HIP_LAUNCH_CHECK(pdrnn_slab2_reduce_pass1(slab.data_ptr<float>(), slab_rows, P_rnn, head_slab.data_ptr<float>(), B, PH,
-                                              work.data_ptr<float>(), split, colmap, L.P, st));
-    HIP_LAUNCH_CHECK(pdrnn_adam_partials(&ad, work.data_ptr<float>(), split, P_rnn + PH, flat_grad.data_ptr<float>(),
-                                         stats.data_ptr<float>(), 3, st));
-    return;
   }
-  if (one_pass) {
-    HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(nullptr, slab.data_ptr<float>(), slab_rows, P_rnn, L.P, colmap,
-                                            head_slab.data_ptr<float>(), B, PH, P_params, flat_grad.data_ptr<float>(),
-                                            stats.data_ptr<float>(), slot_step, (int)stats_slot_offset, ring_rows, st));
-    return;
-  }
-  HIP_LAUNCH_CHECK(pdrnn_slab2_reduce(slab.data_ptr<float>(), slab_rows, P_rnn, head_slab.data_ptr<float>(), B, PH,
-                                      P_params, flat_grad.data_ptr<float>(), stats.data_ptr<float>(),
-                                      work.data_ptr<float>(), split, colmap, L.P, st));
+  HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(fold_adam ? &ad : nullptr, slab.data_ptr<float>(), slab_rows, P_rnn, L.P,
+                                          colmap, head_slab.data_ptr<float>(), B, PH, P_params,
+                                          flat_grad.data_ptr<float>(), stats.data_ptr<float>(), slot_step,
+                                          (int)stats_slot_offset, ring_rows, st));
 }
 
 std::vector<Tensor> xent_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore_index, bool need_grad) {
@@ -786,10 +764,7 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     const char* e = std::getenv("PDRNN_LSTM_PERSIST_CHECK");
     return e && std::atoi(e) != 0;
   }();
-  static const int mode = [] {  // timing diagnostics only: results are wrong
-    const char* e = std::getenv("PDRNN_PS_MODE");
-    return e ? std::atoi(e) : 0;
-  }();
+  const int mode = 0;  // kernel mode bits: 16 = test hook (persist_inject_timeouts)
   if (env == 0 || tile >= 0 || g_persist_disabled.load()) return kPersistNotRun;
   int dev = 0;
   TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
@@ -807,8 +782,8 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
   }
   TORCH_CHECK(sticky_host[dev].data_ptr<int>()[0] == 0,
               "persistent LSTM recurrence: a grid-sync wait timed out in an earlier launch (results invalid)");
-  // [counters | err | pad | 64 x 8 int64 stamps (diagnostic mode bit 3)]
-  const int64_t stamp_ints = (mode & 8) ? 2 + 64 * 8 * 2 : 1;
+  // [counters | err | pad]
+  const int64_t stamp_ints = 1;
   Tensor sync = at::zeros({ndir * nmb + 1 + stamp_ints + 2}, opts.dtype(at::kInt));
   int* cnt = sync.data_ptr<int>();
   int m = mode;
@@ -837,16 +812,6 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
                    keep ? "" : " and using them for the rest of the process");
       TORCH_CHECK(hipMemsetAsync(sticky[dev].data_ptr<int>(), 0, sizeof(int), st) == hipSuccess, "sticky reset");
       return kPersistFailed;
-    }
-  }
-  if (mode & 8) {
-    // int64 stamps start at the first 8-byte boundary after err
-    Tensor st64 = sync.narrow(0, ndir * nmb + 1 + ((ndir * nmb + 1) & 1), 64 * 8 * 2).cpu();
-    const long long* v = reinterpret_cast<const long long*>(st64.data_ptr<int>());
-    for (int i = 1; i < 64; ++i) {
-      std::fprintf(stderr, "ps-stamp %s step %d:", backward ? "bwd" : "fwd", i);
-      for (int k = 1; k < 8; ++k) std::fprintf(stderr, " %lld", v[i * 8 + k] ? v[i * 8 + k] - v[i * 8] : -1);
-      std::fprintf(stderr, " | next %lld\n", v[(i + 1 < 64 ? i + 1 : i) * 8] - v[i * 8]);
     }
   }
   sticky_host[dev].copy_(sticky[dev], /*non_blocking=*/true);
@@ -975,16 +940,11 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
     dd.dh0 = dh0.data_ptr<float>() + d * B * H;
     dd.dc0 = dc0.data_ptr<float>() + d * B * H;
   }
-  static const int env_splitk = [] {
-    const char* e = std::getenv("PDRNN_LSTM_LARGE_SPLITK");
-    return e ? std::atoi(e) : 0;
-  }();
   int big = 0;
-  const int auto_splitk = pdrnn_lstm_large_bwd_splitk((int)B, (int)H, ndir, &big);
-  a.splitk = env_splitk > 0 ? env_splitk : auto_splitk;
-  a.splitk_big = env_splitk > 0 ? (B >= 128 && H % 128 == 0) : big;
+  a.splitk = pdrnn_lstm_large_bwd_splitk((int)B, (int)H, ndir, &big);
+  a.splitk_big = big;
   // large batch: ping-pong GEMM + cell kernel (fp32 dh through ws)
-  a.bwd_pp = (env_splitk <= 0 && a.splitk == 1) ? pdrnn_lstm_large_bwd_pp((int)B, (int)H, ndir, dt) : 0;
+  a.bwd_pp = a.splitk == 1 ? pdrnn_lstm_large_bwd_pp((int)B, (int)H, ndir, dt) : 0;
   Tensor ws;
   if (a.splitk > 1 || a.bwd_pp) {
     ws = at::empty({a.splitk, 2, B, H}, o32);
@@ -1149,6 +1109,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("split_bwd"), py::arg("nb_fwd"), py::arg("nb_bwd"), py::arg("adam_state") = py::none(),
         py::arg("adam_hp") = py::none(), py::arg("cell") = 0, py::arg("grad_colmap") = py::none(),
         py::arg("stats_slot_step") = py::none(), py::arg("stats_slot_offset") = 0);
+  m.def("gemm_variants", []() {
+    int v[8];
+    const int n = pdrnn_gemm_variants(v, 8);
+    return std::vector<int>(v, v + n);
+  }, "schedule variants of the in-tree GEMM compiled into this build (first = default)");
   m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
   m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
   m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer", py::arg("param"), py::arg("grad"),

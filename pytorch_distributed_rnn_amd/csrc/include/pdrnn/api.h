@@ -320,6 +320,8 @@ typedef struct {
   int variant;             // schedule variant (tuning)
 } PdrnnGemmArgs;
 int pdrnn_gemm_supported(const PdrnnGemmArgs* a);
+// schedule variants compiled into this build (first = default)
+int pdrnn_gemm_variants(int* out, int max);
 hipError_t pdrnn_gemm(const PdrnnGemmArgs* a, hipStream_t stream);
 // tile: -1 auto, 0..3 = 32x64 / 64x64 / 128x128 / 256x128 block tiles
 hipError_t pdrnn_gemm_nt(const void* A, int64_t lda, const void* Bt, int64_t ldb, float* C, int64_t ldc,

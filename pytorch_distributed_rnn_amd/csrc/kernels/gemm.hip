@@ -192,16 +192,19 @@ hipError_t launch_v(const PdrnnGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((gemm256_kernel<DT, AKM, BKM, false, V>), grid, dim3(512), LDS_BYTES, st, a);
   return hipGetLastError();
 }
+// Schedule variants (V bits: 1 = B_n1 refill in Q3, 2 = DMA after the fragment
+// reads, 32 / 64 = raster groups of 4 / 16 tile-rows).  The product build
+// compiles the default, 35 (profiles/r3_gemm/raster.log); an A/B build adds
+// ONE more: PDRNN_HIP_EXTRA_FLAGS=-DPDRNN_GEMM_AB=<V> python -m
+// pytorch_distributed_rnn_amd._build, then gemm16(..., variant=<V>).
+constexpr int kGemmDefaultVariant = 35;
 template <class DT, bool AKM, bool BKM>
 hipError_t launch(const PdrnnGemmArgs& a, hipStream_t st) {
-  switch (a.variant) {
-    case 1: return launch_v<DT, AKM, BKM, 1>(a, st);
-    case 2: return launch_v<DT, AKM, BKM, 2>(a, st);
-    case 3: return launch_v<DT, AKM, BKM, 3>(a, st);
-    case 35: return launch_v<DT, AKM, BKM, 35>(a, st);
-    case 67: return launch_v<DT, AKM, BKM, 67>(a, st);
-    default: return launch_v<DT, AKM, BKM, 0>(a, st);
-  }
+#ifdef PDRNN_GEMM_AB
+  if (a.variant == PDRNN_GEMM_AB) return launch_v<DT, AKM, BKM, PDRNN_GEMM_AB>(a, st);
+#endif
+  if (a.variant <= 0 || a.variant == kGemmDefaultVariant) return launch_v<DT, AKM, BKM, kGemmDefaultVariant>(a, st);
+  return hipErrorInvalidValue;  // not compiled into this build
 }
 
 template <class DT>
@@ -229,6 +232,15 @@ int pdrnn_gemm_supported(const PdrnnGemmArgs* a) {
   // split-K: fp32 partials only, at least one K-tile per split
   if (a->splitk > 1 && (a->c_16bit || a->accumulate || (a->K + a->K2) / 64 < a->splitk)) return 0;
   return 1;
+}
+
+int pdrnn_gemm_variants(int* out, int max) {
+  int n = 0;
+  if (n < max) out[n++] = pdrnn::kGemmDefaultVariant;
+#ifdef PDRNN_GEMM_AB
+  if (n < max && PDRNN_GEMM_AB != pdrnn::kGemmDefaultVariant) out[n++] = PDRNN_GEMM_AB;
+#endif
+  return n;
 }
 
 hipError_t pdrnn_gemm(const PdrnnGemmArgs* a, hipStream_t stream) {

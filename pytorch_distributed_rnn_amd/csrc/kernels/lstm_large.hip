@@ -220,7 +220,7 @@ struct GemmPipe {
 };
 
 // Tile configurations (BM, BN, WM, WN, STAGES)
-#define PDRNN_TILE_CFGS(X)   \
+#define TILE_CFGS_X(X)   \
   X(0, 32, 64, 1, 4, 4)      \
   X(1, 64, 64, 2, 2, 4)      \
   X(2, 128, 128, 2, 2, 3)    \
@@ -952,17 +952,17 @@ hipError_t dispatch_step(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwar
   }
   if (tile < 0 || tile > 4) tile = pick_tile(a->B, N, ndir);
   switch (tile) {
-#define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_) \
+#define TILE_CASE(ID, BM_, BN_, WM_, WN_, ST_) \
   case ID: return launch_step<DT, CELL, BM_, BN_, WM_, WN_, ST_>(a, ndir, backward, st);
-    PDRNN_TILE_CFGS(PDRNN_CASE)
-#undef PDRNN_CASE
+    TILE_CFGS_X(TILE_CASE)
+#undef TILE_CASE
     default: return hipErrorInvalidValue;
   }
 }
 
 // Tile shapes reachable only through the plain GEMM entry (tile-shape
 // experiments for the large-batch step GEMMs; ids >= 10).
-#define PDRNN_GEMM_ONLY_CFGS(X) \
+#define GEMM_ONLY_CFGS_X(X) \
   X(10, 256, 256, 2, 4, 2)      \
   X(11, 128, 128, 2, 2, 4)      \
   X(12, 128, 256, 2, 4, 3)      \
@@ -975,7 +975,7 @@ hipError_t gemm_nt_dispatch(const void* Av, int64_t lda, const void* Btv, int64_
   const typename DT::S* Bt = static_cast<const typename DT::S*>(Btv);
   if (tile < 0 || (tile > 4 && tile < 10) || tile > 13) tile = pick_tile(M, N, 1);
   switch (tile) {
-#define PDRNN_CASE(ID, BM_, BN_, WM_, WN_, ST_)                                                      \
+#define TILE_CASE(ID, BM_, BN_, WM_, WN_, ST_)                                                      \
   case ID: {                                                                                        \
     typedef GemmPipe<DT, BM_, BN_, WM_, WN_, ST_> G;                                                 \
     if (N % BN_) return hipErrorInvalidValue;                                                        \
@@ -984,9 +984,9 @@ hipError_t gemm_nt_dispatch(const void* Av, int64_t lda, const void* Btv, int64_
                        sizeof(typename DT::S) * G::LDS_ELEMS, st, A, lda, Bt, ldb, C, ldc, M, N, K); \
     return hipGetLastError();                                                                        \
   }
-    PDRNN_TILE_CFGS(PDRNN_CASE)
-    PDRNN_GEMM_ONLY_CFGS(PDRNN_CASE)
-#undef PDRNN_CASE
+    TILE_CFGS_X(TILE_CASE)
+    GEMM_ONLY_CFGS_X(TILE_CASE)
+#undef TILE_CASE
     default: return hipErrorInvalidValue;
   }
 }

@@ -40,20 +40,6 @@ namespace {
 // per-step global load on the recurrence's critical path.
 constexpr int kXldsBytes = 48 * 1024;
 
-// Timing ablations (diagnostic builds only, -DPDRNN_ABLATE=bits; results are
-// wrong): 1 no dW FMAs, 2 no W^T g FMAs, 4 no per-step operand loads (bwd),
-// 8 no bwd barrier, 16 no bwd tanh, 32 no fwd LDS operand reads, 64 no fwd
-// barrier, 128 no fwd transcendentals.
-#ifndef PDRNN_ABLATE
-#define PDRNN_ABLATE 0
-#endif
-#ifndef PDRNN_BWD_PIN_DW
-#define PDRNN_BWD_PIN_DW 1
-#endif
-#ifndef PDRNN_FWD_BULK_LDS
-#define PDRNN_FWD_BULK_LDS 1
-#endif
-constexpr bool kFwdBulkLds = PDRNN_FWD_BULK_LDS;
 
 // Stage one sequence's inputs x[t][0..I) into the LDS image xs[t][0..H)
 // (columns >= I zero): only the I real columns are loaded (not H), 4 loads
@@ -562,10 +548,9 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
         float4 vin4[K / 4];
 #pragma unroll
         for (int k4 = 0; k4 < K / 4; ++k4)
-          vin4[k4] = (PDRNN_ABLATE & 32) ? make_float4(hl[n], c[n], hl[n], c[n])
-                     : (4 * k4 < H) ? reinterpret_cast<const float4*>(src_in)[k4]
-                                    : reinterpret_cast<const float4*>(src_h)[k4 - H / 4];
-        if constexpr (kFwdBulkLds) __builtin_amdgcn_sched_barrier(0);
+          vin4[k4] = (4 * k4 < H) ? reinterpret_cast<const float4*>(src_in)[k4]
+                                  : reinterpret_cast<const float4*>(src_h)[k4 - H / 4];
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k4 = 0; k4 < K / 4; ++k4) {
           const float4 v = vin4[k4];
@@ -575,7 +560,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
         }
         const pdrnn_f2 s2 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         const float z = (s2.x + s2.y) + bias;  // = -log2(e) * gsc * preactivation
-        const float sg = (PDRNN_ABLATE & 128) ? z : fast_rcp(1.f + __builtin_amdgcn_exp2f(z));
+        const float sg = fast_rcp(1.f + __builtin_amdgcn_exp2f(z));
         const float act = lin ? z : fmaf(sg, am, ab);  // sigmoid, or tanh for the g gate
         const float ig = quad_bcast(act, 0);
         const float fg = quad_bcast(act, 1);
@@ -584,7 +569,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
         float cn, h;
         if constexpr (CELL == 0) {
           cn = fmaf(fg, c[n], ig * gg);
-          const float th = (PDRNN_ABLATE & 128) ? cn : fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(cn * (2.f * kNegLog2e))), 2.f, -1.f);
+          const float th = fmaf(fast_rcp(1.f + __builtin_amdgcn_exp2f(cn * (2.f * kNegLog2e))), 2.f, -1.f);
           h = og * th;
         } else {  // GRU: ig = r, fg = z, gg = n_x, og = n_h; cn carries n
           const float pre = fmaf(ig, og, gg);
@@ -605,8 +590,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
         for (int n = 0; n < NB; ++n) vin(n, 0, p ^ 1)[lg] = xnext[n];
       }
     }
-    if constexpr (PDRNN_ABLATE & 64) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else lds_barrier();
+    lds_barrier();
   }
   if (a.stamps && tid == 0) {
     uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
@@ -1156,7 +1140,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
         float dgv, dcn;
         if constexpr (CELL == 0) {
           const float cp = (t > 0 || c0p) ? op[n].cp : 0.f;
-          const float tc = (PDRNN_ABLATE & 16) ? op[n].ct : tanhf_fast(op[n].ct);
+          const float tc = tanhf_fast(op[n].ct);
           const float dcp = fmaf(dht * og, 1.f - tc * tc, dc[n]);
           // i: dcp gg s'(i)  f: dcp cp s'(f)  g: dcp ig t'(g)  o: dht tc s'(o)
           const float oth = fmaf(gm[0], gg, fmaf(gm[1], cp, fmaf(gm[2], ig, gm[3] * tc)));
@@ -1192,8 +1176,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
                                                 st_ok ? vo_q : 0x80000000u, so, 0);
         }
       }
-      if constexpr (PDRNN_ABLATE & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      else lds_barrier();
+      lds_barrier();
       // ---------------- column phase ----------------
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
@@ -1219,17 +1202,13 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
         for (int r4 = 0; r4 < RS / 4; ++r4) {
           const float4 g = gv[r4];
           const pdrnn_f2 g01 = {g.x, g.y}, g23 = {g.z, g.w};
-          if constexpr (!(PDRNN_ABLATE & 2)) {
-            sh[0] = __builtin_elementwise_fma(whh[2 * r4], g01, sh[0]);
-            sh[1] = __builtin_elementwise_fma(whh[2 * r4 + 1], g23, sh[1]);
-            if (need_dx) {  // wave-uniform (one layer per wave); no loads inside
-              sx[0] = __builtin_elementwise_fma(wih[2 * r4], g01, sx[0]);
-              sx[1] = __builtin_elementwise_fma(wih[2 * r4 + 1], g23, sx[1]);
-            }
-          } else {
-            sh[0] += g01; sx[1] += g23;
+          sh[0] = __builtin_elementwise_fma(whh[2 * r4], g01, sh[0]);
+          sh[1] = __builtin_elementwise_fma(whh[2 * r4 + 1], g23, sh[1]);
+          if (need_dx) {  // wave-uniform (one layer per wave); no loads inside
+            sx[0] = __builtin_elementwise_fma(wih[2 * r4], g01, sx[0]);
+            sx[1] = __builtin_elementwise_fma(wih[2 * r4 + 1], g23, sx[1]);
           }
-          if constexpr (!(PDRNN_ABLATE & 1) && !DWOUT) {
+          if constexpr (!DWOUT) {
             dwhh[2 * r4] = __builtin_elementwise_fma(g01, hb, dwhh[2 * r4]);
             dwhh[2 * r4 + 1] = __builtin_elementwise_fma(g23, hb, dwhh[2 * r4 + 1]);
             dwih[2 * r4] = __builtin_elementwise_fma(g01, xb, dwih[2 * r4]);
@@ -1239,7 +1218,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
         // pin this step's dW updates here: they feed nothing until the
         // epilogue, and left free the scheduler sinks them into the next
         // step (keeping this step's gate-gradient slice live across it)
-        if constexpr (PDRNN_BWD_PIN_DW && !DWOUT) {
+        if constexpr (!DWOUT) {
 #pragma unroll
           for (int rr = 0; rr < RS / 2; ++rr) asm volatile("" : "+v"(dwhh[rr]), "+v"(dwih[rr]));
         }
@@ -1265,11 +1244,7 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
       }
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
-        if constexpr (PDRNN_ABLATE & 4) {
-          op[n].aq += 1e-3f; op[n].ct += 1e-3f; op[n].hprev += 1e-3f; op[n].xin += 1e-3f;
-        } else {
-          op[n] = load_ops(n, t - 2);  // refill for two steps ahead
-        }
+        op[n] = load_ops(n, t - 2);  // refill for two steps ahead
       }
     };
 
@@ -1565,15 +1540,12 @@ hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
 // Lanes per hidden unit of the unit-group backward: 8 when the workgroup still
 // fits (NL*H*8 <= 512; shorter per-lane row slices), else 4.
 // PDRNN_LSTM_BWD_L=4|8 overrides (sweeps).
+// lanes per hidden unit of the unit-group backward: 8 at H = 64 (row slices
+// of 32), else 4
 template <int H>
 int bwd_gs_lanes(int NL) {
-  static const int env = [] {
-    const char* e = getenv("PDRNN_LSTM_BWD_L");
-    return e ? atoi(e) : 0;
-  }();
-  if (H == 64) return 8;
-  if (env == 4 || env == 8) return (env == 8 && NL * H * 8 > 512) ? 4 : env;
-  return 4;
+  (void)NL;
+  return H == 64 ? 8 : 4;
 }
 
 // Persistent grid for the backward: as many workgroups as can be resident
@@ -1972,14 +1944,9 @@ hipError_t pdrnn_lstm_small_bwd_dw(const PdrnnLstmSmallBwdArgs* a, const PdrnnLs
 // 1 when the fused one-launch step covers (H, NL, B, launch config): the
 // gate-split forward with one sequence per workgroup, the L = 4 unit-group
 // backward, and a backward grid of one sequence per workgroup (gridb == B).
-// PDRNN_STEP_ONE_LAUNCH=0 disables it (A/B measurements).
 int pdrnn_lstm_small_step_ok(int H, int NL, int B, int nb_fwd, int split_fwd, int nb_bwd, int split_bwd,
                              int gridb) {
-  static const bool off = [] {
-    const char* e = getenv("PDRNN_STEP_ONE_LAUNCH");
-    return e && e[0] == '0';
-  }();
-  if (off || (H != 16 && H != 32) || nb_fwd != 1 || split_fwd != 1 || nb_bwd != 1 || split_bwd != 1) return 0;
+  if ((H != 16 && H != 32) || nb_fwd != 1 || split_fwd != 1 || nb_bwd != 1 || split_bwd != 1) return 0;
   if (NL * 4 * H > 512 || gridb != B) return 0;
   const int lanes = H == 16 ? pdrnn::bwd_gs_lanes<16>(NL) : pdrnn::bwd_gs_lanes<32>(NL);
   return lanes == 4 ? 1 : 0;
@@ -2056,7 +2023,7 @@ int pdrnn_lstm_small_bwd_grid(int H, int NL, int T, int B, int nb, int split) {
   if (split != 1) return (B + nb - 1) / nb;
   PdrnnLstmSmallBwdArgs a{};
   a.NL = NL; a.T = T; a.B = B;
-#define PDRNN_BWD_GRID(HH, LL)                                   \
+#define BWD_GRID_CASE(HH, LL)                                   \
   switch (nb) {                                                  \
     case 1: return pdrnn::bwd_gs_grid<HH, LL, 1>(&a);            \
     case 2: return pdrnn::bwd_gs_grid<HH, LL, 2>(&a);            \
@@ -2065,17 +2032,17 @@ int pdrnn_lstm_small_bwd_grid(int H, int NL, int T, int B, int nb, int split) {
   }
   switch (H) {
     case 16:
-      if (pdrnn::bwd_gs_lanes<16>(NL) == 8) { PDRNN_BWD_GRID(16, 8) }
-      PDRNN_BWD_GRID(16, 4)
+      if (pdrnn::bwd_gs_lanes<16>(NL) == 8) { BWD_GRID_CASE(16, 8) }
+      BWD_GRID_CASE(16, 4)
     case 32:
-      if (pdrnn::bwd_gs_lanes<32>(NL) == 8) { PDRNN_BWD_GRID(32, 8) }
-      PDRNN_BWD_GRID(32, 4)
+      if (pdrnn::bwd_gs_lanes<32>(NL) == 8) { BWD_GRID_CASE(32, 8) }
+      BWD_GRID_CASE(32, 4)
     case 64:
       if (nb != 1) return -1;
       return pdrnn::bwd_gs_grid<64, 8, 1>(&a);
     default: return -1;
   }
-#undef PDRNN_BWD_GRID
+#undef BWD_GRID_CASE
 }
 
 hipError_t pdrnn_slab_reduce(const float* slab, int64_t rows, int64_t P, float* out, float beta,

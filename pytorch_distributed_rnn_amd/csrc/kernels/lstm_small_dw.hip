@@ -70,12 +70,8 @@ extern "C" {
 
 int pdrnn_lstm_small_dw_chunks(int H, int NL, int B, int T) {
   (void)H; (void)NL;
-  static const int env = [] {
-    const char* e = getenv("PDRNN_DW_CHUNKS");
-    return e ? atoi(e) : 0;
-  }();
   const int64_t stages = ((int64_t)B * T + pdrnn::kDwRows - 1) / pdrnn::kDwRows;
-  int64_t c = env > 0 ? env : 256;
+  int64_t c = 256;
   if (c > stages / 4) c = stages / 4;  // at least 4 stages per chunk (amortise the pipeline fill)
   if (c < 1) c = 1;
   return (int)c;

@@ -36,9 +36,10 @@ def _native(t: Tensor):
 
 
 def _variant() -> int:
-    # 3: B_n1 refill in Q3 + DMA after the fragment reads; +32: raster groups of
-    # 4 tile-rows (+2-4 % over 8 on the bi-LSTM shapes, profiles/r3_gemm/raster.log)
-    return int(os.environ.get("PDRNN_GEMM_VARIANT", "35"))
+    # the build's default schedule (kernels/gemm.hip: 3 = B_n1 refill in Q3 +
+    # DMA after the fragment reads; +32 = raster groups of 4 tile-rows, +2-4 %
+    # over 8 on the bi-LSTM shapes, profiles/r3_gemm/raster.log)
+    return 0
 
 
 def _cus(dev) -> int:

@@ -52,6 +52,45 @@ def _hprev(hseq_d: Tensor, h0d: Optional[Tensor], d: int) -> Tensor:
     return torch.cat([h0d, hseq_d[:-1]], 0) if d == 0 else torch.cat([hseq_d[1:], h0d], 0)
 
 
+def _gru_shadows(weights, ndir: int, H: int, I: int, cdt, device):
+    """The packed compute-dtype copies the kernels read -- per direction W_ih
+    (dX GEMM), the [r | z | n_x | 0] projection stack (gate-interleaved, both
+    directions concatenated), the [r | z | 0 | n_h] recurrent stack, its
+    gate-interleaved form (forward step) and its transpose (BPTT step) -- plus
+    the folded projection bias.  Cached on the first weight and rebuilt only
+    when a parameter's version counter or storage changes (an optimizer step),
+    like the large LSTM's shadows (ops/lstm_large.py:_shadow_cat)."""
+    ver = tuple((w._version, w.data_ptr()) if w is not None else None for w in weights[:4 * ndir])
+    key = ("gru", cdt, ndir, H, I)
+    cache = getattr(weights[0], "_pdrnn_shadow", None)
+    if cache is None:
+        cache = {}
+        weights[0]._pdrnn_shadow = cache
+    ent = cache.get(key)
+    if ent is not None and ent[0] == ver:
+        return ent[1]
+    perm = _perm(H, device)
+    wih, whh4, wih4, b4 = [], [], [], []
+    with torch.no_grad():
+        for d in range(ndir):
+            w_ih, w_hh, b_ih, b_hh = weights[4 * d:4 * d + 4]
+            w_ih16, w_hh16 = w_ih.detach().to(cdt), w_hh.detach().to(cdt)
+            wih.append(w_ih16.contiguous())
+            wih4.append(_interleave(torch.cat([w_ih16, w_ih16.new_zeros(H, I)]), H))
+            whh4.append(torch.cat([w_hh16[:2 * H], w_hh16.new_zeros(H, H), w_hh16[2 * H:]]))
+            b = torch.zeros(4 * H, device=device, dtype=torch.float32)
+            if b_ih is not None:
+                b[:3 * H] += b_ih.detach().float()
+            if b_hh is not None:
+                b[:2 * H] += b_hh.detach()[:2 * H].float()
+                b[3 * H:] += b_hh.detach()[2 * H:].float()
+            b4.append(b[perm])
+        out = (wih, torch.cat(wih4).contiguous(), whh4, [_interleave(w, H).contiguous() for w in whh4],
+               [w.t().contiguous() for w in whh4], torch.cat(b4))
+    cache[key] = (ver, out)
+    return out
+
+
 class _LargeGRULayer(torch.autograd.Function):
     """One layer, 1 or 2 directions.  x: [T, B, I] (compute dtype); weights per
     direction (w_ih, w_hh, b_ih, b_hh), fp32 masters (biases may be None)."""
@@ -62,31 +101,16 @@ class _LargeGRULayer(torch.autograd.Function):
         cdt = x.dtype
         T, B, I = x.shape
         mod = _ext.native(x.device)
-        perm = _perm(H, x.device)
-        wih, whh4, wih4, b4 = [], [], [], []
-        for d in range(ndir):
-            w_ih, w_hh, b_ih, b_hh = weights[4 * d:4 * d + 4]
-            w_ih16, w_hh16 = w_ih.to(cdt), w_hh.to(cdt)
-            wih.append(w_ih16)
-            wih4.append(_interleave(torch.cat([w_ih16, w_ih16.new_zeros(H, I)]), H))
-            whh4.append(torch.cat([w_hh16[:2 * H], w_hh16.new_zeros(H, H), w_hh16[2 * H:]]))
-            b = torch.zeros(4 * H, device=x.device, dtype=torch.float32)
-            if b_ih is not None:
-                b[:3 * H] += b_ih.float()
-            if b_hh is not None:
-                b[:2 * H] += b_hh[:2 * H].float()
-                b[3 * H:] += b_hh[2 * H:].float()
-            b4.append(b[perm])
-        xp = linear16(x.reshape(T * B, I), torch.cat(wih4), torch.cat(b4))  # in-tree MFMA GEMM (16-bit)
+        wih, wih4_all, whh4, whh_p, wt, b4_all = _gru_shadows(weights, ndir, H, I, cdt, x.device)
+        xp = linear16(x.reshape(T * B, I), wih4_all, b4_all)  # in-tree MFMA GEMM (16-bit)
         xp = xp.view(T, B, ndir * 4 * H)
-        whh_p = [_interleave(w, H).contiguous() for w in whh4]
         h0c = h0.to(cdt).contiguous() if h0 is not None else None
         h0f = h0.float().contiguous() if h0 is not None else None
         rev_mask = 2 if ndir == 2 else 0
         hseq, hs32, acts = mod.lstm_large_fwd(xp, whh_p, h0c, h0f, H, rev_mask, tile, 1)
         last = [T - 1, 0][:ndir]
         hn = torch.stack([hseq[last[d], :, d * H:(d + 1) * H] for d in range(ndir)], 0)
-        ctx.save_for_backward(x, hseq, hs32, acts, h0c, h0f, *wih, *whh4)
+        ctx.save_for_backward(x, hseq, hs32, acts, h0c, h0f, *wih, *wt)
         ctx.cfg = (H, ndir, tile, rev_mask, [w is not None for w in weights], h0 is not None,
                    h0.dtype if h0 is not None else None)
         return hseq, hn
@@ -95,13 +119,12 @@ class _LargeGRULayer(torch.autograd.Function):
     def backward(ctx, dhseq, dhn):
         H, ndir, tile, rev_mask, has_w, has_h0, h0_dtype = ctx.cfg
         x, hseq, hs32, acts, h0c, h0f, *ws = ctx.saved_tensors
-        wih, whh4 = ws[:ndir], ws[ndir:]
+        wih, wt = ws[:ndir], list(ws[ndir:])                        # wt: [H, 4H], gate-blocked
         cdt = x.dtype
         T, B, I = x.shape
         mod = _ext.native(x.device)
         dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
         dhn_f = dhn.float().contiguous() if dhn is not None else None
-        wt = [w.t().contiguous() for w in whh4]                     # [H, 4H], gate-blocked
         dgates, dh0, _ = mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1)
         grads: List[Optional[Tensor]] = []
         dx = None
