@@ -111,6 +111,7 @@ def persist_stats() -> dict:
     (bindings.cpp large_persist)."""
     mod = extension()
     if mod is None or not hasattr(mod, "persist_fallbacks"):
-        return {"persist_verify": False, "persist_fallbacks": 0, "persist_disabled": False}
-    return {"persist_verify": bool(mod.persist_verify_on()), "persist_fallbacks": int(mod.persist_fallbacks()),
-            "persist_disabled": bool(mod.persist_disabled())}
+        return {"persist_verify": "off", "persist_fallbacks": 0, "persist_disabled": False}
+    mode = int(mod.persist_verify_mode())
+    return {"persist_verify": ("off", "launch", "step")[mode] if 0 <= mode <= 2 else str(mode),
+            "persist_fallbacks": int(mod.persist_fallbacks()), "persist_disabled": bool(mod.persist_disabled())}

@@ -733,23 +733,31 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 //     synchronisation; a sticky per-device flag is copied to pinned memory
 //     after every launch and checked at the next one (fails loudly one call
 //     later), and by persist_check() at epoch end.
+//   * verify per step (set_persist_verify(2) -- the multi-rank trainers do
+//     it): no synchronisation per launch; a timed-out launch leaves the sticky
+//     flag set, the step's later persistent launches run per step, and the
+//     trainer's persist_step_check() before the optimizer update (one host
+//     read per step, agreed across ranks) re-runs the whole step when any
+//     rank saw a timeout (train/lm.py).  Launch-verify costs 6.7 % of the
+//     char-LM step (profiles/r4/nb1_charlm_verify*.log); this costs one sync.
 enum PersistResult { kPersistNotRun = 0, kPersistOk = 1, kPersistFailed = 2 };
-std::atomic<int> g_persist_verify{-1};     // -1: PDRNN_LSTM_PERSIST_VERIFY (default off)
+std::atomic<int> g_persist_verify{-1};     // -1: PDRNN_LSTM_PERSIST_VERIFY (default off); 1 launch, 2 step
 std::atomic<int> g_persist_inject{0};      // tests: flag the next N launches as timed out
 std::atomic<long long> g_persist_fallbacks{0};
 // after the first timed-out launch in a process the persistent path is off for
 // good: a lost co-residency (RCCL kernels beside it) tends to recur every step,
 // and each occurrence costs the 2 s spin bound plus the per-step re-run
 std::atomic<int> g_persist_disabled{0};
-bool persist_verify_on() {
+int persist_verify_mode() {
   const int v = g_persist_verify.load();
-  if (v >= 0) return v != 0;
-  static const bool env = [] {
+  if (v >= 0) return v;
+  static const int env = [] {
     const char* e = std::getenv("PDRNN_LSTM_PERSIST_VERIFY");
-    return e && std::atoi(e) != 0;
+    return e ? std::atoi(e) : 0;
   }();
   return env;
 }
+bool persist_verify_on() { return persist_verify_mode() == 1; }
 // leaked on purpose: no tensor destructor runs after the HIP runtime is gone
 std::vector<Tensor>& persist_sticky() { static auto& v = *new std::vector<Tensor>(64); return v; }
 std::vector<Tensor>& persist_sticky_host() { static auto& v = *new std::vector<Tensor>(64); return v; }
@@ -780,8 +788,12 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     sticky[dev] = at::zeros({1}, opts.dtype(at::kInt));
     sticky_host[dev] = at::zeros({1}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
   }
-  TORCH_CHECK(sticky_host[dev].data_ptr<int>()[0] == 0,
-              "persistent LSTM recurrence: a grid-sync wait timed out in an earlier launch (results invalid)");
+  if (sticky_host[dev].data_ptr<int>()[0] != 0) {
+    // per-step verification: an earlier launch of this step timed out -- the
+    // step's check re-runs it; the rest of the step takes the per-step kernels
+    if (persist_verify_mode() == 2) return kPersistNotRun;
+    TORCH_CHECK(false, "persistent LSTM recurrence: a grid-sync wait timed out in an earlier launch (results invalid)");
+  }
   // [counters | err | pad]
   const int64_t stamp_ints = 1;
   Tensor sync = at::zeros({ndir * nmb + 1 + stamp_ints + 2}, opts.dtype(at::kInt));
@@ -820,6 +832,23 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     TORCH_CHECK(err == 0, "persistent LSTM grid sync timed out");
   }
   return kPersistOk;
+}
+
+// Per-step verification: true when a persistent launch on this device timed
+// out since the last check (synchronises); the flag is cleared, the timeout
+// counted, and the persistent path turned off for the process.
+bool persist_step_check() {
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
+  if (dev < 0 || dev >= 64 || !persist_sticky()[dev].defined()) return false;
+  if (persist_sticky()[dev].item<int>() == 0) return false;  // synchronises
+  persist_sticky()[dev].zero_();
+  persist_sticky_host()[dev].zero_();
+  g_persist_fallbacks++;
+  if (std::getenv("PDRNN_LSTM_PERSIST_RETRY") == nullptr) g_persist_disabled = 1;
+  std::fprintf(stderr, "[pdrnn] persistent LSTM recurrence: a grid-sync wait timed out in this step (fallback #%lld); "
+               "the step is re-run on the per-step kernels\n", (long long)g_persist_fallbacks.load());
+  return true;
 }
 
 // End-of-epoch check of the deferred (verify-off) path: raises if any
@@ -1124,16 +1153,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
   m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
   m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });
-  m.def("set_persist_verify", [](bool on) { g_persist_verify = on ? 1 : 0; },
-        "synchronise after every persistent-recurrence launch and re-run a timed-out layer on the per-step kernels");
+  m.def("set_persist_verify", [](int mode) { g_persist_verify = mode; },
+        "0 off; 1 synchronise after every persistent-recurrence launch and re-run a timed-out layer on the "
+        "per-step kernels; 2 per step: persist_step_check() before the optimizer update re-runs the step");
+  m.def("persist_verify_mode", []() { return persist_verify_mode(); });
+  m.def("persist_step_check", &persist_step_check,
+        "per-step verification: True when a persistent launch timed out since the last check (synchronises)");
   m.def("persist_inject_timeouts", [](int64_t n) { g_persist_inject = (int)n; },
         "tests: flag the next n persistent launches as timed out");
   m.def("persist_fallbacks", []() { return (int64_t)g_persist_fallbacks.load(); },
         "persistent launches re-run on the per-step kernels after a timeout");
-  m.def("persist_verify_on", []() { return persist_verify_on(); },
-        "every persistent launch is verified (host sync + flag read) before its result is used");
+  m.def("persist_verify_on", []() { return persist_verify_mode() != 0; },
+        "persistent launches are verified (per launch or per step) before the optimizer uses their results");
   m.def("persist_disabled", []() { return g_persist_disabled.load() != 0; },
         "the persistent recurrence is off for this process (after a timed-out launch)");
+  m.def("persist_disable", []() { g_persist_disabled = 1; },
+        "turn the persistent recurrence off for this process (a job-wide re-run after a timeout)");
   m.def("persist_reset", []() { g_persist_disabled = 0; g_persist_fallbacks = 0; },
         "tests: re-enable the persistent recurrence and clear the fallback count");
   m.def("debug_spin_cus", [](double ms, int64_t workgroups, int64_t threads, int64_t lds_bytes) {

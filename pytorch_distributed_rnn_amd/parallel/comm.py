@@ -140,9 +140,12 @@ def get_comm(group=None, prefer_native: bool = True):
     if mod is not None and torch.cuda.is_available() and dist.get_world_size(g) > 1 \
             and hasattr(mod, "set_persist_verify"):
         # collectives now run beside the compute stream: a persistent
-        # recurrence can lose co-residency to them, so its launches are
-        # verified and a timed-out layer is re-run (bindings.cpp large_persist)
-        mod.set_persist_verify(True)
+        # recurrence can lose co-residency to them, so every step is verified
+        # before its optimizer update and re-run after a timeout (per-step
+        # mode: bindings.cpp large_persist / persist_step_check, train/lm.py);
+        # PDRNN_LSTM_PERSIST_VERIFY=1 selects the per-launch check instead
+        if os.environ.get("PDRNN_LSTM_PERSIST_VERIFY") is None:
+            mod.set_persist_verify(2)
     return comm
 
 

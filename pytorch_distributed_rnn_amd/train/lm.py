@@ -69,13 +69,45 @@ class LMTrainer:
             norm = torch.linalg.vector_norm(g)
             g.mul_(torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0))
 
-    def train_step(self, inp: Tensor, tgt: Tensor) -> Tensor:
+    def _fwd_bwd(self, inp: Tensor, tgt: Tensor) -> Tensor:
         self.optimizer.zero_grad()
         with trace_range("pdrnn.forward"):
             logits = self.model(inp, carry=True)                               # [T, B, V]
             loss = cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt.t().reshape(-1))
         with trace_range("pdrnn.backward"):
             loss.backward()
+        return loss
+
+    def _persist_timed_out(self) -> bool:
+        """Per-step verification of the persistent recurrence (multi-rank
+        jobs, bindings.cpp persist_step_check): True when any rank's
+        persistent launch lost co-residency during this step -- then every
+        rank re-runs the step on the per-step kernels (the re-run's
+        collectives must match on all ranks)."""
+        mod = _ext.extension() if self.device.type == "cuda" else None
+        if mod is None or not hasattr(mod, "persist_step_check") or mod.persist_verify_mode() != 2:
+            return False
+        local = bool(mod.persist_step_check())
+        if self.world > 1:
+            from ..parallel.comm import get_comm
+            flag = torch.tensor([1.0 if local else 0.0], device=self.device)
+            comm = get_comm()
+            comm.all_reduce(flag, "max")
+            comm.wait()
+            local = bool(flag.item())
+        if local:
+            mod.persist_disable()
+        return local
+
+    def train_step(self, inp: Tensor, tgt: Tensor) -> Tensor:
+        carry0 = getattr(self.inner, "_state", None)
+        loss = self._fwd_bwd(inp, tgt)
+        if self._persist_timed_out():
+            # a persistent launch of this step lost co-residency (results
+            # invalid, parameters untouched): the whole step again from the
+            # same carried state, now on the per-step kernels
+            self.inner._state = carry0
+            loss = self._fwd_bwd(inp, tgt)
         with trace_range("pdrnn.optimizer"):
             self._clip()
             self.optimizer.step()
@@ -104,7 +136,7 @@ class LMTrainer:
         out.update(ps)
         logging.info(f"{self.rank}: Epoch {epoch} loss {mean:.6f} tokens/s {out['tokens_per_sec']:.1f} "
                      f"(x{self.world} ranks) device_peak_mib={out['device_peak_mib']:.1f} "
-                     f"persist_verify={int(ps['persist_verify'])} persist_fallbacks={ps['persist_fallbacks']}")
+                     f"persist_verify={ps['persist_verify']} persist_fallbacks={ps['persist_fallbacks']}")
         return out
 
     # ------------------------------------------------------------ checkpoints
