@@ -1070,15 +1070,120 @@ Tensor gemm16(const Tensor& A, bool a_kmajor, const Tensor& B, bool b_kmajor, co
               "gemm16: shape not covered (K % 64, k-major M/N % 8, 16-bit output N % 8)");
   HIP_LAUNCH_CHECK(pdrnn_gemm(&a, cur_stream()));
   if (splitk > 1) {
-    Tensor r = C.sum(0);
-    if (out.has_value()) {
-      if (accumulate) out->add_(r);
-      else out->copy_(r);
-      return *out;
-    }
+    // fixed-order sum of the partials (in-tree, deterministic)
+    Tensor r = out.has_value() ? *out : at::empty({M, N}, A.options().dtype(at::kFloat));
+    TORCH_CHECK(r.is_contiguous(), "gemm16: split-K output must be contiguous");
+    HIP_LAUNCH_CHECK(pdrnn_splitk_sum(C.data_ptr<float>(), (int)splitk, M * N, r.data_ptr<float>(),
+                                      out.has_value() && accumulate ? 1 : 0, cur_stream()));
     return r;
   }
   return C;
+}
+
+int any_dtype(const Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return 2;
+  return dtype_code(t);
+}
+
+// fp32-product GEMM (kernels/gemm_f32.hip): returns (C, rowsum) -- rowsum [M]
+// fp32 = sums over K of op(A) when requested (the bias gradient of dW = G^T X).
+std::vector<Tensor> gemm_f32(const Tensor& A, bool a_kmajor, const Tensor& B, bool b_kmajor,
+                             const optional<Tensor>& A2, const optional<Tensor>& B2, const optional<Tensor>& bias,
+                             bool out16, const optional<Tensor>& out, bool accumulate, int64_t splitk, bool rowsum) {
+  CHECK_HIP_TENSOR(A);
+  CHECK_HIP_TENSOR(B);
+  const c10::DeviceGuard guard(A.device());
+  const int dt = any_dtype(A);
+  TORCH_CHECK(any_dtype(B) == dt && A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1,
+              "gemm_f32: 2-D operands of one dtype with unit inner stride");
+  const int64_t M = a_kmajor ? A.size(1) : A.size(0), K = a_kmajor ? A.size(0) : A.size(1);
+  const int64_t N = b_kmajor ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == K, "gemm_f32: K mismatch");
+  PdrnnGemmF32Args a{};
+  a.A = A.data_ptr(); a.B = B.data_ptr(); a.lda = A.stride(0); a.ldb = B.stride(0);
+  if (A2.has_value() || B2.has_value()) {
+    TORCH_CHECK(A2.has_value() && B2.has_value(), "gemm_f32: A2 and B2 together");
+    const Tensor& a2 = *A2;
+    const Tensor& b2 = *B2;
+    TORCH_CHECK(any_dtype(a2) == dt && any_dtype(b2) == dt && a2.dim() == 2 && b2.dim() == 2 && a2.stride(1) == 1 &&
+                b2.stride(1) == 1, "gemm_f32: segment-2 operands");
+    const int64_t K2 = a_kmajor ? a2.size(0) : a2.size(1);
+    TORCH_CHECK((a_kmajor ? a2.size(1) : a2.size(0)) == M && (b_kmajor ? b2.size(1) : b2.size(0)) == N &&
+                (b_kmajor ? b2.size(0) : b2.size(1)) == K2, "gemm_f32: segment-2 shapes");
+    a.A2 = a2.data_ptr(); a.B2 = b2.data_ptr(); a.lda2 = a2.stride(0); a.ldb2 = b2.stride(0); a.K2 = (int)K2;
+  }
+  bool vec = true;
+  for (const int64_t ld : {a.lda, a.ldb, a.A2 ? a.lda2 : (int64_t)4, a.B2 ? a.ldb2 : (int64_t)4}) vec = vec && ld % 4 == 0;
+  for (const void* ptr : {a.A, a.B, a.A2, a.B2})
+    vec = vec && reinterpret_cast<uintptr_t>(ptr) % (dt == 2 ? 16 : 8) == 0;
+  a.vec = vec ? 1 : 0;
+  if (splitk < 1) splitk = 1;
+  Tensor C;
+  if (splitk > 1) {
+    TORCH_CHECK(!out16 && !bias.has_value(), "gemm_f32: split-K gives fp32 partials without bias");
+    C = at::empty({splitk, M, N}, A.options().dtype(at::kFloat));
+    a.c_split_stride = M * N;
+  } else if (out.has_value()) {
+    C = *out;
+    TORCH_CHECK(C.dim() == 2 && C.size(0) == M && C.size(1) == N && C.stride(1) == 1 &&
+                (out16 ? C.scalar_type() == A.scalar_type() : C.scalar_type() == at::kFloat), "gemm_f32: out");
+  } else {
+    C = at::empty({M, N}, A.options().dtype(out16 ? A.scalar_type() : at::kFloat));
+  }
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N,
+                "gemm_f32: fp32 bias[N]");
+    a.bias = bias->data_ptr<float>();
+  }
+  Tensor rs;
+  if (rowsum) {
+    rs = at::empty({splitk, M}, A.options().dtype(at::kFloat));
+    a.rowsum = rs.data_ptr<float>();
+  }
+  a.C = C.data_ptr();
+  a.ldc = splitk > 1 ? N : C.stride(0);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.in_dtype = dt;
+  a.out_dtype = out16 ? dt : 2;
+  TORCH_CHECK(!out16 || dt != 2, "gemm_f32: out16 needs 16-bit inputs");
+  a.a_kmajor = a_kmajor; a.b_kmajor = b_kmajor;
+  a.accumulate = splitk > 1 ? 0 : accumulate;
+  a.splitk = (int)splitk;
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && pdrnn_gemm_f32_supported(&a),
+              "gemm_f32: configuration not covered");
+  hipStream_t st = cur_stream();
+  HIP_LAUNCH_CHECK(pdrnn_gemm_f32(&a, st));
+  if (splitk > 1) {
+    Tensor r = out.has_value() ? *out : at::empty({M, N}, A.options().dtype(at::kFloat));
+    TORCH_CHECK(r.is_contiguous(), "gemm_f32: split-K output must be contiguous");
+    HIP_LAUNCH_CHECK(pdrnn_splitk_sum(C.data_ptr<float>(), (int)splitk, M * N, r.data_ptr<float>(),
+                                      out.has_value() && accumulate ? 1 : 0, st));
+    C = r;
+  }
+  if (rowsum && splitk > 1) {
+    Tensor r = at::empty({M}, A.options().dtype(at::kFloat));
+    HIP_LAUNCH_CHECK(pdrnn_splitk_sum(rs.data_ptr<float>(), (int)splitk, M, r.data_ptr<float>(), 0, st));
+    rs = r;
+  } else if (rowsum) {
+    rs = rs.view({M});
+  }
+  return {C, rs};
+}
+
+// column sums of a 2-D tensor (fp32 or 16-bit; unit column stride) -> fp32 [cols]
+Tensor col_sum(const Tensor& X) {
+  CHECK_HIP_TENSOR(X);
+  const c10::DeviceGuard guard(X.device());
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "col_sum: 2-D tensor with unit column stride");
+  const int64_t rows = X.size(0), cols = X.size(1);
+  Tensor out = at::empty({cols}, X.options().dtype(at::kFloat));
+  if (rows == 0) return out.zero_();
+  const int g = pdrnn_col_sum_groups(rows, cols);
+  Tensor part = at::empty({g, cols}, X.options().dtype(at::kFloat));
+  hipStream_t st = cur_stream();
+  HIP_LAUNCH_CHECK(pdrnn_col_sum(X.data_ptr(), any_dtype(X), rows, cols, X.stride(0), part.data_ptr<float>(), g, st));
+  HIP_LAUNCH_CHECK(pdrnn_splitk_sum(part.data_ptr<float>(), g, cols, out.data_ptr<float>(), 0, st));
+  return out;
 }
 
 // C[M, N] f32 = A[M, K] Bt[N, K]^T on the MFMA core (tests).
@@ -1138,6 +1243,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("split_bwd"), py::arg("nb_fwd"), py::arg("nb_bwd"), py::arg("adam_state") = py::none(),
         py::arg("adam_hp") = py::none(), py::arg("cell") = 0, py::arg("grad_colmap") = py::none(),
         py::arg("stats_slot_step") = py::none(), py::arg("stats_slot_offset") = 0);
+  m.def("gemm_f32", &gemm_f32, "fp32-product MFMA GEMM: (C, rowsum of op(A) over K)", py::arg("A"),
+        py::arg("a_kmajor"), py::arg("B"), py::arg("b_kmajor"), py::arg("A2") = py::none(), py::arg("B2") = py::none(),
+        py::arg("bias") = py::none(), py::arg("out16") = false, py::arg("out") = py::none(),
+        py::arg("accumulate") = false, py::arg("splitk") = 1, py::arg("rowsum") = false);
+  m.def("col_sum", &col_sum, "deterministic fp32 column sums of a 2-D tensor");
   m.def("gemm_variants", []() {
     int v[8];
     const int n = pdrnn_gemm_variants(v, 8);

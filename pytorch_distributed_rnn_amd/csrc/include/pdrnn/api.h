@@ -327,6 +327,36 @@ hipError_t pdrnn_gemm(const PdrnnGemmArgs* a, hipStream_t stream);
 hipError_t pdrnn_gemm_nt(const void* A, int64_t lda, const void* Bt, int64_t ldb, float* C, int64_t ldc,
                          int M, int N, int K, int dtype, int tile, hipStream_t stream);
 
+// fp32-product GEMM on the matrix cores (kernels/gemm_f32.hip): fp32 or
+// 16-bit inputs (widened exactly), any of the four operand layouts, optional
+// second K segment, fp32 bias, row sums of op(A) over K (bias gradients), split-K.
+typedef struct {
+  const void* A;
+  const void* B;
+  const void* A2;
+  const void* B2;
+  void* C;
+  const float* bias;         // [N], added in the epilogue (not with split-K)
+  float* rowsum;             // optional [splitk][M]: sum over K of op(A)(m, k)
+  int64_t lda, ldb, lda2, ldb2, ldc;
+  int M, N, K, K2;
+  int in_dtype;              // 0 bf16, 1 fp16, 2 fp32 (A, B, A2, B2)
+  int out_dtype;             // 2 fp32, else the 16-bit input dtype
+  int a_kmajor, b_kmajor, accumulate;
+  int splitk;                // > 1: fp32 partials at C + s * c_split_stride (ldc = N)
+  int64_t c_split_stride;
+  int vec;                   // every row stride a multiple of 4 elements and every base 16-byte aligned
+} PdrnnGemmF32Args;
+int pdrnn_gemm_f32_supported(const PdrnnGemmF32Args* a);
+hipError_t pdrnn_gemm_f32(const PdrnnGemmF32Args* a, hipStream_t stream);
+// out[i] (= or +=) sum_s part[s * n + i] in a fixed order
+hipError_t pdrnn_splitk_sum(const float* part, int splitk, int64_t n, float* out, int accumulate, hipStream_t stream);
+// column sums of X [rows, cols] (row stride ld, dtype 0 bf16 / 1 fp16 / 2 fp32):
+// partials part[groups][cols], then pdrnn_splitk_sum(part, groups, cols, out)
+int pdrnn_col_sum_groups(int64_t rows, int64_t cols);
+hipError_t pdrnn_col_sum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ld, float* part, int groups,
+                         hipStream_t stream);
+
 // Adam whose gradient is the fixed-order sum of `split` rows of work[split][P_total]
 // (columns [0, a->n)); grad_out receives it, columns [n, n + n_stats) -> stats_out.
 hipError_t pdrnn_adam_partials(const PdrnnAdamArgs* a, const float* work, int split, int64_t P_total,

@@ -1,0 +1,342 @@
+// fp32-product GEMM on the matrix cores (v_mfma_f32_16x16x4_f32) for the
+// large-H layers' time-batched products that the 16-bit ping-pong GEMM
+// (kernels/gemm.hip) does not serve:
+//   * fp32 models (the reference trains in fp32 with a user-set hidden size:
+//     reference src/motion/main.py:20-21, src/motion/model.py:9): the input
+//     projection Xp = X W_ih^T + b, dW_hh, dW_ih (+ db as the row sums of
+//     dgates^T, fused into the same pass) and dX of ops/lstm_large.py /
+//     ops/gru_large.py for H >= 128;
+//   * narrow outputs (N < 128, e.g. the bi-LSTM's 32-wide head) with 16-bit
+//     inputs, which would idle most of a 256-wide ping-pong tile.
+// 16-bit inputs are widened to fp32 on their way into LDS, so every product
+// is exact and accumulation is fp32 (same numerics as torch's fp32 matmul up
+// to summation order).
+//
+//   C[M, N] (= or +=) sum over the K segments of op(A) op(B) (+ bias[n])
+//   A: a_kmajor ? (m, k) at A[k * lda + m] : A[m * lda + k]    (same for B / n)
+//   segment 2 (K2 > 0): A2 / B2 with lda2 / ldb2, same layouts
+//   rowsum (optional): [splitk][M] sums over K of op(A)(m, k) -- the bias
+//   gradient of a dW = dgates^T x product, free beside the MFMAs
+//   splitk > 1: fp32 partials at C + s * c_split_stride (ldc = N), summed in a
+//   fixed order by pdrnn_splitk_sum (deterministic).
+//
+// Tile: 128 x BN (BN in {32, 64, 128}) x 16, 256 threads = 4 waves, each wave
+// a (128 / WAVES_M) x (BN / WAVES_N) block of 16 x 16 MFMA tiles.  Operands
+// are staged k-major in LDS ([k][m] / [k][n], rows padded by 16 floats: the 4
+// k-rows a fragment read touches land on 4 distinct 16-bank groups), double
+// buffered with the next tile's global loads in registers during the MFMAs.
+#include "pdrnn/api.h"
+#include "pdrnn/common.h"
+
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+
+namespace pdrnn {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int GF_BM = 128, GF_BK = 16, GF_THREADS = 256, GF_PAD = 16;
+
+template <int IN>
+__device__ __forceinline__ float ld1(const void* p, int64_t i) {
+  if constexpr (IN == 2) return static_cast<const float*>(p)[i];
+  else if constexpr (IN == 0) return bf16_to_f32(static_cast<const uint16_t*>(p)[i]);
+  else return __half2float(static_cast<const __half*>(p)[i]);
+}
+
+// 4 consecutive elements of a row starting at column c (of `cols`), row r (of
+// `rows`); out-of-range elements read 0.  vec: row stride and base allow one
+// aligned vector load when the whole quad is in range.
+template <int IN>
+__device__ __forceinline__ float4 quad(const void* p, int64_t ld, int r, int c, int rows, int cols, bool vec) {
+  const int64_t i = (int64_t)r * ld + c;
+  if (vec && r < rows && c + 3 < cols) {
+    if constexpr (IN == 2) {
+      return *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+    } else {
+      const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p) + i);
+      if constexpr (IN == 0) {
+        return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                           __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      } else {
+        const __half2 h0 = __builtin_bit_cast(__half2, u.x), h1 = __builtin_bit_cast(__half2, u.y);
+        return make_float4(__low2float(h0), __high2float(h0), __low2float(h1), __high2float(h1));
+      }
+    }
+  }
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (r < rows && c + j < cols) ? ld1<IN>(p, i + j) : 0.f;
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <int BN>
+struct GfCfg {
+  static constexpr int WN_WAVES = BN == 128 ? 2 : 1;
+  static constexpr int WM_WAVES = 4 / WN_WAVES;
+  static constexpr int WM = GF_BM / WM_WAVES, WN = BN / WN_WAVES;
+  static constexpr int MI = WM / 16, NI = WN / 16;
+  static constexpr int A_QUADS = GF_BM * GF_BK / 4 / GF_THREADS;     // per thread (2)
+  static constexpr int B_QUADS = (BN * GF_BK / 4 + GF_THREADS - 1) / GF_THREADS;
+  static constexpr int LDA_S = GF_BM + GF_PAD, LDB_S = BN + GF_PAD;
+};
+
+template <int IN, bool AKM, bool BKM, int BN>
+__global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p) {
+  using Cfg = GfCfg<BN>;
+  __shared__ __attribute__((aligned(16))) float As[2][GF_BK][Cfg::LDA_S];
+  __shared__ __attribute__((aligned(16))) float Bs[2][GF_BK][Cfg::LDB_S];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / Cfg::WN_WAVES, wn = wave % Cfg::WN_WAVES;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int m0 = tm * GF_BM, n0 = tn * BN;
+  const int nt1 = (p.K + GF_BK - 1) / GF_BK, nt2 = p.K2 > 0 ? (p.K2 + GF_BK - 1) / GF_BK : 0;
+  const int nt = nt1 + nt2;
+  const int split = blockIdx.y, nsplit = gridDim.y;
+  const int t_begin = (int)((int64_t)nt * split / nsplit), t_end = (int)((int64_t)nt * (split + 1) / nsplit);
+  const bool vec = p.vec != 0;
+  const bool do_rs = p.rowsum != nullptr && tn == 0 && wn == 0;
+
+  float4 ra[Cfg::A_QUADS], rb[Cfg::B_QUADS];
+  // global -> registers: the quads of k-tile t (segment 1 or 2)
+  auto load = [&](int t) {
+    const bool s2 = t >= nt1;
+    const void* A = s2 ? p.A2 : p.A;
+    const void* B = s2 ? p.B2 : p.B;
+    const int64_t lda = s2 ? p.lda2 : p.lda, ldb = s2 ? p.ldb2 : p.ldb;
+    const int K = s2 ? p.K2 : p.K;
+    const int k0 = (s2 ? t - nt1 : t) * GF_BK;
+#pragma unroll
+    for (int j = 0; j < Cfg::A_QUADS; ++j) {
+      const int q = tid + j * GF_THREADS;
+      if constexpr (AKM) ra[j] = quad<IN>(A, lda, k0 + q / (GF_BM / 4), m0 + (q % (GF_BM / 4)) * 4, K, p.M, vec);
+      else ra[j] = quad<IN>(A, lda, m0 + q / (GF_BK / 4), k0 + (q % (GF_BK / 4)) * 4, p.M, K, vec);
+    }
+#pragma unroll
+    for (int j = 0; j < Cfg::B_QUADS; ++j) {
+      const int q = tid + j * GF_THREADS;
+      if (q < BN * GF_BK / 4) {
+        if constexpr (BKM) rb[j] = quad<IN>(B, ldb, k0 + q / (BN / 4), n0 + (q % (BN / 4)) * 4, K, p.N, vec);
+        else rb[j] = quad<IN>(B, ldb, n0 + q / (GF_BK / 4), k0 + (q % (GF_BK / 4)) * 4, p.N, K, vec);
+      }
+    }
+  };
+  // registers -> LDS (k-major images)
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < Cfg::A_QUADS; ++j) {
+      const int q = tid + j * GF_THREADS;
+      if constexpr (AKM) {
+        *reinterpret_cast<float4*>(&As[buf][q / (GF_BM / 4)][(q % (GF_BM / 4)) * 4]) = ra[j];
+      } else {
+        const int m = q / (GF_BK / 4), k = (q % (GF_BK / 4)) * 4;
+        As[buf][k][m] = ra[j].x; As[buf][k + 1][m] = ra[j].y; As[buf][k + 2][m] = ra[j].z; As[buf][k + 3][m] = ra[j].w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < Cfg::B_QUADS; ++j) {
+      const int q = tid + j * GF_THREADS;
+      if (q < BN * GF_BK / 4) {
+        if constexpr (BKM) {
+          *reinterpret_cast<float4*>(&Bs[buf][q / (BN / 4)][(q % (BN / 4)) * 4]) = rb[j];
+        } else {
+          const int n = q / (GF_BK / 4), k = (q % (GF_BK / 4)) * 4;
+          Bs[buf][k][n] = rb[j].x; Bs[buf][k + 1][n] = rb[j].y; Bs[buf][k + 2][n] = rb[j].z; Bs[buf][k + 3][n] = rb[j].w;
+        }
+      }
+    }
+  };
+
+  f32x4 acc[Cfg::MI][Cfg::NI];
+#pragma unroll
+  for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < Cfg::NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rs[Cfg::MI];
+#pragma unroll
+  for (int i = 0; i < Cfg::MI; ++i) rs[i] = 0.f;
+
+  const int fr = lane & 15, fk = lane >> 4;  // fragment row / column, k within a 4-step
+  const int am = wm * Cfg::WM + fr, bn = wn * Cfg::WN + fr;
+  int buf = 0;
+  if (t_begin < t_end) {
+    load(t_begin);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = t_begin; t < t_end; ++t) {
+    const bool more = t + 1 < t_end;
+    if (more) load(t + 1);  // in flight during the MFMAs below
+#pragma unroll
+    for (int ks = 0; ks < GF_BK / 4; ++ks) {
+      const int k = ks * 4 + fk;
+      float a[Cfg::MI], b[Cfg::NI];
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i) a[i] = As[buf][k][am + i * 16];
+#pragma unroll
+      for (int j = 0; j < Cfg::NI; ++j) b[j] = Bs[buf][k][bn + j * 16];
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < Cfg::NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      if (do_rs) {
+#pragma unroll
+        for (int i = 0; i < Cfg::MI; ++i) rs[i] += a[i];
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // ---- epilogue: lane holds rows 4 fk + r, column fr of every 16 x 16 tile
+  const bool partial = nsplit > 1;
+  float* Cf = static_cast<float*>(p.C) + (partial ? (int64_t)split * p.c_split_stride : 0);
+#pragma unroll
+  for (int i = 0; i < Cfg::MI; ++i) {
+#pragma unroll
+    for (int j = 0; j < Cfg::NI; ++j) {
+      const int n = n0 + wn * Cfg::WN + j * 16 + fr;
+      if (n >= p.N) continue;
+      const float bias = (!partial && p.bias) ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * Cfg::WM + i * 16 + 4 * fk + r;
+        if (m >= p.M) continue;
+        const int64_t o = (int64_t)m * p.ldc + n;
+        float v = acc[i][j][r] + bias;
+        if (p.out_dtype == 2 || partial) {
+          if (p.accumulate && !partial) v += Cf[o];
+          Cf[o] = v;
+        } else if (p.out_dtype == 0) {
+          static_cast<__hip_bfloat16*>(p.C)[o] = __float2bfloat16(v);
+        } else {
+          static_cast<__half*>(p.C)[o] = __float2half(v);
+        }
+      }
+    }
+  }
+  if (do_rs) {
+#pragma unroll
+    for (int i = 0; i < Cfg::MI; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int m = m0 + wm * Cfg::WM + i * 16 + fr;
+      if (fk == 0 && m < p.M) p.rowsum[(int64_t)split * p.M + m] = v;
+    }
+  }
+}
+
+template <int IN, bool AKM, bool BKM>
+hipError_t launch_f32(const PdrnnGemmF32Args& a, hipStream_t st) {
+  const int bn = a.N <= 32 ? 32 : a.N <= 64 ? 64 : 128;
+  const int tiles = ((a.M + GF_BM - 1) / GF_BM) * ((a.N + bn - 1) / bn);
+  const dim3 grid(tiles, a.splitk > 1 ? a.splitk : 1);
+  switch (bn) {
+    case 32: hipLaunchKernelGGL((gemm_f32_kernel<IN, AKM, BKM, 32>), grid, dim3(GF_THREADS), 0, st, a); break;
+    case 64: hipLaunchKernelGGL((gemm_f32_kernel<IN, AKM, BKM, 64>), grid, dim3(GF_THREADS), 0, st, a); break;
+    default: hipLaunchKernelGGL((gemm_f32_kernel<IN, AKM, BKM, 128>), grid, dim3(GF_THREADS), 0, st, a); break;
+  }
+  return hipGetLastError();
+}
+
+template <int IN>
+hipError_t dispatch_f32(const PdrnnGemmF32Args& a, hipStream_t st) {
+  if (a.a_kmajor) return a.b_kmajor ? launch_f32<IN, true, true>(a, st) : launch_f32<IN, true, false>(a, st);
+  return a.b_kmajor ? launch_f32<IN, false, true>(a, st) : launch_f32<IN, false, false>(a, st);
+}
+
+// out[i] (= or +=) sum_s part[s * n + i], fixed order (deterministic)
+__global__ void __launch_bounds__(256) splitk_sum_kernel(const float* __restrict__ part, int splitk, int64_t n,
+                                                         float* __restrict__ out, int accumulate) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = accumulate ? out[i] : 0.f;
+    float acc = 0.f;
+    for (int k = 0; k < splitk; ++k) acc += part[(int64_t)k * n + i];
+    out[i] = s + acc;
+  }
+}
+
+// Column sums of a [rows, cols] matrix (row stride ld), pass 1: block (cx, ry)
+// sums columns [64 cx, 64 cx + 64) over row group ry into part[ry][cols]; the
+// row groups are then summed by splitk_sum_kernel (fixed order).
+template <int IN>
+__global__ void __launch_bounds__(256) col_sum_kernel(const void* __restrict__ X, int64_t rows, int64_t cols,
+                                                      int64_t ld, float* __restrict__ part) {
+  __shared__ float red[256];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + c;
+  const int64_t r0 = rows * blockIdx.y / gridDim.y, r1 = rows * (blockIdx.y + 1) / gridDim.y;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (col < cols) {
+    int64_t r = r0 + g;
+    for (; r + 12 < r1; r += 16) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += ld1<IN>(X, (r + 4 * k) * ld + col);
+    }
+    for (int k = 0; r < r1; r += 4, ++k) acc[k & 3] += ld1<IN>(X, r * ld + col);
+  }
+  red[threadIdx.x] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (g == 0 && col < cols)
+    part[(int64_t)blockIdx.y * cols + col] = ((red[c] + red[64 + c]) + (red[128 + c] + red[192 + c]));
+}
+
+}  // namespace
+}  // namespace pdrnn
+
+extern "C" {
+
+int pdrnn_gemm_f32_supported(const PdrnnGemmF32Args* a) {
+  if (a->M < 1 || a->N < 1 || a->K < 1 || a->K2 < 0 || (a->K2 > 0 && (!a->A2 || !a->B2))) return 0;
+  if (a->in_dtype < 0 || a->in_dtype > 2 || (a->out_dtype != 2 && a->out_dtype != a->in_dtype)) return 0;
+  if (a->splitk > 1 && (a->out_dtype != 2 || a->accumulate || a->bias)) return 0;
+  if (a->out_dtype != 2 && a->accumulate) return 0;
+  return 1;
+}
+
+hipError_t pdrnn_gemm_f32(const PdrnnGemmF32Args* a, hipStream_t stream) {
+  if (!pdrnn_gemm_f32_supported(a)) return hipErrorInvalidValue;
+  switch (a->in_dtype) {
+    case 0: return pdrnn::dispatch_f32<0>(*a, stream);
+    case 1: return pdrnn::dispatch_f32<1>(*a, stream);
+    default: return pdrnn::dispatch_f32<2>(*a, stream);
+  }
+}
+
+hipError_t pdrnn_splitk_sum(const float* part, int splitk, int64_t n, float* out, int accumulate, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pdrnn::splitk_sum_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, part, splitk, n, out,
+                     accumulate);
+  return hipGetLastError();
+}
+
+int pdrnn_col_sum_groups(int64_t rows, int64_t cols) {
+  // ~2 workgroups per CU, at least 64 rows per group
+  const int64_t cblocks = (cols + 63) / 64;
+  int64_t g = (512 + cblocks - 1) / cblocks;
+  if (g > rows / 64) g = rows / 64;
+  if (g > 256) g = 256;
+  return g < 1 ? 1 : (int)g;
+}
+
+hipError_t pdrnn_col_sum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ld, float* part, int groups,
+                         hipStream_t stream) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)groups);
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(pdrnn::col_sum_kernel<0>, grid, dim3(256), 0, stream, X, rows, cols, ld, part); break;
+    case 1: hipLaunchKernelGGL(pdrnn::col_sum_kernel<1>, grid, dim3(256), 0, stream, X, rows, cols, ld, part); break;
+    default: hipLaunchKernelGGL(pdrnn::col_sum_kernel<2>, grid, dim3(256), 0, stream, X, rows, cols, ld, part); break;
+  }
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -147,8 +147,39 @@ class _Linear16(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype).contiguous()
         dx = mm_nk16([(dy2, w16)]).view(ctx.shp) if ctx.needs_input_grad[0] else None
         dw = mm_kk([(dy2, x2)]) if ctx.needs_input_grad[1] else None
-        db = dy2.sum(0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        db = col_sum(dy2) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db
+
+
+class _LinearNarrow(torch.autograd.Function):
+    """y = x W^T + b with fp32 master W / b on the fp32-product GEMM
+    (kernels/gemm_f32.hip): fp32 x (any width), or a 16-bit x with a narrow
+    output (N < 128, e.g. a classifier head: 32 / 64-wide tiles instead of an
+    idle 256-wide ping-pong tile) -- forward, dX, dW and db (the row sums of
+    dy^T, fused into the dW pass)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        w16 = weight.detach().to(x.dtype)
+        o16 = x.dtype != torch.float32
+        y, _ = gemm_f32(x2, False, w16, False, bias=bias.detach().float() if bias is not None else None, out16=o16)
+        ctx.save_for_backward(x2, w16)
+        ctx.has_bias = bias is not None
+        ctx.shp = shp
+        return y.view(*shp[:-1], w16.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w16 = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype).contiguous()
+        o16 = x2.dtype != torch.float32
+        dx = gemm_f32(dy2, False, w16, True, out16=o16)[0].view(ctx.shp) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw, db = gemm_f32(dy2, True, x2, True, rowsum=ctx.has_bias)
+        return dx, dw if ctx.needs_input_grad[1] else None, db if ctx.has_bias and ctx.needs_input_grad[2] else None
 
 
 def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
@@ -160,5 +191,85 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
     N, K = weight.shape
     if mod is not None and N >= 128 and N % 8 == 0 and K % 64 == 0 and x.shape[-1] == K:
         return _Linear16.apply(x.contiguous(), weight, bias)
+    if _native_f32(x) is not None and x.shape[-1] == K and weight.dtype == torch.float32 and (
+            (mod is not None and N < 128) or x.dtype == torch.float32):
+        return _LinearNarrow.apply(x.contiguous(), weight, bias)
     import torch.nn.functional as F
     return F.linear(x, weight.to(x.dtype), bias.to(x.dtype) if bias is not None else None)
+
+
+# ------------------------------------------------------------------ fp32 GEMM
+def _native_f32(t: Tensor):
+    if os.environ.get("PDRNN_GEMM", "mfma") == "torch" or t.device.type != "cuda":
+        return None
+    mod = _ext.native(t.device)
+    return mod if mod is not None and hasattr(mod, "gemm_f32") else None
+
+
+def _unit_inner(t: Tensor) -> bool:
+    return t.dim() == 2 and (t.stride(1) == 1 or t.shape[1] == 1) and t.stride(0) >= 1
+
+
+def _splitk_f32(dev, M: int, N: int, K: int) -> int:
+    """K splits bringing the fp32 GEMM to ~2 workgroups per CU (partials summed
+    in fixed order), at least 8 k-tiles of 16 per split."""
+    bn = 32 if N <= 32 else 64 if N <= 64 else 128
+    tiles = ((M + 127) // 128) * ((N + bn - 1) // bn)
+    want = 2 * _cus(dev)
+    if tiles >= want:
+        return 1
+    return max(1, min((want + tiles - 1) // tiles, max(1, K // (16 * 8)), 128))
+
+
+def gemm_f32(a: Tensor, a_kmajor: bool, b: Tensor, b_kmajor: bool, pairs2=None, bias: Optional[Tensor] = None,
+             rowsum: bool = False, out16: bool = False,
+             out: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+    """C = op(a) op(b)^T (+ op(a2) op(b2)^T) (+ bias), fp32 products and
+    accumulation on the matrix cores (kernels/gemm_f32.hip); ``rowsum``: also
+    the sums over K of op(a) (the bias gradient of a dW = G^T X product).
+    ``op``: a k-major operand is stored [K, rows].  Torch fallback without the
+    extension (CPU)."""
+    mod = _native_f32(a)
+    ops = [a, b] + (list(pairs2) if pairs2 else [])
+    if mod is not None and all(_unit_inner(t) and t.dtype == a.dtype for t in ops):
+        M = a.shape[1] if a_kmajor else a.shape[0]
+        N = b.shape[1] if b_kmajor else b.shape[0]
+        K = (a.shape[0] if a_kmajor else a.shape[1]) + ((pairs2[0].shape[0] if a_kmajor else pairs2[0].shape[1])
+                                                         if pairs2 else 0)
+        sk = 1 if (bias is not None or out16) else _splitk_f32(a.device, M, N, K)
+        kw = dict(bias=bias, rowsum=rowsum, out16=out16, splitk=sk)
+        if pairs2:
+            kw.update(A2=pairs2[0], B2=pairs2[1])
+        if out is not None:
+            if sk > 1 and not out.is_contiguous():
+                kw["splitk"] = 1
+            kw["out"] = out
+        c, rs = mod.gemm_f32(a, a_kmajor, b, b_kmajor, **kw)
+        return c, (rs if rowsum else None)
+    oa = (lambda t: t.t() if a_kmajor else t)
+    ob = (lambda t: t if b_kmajor else t.t())
+    c = oa(a).float() @ ob(b).float()
+    if pairs2:
+        c = c + oa(pairs2[0]).float() @ ob(pairs2[1]).float()
+    if bias is not None:
+        c = c + bias.float()
+    rs = None
+    if rowsum:
+        rs = oa(a).float().sum(1)
+        if pairs2:
+            rs = rs + oa(pairs2[0]).float().sum(1)
+    c = c.to(a.dtype) if out16 else c
+    if out is not None:
+        out.copy_(c)
+        c = out
+    return c, rs
+
+
+def col_sum(x: Tensor) -> Tensor:
+    """fp32 column sums of a 2-D tensor (fp32 or 16-bit): in-tree and
+    deterministic on the GPU, torch on the CPU."""
+    mod = _native_f32(x)
+    if mod is not None and x.dim() == 2 and x.stride(1) == 1 and x.dtype in (torch.float32, torch.bfloat16,
+                                                                              torch.float16):
+        return mod.col_sum(x)
+    return x.sum(0, dtype=torch.float32)

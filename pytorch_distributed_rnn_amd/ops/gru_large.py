@@ -34,8 +34,8 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-from .lstm_large import _interleave, _mm_f32, _mm_tn_f32, _perm, _tile
-from .gemm import linear16, mm_kk, mm_nk16
+from .lstm_large import _interleave, _perm, _tile
+from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
 def supported(x: Tensor, hidden: int) -> bool:
@@ -133,28 +133,48 @@ class _LargeGRULayer(torch.autograd.Function):
         x2 = x.reshape(T * B, I)
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # [r | z | dpre_n | dpre_n r]
-            hprev = _hprev(hseq[:, :, d * H:(d + 1) * H], h0c[d:d + 1] if h0c is not None else None, d)
             Gx = G[:, :3 * H]                                        # x side: [r | z | dpre_n]
             if cdt == torch.float32:
-                dw4 = _mm_tn_f32(G, hprev.reshape(T * B, H), T)
-                dwih = _mm_tn_f32(Gx, x2, T)
+                # fp32-product MFMA GEMM (kernels/gemm_f32.hip) over shifted
+                # views of the output sequence (no h_prev copy), the initial
+                # state as a second K segment; db = the row sums of dgates^T of
+                # the dW_ih pass (every row)
+                # (the [r | z] and n_h gate blocks separately: nn.GRU's W_hh has
+                # no n_x block, so neither product nor concatenation for it)
+                hd = hseq[:, :, d * H:(d + 1) * H]
+                g0 = G[:B] if d == 0 else G[(T - 1) * B:]
+                Gs = G[B:] if d == 0 else G[:(T - 1) * B]
+                hs = (hd[:-1] if d == 0 else hd[1:]).reshape((T - 1) * B, H)
+                dwhh = torch.empty(3 * H, H, device=x.device, dtype=torch.float32)
+                for cols, rows in ((slice(0, 2 * H), slice(0, 2 * H)), (slice(3 * H, 4 * H), slice(2 * H, 3 * H))):
+                    seg2 = (g0[:, cols], h0c[d]) if h0c is not None else None
+                    if T > 1:
+                        gemm_f32(Gs[:, cols], True, hs, True, pairs2=seg2, out=dwhh[rows])
+                    elif seg2 is not None:
+                        gemm_f32(seg2[0], True, seg2[1], True, out=dwhh[rows])
+                    else:
+                        dwhh[rows].zero_()
+                dwih, dbih = gemm_f32(Gx, True, x2, True, rowsum=True)
+                dbhh = torch.empty(3 * H, device=x.device, dtype=torch.float32)
+                dbhh[:2 * H].copy_(dbih[:2 * H])
+                dbhh[2 * H:].copy_(col_sum(G[:, 3 * H:]))
             else:  # in-tree MFMA GEMM (ops/gemm.py)
+                hprev = _hprev(hseq[:, :, d * H:(d + 1) * H], h0c[d:d + 1] if h0c is not None else None, d)
                 dw4 = mm_kk([(G, hprev.reshape(T * B, H))])
                 dwih = mm_kk([(Gx, x2)])
-            dwhh = torch.cat([dw4[:2 * H], dw4[3 * H:]])
-            cs = G.sum(0, dtype=torch.float32)
-            dbih = cs[:3 * H]
-            dbhh = torch.cat([cs[:2 * H], cs[3 * H:]])
+                cs = col_sum(G)
+                dwhh = torch.cat([dw4[:2 * H], dw4[3 * H:]])
+                dbih = cs[:3 * H]
+                dbhh = torch.cat([cs[:2 * H], cs[3 * H:]])
             if not need_dx:
                 pass  # layer input without grad (e.g. the data): no dX GEMM
-            elif cdt != torch.float32:
-                dx_pairs.append((Gx, wih[d]))
-            elif dx is None:
-                dx = torch.mm(Gx, wih[d])
             else:
-                dx.addmm_(Gx, wih[d])
+                dx_pairs.append((Gx, wih[d]))
             grads += [dwih, dwhh, dbih if has_w[4 * d + 2] else None, dbhh if has_w[4 * d + 3] else None]
-        if dx_pairs:
+        if dx_pairs and cdt == torch.float32:  # both directions in one launch (K segments)
+            dx = gemm_f32(dx_pairs[0][0], False, dx_pairs[0][1], True,
+                          pairs2=dx_pairs[1] if len(dx_pairs) > 1 else None)[0]
+        elif dx_pairs:
             dx = mm_nk16(dx_pairs)  # both directions in one launch
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         return (dx.view(T, B, I) if dx is not None else None, dh0_out, None, *grads)

@@ -29,7 +29,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-from .gemm import linear16, mm_kk, mm_nk16
+from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 _PERM_CACHE = {}
 
@@ -161,6 +161,35 @@ def _shadow_cat(ws: List[Tensor], cdt: torch.dtype, hidden: int) -> Tensor:
     return t
 
 
+def _bias_cat(weights, ndir: int, hidden: int, device) -> Tensor:
+    """b_ih + b_hh of every direction, gate-interleaved and concatenated (the
+    projection GEMM's fp32 epilogue bias), cached like the shadow weights and
+    rebuilt only after the biases change."""
+    bs = [weights[4 * d + k] for d in range(ndir) for k in (2, 3)]
+    anchor = weights[0]
+    ver = tuple((b._version, b.data_ptr()) if b is not None else None for b in bs)
+    cache = getattr(anchor, "_pdrnn_shadow", None)
+    if cache is None:
+        cache = {}
+        anchor._pdrnn_shadow = cache
+    key = ("bias", ndir, hidden)
+    ent = cache.get(key)
+    if ent is not None and ent[0] == ver:
+        return ent[1]
+    perm = _perm(hidden, device)
+    with torch.no_grad():
+        out = []
+        for d in range(ndir):
+            b = torch.zeros(4 * hidden, device=device, dtype=torch.float32)
+            for t in bs[2 * d:2 * d + 2]:
+                if t is not None:
+                    b += t.detach().float()
+            out.append(b[perm])
+        t = torch.cat(out, 0)
+    cache[key] = (ver, t)
+    return t
+
+
 class _LargeLSTMLayer(torch.autograd.Function):
     """One layer, 1 or 2 directions.  x: [T, B, I] (compute dtype).
 
@@ -174,24 +203,15 @@ class _LargeLSTMLayer(torch.autograd.Function):
         T, B, I = x.shape
         H = hidden
         mod = _ext.native(x.device)
-        perm = _perm(H, x.device)
         w_ih = [weights[4 * d] for d in range(ndir)]
         w_hh = [weights[4 * d + 1] for d in range(ndir)]
-        bias = []
-        for d in range(ndir):
-            b_ih, b_hh = weights[4 * d + 2], weights[4 * d + 3]
-            b = torch.zeros(4 * H, device=x.device, dtype=torch.float32)
-            if b_ih is not None:
-                b = b + b_ih.float()
-            if b_hh is not None:
-                b = b + b_hh.float()
-            bias.append(b[perm])
         wih_p = _shadow_cat(w_ih, cdt, H)                                  # [ndir*4H, I]
-        bias_p = torch.cat(bias, 0).to(cdt)
-        if cdt == torch.float32:
-            xp = torch.addmm(bias_p, x.reshape(T * B, I), wih_p.t()).view(T, B, ndir * 4 * H)
+        bias_all = _bias_cat(weights, ndir, H, x.device)                   # fp32 [ndir*4H], interleaved
+        if cdt == torch.float32:  # fp32-product MFMA GEMM (kernels/gemm_f32.hip), fp32 bias in the epilogue
+            xp = gemm_f32(x.reshape(T * B, I), False, wih_p, False, bias=bias_all)[0]
+            xp = xp.view(T, B, ndir * 4 * H)
         else:  # in-tree MFMA GEMM, fp32 bias added before the 16-bit rounding (ops/gemm.py)
-            xp = linear16(x.reshape(T * B, I), wih_p, torch.cat(bias, 0)).view(T, B, ndir * 4 * H)
+            xp = linear16(x.reshape(T * B, I), wih_p, bias_all).view(T, B, ndir * 4 * H)
         whh_p = [shadow(w, "i", cdt, H) for w in w_hh]
         h0c = h0.to(cdt).contiguous() if h0 is not None else None
         c0c = c0.float().contiguous() if c0 is not None else None
@@ -228,31 +248,34 @@ class _LargeLSTMLayer(torch.autograd.Function):
         x2 = x.reshape(T * B, I)
         if cdt != torch.float32:
             return _backward_gemms16(ctx, dgates, dh0, dc0, hseq, h0c, x2, wih)
+        # fp32 layers: every product on the fp32-product MFMA GEMM
+        # (kernels/gemm_f32.hip): dW_hh over shifted views of the output
+        # sequence with the initial-state pairing as a second K segment, dW_ih
+        # with db as the row sums of dgates^T in the same pass, dX of both
+        # directions in one launch (K segments)
+        dx_pairs = []
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
             hd = hseq[:, :, d * H:(d + 1) * H]                       # strided view, row stride ndir*H
-            # dW_hh = sum_t dgates_t^T h_prev(t) over shifted views of the output
-            # sequence (no [T, B, H] h_prev copy): forward h_prev(t) = h_{t-1},
+            # dW_hh = sum_t dgates_t^T h_prev(t): forward h_prev(t) = h_{t-1},
             # reverse h_{t+1}; the step next to the initial state pairs with h0
+            g0 = G[:B] if d == 0 else G[(T - 1) * B:]
+            seg2 = (g0, h0c[d]) if h0c is not None else None
             if T > 1:
-                if d == 0:
-                    dwhh = _mm_tn_f32(G[B:], hd[:-1].reshape((T - 1) * B, H), T - 1)
-                else:
-                    dwhh = _mm_tn_f32(G[:(T - 1) * B], hd[1:].reshape((T - 1) * B, H), T - 1)
+                Gs = G[B:] if d == 0 else G[:(T - 1) * B]
+                hs = (hd[:-1] if d == 0 else hd[1:]).reshape((T - 1) * B, H)
+                dwhh = gemm_f32(Gs, True, hs, True, pairs2=seg2)[0]
+            elif seg2 is not None:
+                dwhh = gemm_f32(seg2[0], True, seg2[1], True)[0]
             else:
                 dwhh = torch.zeros(4 * H, H, device=x.device, dtype=torch.float32)
-            if h0c is not None:
-                g0 = G[:B] if d == 0 else G[(T - 1) * B:]
-                _addmm_f32_(dwhh, g0.t(), h0c[d])
-            dwih = _mm_tn_f32(G, x2, T)
-            db = G.sum(0, dtype=torch.float32)  # fp32 accumulation, no fp32 copy of G
-            if not need_dx:
-                pass  # layer input without grad (e.g. the data): no dX GEMM
-            elif dx is None:
-                dx = torch.mm(G, wih[d])
-            else:
-                dx.addmm_(G, wih[d])
+            dwih, db = gemm_f32(G, True, x2, True, rowsum=True)
+            if need_dx:
+                dx_pairs.append((G, wih[d]))
             grads += [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
+        if dx_pairs:
+            dx = gemm_f32(dx_pairs[0][0], False, dx_pairs[0][1], True,
+                          pairs2=dx_pairs[1] if len(dx_pairs) > 1 else None)[0]
         dx = dx.view(T, B, I) if dx is not None else None
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         dc0_out = dc0.to(c0_dtype) if has_c0 else None
@@ -282,7 +305,7 @@ def _backward_gemms16(ctx, dgates, dh0, dc0, hseq, h0c, x2, wih):
             pairs.append((G[:B] if d == 0 else G[(T - 1) * B:], h0c[d]))
         dwhh = mm_kk(pairs) if pairs else torch.zeros(4 * H, H, device=G.device, dtype=torch.float32)
         dwih = mm_kk([(G, x2)])
-        db = G.sum(0, dtype=torch.float32)
+        db = col_sum(G)  # in-tree deterministic column sums (fp32 accumulation of the 16-bit G)
         grads += [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
     dx = mm_nk16([(Gs[d], wih[d]) for d in range(ndir)]).view(T, B, I) if ctx.needs_input_grad[0] else None
     dh0_out = dh0.to(h0_dtype) if has_h0 else None

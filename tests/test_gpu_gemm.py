@@ -135,3 +135,68 @@ def test_gemm16_schedule_variants(variant):
         B = torch.randn(*((K, N) if bkm else (N, K)), device="cuda").bfloat16()
         C = mod.gemm16(A, akm, B, bkm, variant=variant)
         torch.testing.assert_close(C, _op(A, akm) @ _op(B, bkm).t(), rtol=1e-3, atol=3e-2)
+
+
+# ---------------------------------------------------------------- fp32 GEMM
+F32_SHAPES = [(520, 776, 64 * 9), (37, 29, 9), (1024, 512, 1000), (130, 32, 4096), (300, 64, 128)]
+
+
+def _mk(shape_mk, kmajor, dtype, gen_scale=1.0):
+    r, c = shape_mk
+    t = torch.randn(*((c, r) if kmajor else (r, c)), device="cuda") * gen_scale
+    return t.to(dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("akm,bkm", [(False, False), (True, True), (False, True), (True, False)])
+@pytest.mark.parametrize("M,N,K", F32_SHAPES)
+def test_gemm_f32_layouts_against_fp64(dtype, akm, bkm, M, N, K):
+    """The fp32-product MFMA GEMM (kernels/gemm_f32.hip) against an fp64
+    matmul of the same (widened) operands: every layout, ragged M/N/K (K = 9:
+    the layer-0 projection of the motion model), all three tile widths."""
+    mod = _mod()
+    torch.manual_seed(7)
+    A = _mk((M, K), akm, dtype)
+    B = _mk((N, K), bkm, dtype)
+    C, rs = mod.gemm_f32(A, akm, B, bkm)
+    ref = _op(A, akm).double() @ _op(B, bkm).double().t()
+    torch.testing.assert_close(C.double(), ref, rtol=2e-5, atol=2e-4 * (K ** 0.5))
+
+
+@pytest.mark.parametrize("splitk", [1, 3])
+def test_gemm_f32_segment_rowsum_bias_accumulate(splitk):
+    """dW_hh-shaped product: two K segments (shifted h sequence + the initial
+    state), split-K partials summed in fixed order, the row sums of op(A) over
+    K (= the bias gradient), and accumulation into an existing output."""
+    mod = _mod()
+    torch.manual_seed(8)
+    K1, K2, M, N = 1900, 95, 512, 128
+    G1, G2 = torch.randn(K1, M, device="cuda"), torch.randn(K2, M, device="cuda")
+    H1, H2 = torch.randn(K1, N, device="cuda"), torch.randn(K2, N, device="cuda")
+    C, rs = mod.gemm_f32(G1, True, H1, True, A2=G2, B2=H2, splitk=splitk, rowsum=True)
+    ref = G1.double().t() @ H1.double() + G2.double().t() @ H2.double()
+    torch.testing.assert_close(C.double(), ref, rtol=2e-5, atol=2e-3)
+    torch.testing.assert_close(rs.double(), G1.double().sum(0) + G2.double().sum(0), rtol=2e-5, atol=1e-3)
+    out = torch.ones(M, N, device="cuda")
+    mod.gemm_f32(G1, True, H1, True, out=out, accumulate=True, splitk=splitk)
+    torch.testing.assert_close(out.double(), 1 + G1.double().t() @ H1.double(), rtol=2e-5, atol=2e-3)
+    # projection with bias, 16-bit output (narrow head: N = 32)
+    X = torch.randn(700, 256, device="cuda").bfloat16()
+    W = torch.randn(32, 256, device="cuda").bfloat16()
+    b = torch.randn(32, device="cuda")
+    Y, _ = mod.gemm_f32(X, False, W, False, bias=b, out16=True)
+    assert Y.dtype == torch.bfloat16
+    torch.testing.assert_close(Y.float(), (X.double() @ W.double().t() + b.double()).float().bfloat16().float(),
+                               rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,cols", [(184320, 512), (95, 7), (4096, 32)])
+def test_col_sum_matches_fp64(dtype, rows, cols):
+    mod = _mod()
+    X = torch.randn(rows, cols, device="cuda").to(dtype)
+    got = mod.col_sum(X)
+    torch.testing.assert_close(got.double(), X.double().sum(0), rtol=1e-5, atol=1e-3)
+    # a strided view (row stride > cols)
+    Y = torch.randn(rows, cols + 5, device="cuda").to(dtype)[:, 2:2 + cols]
+    torch.testing.assert_close(mod.col_sum(Y).double(), Y.double().sum(0), rtol=1e-5, atol=1e-3)

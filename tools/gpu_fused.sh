@@ -1,4 +1,6 @@
-# BPTT + own-tile dW kernel: numerics and A/B against the separate dW launch
+# one GPU round trip: motion fused-step tests + A/B of the own-tile dW backward,
+# stamps and a kernel-trace window; then the GEMM / large-H tests and LM benches
+#   tools/gpu_fused.sh TAG
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -17,3 +19,4 @@ cd $GRAFT_REPO_ROOT
 db=$(find /tmp/prof_${tag} -name '*.db' | head -1)
 python tools/prof_window.py "$db" --anchor lstm_small_fwd --last 50 --out gpurun_out/${tag}_b1440_window.md
 head -12 gpurun_out/${tag}_b1440_window.md
+bash tools/gpu_lm.sh ${tag}lm
