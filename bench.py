@@ -55,6 +55,9 @@ def parse(argv=None):
     ap.add_argument("--hidden", type=int, default=32)
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--epoch-sequences", type=int, default=EPOCH_SEQUENCES,
+                    help="training-set size (default: the reference's 6912); e.g. 864 with --global-batch 180 "
+                         "rehearses one rank's epoch of the 8-GPU run on one GPU")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong: global batch fixed (reference); weak: --global-batch per GPU")
     ap.add_argument("--trainer", choices=("distributed", "horovod"), default="distributed")
@@ -105,7 +108,7 @@ def main(argv=None):
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but world size is {world}", file=sys.stderr)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-    n_train = max(EPOCH_SEQUENCES, args.global_batch * (world if args.scaling == "weak" else 1))
+    n_train = max(args.epoch_sequences, args.global_batch * (world if args.scaling == "weak" else 1))
     train_set, _, _ = synthetic_motion(n_train=n_train, n_validation=1, n_test=1,
                                        seq_length=args.seq_len, seed=args.seed)
     model = MotionModel(train_set.num_features, args.hidden, args.layers,

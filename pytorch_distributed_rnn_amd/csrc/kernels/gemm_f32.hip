@@ -8,9 +8,10 @@
 //     ops/gru_large.py for H >= 128;
 //   * narrow outputs (N < 128, e.g. the bi-LSTM's 32-wide head) with 16-bit
 //     inputs, which would idle most of a 256-wide ping-pong tile.
-// 16-bit inputs are widened to fp32 on their way into LDS, so every product
-// is exact and accumulation is fp32 (same numerics as torch's fp32 matmul up
-// to summation order).
+// 16-bit inputs are widened to fp32 on their way into LDS (exact) and multiplied
+// on v_mfma_f32_16x16x16{bf16,f16} (one instruction per 16-deep k-tile); fp32
+// inputs on v_mfma_f32_16x16x4_f32.  Products exact, accumulation fp32 (the
+// numerics of torch's matmul up to summation order).
 //
 //   C[M, N] (= or +=) sum over the K segments of op(A) op(B) (+ bias[n])
 //   A: a_kmajor ? (m, k) at A[k * lda + m] : A[m * lda + k]    (same for B / n)
@@ -171,22 +172,65 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
   for (int t = t_begin; t < t_end; ++t) {
     const bool more = t + 1 < t_end;
     if (more) load(t + 1);  // in flight during the MFMAs below
+    if constexpr (IN == 2) {
+      // fp32: 4 k-steps of v_mfma_f32_16x16x4_f32 (lane: row fr, k = 4 ks + fk)
 #pragma unroll
-    for (int ks = 0; ks < GF_BK / 4; ++ks) {
-      const int k = ks * 4 + fk;
-      float a[Cfg::MI], b[Cfg::NI];
+      for (int ks = 0; ks < GF_BK / 4; ++ks) {
+        const int k = ks * 4 + fk;
+        float a[Cfg::MI], b[Cfg::NI];
 #pragma unroll
-      for (int i = 0; i < Cfg::MI; ++i) a[i] = As[buf][k][am + i * 16];
+        for (int i = 0; i < Cfg::MI; ++i) a[i] = As[buf][k][am + i * 16];
 #pragma unroll
-      for (int j = 0; j < Cfg::NI; ++j) b[j] = Bs[buf][k][bn + j * 16];
+        for (int j = 0; j < Cfg::NI; ++j) b[j] = Bs[buf][k][bn + j * 16];
+#pragma unroll
+        for (int i = 0; i < Cfg::MI; ++i)
+#pragma unroll
+          for (int j = 0; j < Cfg::NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        if (do_rs) {
+#pragma unroll
+          for (int i = 0; i < Cfg::MI; ++i) rs[i] += a[i];
+        }
+      }
+    } else {
+      // 16-bit inputs (staged as exact fp32): the whole k-tile in ONE
+      // v_mfma_f32_16x16x16{bf16,f16} per output tile (lane: row fr, k = 4 fk + e),
+      // the fp32 -> 16-bit re-pack exact
+      typedef short s16x4 __attribute__((ext_vector_type(4)));
+      typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+      s16x4 a[Cfg::MI], b[Cfg::NI];
+      auto pack = [](float x0, float x1, float x2, float x3) {
+        s16x4 v;
+        if constexpr (IN == 0) {
+          v = s16x4{(short)(__float_as_uint(x0) >> 16), (short)(__float_as_uint(x1) >> 16),
+                    (short)(__float_as_uint(x2) >> 16), (short)(__float_as_uint(x3) >> 16)};
+        } else {
+          const h16x4 h = h16x4{(_Float16)x0, (_Float16)x1, (_Float16)x2, (_Float16)x3};
+          v = __builtin_bit_cast(s16x4, h);
+        }
+        return v;
+      };
+#pragma unroll
+      for (int i = 0; i < Cfg::MI; ++i) {
+        const float x0 = As[buf][4 * fk][am + i * 16], x1 = As[buf][4 * fk + 1][am + i * 16];
+        const float x2 = As[buf][4 * fk + 2][am + i * 16], x3 = As[buf][4 * fk + 3][am + i * 16];
+        a[i] = pack(x0, x1, x2, x3);
+        if (do_rs) rs[i] += (x0 + x1) + (x2 + x3);
+      }
+#pragma unroll
+      for (int j = 0; j < Cfg::NI; ++j)
+        b[j] = pack(Bs[buf][4 * fk][bn + j * 16], Bs[buf][4 * fk + 1][bn + j * 16], Bs[buf][4 * fk + 2][bn + j * 16],
+                    Bs[buf][4 * fk + 3][bn + j * 16]);
 #pragma unroll
       for (int i = 0; i < Cfg::MI; ++i)
 #pragma unroll
-        for (int j = 0; j < Cfg::NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
-      if (do_rs) {
-#pragma unroll
-        for (int i = 0; i < Cfg::MI; ++i) rs[i] += a[i];
-      }
+        for (int j = 0; j < Cfg::NI; ++j) {
+          if constexpr (IN == 0)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[i], b[j], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h16x4, a[i]),
+                                                              __builtin_bit_cast(h16x4, b[j]), acc[i][j], 0, 0, 0);
+        }
     }
     if (more) store(buf ^ 1);
     __syncthreads();

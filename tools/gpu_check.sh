@@ -21,8 +21,11 @@ for B in 1440 720 360 180; do
   timeout -k 10 180 python bench.py --steps 200 --warmup 20 --global-batch $B > gpurun_out/${tag}_bench$B.log 2>&1 || { tail -20 gpurun_out/${tag}_bench$B.log; exit 1; }
   tail -1 gpurun_out/${tag}_bench$B.log | python tools/bench_line.py "B=$B eager"
 done
+# one rank's epoch of the 2/4/8-GPU run (per-rank batch B, 6912 / N sequences),
+# synced step (forced one-rank RCCL all-reduce + Adam) replayed per epoch
 for B in 720 360 180; do
-  PDRNN_FORCE_GRAD_SYNC=1 PDRNN_FORCE_COLLECTIVE=1 timeout -k 10 180 python bench.py --steps 200 --warmup 20 --global-batch $B --cuda-graph > gpurun_out/${tag}_synced$B.log 2>&1 || { tail -20 gpurun_out/${tag}_synced$B.log; exit 1; }
+  E=$((B * 24 / 5))
+  PDRNN_FORCE_GRAD_SYNC=1 PDRNN_FORCE_COLLECTIVE=1 timeout -k 10 180 python bench.py --steps 200 --warmup 20 --global-batch $B --epoch-sequences $E --cuda-graph > gpurun_out/${tag}_synced$B.log 2>&1 || { tail -20 gpurun_out/${tag}_synced$B.log; exit 1; }
   tail -1 gpurun_out/${tag}_synced$B.log | python tools/bench_line.py "B=$B synced-graph"
 done
 cd /tmp
