@@ -307,28 +307,54 @@ __global__ void __launch_bounds__(256) splitk_sum_kernel(const float* __restrict
 }
 
 // Column sums of a [rows, cols] matrix (row stride ld), pass 1: block (cx, ry)
-// sums columns [64 cx, 64 cx + 64) over row group ry into part[ry][cols]; the
-// row groups are then summed by splitk_sum_kernel (fixed order).
+// sums columns [256 cx, 256 cx + 256) over row group ry into part[ry][cols];
+// the row groups are then summed by splitk_sum_kernel (fixed order).  A thread
+// owns 4 consecutive columns (one 8- or 16-byte load per row where aligned)
+// and every 4th row of the group, 4 rows in flight: a wave reads 256 columns
+// of a row per instruction.
 template <int IN>
 __global__ void __launch_bounds__(256) col_sum_kernel(const void* __restrict__ X, int64_t rows, int64_t cols,
-                                                      int64_t ld, float* __restrict__ part) {
-  __shared__ float red[256];
-  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + c;
+                                                      int64_t ld, float* __restrict__ part, int vec) {
+  __shared__ float4 red[256];
+  const int c4 = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = (int)blockIdx.x * 256 + 4 * c4;
   const int64_t r0 = rows * blockIdx.y / gridDim.y, r1 = rows * (blockIdx.y + 1) / gridDim.y;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (col < cols) {
+  const int ncols = (int)cols;
+  float4 acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < ncols) {
     int64_t r = r0 + g;
     for (; r + 12 < r1; r += 16) {
+      float4 v[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) acc[k] += ld1<IN>(X, (r + 4 * k) * ld + col);
+      for (int k = 0; k < 4; ++k) v[k] = quad<IN>(X, ld, (int)(r + 4 * k), col, (int)r1, ncols, vec != 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[k].x += v[k].x; acc[k].y += v[k].y; acc[k].z += v[k].z; acc[k].w += v[k].w;
+      }
     }
-    for (int k = 0; r < r1; r += 4, ++k) acc[k & 3] += ld1<IN>(X, r * ld + col);
+    for (int k = 0; r < r1; r += 4, ++k) {
+      const float4 v = quad<IN>(X, ld, (int)r, col, (int)r1, ncols, vec != 0);
+      acc[k & 3].x += v.x; acc[k & 3].y += v.y; acc[k & 3].z += v.z; acc[k & 3].w += v.w;
+    }
   }
-  red[threadIdx.x] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  float4 t;
+  t.x = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x);
+  t.y = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
+  t.z = (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z);
+  t.w = (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w);
+  red[threadIdx.x] = t;
   __syncthreads();
-  if (g == 0 && col < cols)
-    part[(int64_t)blockIdx.y * cols + col] = ((red[c] + red[64 + c]) + (red[128 + c] + red[192 + c]));
+  if (g == 0 && col < ncols) {
+    const float4 a = red[c4], b = red[64 + c4], c = red[128 + c4], d = red[192 + c4];
+    const float o[4] = {(a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
+                        (a.w + b.w) + (c.w + d.w)};
+    float* dst = part + (int64_t)blockIdx.y * cols + col;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (col + j < ncols) dst[j] = o[j];
+  }
 }
 
 }  // namespace
@@ -363,22 +389,25 @@ hipError_t pdrnn_splitk_sum(const float* part, int splitk, int64_t n, float* out
 }
 
 int pdrnn_col_sum_groups(int64_t rows, int64_t cols) {
-  // ~2 workgroups per CU, at least 64 rows per group
-  const int64_t cblocks = (cols + 63) / 64;
-  int64_t g = (512 + cblocks - 1) / cblocks;
+  // ~4 workgroups per CU, at least 64 rows per group
+  const int64_t cblocks = (cols + 255) / 256;
+  int64_t g = (1024 + cblocks - 1) / cblocks;
   if (g > rows / 64) g = rows / 64;
-  if (g > 256) g = 256;
+  if (g > 1024) g = 1024;
   return g < 1 ? 1 : (int)g;
 }
 
 hipError_t pdrnn_col_sum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ld, float* part, int groups,
                          hipStream_t stream) {
   if (rows <= 0 || cols <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)groups);
+  if (rows >= (1LL << 31) || cols >= (1LL << 31)) return hipErrorInvalidValue;
+  const int esz = dtype == 2 ? 4 : 2;
+  const int vec = (ld % 4 == 0 && reinterpret_cast<uintptr_t>(X) % (4 * esz) == 0) ? 1 : 0;
+  const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)groups);
   switch (dtype) {
-    case 0: hipLaunchKernelGGL(pdrnn::col_sum_kernel<0>, grid, dim3(256), 0, stream, X, rows, cols, ld, part); break;
-    case 1: hipLaunchKernelGGL(pdrnn::col_sum_kernel<1>, grid, dim3(256), 0, stream, X, rows, cols, ld, part); break;
-    default: hipLaunchKernelGGL(pdrnn::col_sum_kernel<2>, grid, dim3(256), 0, stream, X, rows, cols, ld, part); break;
+    case 0: hipLaunchKernelGGL(pdrnn::col_sum_kernel<0>, grid, dim3(256), 0, stream, X, rows, cols, ld, part, vec); break;
+    case 1: hipLaunchKernelGGL(pdrnn::col_sum_kernel<1>, grid, dim3(256), 0, stream, X, rows, cols, ld, part, vec); break;
+    default: hipLaunchKernelGGL(pdrnn::col_sum_kernel<2>, grid, dim3(256), 0, stream, X, rows, cols, ld, part, vec); break;
   }
   return hipGetLastError();
 }
