@@ -399,7 +399,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
                           const optional<std::vector<Tensor>>& adam_state,
                           const optional<std::vector<double>>& adam_hp, int64_t cell,
                           const optional<Tensor>& grad_colmap, const optional<Tensor>& stats_slot_step,
-                          int64_t stats_slot_offset) {
+                          int64_t stats_slot_offset, bool round_bf16) {
   CHECK_HIP_TENSOR(x);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be float32 or bfloat16");
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [N, T, I] with contiguous rows");
@@ -497,6 +497,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   f.inv_batch = 1.f / (float)std::max<int64_t>(B, 1);
   f.C = (int)C;
   f.B = (int)B; f.T = (int)T; f.I = (int)I; f.NL = (int)NL; f.cell = (int)cell;
+  f.w_bf16 = round_bf16 ? 1 : 0;
   hipStream_t st = cur_stream();
   Tensor st_f, st_b;
   if (stamps_enabled()) {
@@ -523,6 +524,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.dhn = dh_top.data_ptr<float>(); bk.dhn_top_only = 1;
   bk.slab = slab.data_ptr<float>(); bk.P = L.P;
   bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL; bk.cell = (int)cell;
+  bk.w_bf16 = f.w_bf16;
   int grid_dw = gridb;
   Tensor xg;
   if (dwout) {
@@ -1242,7 +1244,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("flat_grad"), py::arg("stats"), py::arg("H"), py::arg("NL"), py::arg("split_fwd"),
         py::arg("split_bwd"), py::arg("nb_fwd"), py::arg("nb_bwd"), py::arg("adam_state") = py::none(),
         py::arg("adam_hp") = py::none(), py::arg("cell") = 0, py::arg("grad_colmap") = py::none(),
-        py::arg("stats_slot_step") = py::none(), py::arg("stats_slot_offset") = 0);
+        py::arg("stats_slot_step") = py::none(), py::arg("stats_slot_offset") = 0, py::arg("round_bf16") = false);
   m.def("gemm_f32", &gemm_f32, "fp32-product MFMA GEMM: (C, rowsum of op(A) over K)", py::arg("A"),
         py::arg("a_kmajor"), py::arg("B"), py::arg("b_kmajor"), py::arg("A2") = py::none(), py::arg("B2") = py::none(),
         py::arg("bias") = py::none(), py::arg("out16") = false, py::arg("out") = py::none(),

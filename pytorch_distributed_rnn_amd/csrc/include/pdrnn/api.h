@@ -55,6 +55,7 @@ typedef struct {
   int cell;                  // 0 = LSTM, 1 = GRU (packed as a 4-row-block stack, see ops/gru.py)
   int x_bf16;                // x holds bf16 values (read once into LDS; requires the LDS-resident x path)
   int prio;                  // lower the waves' issue priority as the recurrence progresses (see prio_by_progress)
+  int w_bf16;                // round the fp32 W_ih / W_hh to bf16 as they are loaded (bf16 models: no cast pass)
 } PdrnnLstmSmallFwdArgs;
 
 typedef struct {
@@ -96,6 +97,7 @@ typedef struct {
   float* xg_out;             // DWOUT: [B*T][xg_ld] fp32 copy of the (gathered, widened) layer-0 input
   int xg_ld;
   int prio;                  // see the forward
+  int w_bf16;                // see the forward
 } PdrnnLstmSmallBwdArgs;
 
 // Weight gradients of the small-H stack from saved gate gradients, on the

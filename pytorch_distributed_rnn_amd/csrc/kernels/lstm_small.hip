@@ -40,6 +40,10 @@ namespace {
 // per-step global load on the recurrence's critical path.
 constexpr int kXldsBytes = 48 * 1024;
 
+// bf16 models keep fp32 master weights; the kernels use them rounded to bf16
+// (round-to-nearest-even, v_cvt_pk_bf16_f32) as they load them
+__device__ __forceinline__ float wround(float v, int w_bf16) { return w_bf16 ? (float)(__bf16)v : v; }
+
 
 // Stage one sequence's inputs x[t][0..I) into the LDS image xs[t][0..H)
 // (columns >= I zero): only the I real columns are loaded (not H), 4 loads
@@ -219,7 +223,8 @@ lstm_small_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
 #pragma unroll
         for (int k4 = 0; k4 < KS / 4; ++k4) {
           const float4 v = *reinterpret_cast<const float4*>(src + r * ld + c0 + 4 * k4);
-          w[q][4 * k4 + 0] = v.x; w[q][4 * k4 + 1] = v.y; w[q][4 * k4 + 2] = v.z; w[q][4 * k4 + 3] = v.w;
+          w[q][4 * k4 + 0] = wround(v.x, a.w_bf16); w[q][4 * k4 + 1] = wround(v.y, a.w_bf16);
+          w[q][4 * k4 + 2] = wround(v.z, a.w_bf16); w[q][4 * k4 + 3] = wround(v.w, a.w_bf16);
         }
       } else {
         // only the live columns are loaded: for the layer-0 input slice
@@ -231,7 +236,7 @@ lstm_small_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
           const int c = c0 + kk;
           float v = 0.f;
           if (c < lim) v = src[r * ld + c];
-          w[q][kk] = v;
+          w[q][kk] = wround(v, a.w_bf16);
         }
       }
       bias[q] = (a.b_ih[layer] ? a.b_ih[layer][r] : 0.f) + (a.b_hh[layer] ? a.b_hh[layer][r] : 0.f);
@@ -468,7 +473,7 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
         v0 = whh[k - H];
         v1 = whh[k + 1 - H];
       }
-      w2[kk] = pdrnn_f2{v0 * wsc, v1 * wsc};
+      w2[kk] = pdrnn_f2{wround(v0, a.w_bf16) * wsc, wround(v1, a.w_bf16) * wsc};
     }
     bias = ((a.b_ih[layer] ? a.b_ih[layer][r] : 0.f) + (a.b_hh[layer] ? a.b_hh[layer][r] : 0.f)) * wsc;
   }
@@ -663,7 +668,7 @@ __global__ void __launch_bounds__(512) lstm_small_bwd_kernel(PdrnnLstmSmallBwdAr
 #pragma unroll
     for (int j = 0; j < RS; ++j) {
       const float v = base[j * col_stride];
-      W[j] = col_live ? v : 0.f;
+      W[j] = col_live ? wround(v, a.w_bf16) : 0.f;
       dW[j] = 0.f;
     }
   }
@@ -916,9 +921,9 @@ __device__ __forceinline__ BwdCols<H, L> bwd_load_cols(const PdrnnLstmSmallBwdAr
   const float* pi = a.w_ih[layer] + (int64_t)r0 * Iin + min(u, Iin - 1);
 #pragma unroll
   for (int rr = 0; rr < RS / 2; ++rr) {
-    w.whh[rr] = pdrnn_f2{ph[(2 * rr) * H], ph[(2 * rr + 1) * H]};
+    w.whh[rr] = pdrnn_f2{wround(ph[(2 * rr) * H], a.w_bf16), wround(ph[(2 * rr + 1) * H], a.w_bf16)};
     const float x0 = pi[(int64_t)(2 * rr) * Iin], x1 = pi[(int64_t)(2 * rr + 1) * Iin];
-    w.wih[rr] = ih_live ? pdrnn_f2{x0, x1} : pdrnn_f2{0.f, 0.f};
+    w.wih[rr] = ih_live ? pdrnn_f2{wround(x0, a.w_bf16), wround(x1, a.w_bf16)} : pdrnn_f2{0.f, 0.f};
   }
   return w;
 }

@@ -120,8 +120,9 @@ class MotionTrainStep:
         # kernel per step); a row is reused after RING steps
         self.ring = torch.zeros(self.RING, 3, dtype=torch.float32, device=self.flat.grad.device)
         self._slot = 0
-        # bf16 model: recurrent weights used rounded to bf16 (one cast of the
-        # flat master buffer per step); gradients land on the fp32 masters
+        # bf16 model: the kernels round the fp32 master W_ih / W_hh to bf16 as
+        # they load them (round_bf16; no cast pass, graph-capturable);
+        # gradients land on the fp32 masters
         self.bf16 = getattr(self.m, "compute_dtype", torch.float32) == torch.bfloat16
         self.colmap = None
         if self.gru:
@@ -148,10 +149,6 @@ class MotionTrainStep:
         self._graph = None       # last replayed synced step (torch.cuda.CUDAGraph = hipGraph)
         self._graphs = {}        # configuration key -> captured step
 
-    def _rounded(self):
-        r = self.flat.data.to(torch.bfloat16).float()
-        return [r[o:o + int(torch.Size(s).numel())].view(s) for o, s in self._offs]
-
     def run_steps(self, features: Tensor, labels: Tensor, idx_list) -> Optional[list]:
         """Consecutive training steps (an epoch's batches, the short last one
         included) as ONE HIP-graph replay of the synced step -- forward/BPTT,
@@ -163,7 +160,7 @@ class MotionTrainStep:
         step's statistics row, or None when this configuration runs per step
         (no gradient sync / no graph replay, bf16 or GRU packing, host-gathered
         batches, the first two calls of a configuration)."""
-        if self.grad_sync is None or not self.cuda_graph or self.bf16 or self.gru:
+        if self.grad_sync is None or not self.cuda_graph or self.gru:
             return None
         if not idx_list or any(i is None for i in idx_list):
             return None
@@ -247,7 +244,7 @@ class MotionTrainStep:
         capture -- then the capture itself, which runs nothing.  Parameters
         and optimizer state are untouched; the flat gradient (rewritten by
         every step) is left zeroed.  True when the graph is ready."""
-        if self.grad_sync is None or not self.cuda_graph or self.bf16 or self.gru or not sizes:
+        if self.grad_sync is None or not self.cuda_graph or self.gru or not sizes:
             return False
         adam = self._flat_adam_peek()
         if adam is None:
@@ -294,7 +291,7 @@ class MotionTrainStep:
             for view, ((nb, sp), nb_bwd) in zip(views, cfgs):
                 self.mod.lstm_head_train_step(features, view, labels, self.weights, hw, hb, self.flat.grad, self.ring,
                                               self.H, self.NL, sp, 0, nb, nb_bwd, None, None, 0, None, ent["step"],
-                                              ent["slot_off"])
+                                              ent["slot_off"], round_bf16=self.bf16)
                 self.grad_sync()
                 self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step + 1.0, 1.0, bool(dec),
                                    False, None, ent["step"], ent["ticket"])
@@ -340,7 +337,7 @@ class MotionTrainStep:
             nb_fwd, sp_fwd = 1, 1
         hw, hb = self.m.fc.weight, self.m.fc.bias  # the classifier head stays fp32
         if self.bf16:
-            ws = self._rounded()
+            ws = self.weights  # rounded to bf16 in-kernel (round_bf16)
             if features.dtype != torch.bfloat16:
                 features = features.to(torch.bfloat16)
         elif self.gru:
@@ -356,7 +353,8 @@ class MotionTrainStep:
         if adam is not None and self.grad_sync is None:
             with trace_range("pdrnn.fwd_bwd_adam"):
                 self.mod.lstm_head_train_step(features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H,
-                                              self.NL, sp_fwd, 0, nb_fwd, nb_bwd, adam[0], adam[1], cell, self.colmap)
+                                              self.NL, sp_fwd, 0, nb_fwd, nb_bwd, adam[0], adam[1], cell, self.colmap,
+                                              round_bf16=self.bf16)
             return stats
         if self.grad_sync is not None and adam is not None and self.cuda_graph:
             if self._graph_step(features, labels, idx, ws, (nb_fwd, sp_fwd), nb_bwd, adam, stats, slot):
@@ -364,7 +362,7 @@ class MotionTrainStep:
         with trace_range("pdrnn.fwd_bwd"):
             self.mod.lstm_head_train_step(
                 features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, sp_fwd, 0, nb_fwd, nb_bwd,
-                None, None, cell, self.colmap)
+                None, None, cell, self.colmap, round_bf16=self.bf16)
         if self.grad_sync is not None:
             with trace_range("pdrnn.grad_allreduce"):
                 self.grad_sync()
@@ -390,7 +388,7 @@ class MotionTrainStep:
         if self.gru:
             nb_fwd, sp_fwd = 1, 1
         if self.bf16:
-            ws = self._rounded()
+            ws = self.weights  # rounded to bf16 in-kernel (round_bf16)
             if features.dtype != torch.bfloat16:
                 features = features.to(torch.bfloat16)
         elif self.gru:
@@ -410,7 +408,7 @@ class MotionTrainStep:
                 adam_bufs = [p.clone(), m.clone(), v.clone()]
         self.mod.lstm_head_train_step(features, idx, labels, ws, self.m.fc.weight, self.m.fc.bias, self.flat.grad,
                                       stats, self.H, self.NL, sp_fwd, 0, nb_fwd, nb_bwd, adam_bufs, adam_hp,
-                                      1 if self.gru else 0, self.colmap)
+                                      1 if self.gru else 0, self.colmap, round_bf16=self.bf16)
         self.flat.grad.zero_()
 
     def _flat_adam_peek(self):
@@ -433,11 +431,11 @@ class MotionTrainStep:
     def _graph_step(self, features: Tensor, labels: Tensor, idx: Optional[Tensor], ws, nb_fwd,
                     nb_bwd: int, adam, stats: Tensor, slot: int) -> bool:
         """Run the synced step as a graph replay.  False: run it eagerly --
-        the bf16 model (its per-step weight cast allocates), and the first two
+        the GRU (its per-step weight packing allocates), and the first two
         steps of a configuration, so that RCCL's lazy connection setup and the
         kernels' first-use allocations happen outside the capture."""
-        if self.bf16 or self.gru:
-            return False  # per-step weight cast / packing allocates
+        if self.gru:
+            return False  # per-step weight packing allocates
         if idx is None:
             return False  # host-gathered batches change pointers every step
         (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
@@ -501,7 +499,7 @@ class MotionTrainStep:
             nb, sp = nb_fwd  # (sequences per forward workgroup, forward lanes per unit)
             self.mod.lstm_head_train_step(features, ent["idx"], labels, ws, hw, hb, self.flat.grad, self.ring,
                                           self.H, self.NL, sp, 0, nb, nb_bwd, None, None, 0, None, ent["step"],
-                                          ent["slot_off"])
+                                          ent["slot_off"], round_bf16=self.bf16)
             self.grad_sync()
             self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step, 1.0, bool(dec), False,
                                None, ent["step"], ent["ticket"])

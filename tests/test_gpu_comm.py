@@ -233,7 +233,7 @@ def _epoch_of(step, feats, labels, idx_list):
     return [r.clone() for r in res], replayed
 
 
-@pytest.mark.parametrize("mode", ["ddp", "horovod"])
+@pytest.mark.parametrize("mode", ["ddp", "horovod", "ddp-bf16"])
 def test_epoch_graph_replay_matches_local(rccl_group, mode):
     """every step of an epoch (4 full batches + the short
     last one, indices as consecutive views of one tensor like the loader's)
@@ -250,12 +250,15 @@ def test_epoch_graph_replay_matches_local(rccl_group, mode):
     from pytorch_distributed_rnn_amd.utils.flat import flatten_module
     torch.manual_seed(5)
     train, _, _ = synthetic_motion(n_train=448, n_validation=1, n_test=1, seed=5)
+    bf16 = mode.endswith("bf16")  # BASELINE config 2: weights rounded to bf16 in-kernel, graph-replayed too
     feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
-    m1 = MotionModel(9, 32, 2, 6).cuda()
+    if bf16:
+        feats = feats.to(torch.bfloat16)
+    m1 = MotionModel(9, 32, 2, 6, compute_dtype=torch.bfloat16 if bf16 else torch.float32).cuda()
     m2 = copy.deepcopy(m1)
     flatten_module(m2)
     o2 = FusedAdam(m2.parameters(), lr=2.5e-3)
-    if mode == "ddp":
+    if mode.startswith("ddp"):
         ddp = DistributedDataParallel(m1)
         o1 = FusedAdam(m1.parameters(), lr=2.5e-3)
         s1 = MotionTrainStep(ddp, o1, ddp.reducer.all_reduce_inline, cuda_graph=True)
