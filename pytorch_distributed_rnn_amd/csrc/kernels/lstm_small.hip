@@ -239,7 +239,8 @@ lstm_small_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
           w[q][kk] = wround(v, a.w_bf16);
         }
       }
-      bias[q] = (a.b_ih[layer] ? a.b_ih[layer][r] : 0.f) + (a.b_hh[layer] ? a.b_hh[layer][r] : 0.f);
+      bias[q] = (a.b_ih[layer] ? wround(a.b_ih[layer][r], a.w_bf16) : 0.f) +
+                (a.b_hh[layer] ? wround(a.b_hh[layer][r], a.w_bf16) : 0.f);
     }
     if constexpr (S == 2) {
       // pre-scaled rows (as in the gate-split map): the pre-activation comes
@@ -475,7 +476,8 @@ __device__ __forceinline__ void lstm_small_fwd_gs_body(const PdrnnLstmSmallFwdAr
       }
       w2[kk] = pdrnn_f2{wround(v0, a.w_bf16) * wsc, wround(v1, a.w_bf16) * wsc};
     }
-    bias = ((a.b_ih[layer] ? a.b_ih[layer][r] : 0.f) + (a.b_hh[layer] ? a.b_hh[layer][r] : 0.f)) * wsc;
+    bias = ((a.b_ih[layer] ? wround(a.b_ih[layer][r], a.w_bf16) : 0.f) +
+            (a.b_hh[layer] ? wround(a.b_hh[layer][r], a.w_bf16) : 0.f)) * wsc;
   }
 
   int bsrc[NB];
