@@ -829,7 +829,7 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     }
   }
   sticky_host[dev].copy_(sticky[dev], /*non_blocking=*/true);
-  if (check) {
+  if (check && persist_verify_mode() != 2) {  // per-step verification re-runs the step instead
     const int err = sync[ndir * nmb].item<int>();
     TORCH_CHECK(err == 0, "persistent LSTM grid sync timed out");
   }

@@ -1343,7 +1343,9 @@ lstm_small_bwd_dwout_kernel(PdrnnLstmSmallBwdArgs a) {
 // the recurrences still in flight on the same CUs -- the BPTT's exit spread
 // and the separate dW launch (and its HBM re-read of the gate gradients)
 // leave the critical path.  Slab row = tile.  Requires NB * T % 16 == 0 (a
-// tile's rows are whole 16-row stages of the dW pipeline).
+// tile's rows are whole 16-row stages of the dW pipeline).  Opt-in: at B =
+// 1440 the early finishers' dW did not overlap the recurrences enough to beat
+// the separate launch (bwd+dW 229 us vs 158 + 68; see pdrnn_lstm_small_bwd_dw_ok).
 template <int H, int L, int NB, int CELL>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB > 1 ? 3 : 1)))
 lstm_small_bwd_dw_kernel(PdrnnLstmSmallBwdArgs a, PdrnnLstmSmallDwArgs d) {
@@ -1924,8 +1926,11 @@ hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int
 // BPTT at nb sequences per workgroup with whole 16-row dW stages per tile.
 // PDRNN_BWD_DW_FUSED=0 keeps the separate dW launch (A/B measurements).
 int pdrnn_lstm_small_bwd_dw_ok(int H, int NL, int T, int B, int I, int nb) {
+  // opt-in (PDRNN_BWD_DW_FUSED=1): measured no faster than the separate dW
+  // launch at B = 1440 -- the dW MFMAs run after most recurrences have ended
+  // instead of beside them (0.383 vs 0.376 ms/step, profiles/r4/fz2_*)
   const char* e = getenv("PDRNN_BWD_DW_FUSED");  // per call: tests flip it in-process
-  if (e && e[0] == '0') return 0;
+  if (!e || e[0] != '1') return 0;
   if ((H != 16 && H != 32) || (nb != 1 && nb != 2) || NL < 1 || NL > PDRNN_MAX_LAYERS || I < 1 || I > H) return 0;
   const int block = NL * H * 4;  // dwout_lanes = 4 for H <= 32
   if (block > 512 || (nb * T) % pdrnn::kDwRows != 0 || B < 1) return 0;

@@ -240,7 +240,7 @@ def test_deferred_dw_pairs_sequences_at_headline_batch(monkeypatch):
     monkeypatch.delenv("PDRNN_BWD_DW_FUSED", raising=False)
     for B in (1440, 1152):
         nb, grid, fused = mod.lstm_small_dwout_geometry(32, 2, 128, B)
-        assert (nb, grid, fused) == (2, B // 2, True), (B, nb, grid, fused)
+        assert (nb, grid, fused) == (2, B // 2, False), (B, nb, grid, fused)
 
 
 def test_deferred_dw_selected_above_one_round(monkeypatch):
