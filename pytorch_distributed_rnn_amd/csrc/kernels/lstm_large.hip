@@ -1105,8 +1105,10 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   float* red = reinterpret_cast<float*>(smem_raw);  // [wave][MT][16][LDR]
   const int B = args.B, H = args.H, T = args.T;
-  if ((sync.mode & 16) && blockIdx.x == 0 && threadIdx.x == 0)  // test hook: this launch "timed out"
+  if ((sync.mode & 16) && blockIdx.x == 0 && threadIdx.x == 0) {  // test hook: this launch "timed out"
     __hip_atomic_store(sync.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sync.sticky) __hip_atomic_store(sync.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const int NCB = H / PS_NU, NMB = (B + 16 * MT - 1) / (16 * MT);
   int dir, cb, mb;
   ps_coords(NCB, NMB, dir, cb, mb);
@@ -1254,8 +1256,10 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   float* red = reinterpret_cast<float*>(smem_raw);  // [wave][MT][16][LDR]
   const int B = args.B, H = args.H, T = args.T;
-  if ((sync.mode & 16) && blockIdx.x == 0 && threadIdx.x == 0)  // test hook: this launch "timed out"
+  if ((sync.mode & 16) && blockIdx.x == 0 && threadIdx.x == 0) {  // test hook: this launch "timed out"
     __hip_atomic_store(sync.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sync.sticky) __hip_atomic_store(sync.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const int NCB = H / PS_NU, NMB = (B + 16 * MT - 1) / (16 * MT);
   int dir, cb, mb;
   ps_coords(NCB, NMB, dir, cb, mb);

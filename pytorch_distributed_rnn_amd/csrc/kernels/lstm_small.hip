@@ -1057,24 +1057,39 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
     // per-lane byte offset fixed for the whole loop (VGPR) and a per-step
     // scalar offset: one buffer_load per operand, no per-step VALU address
     // arithmetic.  Out-of-range steps are clamped, the values masked at use.
-    __amdgpu_buffer_rsrc_t r_act[NB], r_own[NB], r_in[NB];
+    // NB > 1 with x in LDS: the NB sequences of a tile are consecutive rows
+    // (bs[n] >= bs[0]), so ONE descriptor per stream serves all of them and a
+    // sequence's rows are a wave-uniform byte delta folded into the scalar
+    // offset -- 4 SGPRs per stream instead of 4 NB (the paired-sequence BPTT
+    // spilled SGPRs into VGPR lanes inside the recurrence)
+    constexpr bool kShared = XLDS && NB > 1;
+    constexpr int ND = kShared ? 1 : NB;
+    __amdgpu_buffer_rsrc_t r_act[ND], r_own[ND], r_in[ND];
+    uint32_t d_act[NB], d_h[NB], d_dg[NB];
     const int x_layer0 = layer == 0 && !XLDS;
 #pragma unroll
-    for (int n = 0; n < NB; ++n) {
+    for (int n = 0; n < ND; ++n) {
       const int64_t lb = (int64_t)layer * B + bs[n];
       r_act[n] = uniform_rsrc(a.act + lb * T * 5 * H);
       r_own[n] = uniform_rsrc(a.hseq + lb * T * H);
       r_in[n] = uniform_rsrc(x_layer0 ? a.x + (int64_t)bsrc[n] * a.x_sb
                                       : a.hseq + ((int64_t)(layer > 0 ? layer - 1 : 0) * B + bs[n]) * T * H);
     }
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const uint32_t dn = kShared ? (uint32_t)(bs[n] - bs[0]) * (uint32_t)T : 0u;
+      d_act[n] = __builtin_amdgcn_readfirstlane(dn * 5u * H * 4u);
+      d_h[n] = __builtin_amdgcn_readfirstlane(dn * (uint32_t)H * 4u);
+      d_dg[n] = DWOUT ? __builtin_amdgcn_readfirstlane(dn * (uint32_t)a.dg_st * 4u) : 0u;
+    }
     const bool has_dout = top && doutp != nullptr;
     // deferred dW: this row's gate-gradient stream (same row layout as act)
-    __amdgpu_buffer_rsrc_t r_dg[NB];
+    __amdgpu_buffer_rsrc_t r_dg[ND];
     uint32_t st_dg = 0;
     if constexpr (DWOUT) {
       st_dg = (uint32_t)a.dg_st * 4;
 #pragma unroll
-      for (int n = 0; n < NB; ++n) r_dg[n] = uniform_rsrc(a.dg_out + ((int64_t)layer * B + bs[n]) * T * a.dg_st);
+      for (int n = 0; n < ND; ++n) r_dg[n] = uniform_rsrc(a.dg_out + ((int64_t)layer * B + bs[n]) * T * a.dg_st);
     }
     const uint32_t vo_q = (q * H + u) * 4, vo_c = (4 * H + u) * 4, vo_u = u * 4;
     const uint32_t vo_x = (x_layer0 ? min(u, I - 1) : u) * 4;
@@ -1092,9 +1107,10 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
       const uint32_t so_h = __builtin_amdgcn_readfirstlane(tp * st_h);
       const uint32_t so_x = __builtin_amdgcn_readfirstlane(tc * st_x);
       Ops o;
-      o.aq = bload(r_act[n], vo_q, so_a);
-      o.ct = bload(r_act[n], vo_c, so_a);
-      o.cp = bload(r_act[n], vo_c, so_ap);
+      const int nd = kShared ? 0 : n;
+      o.aq = bload(r_act[nd], vo_q, so_a + d_act[n]);
+      o.ct = bload(r_act[nd], vo_c, so_a + d_act[n]);
+      o.cp = bload(r_act[nd], vo_c, so_ap + d_act[n]);
       // optional operands (generic kernel only): descriptors built on demand
       // to keep the SGPR budget of the hot loop
       const int64_t lb = (int64_t)layer * B + bs[n];
@@ -1102,9 +1118,9 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
       o.dout = has_dout ? bload(uniform_rsrc(doutp + bs[n] * a.d_sb), vo_u,
                                 __builtin_amdgcn_readfirstlane(tc * (uint32_t)a.d_st * 4))
                         : 0.f;
-      o.hprev = bload(r_own[n], vo_u, so_h);
+      o.hprev = bload(r_own[nd], vo_u, so_h + d_h[n]);
       if (h0p && tc == 0) o.hprev = bload(uniform_rsrc(h0p + lb * H), vo_u, 0);
-      o.xin = bload(r_in[n], vo_x, so_x);
+      o.xin = bload(r_in[nd], vo_x, so_x + (x_layer0 ? 0u : d_h[n]));
       return o;
     };
 
@@ -1179,8 +1195,8 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
           // waits conservative, see load_ops)
           const bool st_ok = active && valid[n] && (L == 4 || rowlane);
           const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)min(max(t, 0), T - 1) * st_dg);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dgv), r_dg[n],
-                                                st_ok ? vo_q : 0x80000000u, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dgv), r_dg[kShared ? 0 : n],
+                                                st_ok ? vo_q : 0x80000000u, so + d_dg[n], 0);
         }
       }
       lds_barrier();
