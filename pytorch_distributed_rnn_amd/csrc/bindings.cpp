@@ -631,7 +631,8 @@ Tensor xent_bwd(const Tensor& dlogits, const Tensor& grad_out, const Tensor& sta
 void adam_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_sq,
                const optional<Tensor>& max_exp_avg_sq, double lr, double beta1, double beta2, double eps,
                double weight_decay, double step, double grad_scale, bool decoupled, bool maximize,
-               const optional<Tensor>& lr_t, const optional<Tensor>& step_t, const optional<Tensor>& ticket) {
+               const optional<Tensor>& lr_t, const optional<Tensor>& step_t, const optional<Tensor>& ticket,
+               const optional<Tensor>& skip) {
   CHECK_HIP_TENSOR(param);
   for (const Tensor* t : std::initializer_list<const Tensor*>{&param, &grad, &exp_avg, &exp_avg_sq}) {
     CHECK_F32(*t);
@@ -662,6 +663,11 @@ void adam_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_
     a.step_advance = step_t->data_ptr<float>();
     a.ticket = reinterpret_cast<unsigned int*>(ticket->data_ptr<int>());
     a.step_ptr = nullptr;
+  }
+  if (skip.has_value() && skip->defined()) {
+    TORCH_CHECK(skip->is_cuda() && skip->scalar_type() == at::kInt && skip->numel() >= 1,
+                "adam_flat: skip must be a device int32 tensor");
+    a.skip = skip->data_ptr<int>();
   }
   HIP_LAUNCH_CHECK(pdrnn_adam_flat(&a, cur_stream()));
 }
@@ -762,7 +768,16 @@ int persist_verify_mode() {
 bool persist_verify_on() { return persist_verify_mode() == 1; }
 // leaked on purpose: no tensor destructor runs after the HIP runtime is gone
 std::vector<Tensor>& persist_sticky() { static auto& v = *new std::vector<Tensor>(64); return v; }
-std::vector<Tensor>& persist_sticky_host() { static auto& v = *new std::vector<Tensor>(64); return v; }
+// host mirrors: raw pinned words, never freed (a pinned tensor held in a
+// static is released by the host caching allocator at exit, after tools such
+// as the profiler have finalised)
+int* pinned_word() {
+  void* p = nullptr;
+  TORCH_CHECK(hipHostMalloc(&p, sizeof(int), hipHostMallocDefault) == hipSuccess, "hipHostMalloc");
+  *static_cast<int*>(p) = 0;
+  return static_cast<int*>(p);
+}
+std::vector<int*>& persist_sticky_host() { static auto& v = *new std::vector<int*>(64, nullptr); return v; }
 
 int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int dt, int64_t tile,
                   const at::TensorOptions& opts, hipStream_t st) {
@@ -784,13 +799,13 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
   if (mt == 0) return kPersistNotRun;
   const int nmb = (a.B + 16 * mt - 1) / (16 * mt);
   std::vector<Tensor>& sticky = persist_sticky();
-  std::vector<Tensor>& sticky_host = persist_sticky_host();
+  std::vector<int*>& sticky_host = persist_sticky_host();
   TORCH_CHECK(dev >= 0 && dev < 64, "device index");
   if (!sticky[dev].defined()) {
     sticky[dev] = at::zeros({1}, opts.dtype(at::kInt));
-    sticky_host[dev] = at::zeros({1}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
+    sticky_host[dev] = pinned_word();
   }
-  if (sticky_host[dev].data_ptr<int>()[0] != 0) {
+  if (__atomic_load_n(sticky_host[dev], __ATOMIC_RELAXED) != 0) {
     // per-step verification: an earlier launch of this step timed out -- the
     // step's check re-runs it; the rest of the step takes the per-step kernels
     if (persist_verify_mode() == 2) return kPersistNotRun;
@@ -810,9 +825,9 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     return kPersistNotRun;
   }
   if (persist_verify_on()) {
-    static std::vector<Tensor>& flag = *new std::vector<Tensor>(64);
-    if (!flag[dev].defined()) flag[dev] = at::zeros({1}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
-    int* hf = flag[dev].data_ptr<int>();
+    static std::vector<int*>& flag = *new std::vector<int*>(64, nullptr);
+    if (!flag[dev]) flag[dev] = pinned_word();
+    int* hf = flag[dev];
     hf[0] = 0;
     TORCH_CHECK(hipMemcpyAsync(hf, cnt + ndir * nmb, sizeof(int), hipMemcpyDeviceToHost, st) == hipSuccess, "flag copy");
     TORCH_CHECK(hipStreamSynchronize(st) == hipSuccess, "persistent LSTM: stream synchronisation failed");
@@ -828,12 +843,28 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
       return kPersistFailed;
     }
   }
-  sticky_host[dev].copy_(sticky[dev], /*non_blocking=*/true);
+  TORCH_CHECK(hipMemcpyAsync(sticky_host[dev], sticky[dev].data_ptr<int>(), sizeof(int), hipMemcpyDeviceToHost, st) ==
+                  hipSuccess, "sticky copy");
   if (check && persist_verify_mode() != 2) {  // per-step verification re-runs the step instead
     const int err = sync[ndir * nmb].item<int>();
     TORCH_CHECK(err == 0, "persistent LSTM grid sync timed out");
   }
   return kPersistOk;
+}
+
+// The current device's sticky timeout flag (device int32 [1], created on
+// first use): the deferred per-step verification all-reduces it across ranks
+// and hands it to the optimizer launch as its skip word.
+Tensor persist_sticky_flag() {
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
+  TORCH_CHECK(dev >= 0 && dev < 64, "device index");
+  std::vector<Tensor>& sticky = persist_sticky();
+  if (!sticky[dev].defined()) {
+    sticky[dev] = at::zeros({1}, at::TensorOptions().device(at::kCUDA, dev).dtype(at::kInt));
+    persist_sticky_host()[dev] = pinned_word();
+  }
+  return sticky[dev];
 }
 
 // Per-step verification: true when a persistent launch on this device timed
@@ -845,7 +876,7 @@ bool persist_step_check() {
   if (dev < 0 || dev >= 64 || !persist_sticky()[dev].defined()) return false;
   if (persist_sticky()[dev].item<int>() == 0) return false;  // synchronises
   persist_sticky()[dev].zero_();
-  persist_sticky_host()[dev].zero_();
+  if (persist_sticky_host()[dev]) __atomic_store_n(persist_sticky_host()[dev], 0, __ATOMIC_RELAXED);
   g_persist_fallbacks++;
   if (std::getenv("PDRNN_LSTM_PERSIST_RETRY") == nullptr) g_persist_disabled = 1;
   std::fprintf(stderr, "[pdrnn] persistent LSTM recurrence: a grid-sync wait timed out in this step (fallback #%lld); "
@@ -1261,7 +1292,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("exp_avg"), py::arg("exp_avg_sq"), py::arg("max_exp_avg_sq"), py::arg("lr"), py::arg("beta1"),
         py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"), py::arg("grad_scale"),
         py::arg("decoupled"), py::arg("maximize"), py::arg("lr_t") = py::none(), py::arg("step_t") = py::none(),
-        py::arg("ticket") = py::none());
+        py::arg("ticket") = py::none(), py::arg("skip") = py::none());
   m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
   m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
   m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });
@@ -1269,6 +1300,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "0 off; 1 synchronise after every persistent-recurrence launch and re-run a timed-out layer on the "
         "per-step kernels; 2 per step: persist_step_check() before the optimizer update re-runs the step");
   m.def("persist_verify_mode", []() { return persist_verify_mode(); });
+  m.def("persist_sticky_flag", &persist_sticky_flag,
+        "the current device's sticky persistent-timeout flag (device int32 [1])");
   m.def("persist_step_check", &persist_step_check,
         "per-step verification: True when a persistent launch timed out since the last check (synchronises)");
   m.def("persist_inject_timeouts", [](int64_t n) { g_persist_inject = (int)n; },

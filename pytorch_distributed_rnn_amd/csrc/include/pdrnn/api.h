@@ -222,6 +222,9 @@ typedef struct {
   // back by the last workgroup to finish (arrival ticket, reset to 0 after)
   float* step_advance;
   unsigned int* ticket;
+  // != nullptr and nonzero at run time: the launch returns without touching
+  // anything (a step whose results are invalid, decided on the device)
+  const int* skip;
 } PdrnnAdamArgs;
 hipError_t pdrnn_adam_flat(const PdrnnAdamArgs* a, hipStream_t stream);
 

@@ -40,6 +40,7 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 }
 
 __global__ void __launch_bounds__(256) adam_flat_kernel(PdrnnAdamArgs a) {
+  if (a.skip && *a.skip != 0) return;  // uniform: every workgroup reads the same word
   AdamScalars s;
   s.lr = a.lr_ptr ? *a.lr_ptr : a.lr;
   s.b1 = a.beta1; s.b2 = a.beta2; s.eps = a.eps; s.wd = a.weight_decay;

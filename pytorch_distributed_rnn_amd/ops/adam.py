@@ -85,7 +85,10 @@ class FusedAdam(torch.optim.Adam):
         return cached
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, skip: Optional[Tensor] = None):
+        """``skip``: device int32 word read by the native launch -- nonzero at
+        run time leaves parameters and moments untouched (the step count still
+        advances on the host: :meth:`rewind` takes such steps back)."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -97,12 +100,16 @@ class FusedAdam(torch.optim.Adam):
             dev = params[0].device
             mod = _ext.native(dev)
             if mod is None or params[0].dtype != torch.float32:
+                if skip is not None and bool(skip.item()):
+                    continue
                 self._reference_group_step(group)
                 continue
             fs = self._group_flat(gi, group)
             grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
             gspan = contiguous_span(grads)
             if fs is None:
+                if skip is not None and bool(skip.item()):
+                    continue
                 self._reference_group_step(group)
                 continue
             gflat = gspan[0] if gspan is not None else torch.cat([g.reshape(-1) for g in grads])
@@ -112,7 +119,7 @@ class FusedAdam(torch.optim.Adam):
             mod.adam_flat(fs["flat_p"], gflat, fs["exp_avg"], fs["exp_avg_sq"], fs["max_sq"],
                           float(group["lr"]), beta1, beta2, group["eps"], group["weight_decay"],
                           step, self._pdrnn_grad_scale, bool(group.get("decoupled_weight_decay", False)),
-                          bool(group.get("maximize", False)), None, None)
+                          bool(group.get("maximize", False)), None, None, None, skip)
             self.native_steps = getattr(self, "native_steps", 0) + 1  # groups stepped by the native kernel
             # the native kernel wrote the parameters through raw pointers: move
             # their version counters like any in-place torch update would, so
@@ -121,6 +128,12 @@ class FusedAdam(torch.optim.Adam):
             for p in params:
                 torch.autograd.graph.increment_version(p)
         return loss
+
+    def rewind(self, steps: int) -> None:
+        """Take ``steps`` native steps back from the step count (steps whose
+        launch was skipped on the device, see :meth:`step`)."""
+        for fs in self._flat_state.values():
+            fs["step"] -= float(steps)
 
     def _reference_group_step(self, group):
         # torch's own Adam for this group only (CPU path / unsupported layout).

@@ -211,11 +211,14 @@ def _unit_inner(t: Tensor) -> bool:
 
 
 def _splitk_f32(dev, M: int, N: int, K: int) -> int:
-    """K splits bringing the fp32 GEMM to ~2 workgroups per CU (partials summed
-    in fixed order), at least 8 k-tiles of 16 per split."""
+    """K splits bringing the fp32 GEMM to ~4 workgroups per CU (partials summed
+    in fixed order), at least 8 k-tiles of 16 per split.  A few output tiles
+    over a long K (the bi-LSTM head's dW: 64 tiles, K = 262144) carry little
+    MFMA work per k-tile and are bound by load latency: the more workgroups in
+    flight (LDS holds 4 per CU), the more k-tiles in flight."""
     bn = 32 if N <= 32 else 64 if N <= 64 else 128
     tiles = ((M + 127) // 128) * ((N + bn - 1) // bn)
-    want = 2 * _cus(dev)
+    want = 4 * _cus(dev)
     if tiles >= want:
         return 1
     return max(1, min((want + tiles - 1) // tiles, max(1, K // (16 * 8)), 128))

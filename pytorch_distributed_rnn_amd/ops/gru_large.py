@@ -34,7 +34,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-from .lstm_large import _interleave, _perm, _tile
+from .lstm_large import _interleave, _perm, _tile, final_hidden, stack_layers
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
@@ -109,7 +109,7 @@ class _LargeGRULayer(torch.autograd.Function):
         rev_mask = 2 if ndir == 2 else 0
         hseq, hs32, acts = mod.lstm_large_fwd(xp, whh_p, h0c, h0f, H, rev_mask, tile, 1)
         last = [T - 1, 0][:ndir]
-        hn = torch.stack([hseq[last[d], :, d * H:(d + 1) * H] for d in range(ndir)], 0)
+        hn = final_hidden(hseq, last, H)
         ctx.save_for_backward(x, hseq, hs32, acts, h0c, h0f, *wih, *wt)
         ctx.cfg = (H, ndir, tile, rev_mask, [w is not None for w in weights], h0 is not None,
                    h0.dtype if h0 is not None else None)
@@ -163,9 +163,11 @@ class _LargeGRULayer(torch.autograd.Function):
                 dw4 = mm_kk([(G, hprev.reshape(T * B, H))])
                 dwih = mm_kk([(Gx, x2)])
                 cs = col_sum(G)
-                dwhh = torch.cat([dw4[:2 * H], dw4[3 * H:]])
                 dbih = cs[:3 * H]
-                dbhh = torch.cat([cs[:2 * H], cs[3 * H:]])
+                dwhh, dbhh = dw4.new_empty(3 * H, H), cs.new_empty(3 * H)  # nn.GRU has no n_x block in W_hh
+                for dst, src in ((dwhh, dw4), (dbhh, cs)):
+                    dst[:2 * H].copy_(src[:2 * H])
+                    dst[2 * H:].copy_(src[3 * H:])
             if not need_dx:
                 pass  # layer input without grad (e.g. the data): no dX GEMM
             else:
@@ -205,4 +207,4 @@ def gru_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Option
         if dropout > 0 and training and l < num_layers - 1:
             seq = torch.nn.functional.dropout(seq, dropout, True)
     out = seq.transpose(0, 1) if batch_first else seq
-    return out, torch.cat(hns, 0)
+    return out, stack_layers(hns)

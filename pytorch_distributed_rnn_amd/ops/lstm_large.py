@@ -190,6 +190,27 @@ def _bias_cat(weights, ndir: int, hidden: int, device) -> Tensor:
     return t
 
 
+def final_hidden(hseq: Tensor, last: Sequence[int], H: int) -> Tensor:
+    """[ndir, B, H] final hidden states out of hseq [T, B, ndir*H]: one copy
+    per direction into a fresh tensor (no ATen concatenation kernel)."""
+    hn = hseq.new_empty(len(last), hseq.shape[1], H)
+    for d, t in enumerate(last):
+        hn[d].copy_(hseq[t, :, d * H:(d + 1) * H])
+    return hn
+
+
+def stack_layers(states: List[Tensor]) -> Tensor:
+    """Per-layer [ndir, B, H] states -> [layers*ndir, B, H] (slice copies,
+    autograd-tracked; a single layer is returned as is)."""
+    if len(states) == 1:
+        return states[0]
+    n = states[0].shape[0]
+    out = states[0].new_empty(n * len(states), *states[0].shape[1:])
+    for l, s in enumerate(states):
+        out[l * n:(l + 1) * n] = s
+    return out
+
+
 class _LargeLSTMLayer(torch.autograd.Function):
     """One layer, 1 or 2 directions.  x: [T, B, I] (compute dtype).
 
@@ -218,8 +239,10 @@ class _LargeLSTMLayer(torch.autograd.Function):
         rev_mask = 2 if ndir == 2 else 0
         hseq, cseq, acts = mod.lstm_large_fwd(xp, whh_p, h0c, c0c, H, rev_mask, tile, 0)
         last = [T - 1, 0][:ndir]
-        hn = torch.stack([hseq[last[d], :, d * H:(d + 1) * H] for d in range(ndir)], 0)
-        cn = torch.stack([cseq[d, last[d]] for d in range(ndir)], 0)
+        hn = final_hidden(hseq, last, H)
+        cn = cseq.new_empty(ndir, B, H, dtype=cdt)
+        for d in range(ndir):
+            cn[d].copy_(cseq[d, last[d]])
         # backward works in torch's gate-blocked order: W_ih as stored (dX GEMM),
         # W_hh transposed (BPTT step GEMM), both 16-bit shadows
         ctx.save_for_backward(x, hseq, cseq, acts, h0c, c0c, *[shadow(w, "p", cdt, H) for w in w_ih],
@@ -227,7 +250,7 @@ class _LargeLSTMLayer(torch.autograd.Function):
         ctx.cfg = (H, ndir, tile, rev_mask, [w is not None for w in weights], h0 is not None,
                    c0 is not None, h0.dtype if h0 is not None else None,
                    c0.dtype if c0 is not None else None)
-        return hseq, hn, cn.to(cdt)
+        return hseq, hn, cn
 
     @staticmethod
     def backward(ctx, dhseq, dhn, dcn):
@@ -343,4 +366,4 @@ def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optio
         if dropout > 0 and training and l < num_layers - 1:
             seq = torch.nn.functional.dropout(seq, dropout, True)
     out = seq.transpose(0, 1) if batch_first else seq
-    return out, torch.cat(hns, 0), torch.cat(cns, 0)
+    return out, stack_layers(hns), stack_layers(cns)

@@ -62,6 +62,7 @@ class LMTrainer:
         self.global_batch = gb
         self.streams = corpus.streams(gb, self.rank, self.world).to(device)
         self.vocab = corpus.vocab_size
+        self._pending: List[dict] = []  # steps not yet verified (deferred verification)
 
     def _clip(self) -> None:
         if self.grad_clip and self.grad_clip > 0:
@@ -78,40 +79,82 @@ class LMTrainer:
             loss.backward()
         return loss
 
-    def _persist_timed_out(self) -> bool:
-        """Per-step verification of the persistent recurrence (multi-rank
-        jobs, bindings.cpp persist_step_check): True when any rank's
-        persistent launch lost co-residency during this step -- then every
-        rank re-runs the step on the per-step kernels (the re-run's
-        collectives must match on all ranks)."""
-        mod = _ext.extension() if self.device.type == "cuda" else None
-        if mod is None or not hasattr(mod, "persist_step_check") or mod.persist_verify_mode() != 2:
+    # ---------------------------------------------- persistent-path verification
+    def _deferred_verify(self) -> bool:
+        """Per-step verification of the persistent recurrence (multi-rank jobs:
+        bindings.cpp large_persist, persist_verify_mode() == 2), without a host
+        synchronisation in the step: the device's sticky timeout flag is
+        all-reduced (MAX) across ranks on the stream and handed to the Adam
+        launch as its skip word, so a step whose persistent launch lost
+        co-residency on ANY rank leaves the parameters untouched everywhere;
+        the host reads the flag's pinned copy one step later (:meth:`settle`)
+        and re-runs the skipped steps on the per-step kernels."""
+        if self.device.type != "cuda":
             return False
-        local = bool(mod.persist_step_check())
+        mod = _ext.extension()
+        return mod is not None and hasattr(mod, "persist_sticky_flag") and mod.persist_verify_mode() == 2
+
+    def _step_flag(self):
+        mod = _ext.extension()
+        flag = mod.persist_sticky_flag()
         if self.world > 1:
             from ..parallel.comm import get_comm
-            flag = torch.tensor([1.0 if local else 0.0], device=self.device)
             comm = get_comm()
-            comm.all_reduce(flag, "max")
-            comm.wait()
-            local = bool(flag.item())
-        if local:
+            comm.all_reduce(flag, "max")  # in place: every rank's sticky flag agrees
+            comm.wait()                   # stream-ordered (no host wait)
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(flag, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return flag, host, ev
+
+    def settle(self, keep: int = 0) -> int:
+        """Confirm unverified steps until at most ``keep`` remain; re-runs (in
+        order, from the first one's carried state) every unverified step once
+        one of them turns out to have been skipped.  Returns the number of
+        re-run steps."""
+        pend = self._pending
+        while len(pend) > keep:
+            p = pend[0]
+            p["ev"].synchronize()
+            if int(p["host"][0]) == 0:
+                pend.pop(0)
+                continue
+            # skipped on the device: this step and every later unverified one
+            # (the flag stays set until cleared here) -- the same on every rank
+            mod = _ext.extension()
+            mod.persist_step_check()  # clear, count, turn the persistent path off
             mod.persist_disable()
-        return local
+            redo = list(pend)
+            pend.clear()
+            self.optimizer.rewind(len(redo))
+            self.inner._state = redo[0]["carry0"]
+            for q in redo:
+                loss = self._fwd_bwd(q["inp"], q["tgt"])
+                with trace_range("pdrnn.optimizer"):
+                    self._clip()
+                    self.optimizer.step()
+                q["out"].copy_(loss.detach())
+            return len(redo)
+        return 0
 
     def train_step(self, inp: Tensor, tgt: Tensor) -> Tensor:
+        if not self._deferred_verify():
+            loss = self._fwd_bwd(inp, tgt)
+            with trace_range("pdrnn.optimizer"):
+                self._clip()
+                self.optimizer.step()
+            return loss.detach()
+        self.settle(keep=1)  # the step before the previous one is done by now
         carry0 = getattr(self.inner, "_state", None)
         loss = self._fwd_bwd(inp, tgt)
-        if self._persist_timed_out():
-            # a persistent launch of this step lost co-residency (results
-            # invalid, parameters untouched): the whole step again from the
-            # same carried state, now on the per-step kernels
-            self.inner._state = carry0
-            loss = self._fwd_bwd(inp, tgt)
+        flag, host, ev = self._step_flag()
         with trace_range("pdrnn.optimizer"):
             self._clip()
-            self.optimizer.step()
-        return loss.detach()
+            self.optimizer.step(skip=flag)
+        out = loss.detach()  # a re-run overwrites it in place
+        self._pending.append(dict(inp=inp, tgt=tgt, carry0=carry0, host=host, ev=ev, out=out))
+        return out
 
     def train_epoch(self, epoch: int = 0, max_steps: Optional[int] = None) -> Dict[str, float]:
         self.inner.train()
@@ -123,9 +166,11 @@ class LMTrainer:
             losses.append(self.train_step(inp, tgt))
             tokens += inp.numel()
             if self.log_interval and (step + 1) % self.log_interval == 0:
+                self.settle()
                 cur = float(torch.stack(losses[-self.log_interval:]).mean())
                 logging.info(f"Rank: {self.rank:02d}   Epoch {epoch} Step {step + 1}\tLoss: {cur:.6f}"
                              f"\tbpc: {cur / math.log(2):.4f}")
+        self.settle()
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
@@ -143,6 +188,7 @@ class LMTrainer:
     def save(self, path, epoch: int, loss: float):
         """Rank 0 writes the reference checkpoint layout (epoch, model_state,
         optimizer_state, loss); returns the path or None on other ranks."""
+        self.settle()
         if self.rank != 0:
             return None
         return save_checkpoint(path, epoch, self.model, self.optimizer, loss)

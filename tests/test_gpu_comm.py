@@ -288,8 +288,12 @@ def test_epoch_graph_replay_matches_local(rccl_group, mode):
     for a, b in outs:
         for x, y in zip(a, b):
             torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+    # bf16: the synced step reduces dW in another order than the local step;
+    # fp32-level gradient differences flip bf16 roundings of the weights inside
+    # the kernels and Adam carries them over 25 steps (~1 % of one lr step)
+    ptol = dict(rtol=1e-3, atol=1e-4) if bf16 else dict(rtol=1e-5, atol=1e-6)
     for p, q in zip(m1.parameters(), m2.parameters()):
-        torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(p, q, **ptol)
     assert o1.state_dict()["state"][0]["step"] == o2.state_dict()["state"][0]["step"] == 25
 
 

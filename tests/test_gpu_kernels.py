@@ -150,6 +150,30 @@ def test_adam_flat_device_step_advance():
     torch.testing.assert_close(v2, v1, rtol=0, atol=0)
 
 
+def test_adam_flat_skip_word():
+    """The device skip word (deferred persistent-path verification): nonzero
+    -> the launch changes nothing; zero -> an ordinary step."""
+    from pytorch_distributed_rnn_amd import _ext
+    mod = _ext.require()
+    torch.manual_seed(0)
+    n = 1 << 18
+    p = torch.randn(n, device="cuda")
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    p0 = p.clone()
+    g = torch.randn(n, device="cuda")
+    skip = torch.ones(1, dtype=torch.int32, device="cuda")
+    mod.adam_flat(p, g, m, v, None, 1e-2, 0.9, 0.999, 1e-8, 0.0, 1.0, 1.0, False, False, None, None, None, skip)
+    torch.cuda.synchronize()
+    assert torch.equal(p, p0) and int(m.abs().sum()) == 0 and int(v.abs().sum()) == 0
+    skip.zero_()
+    mod.adam_flat(p, g, m, v, None, 1e-2, 0.9, 0.999, 1e-8, 0.0, 1.0, 1.0, False, False, None, None, None, skip)
+    ref = p0.clone()
+    m2, v2 = torch.zeros_like(p), torch.zeros_like(p)
+    mod.adam_flat(ref, g, m2, v2, None, 1e-2, 0.9, 0.999, 1e-8, 0.0, 1.0, 1.0, False, False)
+    torch.cuda.synchronize()
+    assert torch.equal(p, ref)
+
+
 def test_embedding_matches_torch():
     C = _C()
     V, D, N = 97, 64, 5000

@@ -167,10 +167,12 @@ def test_persistent_backward_beside_cu_spinner(verified):
 
 def test_step_verified_charlm_reruns_timed_out_step(monkeypatch):
     """ADVICE r3 / VERDICT r3 item 5a: per-step verification (the multi-rank
-    default): a timed-out persistent launch is caught by the trainer's check
-    before the optimizer update and the whole step re-runs from the same
-    carried state on the per-step kernels -- the parameters after the step
-    equal a run that never took the persistent path."""
+    default) without a host sync in the step: a timed-out persistent launch
+    sets the device flag, the Adam launches of that step and of the next one
+    (issued before the host saw the flag) skip themselves on the device, and
+    the trainer re-runs both from the first one's carried state on the
+    per-step kernels -- parameters and the returned losses equal a run that
+    never took the persistent path."""
     import copy
     from pytorch_distributed_rnn_amd.data.charlm import CharCorpus
     from pytorch_distributed_rnn_amd.models.charlm import CharLM
@@ -181,7 +183,7 @@ def test_step_verified_charlm_reruns_timed_out_step(monkeypatch):
     corpus = CharCorpus.synthetic(200_000, seed=3)
     torch.manual_seed(0)
     m0 = CharLM(256, 64, 1024, 1, compute_dtype=torch.bfloat16)
-    results = []
+    results, losses = [], []
     try:
         for inject in (True, False):
             mod.persist_reset()
@@ -189,16 +191,21 @@ def test_step_verified_charlm_reruns_timed_out_step(monkeypatch):
             if not inject:
                 mod.persist_disable()  # reference run: per-step kernels only
             tr = LMTrainer(copy.deepcopy(m0), corpus, global_batch=16, seq_len=32, device=torch.device("cuda"))
-            inp, tgt = next(iter(CharCorpus.segments(tr.streams, 32, 1)))
+            segs = list(CharCorpus.segments(tr.streams, 32, 3))
+            tr.inner.reset_hidden_state()
             if inject:
-                mod.persist_inject_timeouts(1)
-            tr.train_step(inp, tgt)
+                mod.persist_inject_timeouts(1)  # the first persistent launch of step 1
+            out = [tr.train_step(inp, tgt) for inp, tgt in segs]
+            tr.settle()
             torch.cuda.synchronize()
             if inject:
                 assert mod.persist_fallbacks() == 1 and mod.persist_disabled()
+                assert tr.optimizer._flat_state[0]["step"].item() == 3.0
             results.append(torch.cat([p.detach().float().reshape(-1) for p in tr.inner.parameters()]))
+            losses.append(torch.stack(out).float())
     finally:
         mod.persist_inject_timeouts(0)
         mod.set_persist_verify(0)
         mod.persist_reset()
+    torch.testing.assert_close(losses[0], losses[1], rtol=1e-3, atol=1e-5)
     torch.testing.assert_close(results[0], results[1], rtol=1e-3, atol=1e-5)

@@ -63,3 +63,23 @@ def test_stats_to_host_ring_slice_and_fallback():
     assert torch.equal(stats_to_host([ring[9], ring[0]]), torch.stack([ring[9], ring[0]]))
     a, b = torch.ones(3), torch.zeros(3)
     assert torch.equal(stats_to_host([a, b]), torch.stack([a, b]))
+
+
+def test_fused_adam_skip_word_leaves_state_untouched():
+    """A nonzero skip word (the deferred persistent-path verification of
+    train/lm.py) leaves parameters and moments untouched; rewind() takes the
+    skipped native step back from the count."""
+    torch.manual_seed(0)
+    m = MotionModel(9, 8, 2, 6)
+    flatten_module(m)
+    opt = FusedAdam(m.parameters(), lr=2.5e-3)
+    _train(m, opt, steps=2)
+    before = [p.detach().clone() for p in m.parameters()]
+    for p in m.parameters():
+        p.grad = torch.randn_like(p)
+    opt.step(skip=torch.ones(1, dtype=torch.int32))
+    for p, q in zip(m.parameters(), before):
+        assert torch.equal(p.detach(), q)
+    opt.step(skip=torch.zeros(1, dtype=torch.int32))
+    assert any(not torch.equal(p.detach(), q) for p, q in zip(m.parameters(), before))
+    opt.rewind(0)  # CPU path: no flat native state to rewind

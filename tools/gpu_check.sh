@@ -17,6 +17,11 @@ fi
 tail -1 gpurun_out/${tag}_gpu_tests.log
 timeout -k 10 300 python bench.py > gpurun_out/${tag}_bench.log 2>&1 || { tail -20 gpurun_out/${tag}_bench.log; exit 1; }
 tail -1 gpurun_out/${tag}_bench.log | cut -c1-400
+# config 2 (bf16 motion) and the GRU cell at the headline shape
+timeout -k 10 300 python bench.py --dtype bf16 > gpurun_out/${tag}_bench_bf16.log 2>&1 || { tail -20 gpurun_out/${tag}_bench_bf16.log; exit 1; }
+tail -1 gpurun_out/${tag}_bench_bf16.log | python tools/bench_line.py "bf16"
+timeout -k 10 300 python bench.py --cell gru > gpurun_out/${tag}_bench_gru.log 2>&1 || { tail -20 gpurun_out/${tag}_bench_gru.log; exit 1; }
+tail -1 gpurun_out/${tag}_bench_gru.log | python tools/bench_line.py "gru"
 for B in 1440 720 360 180; do
   timeout -k 10 180 python bench.py --steps 200 --warmup 20 --global-batch $B > gpurun_out/${tag}_bench$B.log 2>&1 || { tail -20 gpurun_out/${tag}_bench$B.log; exit 1; }
   tail -1 gpurun_out/${tag}_bench$B.log | python tools/bench_line.py "B=$B eager"

@@ -5,5 +5,5 @@
 set -e
 tag=${1:-rd}
 bash tools/gpu_lm.sh ${tag}lm
-bash tools/gpu_tables.sh ${tag}tb
 bash tools/gpu_check.sh ${tag} quick
+bash tools/gpu_tables.sh ${tag}tb
