@@ -742,12 +742,13 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 //     after every launch and checked at the next one (fails loudly one call
 //     later), and by persist_check() at epoch end.
 //   * verify per step (set_persist_verify(2) -- the multi-rank trainers do
-//     it): no synchronisation per launch; a timed-out launch leaves the sticky
-//     flag set, the step's later persistent launches run per step, and the
-//     trainer's persist_step_check() before the optimizer update (one host
-//     read per step, agreed across ranks) re-runs the whole step when any
-//     rank saw a timeout (train/lm.py).  Launch-verify costs 6.7 % of the
-//     char-LM step (profiles/r4/nb1_charlm_verify*.log); this costs one sync.
+//     it): no synchronisation at all; a timed-out launch leaves the sticky
+//     flag set, the step's later persistent launches run per step, the
+//     trainer all-reduces the flag on the stream and hands it to the Adam
+//     launch as its skip word (persist_sticky_flag), reads its pinned copy
+//     one step later and re-runs the skipped steps (train/lm.py settle;
+//     persist_step_check clears and counts).  Launch-verify costs 6.7 % of
+//     the char-LM step (profiles/r4/nb1_charlm_verify*.log).
 enum PersistResult { kPersistNotRun = 0, kPersistOk = 1, kPersistFailed = 2 };
 std::atomic<int> g_persist_verify{-1};     // -1: PDRNN_LSTM_PERSIST_VERIFY (default off); 1 launch, 2 step
 std::atomic<int> g_persist_inject{0};      // tests: flag the next N launches as timed out

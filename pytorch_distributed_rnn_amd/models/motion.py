@@ -20,6 +20,7 @@ import torch
 from torch import Tensor, nn
 
 from .rnn import GRU, LSTM
+from ..ops.gemm import linear
 
 
 class MotionModel(nn.Module):
@@ -51,13 +52,19 @@ class MotionModel(nn.Module):
             if idx is not None:
                 x = x.index_select(0, idx)
             out, _ = self.lstm(x)
-            h = out[:, -1, :]
-            return self.fc(h if h.dtype == self.fc.weight.dtype else h.to(self.fc.weight.dtype))
+            return self._head(out[:, -1, :])
         if self.cell == "lstm":
             _, (hn, _) = self.lstm(x, need_out=False, idx=idx)
         else:
             if idx is not None:
                 x = x.index_select(0, idx)
             _, hn = self.lstm(x)
-        h = hn[-1]
-        return self.fc(h if h.dtype == self.fc.weight.dtype else h.to(self.fc.weight.dtype))
+        return self._head(hn[-1])
+
+    def _head(self, h: Tensor) -> Tensor:
+        """The linear head; on the GPU on the in-tree narrow fp32 GEMM
+        (ops/gemm.linear: forward, dX, dW with db as its row sums)."""
+        h = h if h.dtype == self.fc.weight.dtype else h.to(self.fc.weight.dtype)
+        if h.is_cuda:
+            return linear(h, self.fc.weight, self.fc.bias)
+        return self.fc(h)

@@ -189,7 +189,7 @@ def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
     256-wide tile idle, the library keeps those)."""
     mod = _native(x)
     N, K = weight.shape
-    if mod is not None and N >= 128 and N % 8 == 0 and K % 64 == 0 and x.shape[-1] == K:
+    if mod is not None and x.dtype != torch.float32 and N >= 128 and N % 8 == 0 and K % 64 == 0 and x.shape[-1] == K:
         return _Linear16.apply(x.contiguous(), weight, bias)
     if _native_f32(x) is not None and x.shape[-1] == K and weight.dtype == torch.float32 and (
             (mod is not None and N < 128) or x.dtype == torch.float32):

@@ -34,7 +34,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-from .lstm_large import _interleave, _perm, _tile, final_hidden, stack_layers
+from .lstm_large import _tile, final_hidden, stack_layers
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
@@ -69,24 +69,39 @@ def _gru_shadows(weights, ndir: int, H: int, I: int, cdt, device):
     ent = cache.get(key)
     if ent is not None and ent[0] == ver:
         return ent[1]
-    perm = _perm(H, device)
-    wih, whh4, wih4, b4 = [], [], [], []
+    if ent is None:
+        # buffers allocated once: the zero blocks stay zero, a rebuild after an
+        # optimizer step only copies (and converts) the parameters into them --
+        # strided copies straight into the gate-interleaved / transposed
+        # layouts, no concatenation
+        z = dict(device=device, dtype=cdt)
+        out = ([torch.empty(3 * H, I, **z) for _ in range(ndir)], torch.zeros(ndir * 4 * H, I, **z),
+               [torch.zeros(4 * H, H, **z) for _ in range(ndir)], [torch.zeros(4 * H, H, **z) for _ in range(ndir)],
+               [torch.zeros(H, 4 * H, **z) for _ in range(ndir)],
+               torch.zeros(ndir * 4 * H, device=device, dtype=torch.float32))
+    else:
+        out = ent[1]
+    wih, wih4_all, whh4, whh_p, wt, b4_all = out
     with torch.no_grad():
         for d in range(ndir):
-            w_ih, w_hh, b_ih, b_hh = weights[4 * d:4 * d + 4]
-            w_ih16, w_hh16 = w_ih.detach().to(cdt), w_hh.detach().to(cdt)
-            wih.append(w_ih16.contiguous())
-            wih4.append(_interleave(torch.cat([w_ih16, w_ih16.new_zeros(H, I)]), H))
-            whh4.append(torch.cat([w_hh16[:2 * H], w_hh16.new_zeros(H, H), w_hh16[2 * H:]]))
-            b = torch.zeros(4 * H, device=device, dtype=torch.float32)
+            w_ih, w_hh, b_ih, b_hh = (w.detach() if w is not None else None for w in weights[4 * d:4 * d + 4])
+            wih[d].copy_(w_ih)
+            # projection stack [r | z | n_x | 0], gate-interleaved: row 4u + q
+            wih4_all[d * 4 * H:(d + 1) * 4 * H].view(H, 4, I)[:, :3].copy_(w_ih.view(3, H, I).transpose(0, 1))
+            # recurrent stack [r | z | 0 | n_h] (gate-blocked), its interleaved
+            # form and its transpose
+            whh4[d][:2 * H].copy_(w_hh[:2 * H])
+            whh4[d][3 * H:].copy_(w_hh[2 * H:])
+            whh_p[d].view(H, 4, H).copy_(whh4[d].view(4, H, H).transpose(0, 1))
+            wt[d].copy_(whh4[d].t())
+            # folded bias [b_ir + b_hr | b_iz + b_hz | b_in | b_hn], interleaved
+            b = b4_all[d * 4 * H:(d + 1) * 4 * H].view(H, 4)
+            b.zero_()
             if b_ih is not None:
-                b[:3 * H] += b_ih.detach().float()
+                b[:, :3].add_(b_ih.view(3, H).t())
             if b_hh is not None:
-                b[:2 * H] += b_hh.detach()[:2 * H].float()
-                b[3 * H:] += b_hh.detach()[2 * H:].float()
-            b4.append(b[perm])
-        out = (wih, torch.cat(wih4).contiguous(), whh4, [_interleave(w, H).contiguous() for w in whh4],
-               [w.t().contiguous() for w in whh4], torch.cat(b4))
+                b[:, :2].add_(b_hh[:2 * H].view(2, H).t())
+                b[:, 3].add_(b_hh[2 * H:])
     cache[key] = (ver, out)
     return out
 
@@ -102,7 +117,10 @@ class _LargeGRULayer(torch.autograd.Function):
         T, B, I = x.shape
         mod = _ext.native(x.device)
         wih, wih4_all, whh4, whh_p, wt, b4_all = _gru_shadows(weights, ndir, H, I, cdt, x.device)
-        xp = linear16(x.reshape(T * B, I), wih4_all, b4_all)  # in-tree MFMA GEMM (16-bit)
+        if cdt == torch.float32:  # fp32-product MFMA GEMM (kernels/gemm_f32.hip), fp32 bias in the epilogue
+            xp = gemm_f32(x.reshape(T * B, I), False, wih4_all, False, bias=b4_all)[0]
+        else:  # in-tree MFMA GEMM (16-bit)
+            xp = linear16(x.reshape(T * B, I), wih4_all, b4_all)
         xp = xp.view(T, B, ndir * 4 * H)
         h0c = h0.to(cdt).contiguous() if h0 is not None else None
         h0f = h0.float().contiguous() if h0 is not None else None

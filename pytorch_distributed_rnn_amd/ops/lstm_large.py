@@ -31,24 +31,6 @@ from torch import Tensor
 from .. import _ext
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
-_PERM_CACHE = {}
-
-
-def _perm(hidden: int, device) -> Tensor:
-    """perm[4u + q] = q*H + u: torch gate-blocked rows -> gate-interleaved rows."""
-    key = (hidden, str(device))
-    p = _PERM_CACHE.get(key)
-    if p is None:
-        p = torch.arange(4 * hidden, device=device).view(4, hidden).t().reshape(-1)
-        _PERM_CACHE[key] = p
-    return p
-
-
-def _interleave(w: Tensor, hidden: int) -> Tensor:
-    """Rows q*H+u (torch gate-blocked) -> rows 4u+q (gate-interleaved), one
-    transpose copy (cheaper than an index gather)."""
-    return w.reshape(4, hidden, -1).transpose(0, 1).reshape(4 * hidden, -1)
-
 
 def _tile() -> int:
     try:
@@ -129,16 +111,33 @@ def shadow(w: Tensor, kind: str, cdt: torch.dtype, hidden: int) -> Tensor:
         return ent[1]
     with torch.no_grad():
         src = w.detach()
-        if kind == "i":
-            t = _interleave(src.to(cdt), hidden).contiguous()
-        elif kind == "p":
-            t = src.to(cdt)
-        elif kind == "t":
-            t = src.t().to(cdt).contiguous()
+        if kind == "p" and src.dtype == cdt:
+            t = src  # the master itself
         else:
-            raise ValueError(kind)
+            # rebuilt into the previous buffer (one converting strided copy)
+            if ent is not None and ent[1] is not src:
+                t = ent[1]
+            else:
+                rows, cols = src.shape
+                t = torch.empty((cols, rows) if kind == "t" else (rows, cols), device=src.device, dtype=cdt)
+            if kind == "i":
+                _interleave_into(t, src, hidden)
+            elif kind == "p":
+                t.copy_(src)
+            elif kind == "t":
+                t.copy_(src.t())
+            else:
+                raise ValueError(kind)
     cache[key] = (ver, t)
     return t
+
+
+def _interleave_into(dst: Tensor, src: Tensor, hidden: int) -> Tensor:
+    """dst[4u + q] = src[q*H + u] (gate-blocked -> gate-interleaved rows), one
+    converting strided copy."""
+    k = src.shape[1]
+    dst.view(hidden, 4, k).copy_(src.view(4, hidden, k).transpose(0, 1))
+    return dst
 
 
 def _shadow_cat(ws: List[Tensor], cdt: torch.dtype, hidden: int) -> Tensor:
@@ -155,8 +154,11 @@ def _shadow_cat(ws: List[Tensor], cdt: torch.dtype, hidden: int) -> Tensor:
     ent = cache.get(key)
     if ent is not None and ent[0] == ver:
         return ent[1]
+    n4 = 4 * hidden
     with torch.no_grad():
-        t = torch.cat([_interleave(w.detach().to(cdt), hidden) for w in ws], 0)
+        t = ent[1] if ent is not None else torch.empty(len(ws) * n4, ws[0].shape[1], device=ws[0].device, dtype=cdt)
+        for d, w in enumerate(ws):
+            _interleave_into(t[d * n4:(d + 1) * n4], w.detach(), hidden)
     cache[key] = (ver, t)
     return t
 
@@ -176,16 +178,15 @@ def _bias_cat(weights, ndir: int, hidden: int, device) -> Tensor:
     ent = cache.get(key)
     if ent is not None and ent[0] == ver:
         return ent[1]
-    perm = _perm(hidden, device)
+    n4 = 4 * hidden
     with torch.no_grad():
-        out = []
+        t = ent[1] if ent is not None else torch.empty(ndir * n4, device=device, dtype=torch.float32)
         for d in range(ndir):
-            b = torch.zeros(4 * hidden, device=device, dtype=torch.float32)
-            for t in bs[2 * d:2 * d + 2]:
-                if t is not None:
-                    b += t.detach().float()
-            out.append(b[perm])
-        t = torch.cat(out, 0)
+            b = t[d * n4:(d + 1) * n4].view(hidden, 4)  # interleaved: [u][q] = row q*H + u
+            b.zero_()
+            for src in bs[2 * d:2 * d + 2]:
+                if src is not None:
+                    b.add_(src.detach().view(4, hidden).t())
     cache[key] = (ver, t)
     return t
 

@@ -23,6 +23,7 @@ def main(argv=None):
     ap.add_argument("--anchor", required=True)
     ap.add_argument("--skip", type=int, default=20)
     ap.add_argument("--last", type=int, default=0, help="window = the last N anchor intervals (overrides --skip)")
+    ap.add_argument("--first", type=int, default=0, help="window = N anchor intervals from the --skip-th anchor")
     ap.add_argument("--out")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
@@ -37,8 +38,9 @@ def main(argv=None):
         print(f"only {len(anchors)} anchor dispatches")
         return 1
     skip = len(anchors) - 1 - a.last if a.last else a.skip
-    lo, hi = anchors[skip], anchors[-1]
-    steps = len(anchors) - 1 - skip
+    end = min(skip + a.first, len(anchors) - 1) if a.first and not a.last else len(anchors) - 1
+    lo, hi = anchors[skip], anchors[end]
+    steps = end - skip
     win = [r for r in rows if lo <= r[1] < hi]
     agg = {}
     for name, _, dur in win:
