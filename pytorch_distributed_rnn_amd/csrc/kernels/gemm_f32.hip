@@ -25,7 +25,7 @@
 // a (128 / WAVES_M) x (BN / WAVES_N) block of 16 x 16 MFMA tiles.  Operands
 // are staged k-major in LDS ([k][m] / [k][n], rows padded by 16 floats: the 4
 // k-rows a fragment read touches land on 4 distinct 16-bank groups), double
-// buffered with the next tile's global loads in registers during the MFMAs.
+// buffered, with two k-tiles of global loads in registers ahead of the MFMAs.
 #include "pdrnn/api.h"
 #include "pdrnn/common.h"
 
@@ -102,9 +102,13 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
   const bool vec = p.vec != 0;
   const bool do_rs = p.rowsum != nullptr && tn == 0 && wn == 0;
 
-  float4 ra[Cfg::A_QUADS], rb[Cfg::B_QUADS];
+  // two register sets: k-tile t + 2 is loaded while t is multiplied and t + 1
+  // (loaded one iteration earlier) goes to LDS.  One tile of prefetch left the
+  // long-K weight-gradient products stalled on load latency: a k-tile of MFMA
+  // work (~2k cycles per wave) is shorter than a loaded HBM round trip
+  float4 ra[2][Cfg::A_QUADS], rb[2][Cfg::B_QUADS];
   // global -> registers: the quads of k-tile t (segment 1 or 2)
-  auto load = [&](int t) {
+  auto load = [&](int t, float4 (&xa)[Cfg::A_QUADS], float4 (&xb)[Cfg::B_QUADS]) {
     const bool s2 = t >= nt1;
     const void* A = s2 ? p.A2 : p.A;
     const void* B = s2 ? p.B2 : p.B;
@@ -114,28 +118,28 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
 #pragma unroll
     for (int j = 0; j < Cfg::A_QUADS; ++j) {
       const int q = tid + j * GF_THREADS;
-      if constexpr (AKM) ra[j] = quad<IN>(A, lda, k0 + q / (GF_BM / 4), m0 + (q % (GF_BM / 4)) * 4, K, p.M, vec);
-      else ra[j] = quad<IN>(A, lda, m0 + q / (GF_BK / 4), k0 + (q % (GF_BK / 4)) * 4, p.M, K, vec);
+      if constexpr (AKM) xa[j] = quad<IN>(A, lda, k0 + q / (GF_BM / 4), m0 + (q % (GF_BM / 4)) * 4, K, p.M, vec);
+      else xa[j] = quad<IN>(A, lda, m0 + q / (GF_BK / 4), k0 + (q % (GF_BK / 4)) * 4, p.M, K, vec);
     }
 #pragma unroll
     for (int j = 0; j < Cfg::B_QUADS; ++j) {
       const int q = tid + j * GF_THREADS;
       if (q < BN * GF_BK / 4) {
-        if constexpr (BKM) rb[j] = quad<IN>(B, ldb, k0 + q / (BN / 4), n0 + (q % (BN / 4)) * 4, K, p.N, vec);
-        else rb[j] = quad<IN>(B, ldb, n0 + q / (GF_BK / 4), k0 + (q % (GF_BK / 4)) * 4, p.N, K, vec);
+        if constexpr (BKM) xb[j] = quad<IN>(B, ldb, k0 + q / (BN / 4), n0 + (q % (BN / 4)) * 4, K, p.N, vec);
+        else xb[j] = quad<IN>(B, ldb, n0 + q / (GF_BK / 4), k0 + (q % (GF_BK / 4)) * 4, p.N, K, vec);
       }
     }
   };
   // registers -> LDS (k-major images)
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const float4 (&xa)[Cfg::A_QUADS], const float4 (&xb)[Cfg::B_QUADS]) {
 #pragma unroll
     for (int j = 0; j < Cfg::A_QUADS; ++j) {
       const int q = tid + j * GF_THREADS;
       if constexpr (AKM) {
-        *reinterpret_cast<float4*>(&As[buf][q / (GF_BM / 4)][(q % (GF_BM / 4)) * 4]) = ra[j];
+        *reinterpret_cast<float4*>(&As[buf][q / (GF_BM / 4)][(q % (GF_BM / 4)) * 4]) = xa[j];
       } else {
         const int m = q / (GF_BK / 4), k = (q % (GF_BK / 4)) * 4;
-        As[buf][k][m] = ra[j].x; As[buf][k + 1][m] = ra[j].y; As[buf][k + 2][m] = ra[j].z; As[buf][k + 3][m] = ra[j].w;
+        As[buf][k][m] = xa[j].x; As[buf][k + 1][m] = xa[j].y; As[buf][k + 2][m] = xa[j].z; As[buf][k + 3][m] = xa[j].w;
       }
     }
 #pragma unroll
@@ -143,10 +147,10 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
       const int q = tid + j * GF_THREADS;
       if (q < BN * GF_BK / 4) {
         if constexpr (BKM) {
-          *reinterpret_cast<float4*>(&Bs[buf][q / (BN / 4)][(q % (BN / 4)) * 4]) = rb[j];
+          *reinterpret_cast<float4*>(&Bs[buf][q / (BN / 4)][(q % (BN / 4)) * 4]) = xb[j];
         } else {
           const int n = q / (GF_BK / 4), k = (q % (GF_BK / 4)) * 4;
-          Bs[buf][k][n] = rb[j].x; Bs[buf][k + 1][n] = rb[j].y; Bs[buf][k + 2][n] = rb[j].z; Bs[buf][k + 3][n] = rb[j].w;
+          Bs[buf][k][n] = xb[j].x; Bs[buf][k + 1][n] = xb[j].y; Bs[buf][k + 2][n] = xb[j].z; Bs[buf][k + 3][n] = xb[j].w;
         }
       }
     }
@@ -163,15 +167,7 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
 
   const int fr = lane & 15, fk = lane >> 4;  // fragment row / column, k within a 4-step
   const int am = wm * Cfg::WM + fr, bn = wn * Cfg::WN + fr;
-  int buf = 0;
-  if (t_begin < t_end) {
-    load(t_begin);
-    store(0);
-  }
-  __syncthreads();
-  for (int t = t_begin; t < t_end; ++t) {
-    const bool more = t + 1 < t_end;
-    if (more) load(t + 1);  // in flight during the MFMAs below
+  auto compute = [&](int buf) {
     if constexpr (IN == 2) {
       // fp32: 4 k-steps of v_mfma_f32_16x16x4_f32 (lane: row fr, k = 4 ks + fk)
 #pragma unroll
@@ -232,10 +228,27 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
                                                               __builtin_bit_cast(h16x4, b[j]), acc[i][j], 0, 0, 0);
         }
     }
-    if (more) store(buf ^ 1);
+  };
+  // iteration t: load t + 2 into the set t came from, multiply t (LDS buf),
+  // store t + 1 (loaded one iteration ago) into the other LDS buffer
+  auto iter = [&](int t, int buf, float4 (&xa)[Cfg::A_QUADS], float4 (&xb)[Cfg::B_QUADS],
+                  const float4 (&na)[Cfg::A_QUADS], const float4 (&nb)[Cfg::B_QUADS]) {
+    if (t + 2 < t_end) load(t + 2, xa, xb);
+    compute(buf);
+    if (t + 1 < t_end) store(buf ^ 1, na, nb);
     __syncthreads();
-    buf ^= 1;
+  };
+  if (t_begin < t_end) {
+    load(t_begin, ra[0], rb[0]);
+    if (t_begin + 1 < t_end) load(t_begin + 1, ra[1], rb[1]);
+    store(0, ra[0], rb[0]);
   }
+  __syncthreads();
+  for (int t = t_begin; t < t_end; t += 2) {
+    iter(t, 0, ra[0], rb[0], ra[1], rb[1]);
+    if (t + 1 < t_end) iter(t + 1, 1, ra[1], rb[1], ra[0], rb[0]);
+  }
+
 
   // ---- epilogue: lane holds rows 4 fk + r, column fr of every 16 x 16 tile
   const bool partial = nsplit > 1;
@@ -301,7 +314,16 @@ __global__ void __launch_bounds__(256) splitk_sum_kernel(const float* __restrict
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float s = accumulate ? out[i] : 0.f;
     float acc = 0.f;
-    for (int k = 0; k < splitk; ++k) acc += part[(int64_t)k * n + i];
+    int k = 0;
+    // 8 partial rows in flight per thread, added in the same k order
+    for (; k + 8 <= splitk; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(int64_t)(k + j) * n + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += v[j];
+    }
+    for (; k < splitk; ++k) acc += part[(int64_t)k * n + i];
     out[i] = s + acc;
   }
 }

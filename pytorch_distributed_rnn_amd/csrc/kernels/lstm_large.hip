@@ -27,6 +27,8 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "pdrnn/api.h"
 #include "pdrnn/common.h"
 #include "pdrnn/gemm_pp.h"
@@ -1080,6 +1082,20 @@ __device__ __forceinline__ uint4 ps_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off_
 __device__ __forceinline__ void ps_st2(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes, uint16_t v) {
   __builtin_amdgcn_raw_buffer_store_b16(v, r, off_bytes, 0, PS_SC1);
 }
+__device__ __forceinline__ void ps_st(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes, uint16_t v) { ps_st2(r, off_bytes, v); }
+__device__ __forceinline__ void ps_st(__amdgpu_buffer_rsrc_t r, uint32_t off_bytes, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off_bytes, 0, PS_SC1);
+}
+// the 4 gate values of one (row, unit) pair in storage type S (8 or 16 bytes)
+template <class S>
+using Quad = typename std::conditional<sizeof(S) == 2, uint2, uint4>::type;
+template <class DT>
+__device__ __forceinline__ Quad<typename DT::S> pack4(float a, float b, float c, float d) {
+  Quad<typename DT::S> q;
+  typename DT::S* v = reinterpret_cast<typename DT::S*>(&q);
+  v[0] = DT::from_f(a); v[1] = DT::from_f(b); v[2] = DT::from_f(c); v[3] = DT::from_f(d);
+  return q;
+}
 
 // workgroup -> (direction, column block, batch block)
 __device__ __forceinline__ void ps_coords(int NCB, int NMB, int& dir, int& cb, int& mb) {
@@ -1128,14 +1144,14 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < CT; ++j)
-        wf[ks][j] = *reinterpret_cast<const uint4*>(w + (int64_t)(n0 + j * 16 + fr) * H + k0 + ks * 32 + fq * 8);
+        wf[ks][j] = *reinterpret_cast<const uint4*>(w + (int64_t)(n0 + j * 16 + fr) * H + k0 + ks * 4 * DT::EPC + fq * DT::EPC);
   }
   // this thread's (row, unit) pairs of the cell epilogue: 16 rows x 32 units
   const int eu = threadIdx.x & (PS_NU - 1), er = threadIdx.x / PS_NU;
   const int u = cb * PS_NU + eu;
   int brow[MT];
   float cst[MT];   // cell state (LSTM c / GRU h), fp32, register-resident
-  uint2 xpn[MT];   // next step's 4 gate pre-activations (16-bit x 4)
+  Quad<S> xpn[MT];  // next step's 4 gate pre-activations
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     brow[mt] = min(mb * 16 * MT + mt * 16 + er, B - 1);
@@ -1144,7 +1160,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
   auto load_xp = [&](int t) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
-      xpn[mt] = *reinterpret_cast<const uint2*>(static_cast<const S*>(d.xp) + (int64_t)t * d.xp_st +
+      xpn[mt] = *reinterpret_cast<const Quad<S>*>(static_cast<const S*>(d.xp) + (int64_t)t * d.xp_st +
                                                 (int64_t)brow[mt] * d.xp_sb + 4 * u);
   };
   load_xp(rev ? T - 1 : 0);
@@ -1153,7 +1169,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
     const int t = rev ? T - 1 - s : s;
     const int tp = rev ? t + 1 : t - 1;
     const bool first = s == 0;
-    uint2 xcur[MT];
+    Quad<S> xcur[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) xcur[mt] = xpn[mt];
     PS_STAMP(0)
@@ -1175,7 +1191,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
         const int row = min(mb * 16 * MT + mt * 16 + fr, B - 1);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
-          af[mt][ks] = ps_ld16(ra, (uint32_t)((row * lda + k0 + ks * 32 + fq * 8) * sizeof(S)));
+          af[mt][ks] = ps_ld16(ra, (uint32_t)((row * lda + k0 + ks * 4 * DT::EPC + fq * DT::EPC) * sizeof(S)));
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -1221,7 +1237,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
         cst[mt] = hv = fmaf(g[1], cst[mt] - g[2], g[2]);
       }
       const int b = mb * 16 * MT + mt * 16 + er;
-      if (b < B) ps_st2(rh, (uint32_t)((b * d.hseq_sb + u) * sizeof(S)), DT::from_f(hv));
+      if (b < B) ps_st(rh, (uint32_t)((b * d.hseq_sb + u) * sizeof(S)), DT::from_f(hv));
     }
     PS_STAMP(4)
     if (s + 1 < T) ps_arrive(cnt, sync.mode);
@@ -1234,9 +1250,8 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
       if (b >= B) continue;
       const int64_t bu = (int64_t)b * H + u;
       const float* g = gs[mt];
-      const uint32_t lo = (uint32_t)DT::from_f(g[0]) | ((uint32_t)DT::from_f(g[1]) << 16);
-      const uint32_t hi = (uint32_t)DT::from_f(g[2]) | ((uint32_t)DT::from_f(g[3]) << 16);
-      *reinterpret_cast<uint2*>(static_cast<S*>(d.acts) + (int64_t)t * B * 4 * H + 4 * bu) = make_uint2(lo, hi);
+      *reinterpret_cast<Quad<S>*>(static_cast<S*>(d.acts) + (int64_t)t * B * 4 * H + 4 * bu) =
+          pack4<DT>(g[0], g[1], g[2], g[3]);
       d.cseq[(int64_t)t * B * H + bu] = cst[mt];
     }
     PS_STAMP(6)
@@ -1278,7 +1293,8 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < CT; ++j)
-        wf[ks][j] = *reinterpret_cast<const uint4*>(wt + (int64_t)(n0 + j * 16 + fr) * 4 * H + k0 + ks * 32 + fq * 8);
+        wf[ks][j] = *reinterpret_cast<const uint4*>(wt + (int64_t)(n0 + j * 16 + fr) * 4 * H + k0 + ks * 4 * DT::EPC +
+                                                    fq * DT::EPC);
   }
   const int eu = threadIdx.x & (PS_NU - 1), er = threadIdx.x / PS_NU;
   const int u = cb * PS_NU + eu;
@@ -1286,7 +1302,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
   float carry[MT];
   // next cell-backward operands: dout, the 4 saved gates, c_tn, c_{tn-1}
   float nd[MT], ncur[MT], nsp[MT];
-  uint2 nact[MT];
+  Quad<S> nact[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     brow[mt] = min(mb * 16 * MT + mt * 16 + er, B - 1);
@@ -1301,7 +1317,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
       nd[mt] = d.dout ? DT::to_f(static_cast<const S*>(d.dout)[(int64_t)tn * d.dout_st +
                                                                 (int64_t)brow[mt] * d.dout_sb + u])
                       : 0.f;
-      nact[mt] = *reinterpret_cast<const uint2*>(static_cast<const S*>(d.acts) + ((int64_t)tn * B) * 4 * H + 4 * bu);
+      nact[mt] = *reinterpret_cast<const Quad<S>*>(static_cast<const S*>(d.acts) + ((int64_t)tn * B) * 4 * H + 4 * bu);
       ncur[mt] = CELL == 0 ? d.cseq[(int64_t)tn * B * H + bu] : 0.f;
       nsp[mt] = has_prev ? d.cseq[(int64_t)tpp * B * H + bu] : (d.c0 ? d.c0[bu] : 0.f);
     }
@@ -1316,7 +1332,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
     const int tn = rev ? t + 1 : t - 1;
     const bool cell = rev ? tn < T : tn >= 0;
     float od[MT], ocur[MT], osp[MT];
-    uint2 oact[MT];
+    Quad<S> oact[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) { od[mt] = nd[mt]; ocur[mt] = ncur[mt]; osp[mt] = nsp[mt]; oact[mt] = nact[mt]; }
     // dgates_t of the whole batch block: written by every column block (the
@@ -1339,7 +1355,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
           const int row = min(mb * 16 * MT + mt * 16 + fr, B - 1);
 #pragma unroll
           for (int k = 0; k < KC; ++k)
-            af[mt][k] = ps_ld16(ra, (uint32_t)((row * 4 * H + k0 + (kc + k) * 32 + fq * 8) * sizeof(S)));
+            af[mt][k] = ps_ld16(ra, (uint32_t)((row * 4 * H + k0 + (kc + k) * 4 * DT::EPC + fq * DT::EPC) * sizeof(S)));
         }
 #pragma unroll
         for (int k = 0; k < KC; ++k)
@@ -1395,10 +1411,10 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
       // gate-blocked dgates_tn (read by the batch block's other workgroups
       // at the next step: device-coherent stores)
       const uint32_t o = (uint32_t)(((int64_t)b * 4 * H + u) * sizeof(S));
-      ps_st2(rg, o, DT::from_f(g0));
-      ps_st2(rg, o + H * sizeof(S), DT::from_f(g1));
-      ps_st2(rg, o + 2 * H * sizeof(S), DT::from_f(g2));
-      ps_st2(rg, o + 3 * H * sizeof(S), DT::from_f(g3));
+      ps_st(rg, o, DT::from_f(g0));
+      ps_st(rg, o + H * sizeof(S), DT::from_f(g1));
+      ps_st(rg, o + 2 * H * sizeof(S), DT::from_f(g2));
+      ps_st(rg, o + 3 * H * sizeof(S), DT::from_f(g3));
     }
     if (s + 1 < T) {
       ps_arrive(cnt, sync.mode);
@@ -1408,29 +1424,42 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
   }
 }
 
-template <class DT, int CELL, int MT>
+template <class DT, int CELL, int MT, int KSF, int KSB>
 hipError_t persist_launch(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, PersistSync sy, hipStream_t st) {
+  // the K split: 8 waves x KS chunk steps x 4 lane groups x EPC elements
+  if (a->H != PS_WAVES * KSF * 4 * DT::EPC || 4 * a->H != PS_WAVES * KSB * 4 * DT::EPC) return hipErrorInvalidValue;
   const int NCB = a->H / PS_NU, NMB = (a->B + 16 * MT - 1) / (16 * MT);
   dim3 grid(NCB * NMB * ndir), block(PS_THREADS);
   PdrnnLstmLargeStepArgs args = *a;
   void* kargs[] = {&args, &sy};
   if (backward) {
     const size_t lds = (size_t)PS_WAVES * MT * 16 * (PS_NU + 4) * 4;
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_large_persist_bwd_kernel<DT, CELL, 16, MT>),
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_large_persist_bwd_kernel<DT, CELL, KSB, MT>),
                                       grid, block, kargs, (unsigned)lds, st);
   }
   const size_t lds = (size_t)PS_WAVES * MT * 16 * (4 * PS_NU + 4) * 4;
-  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_large_persist_fwd_kernel<DT, CELL, 4, MT>),
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_large_persist_fwd_kernel<DT, CELL, KSF, MT>),
                                     grid, block, kargs, (unsigned)lds, st);
 }
 
-// H = 1024 only: forward K-steps per wave H/256 = 4, backward 4H/256 = 16
-// (32 B fragments per wave either way = 128 VGPRs).
+// 16-bit storage: H = 1024 (forward K-steps per wave H/256 = 4, backward
+// 4H/256 = 16: 32 fragments of 16 B per wave either way = 128 VGPRs).
+// fp32 storage: H = 128 (1 / 4 chunk steps of 16 k: 8 fragments) or H = 256
+// (2 / 8) -- the fp32 models' hidden sizes, whose per-step kernels were
+// latency-bound at 7-9 us a step.
 template <class DT, int CELL>
 hipError_t persist_dispatch(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, int mt, PersistSync sy,
                             hipStream_t st) {
-  return mt == 1 ? persist_launch<DT, CELL, 1>(a, ndir, backward, sy, st)
-                 : persist_launch<DT, CELL, 2>(a, ndir, backward, sy, st);
+  if constexpr (DT::EPC == 8) {
+    return mt == 1 ? persist_launch<DT, CELL, 1, 4, 16>(a, ndir, backward, sy, st)
+                   : persist_launch<DT, CELL, 2, 4, 16>(a, ndir, backward, sy, st);
+  } else {
+    if (a->H == 128)
+      return mt == 1 ? persist_launch<DT, CELL, 1, 1, 4>(a, ndir, backward, sy, st)
+                     : persist_launch<DT, CELL, 2, 1, 4>(a, ndir, backward, sy, st);
+    return mt == 1 ? persist_launch<DT, CELL, 1, 2, 8>(a, ndir, backward, sy, st)
+                   : persist_launch<DT, CELL, 2, 2, 8>(a, ndir, backward, sy, st);
+  }
 }
 
 }  // namespace
@@ -1486,10 +1515,10 @@ hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int 
 
 // Persistent recurrence (see above): batch rows per workgroup / 16 (1 or 2)
 // for a grid that fits one workgroup per CU, or 0 when the shape is not
-// covered (16-bit storage, H = 1024, grid <= cus).
+// covered (16-bit storage with H = 1024, fp32 with H = 128 / 256; grid <= cus).
 int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus) {
-  if (dtype != 0 && dtype != 1) return 0;
-  if (H != 1024 || ndir < 1 || ndir > 2) return 0;
+  if (dtype < 0 || dtype > 2) return 0;
+  if ((dtype == 2 ? (H != 128 && H != 256) : H != 1024) || ndir < 1 || ndir > 2) return 0;
   for (int mt = 1; mt <= 2; ++mt) {
     const int64_t grid = (int64_t)(H / pdrnn::PS_NU) * ((B + 16 * mt - 1) / (16 * mt)) * ndir;
     if (grid <= cus) return mt;
@@ -1499,13 +1528,17 @@ int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus) {
 
 hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int mt,
                                     int* counters, int* err, int* sticky, int mode, hipStream_t stream) {
-  if (a->H != 1024 || (mt != 1 && mt != 2) || (dtype != 0 && dtype != 1)) return hipErrorInvalidValue;
+  if ((mt != 1 && mt != 2) || dtype < 0 || dtype > 2) return hipErrorInvalidValue;
+  if (dtype == 2 ? (a->H != 128 && a->H != 256) : a->H != 1024) return hipErrorInvalidValue;
   if (a->cell != 0 && a->cell != 1) return hipErrorInvalidValue;
   const pdrnn::PersistSync sy{counters, err, sticky, mode, reinterpret_cast<long long*>((reinterpret_cast<uintptr_t>(err + 1) + 7) & ~(uintptr_t)7)};
   const bool bw = backward != 0;
   if (dtype == 0)
     return a->cell ? pdrnn::persist_dispatch<pdrnn::BF16, 1>(a, ndir, bw, mt, sy, stream)
                    : pdrnn::persist_dispatch<pdrnn::BF16, 0>(a, ndir, bw, mt, sy, stream);
+  if (dtype == 2)
+    return a->cell ? pdrnn::persist_dispatch<pdrnn::F32, 1>(a, ndir, bw, mt, sy, stream)
+                   : pdrnn::persist_dispatch<pdrnn::F32, 0>(a, ndir, bw, mt, sy, stream);
   return a->cell ? pdrnn::persist_dispatch<pdrnn::F16, 1>(a, ndir, bw, mt, sy, stream)
                  : pdrnn::persist_dispatch<pdrnn::F16, 0>(a, ndir, bw, mt, sy, stream);
 }

@@ -53,6 +53,41 @@ def test_persistent_matches_per_step(cell, B, T, ndir, rev, dt):
         assert _rel(a, b) < 1e-2, (name, _rel(a, b))
 
 
+@pytest.mark.parametrize("cell", [0, 1])
+@pytest.mark.parametrize("Hs,B,T,ndir,rev", [(128, 1440, 6, 1, 0),  # motion --hidden-units 128 batch: 2 x 16 rows
+                                             (128, 200, 5, 1, 0),
+                                             (128, 40, 6, 2, 2),
+                                             (256, 7, 4, 1, 1),
+                                             (256, 300, 3, 2, 0)])
+def test_persistent_fp32_matches_per_step(cell, Hs, B, T, ndir, rev):
+    """fp32 storage (the reference's precision at --hidden-units 128 / 256):
+    the persistent recurrence on v_mfma_f32_16x16x4_f32 equals the per-step
+    kernels up to fp32 summation order."""
+    mod = _ext.require()
+    assert mod.lstm_large_persist_mt(B, Hs, ndir, 2) > 0
+    torch.manual_seed(B + T + cell + Hs)
+    dev = "cuda"
+    xp = torch.randn(T, B, ndir * 4 * Hs, device=dev) * 0.5
+    w = [torch.randn(4 * Hs, Hs, device=dev) * 0.06 for _ in range(ndir)]
+    wt = [torch.randn(Hs, 4 * Hs, device=dev) * 0.06 for _ in range(ndir)]
+    h0 = torch.randn(ndir, B, Hs, device=dev) * 0.5
+    c0 = torch.randn(ndir, B, Hs, device=dev) * 0.5
+    dout = torch.randn(T, B, ndir * Hs, device=dev) * 0.1
+    dhn = torch.randn(ndir, B, Hs, device=dev) * 0.1
+    dcn = torch.randn(ndir, B, Hs, device=dev) * 0.1
+
+    def run(tile):
+        hseq, cseq, acts = mod.lstm_large_fwd(xp, w, h0, c0, Hs, rev, tile, cell)
+        dg, dh0, dc0 = mod.lstm_large_bwd(dout, dhn, dcn, wt, cseq, acts, c0, Hs, rev, tile, cell)
+        return hseq, cseq, acts, dg, dh0, dc0
+    got, ref = run(-1), run(0)
+    torch.cuda.synchronize()
+    names = ["hseq", "cseq", "acts", "dgates", "dh0", "dc0"][:6 if cell == 0 else 5]
+    for name, a, b in zip(names, got, ref):
+        assert torch.isfinite(a).all(), name
+        assert _rel(a, b) < 1e-5, (name, _rel(a, b))
+
+
 def test_persistent_charlm_layer_matches_torch():
     """nn.LSTM(64 -> 1024) at the char-LM batch on the persistent path vs fp32 torch."""
     torch.manual_seed(5)

@@ -24,6 +24,8 @@ def main(argv=None):
     ap.add_argument("--skip", type=int, default=20)
     ap.add_argument("--last", type=int, default=0, help="window = the last N anchor intervals (overrides --skip)")
     ap.add_argument("--first", type=int, default=0, help="window = N anchor intervals from the --skip-th anchor")
+    ap.add_argument("--end-skip", type=int, default=0,
+                    help="with --first: the window ENDS this many anchors before the last one")
     ap.add_argument("--out")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
@@ -39,6 +41,9 @@ def main(argv=None):
         return 1
     skip = len(anchors) - 1 - a.last if a.last else a.skip
     end = min(skip + a.first, len(anchors) - 1) if a.first and not a.last else len(anchors) - 1
+    if a.first and a.end_skip:
+        end = len(anchors) - 1 - a.end_skip
+        skip = max(end - a.first, 0)
     lo, hi = anchors[skip], anchors[end]
     steps = end - skip
     win = [r for r in rows if lo <= r[1] < hi]
