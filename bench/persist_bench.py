@@ -1,8 +1,10 @@
-"""Large-H recurrence, one layer at the char-LM shape: persistent cooperative
-kernel (tile -1) vs the per-step MFMA kernels (tile 0 / auto split-K), forward
-and BPTT timed separately with HIP events.
+"""Large-H recurrence, one layer: persistent cooperative kernel (tile -1) vs
+the per-step MFMA kernels (tile 0 / auto split-K), forward and BPTT timed
+separately with HIP events.  Defaults: the char-LM layer (bf16, H 1024, B 128,
+T 512); ``--hidden 128 --dtype fp32 --batch 1440 --seq 128`` is the motion
+model's fp32 ``--hidden-units 128`` layer.
 
-    python bench/persist_bench.py [--batch 128] [--seq 512] [--reps 5]
+    python bench/persist_bench.py [--batch 128] [--seq 512] [--hidden 1024] [--dtype bf16] [--reps 5]
 """
 import argparse
 import json
@@ -20,10 +22,14 @@ def main():
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cell", type=int, default=0)
+    ap.add_argument("--hidden", type=int, default=1024)
+    ap.add_argument("--dtype", choices=("bf16", "fp16", "fp32"), default="bf16")
     a = ap.parse_args()
     from pytorch_distributed_rnn_amd import _ext
     mod = _ext.require()
-    H, B, T, dt = 1024, a.batch, a.seq, torch.bfloat16
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
+    code = {"bf16": 0, "fp16": 1, "fp32": 2}[a.dtype]
+    H, B, T = a.hidden, a.batch, a.seq
     torch.manual_seed(0)
     xp = (torch.randn(T, B, 4 * H, device="cuda") * 0.5).to(dt)
     w = [(torch.randn(4 * H, H, device="cuda") * 0.03).to(dt)]
@@ -43,7 +49,8 @@ def main():
             best = min(best, ev[0].elapsed_time(ev[1]))
         return best
 
-    res = {"B": B, "T": T, "H": H, "persist_mt": mod.lstm_large_persist_mt(B, H, 1, 0)}
+    res = {"B": B, "T": T, "H": H, "dtype": a.dtype, "cell": a.cell,
+           "persist_mt": mod.lstm_large_persist_mt(B, H, 1, code)}
     # tile -1: persistent when covered (PDRNN_LSTM_PERSIST=0 -> auto per-step
     # tile); tile 0: per-step 32x64 forward tiles, split-K backward
     for name, t in (("auto", -1), ("per_step_tile0", 0)):

@@ -726,7 +726,7 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 
 
 // ---------------------------------------------------------------------------
-// Persistent recurrence (one cooperative launch per layer direction set,
+// Persistent recurrence (one launch per layer direction set,
 // W_hh register-resident; lstm_large.hip) when the shape is covered and
 // PDRNN_LSTM_PERSIST != 0.  A grid-sync spin that times out (bounded at 2 s
 // in the kernel: co-residency lost, e.g. to RCCL kernels on the comm stream)
@@ -822,7 +822,7 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
   const hipError_t e = pdrnn_lstm_large_persist(&a, ndir, backward ? 1 : 0, dt, mt, cnt, cnt + ndir * nmb,
                                                 sticky[dev].data_ptr<int>(), m, st);
   if (e != hipSuccess) {
-    (void)hipGetLastError();  // e.g. cooperative grid too large: per-step path
+    (void)hipGetLastError();  // e.g. grid cannot be co-resident: per-step path
     return kPersistNotRun;
   }
   if (persist_verify_on()) {

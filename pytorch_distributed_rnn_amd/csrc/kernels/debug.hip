@@ -18,7 +18,7 @@ __global__ void __launch_bounds__(64) debug_spin_kernel(uint64_t ticks) {
 
 // pdrnn_debug_spin_cus: a grid of workgroups (threads, dynamic LDS as
 // given) that spin for a bounded time each -- fills the CUs so that a
-// cooperative launch issued meanwhile on another stream cannot become
+// persistent launch issued meanwhile on another stream cannot become
 // co-resident (test of the persistent recurrence's timeout recovery).
 __global__ void __launch_bounds__(1024) debug_spin_cus_kernel(uint64_t ticks) {
   extern __shared__ float hold[];  // occupancy only

@@ -229,26 +229,46 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
         }
     }
   };
-  // iteration t: load t + 2 into the set t came from, multiply t (LDS buf),
-  // store t + 1 (loaded one iteration ago) into the other LDS buffer
-  auto iter = [&](int t, int buf, float4 (&xa)[Cfg::A_QUADS], float4 (&xb)[Cfg::B_QUADS],
-                  const float4 (&na)[Cfg::A_QUADS], const float4 (&nb)[Cfg::B_QUADS]) {
-    if (t + 2 < t_end) load(t + 2, xa, xb);
-    compute(buf);
-    if (t + 1 < t_end) store(buf ^ 1, na, nb);
+  // Depth 2 (fp32 inputs), iteration t: load t + 2 into the set t came
+  // from, multiply t (LDS buf), store t + 1 (loaded one iteration ago) into
+  // the other LDS buffer.  Depth 1 (16-bit inputs: two sets were no faster
+  // and the bi-LSTM head's dX slower, profiles/r4/h1/): load t + 1 at the
+  // start of iteration t, store it at the end.
+  constexpr int DEPTH = IN == 2 ? 2 : 1;
+  if constexpr (DEPTH == 1) {
+    int buf = 0;
+    if (t_begin < t_end) {
+      load(t_begin, ra[0], rb[0]);
+      store(0, ra[0], rb[0]);
+    }
     __syncthreads();
-  };
-  if (t_begin < t_end) {
-    load(t_begin, ra[0], rb[0]);
-    if (t_begin + 1 < t_end) load(t_begin + 1, ra[1], rb[1]);
-    store(0, ra[0], rb[0]);
+    for (int t = t_begin; t < t_end; ++t) {
+      const bool more = t + 1 < t_end;
+      if (more) load(t + 1, ra[0], rb[0]);  // in flight during the MFMAs below
+      compute(buf);
+      if (more) store(buf ^ 1, ra[0], rb[0]);
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    auto iter = [&](int t, int buf, float4 (&xa)[Cfg::A_QUADS], float4 (&xb)[Cfg::B_QUADS],
+                    const float4 (&na)[Cfg::A_QUADS], const float4 (&nb)[Cfg::B_QUADS]) {
+      if (t + 2 < t_end) load(t + 2, xa, xb);
+      compute(buf);
+      if (t + 1 < t_end) store(buf ^ 1, na, nb);
+      __syncthreads();
+    };
+    if (t_begin < t_end) {
+      load(t_begin, ra[0], rb[0]);
+      if (t_begin + 1 < t_end) load(t_begin + 1, ra[1], rb[1]);
+      store(0, ra[0], rb[0]);
+    }
+    __syncthreads();
+    for (int t = t_begin; t < t_end; t += 2) {
+      iter(t, 0, ra[0], rb[0], ra[1], rb[1]);
+      if (t + 1 < t_end) iter(t + 1, 1, ra[1], rb[1], ra[0], rb[0]);
+    }
   }
-  __syncthreads();
-  for (int t = t_begin; t < t_end; t += 2) {
-    iter(t, 0, ra[0], rb[0], ra[1], rb[1]);
-    if (t + 1 < t_end) iter(t + 1, 1, ra[1], rb[1], ra[0], rb[0]);
-  }
-
 
   // ---- epilogue: lane holds rows 4 fk + r, column fr of every 16 x 16 tile
   const bool partial = nsplit > 1;

@@ -995,7 +995,7 @@ hipError_t gemm_nt_dispatch(const void* Av, int64_t lda, const void* Btv, int64_
 
 
 // ---------------------------------------------------------------------------
-// Persistent recurrence (one cooperative launch for all T steps of a layer).
+// Persistent recurrence (one launch for all T steps of a layer).
 //
 // The per-step kernels above re-stream W_hh (8 MB at H = 1024 bf16) from
 // L2 / MALL every timestep and pay a launch per step; at small batch (char-LM
@@ -1024,8 +1024,8 @@ hipError_t gemm_nt_dispatch(const void* Av, int64_t lda, const void* Btv, int64_
 //   * blockIdx -> (column block, batch block) puts the batch block in the
 //     low bits: workgroups are dispatched round-robin over the 8 XCDs, so the
 //     workgroups of one XCD read the same A rows out of their shared L2.
-// Launched cooperatively (the runtime refuses a grid that cannot be
-// co-resident); the host falls back to the per-step kernels otherwise.
+// The grid must be co-resident (checked against the kernel's occupancy,
+// persist_go below); the host falls back to the per-step kernels otherwise.
 // ---------------------------------------------------------------------------
 constexpr int PS_NU = 32;       // hidden units per workgroup
 constexpr int PS_WAVES = 8;
@@ -1424,22 +1424,45 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
   }
 }
 
+// Every workgroup of a batch block must be resident at once (they wait for
+// each other every step).  The grid is checked against the kernel's occupancy
+// on an idle device and launched as an ordinary dispatch: cooperative
+// launches gave the same placement, and under rocprofv3 their processes
+// segfaulted at exit (char-LM and fp32 --hidden 128 runs, round 4).  Residency
+// lost to other work at run time (RCCL kernels beside it) ends in the bounded
+// spin and the host's fallback, as before.
+template <class K>
+hipError_t persist_go(K kernel, dim3 grid, size_t lds, hipStream_t st, const PdrnnLstmLargeStepArgs& args,
+                      const PersistSync& sy, int* occ_cache) {
+  if (*occ_cache < 0) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kernel), PS_THREADS, lds) !=
+        hipSuccess)
+      occ = 0;
+    *occ_cache = occ;
+  }
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return hipErrorInvalidDevice;
+  if ((int64_t)*occ_cache * cus < (int64_t)grid.x) return hipErrorCooperativeLaunchTooLarge;
+  hipLaunchKernelGGL(kernel, grid, dim3(PS_THREADS), lds, st, args, sy);
+  return hipGetLastError();
+}
+
 template <class DT, int CELL, int MT, int KSF, int KSB>
 hipError_t persist_launch(const PdrnnLstmLargeStepArgs* a, int ndir, bool backward, PersistSync sy, hipStream_t st) {
   // the K split: 8 waves x KS chunk steps x 4 lane groups x EPC elements
   if (a->H != PS_WAVES * KSF * 4 * DT::EPC || 4 * a->H != PS_WAVES * KSB * 4 * DT::EPC) return hipErrorInvalidValue;
   const int NCB = a->H / PS_NU, NMB = (a->B + 16 * MT - 1) / (16 * MT);
-  dim3 grid(NCB * NMB * ndir), block(PS_THREADS);
-  PdrnnLstmLargeStepArgs args = *a;
-  void* kargs[] = {&args, &sy};
+  const dim3 grid(NCB * NMB * ndir);
+  static int occ_bwd = -1, occ_fwd = -1;
   if (backward) {
     const size_t lds = (size_t)PS_WAVES * MT * 16 * (PS_NU + 4) * 4;
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_large_persist_bwd_kernel<DT, CELL, KSB, MT>),
-                                      grid, block, kargs, (unsigned)lds, st);
+    return persist_go(lstm_large_persist_bwd_kernel<DT, CELL, KSB, MT>, grid, lds, st, *a, sy, &occ_bwd);
   }
   const size_t lds = (size_t)PS_WAVES * MT * 16 * (4 * PS_NU + 4) * 4;
-  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_large_persist_fwd_kernel<DT, CELL, KSF, MT>),
-                                    grid, block, kargs, (unsigned)lds, st);
+  return persist_go(lstm_large_persist_fwd_kernel<DT, CELL, KSF, MT>, grid, lds, st, *a, sy, &occ_fwd);
 }
 
 // 16-bit storage: H = 1024 (forward K-steps per wave H/256 = 4, backward

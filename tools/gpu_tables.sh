@@ -16,6 +16,6 @@ run_prof() {  # name, command...
 run_prof bilstm python3 $GRAFT_REPO_ROOT/bench/lm_bench.py --config bilstm --steps 2 --warmup 1
 run_prof motion_h128 python3 $GRAFT_REPO_ROOT/bench.py --hidden 128 --steps 10 --warmup 5
 run_prof gru_h128 python3 $GRAFT_REPO_ROOT/bench.py --hidden 128 --cell gru --steps 10 --warmup 5
-# (the char-LM run is not profiled here: under rocprofv3 its process has
-# segfaulted at exit, after the database was written, in rounds 4 rd2/rd4 --
-# its r3 table is profiles/r3_gemm/charlm_kernel_stats.md)
+# last: the char-LM run (its process segfaulted at exit under rocprofv3 while
+# the persistent recurrence used cooperative launches, rounds 4 rd2/rd4)
+run_prof charlm python3 $GRAFT_REPO_ROOT/bench/lm_bench.py --config charlm --steps 4 --warmup 2
