@@ -672,6 +672,21 @@ void adam_flat(Tensor param, const Tensor& grad, Tensor exp_avg, Tensor exp_avg_
   HIP_LAUNCH_CHECK(pdrnn_adam_flat(&a, cur_stream()));
 }
 
+// Gradient-norm clipping of a flat fp32 gradient in place; returns the
+// device tensor [scale, norm] (no host sync).
+Tensor clip_flat(Tensor g, double max_norm, double eps) {
+  CHECK_HIP_TENSOR(g); CHECK_F32(g);
+  TORCH_CHECK(g.is_contiguous(), "clip_flat: contiguous gradient expected");
+  const c10::DeviceGuard guard(g.device());
+  const int64_t n = g.numel();
+  int64_t nparts = (n + 256 * 16 - 1) / (256 * 16);
+  nparts = std::max<int64_t>(1, std::min<int64_t>(nparts, 1024));
+  Tensor work = at::empty({nparts + 2}, g.options());
+  HIP_LAUNCH_CHECK(pdrnn_clip_flat(g.data_ptr<float>(), n, (float)max_norm, (float)eps, work.data_ptr<float>(),
+                                   (int)nparts, work.data_ptr<float>() + nparts, cur_stream()));
+  return work.narrow(0, nparts, 2);
+}
+
 Tensor embedding_fwd(const Tensor& weight, const Tensor& idx, optional<at::ScalarType> out_dtype) {
   CHECK_HIP_TENSOR(weight); CHECK_F32(weight);
   TORCH_CHECK(weight.is_contiguous() && weight.dim() == 2);
@@ -792,6 +807,16 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
   }();
   const int mode = 0;  // kernel mode bits: 16 = test hook (persist_inject_timeouts)
   if (env == 0 || tile >= 0 || g_persist_disabled.load()) return kPersistNotRun;
+  // fp32 storage: the persistent backward only -- the persistent forward ran
+  // 8.3 us per step against 7.1 for the per-step kernels at the fp32 motion
+  // model's H = 128, B = 1440 (its K = H is too short to pay for the 8-wave
+  // K split's LDS reduction; the backward's K = 4H is not: 8.6 vs 11.7 us;
+  // profiles/r4/h2/h2_persist_f32_cell*.json)
+  static const bool f32_fwd = [] {
+    const char* e = std::getenv("PDRNN_LSTM_PERSIST_F32_FWD");  // A/B: the fp32 persistent forward
+    return e && std::atoi(e) != 0;
+  }();
+  if (dt == 2 && !backward && !f32_fwd) return kPersistNotRun;
   int dev = 0;
   TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
   int cus = 0;
@@ -1301,6 +1326,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "0 off; 1 synchronise after every persistent-recurrence launch and re-run a timed-out layer on the "
         "per-step kernels; 2 per step: persist_step_check() before the optimizer update re-runs the step");
   m.def("persist_verify_mode", []() { return persist_verify_mode(); });
+  m.def("clip_flat", &clip_flat, "in-place gradient-norm clipping of a flat fp32 gradient -> [scale, norm]",
+        py::arg("g"), py::arg("max_norm"), py::arg("eps") = 1e-6);
   m.def("persist_sticky_flag", &persist_sticky_flag,
         "the current device's sticky persistent-timeout flag (device int32 [1])");
   m.def("persist_step_check", &persist_step_check,

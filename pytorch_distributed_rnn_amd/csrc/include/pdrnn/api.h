@@ -227,6 +227,10 @@ typedef struct {
   const int* skip;
 } PdrnnAdamArgs;
 hipError_t pdrnn_adam_flat(const PdrnnAdamArgs* a, hipStream_t stream);
+// g *= min(1, max_norm / (||g|| + eps)) with no host sync; work: [nparts]
+// floats (nparts <= 1024 partial sums of squares), out: [2] = (scale, norm).
+hipError_t pdrnn_clip_flat(float* g, int64_t n, float max_norm, float eps, float* work, int nparts, float* out,
+                           hipStream_t stream);
 
 // ----------------------------------------------------------------------------
 // Embedding gather / deterministic CSR backward (perm = stable argsort of idx,

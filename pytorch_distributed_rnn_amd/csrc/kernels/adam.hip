@@ -217,6 +217,49 @@ __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
   }
 }
 
+// Gradient-norm clipping of a flat fp32 gradient, deterministic and without
+// a host sync: pass 1 -- per-workgroup sums of squares (each thread a fixed
+// strided set, then a fixed LDS tree); pass 2 -- one workgroup sums the
+// partials in order and writes scale = min(1, max_norm / (norm + eps)) (and
+// the norm); pass 3 -- g *= scale.  The reference's trainers do not clip; the
+// LM trainer does (train/lm.py).
+__global__ void __launch_bounds__(256) sumsq_partial_kernel(const float* __restrict__ g, int64_t n,
+                                                            float* __restrict__ part) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) acc = fmaf(g[i], g[i], acc);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) clip_finalize_kernel(const float* __restrict__ part, int nparts, float max_norm,
+                                                            float eps, float* __restrict__ out) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(red[0]);
+    out[0] = fminf(max_norm / (norm + eps), 1.f);
+    out[1] = norm;
+  }
+}
+
+__global__ void __launch_bounds__(256) scale_flat_kernel(float* __restrict__ g, int64_t n, const float* __restrict__ scale) {
+  const float s = scale[0];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) g[i] *= s;
+}
+
 }  // namespace
 }  // namespace pdrnn
 
@@ -247,6 +290,20 @@ extern "C" hipError_t pdrnn_adam_partials(const PdrnnAdamArgs* a, const float* w
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(pdrnn::adam_partials_kernel, dim3((unsigned)blocks), dim3(64), 0, stream, *a, work, split,
                      P_total, grad_out, stats_out, n_stats);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pdrnn_clip_flat(float* g, int64_t n, float max_norm, float eps, float* work, int nparts,
+                                      float* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (nparts < 1 || nparts > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pdrnn::sumsq_partial_kernel, dim3((unsigned)nparts), dim3(256), 0, stream, g, n, work);
+  PDRNN_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(pdrnn::clip_finalize_kernel, dim3(1), dim3(256), 0, stream, work, nparts, max_norm, eps, out);
+  PDRNN_HIP_CHECK(hipGetLastError());
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pdrnn::scale_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, g, n, out);
   return hipGetLastError();
 }
 

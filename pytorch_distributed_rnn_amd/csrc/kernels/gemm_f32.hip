@@ -25,7 +25,7 @@
 // a (128 / WAVES_M) x (BN / WAVES_N) block of 16 x 16 MFMA tiles.  Operands
 // are staged k-major in LDS ([k][m] / [k][n], rows padded by 16 floats: the 4
 // k-rows a fragment read touches land on 4 distinct 16-bank groups), double
-// buffered, with two k-tiles of global loads in registers ahead of the MFMAs.
+// buffered with the next tile's global loads in registers during the MFMAs.
 #include "pdrnn/api.h"
 #include "pdrnn/common.h"
 
@@ -102,11 +102,7 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
   const bool vec = p.vec != 0;
   const bool do_rs = p.rowsum != nullptr && tn == 0 && wn == 0;
 
-  // two register sets: k-tile t + 2 is loaded while t is multiplied and t + 1
-  // (loaded one iteration earlier) goes to LDS.  One tile of prefetch left the
-  // long-K weight-gradient products stalled on load latency: a k-tile of MFMA
-  // work (~2k cycles per wave) is shorter than a loaded HBM round trip
-  float4 ra[2][Cfg::A_QUADS], rb[2][Cfg::B_QUADS];
+  float4 ra[Cfg::A_QUADS], rb[Cfg::B_QUADS];
   // global -> registers: the quads of k-tile t (segment 1 or 2)
   auto load = [&](int t, float4 (&xa)[Cfg::A_QUADS], float4 (&xb)[Cfg::B_QUADS]) {
     const bool s2 = t >= nt1;
@@ -229,45 +225,22 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
         }
     }
   };
-  // Depth 2 (fp32 inputs), iteration t: load t + 2 into the set t came
-  // from, multiply t (LDS buf), store t + 1 (loaded one iteration ago) into
-  // the other LDS buffer.  Depth 1 (16-bit inputs: two sets were no faster
-  // and the bi-LSTM head's dX slower, profiles/r4/h1/): load t + 1 at the
-  // start of iteration t, store it at the end.
-  constexpr int DEPTH = IN == 2 ? 2 : 1;
-  if constexpr (DEPTH == 1) {
-    int buf = 0;
-    if (t_begin < t_end) {
-      load(t_begin, ra[0], rb[0]);
-      store(0, ra[0], rb[0]);
-    }
+  // one k-tile of loads in flight during the MFMAs of the current one (two
+  // register sets for fp32 inputs measured no faster and the dX / Xp shapes
+  // slower: profiles/r4/h2/h2tb_motion_h128_kernel_stats.md vs rd5)
+  int buf = 0;
+  if (t_begin < t_end) {
+    load(t_begin, ra, rb);
+    store(0, ra, rb);
+  }
+  __syncthreads();
+  for (int t = t_begin; t < t_end; ++t) {
+    const bool more = t + 1 < t_end;
+    if (more) load(t + 1, ra, rb);  // in flight during the MFMAs below
+    compute(buf);
+    if (more) store(buf ^ 1, ra, rb);
     __syncthreads();
-    for (int t = t_begin; t < t_end; ++t) {
-      const bool more = t + 1 < t_end;
-      if (more) load(t + 1, ra[0], rb[0]);  // in flight during the MFMAs below
-      compute(buf);
-      if (more) store(buf ^ 1, ra[0], rb[0]);
-      __syncthreads();
-      buf ^= 1;
-    }
-  } else {
-    auto iter = [&](int t, int buf, float4 (&xa)[Cfg::A_QUADS], float4 (&xb)[Cfg::B_QUADS],
-                    const float4 (&na)[Cfg::A_QUADS], const float4 (&nb)[Cfg::B_QUADS]) {
-      if (t + 2 < t_end) load(t + 2, xa, xb);
-      compute(buf);
-      if (t + 1 < t_end) store(buf ^ 1, na, nb);
-      __syncthreads();
-    };
-    if (t_begin < t_end) {
-      load(t_begin, ra[0], rb[0]);
-      if (t_begin + 1 < t_end) load(t_begin + 1, ra[1], rb[1]);
-      store(0, ra[0], rb[0]);
-    }
-    __syncthreads();
-    for (int t = t_begin; t < t_end; t += 2) {
-      iter(t, 0, ra[0], rb[0], ra[1], rb[1]);
-      if (t + 1 < t_end) iter(t + 1, 1, ra[1], rb[1], ra[0], rb[0]);
-    }
+    buf ^= 1;
   }
 
   // ---- epilogue: lane holds rows 4 fk + r, column fr of every 16 x 16 tile

@@ -67,6 +67,10 @@ class LMTrainer:
     def _clip(self) -> None:
         if self.grad_clip and self.grad_clip > 0:
             g = self.flat.grad
+            mod = _ext.extension() if g.is_cuda else None
+            if mod is not None and hasattr(mod, "clip_flat") and g.dtype == torch.float32 and g.is_contiguous():
+                mod.clip_flat(g, float(self.grad_clip), 1e-6)  # deterministic, no host sync (kernels/adam.hip)
+                return
             norm = torch.linalg.vector_norm(g)
             g.mul_(torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0))
 

@@ -174,6 +174,28 @@ def test_adam_flat_skip_word():
     assert torch.equal(p, ref)
 
 
+@pytest.mark.parametrize("n,scale", [(1000, 1.0), (14150, 50.0), (3 << 20, 0.001)])
+def test_clip_flat_matches_torch(n, scale):
+    """In-place gradient-norm clipping (kernels/adam.hip, the LM trainer's
+    clip) vs the torch formula: norm in fp32, scale = min(1, c / (norm + eps))."""
+    from pytorch_distributed_rnn_amd import _ext
+    mod = _ext.require()
+    torch.manual_seed(n)
+    g = torch.randn(n, device="cuda") * scale
+    ref = g.double()
+    norm = ref.norm()
+    ref = ref * torch.clamp(1.0 / (norm + 1e-6), max=1.0)
+    out = mod.clip_flat(g, 1.0, 1e-6)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out[1].double(), norm, rtol=1e-5, atol=0)
+    torch.testing.assert_close(g.double(), ref, rtol=1e-5, atol=1e-9)
+    g2 = torch.randn(n, device="cuda") * scale
+    a, b = g2.clone(), g2.clone()
+    mod.clip_flat(a, 1.0, 1e-6)
+    mod.clip_flat(b, 1.0, 1e-6)
+    assert torch.equal(a, b)  # deterministic
+
+
 def test_embedding_matches_torch():
     C = _C()
     V, D, N = 97, 64, 5000

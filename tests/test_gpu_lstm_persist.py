@@ -62,7 +62,9 @@ def test_persistent_matches_per_step(cell, B, T, ndir, rev, dt):
 def test_persistent_fp32_matches_per_step(cell, Hs, B, T, ndir, rev):
     """fp32 storage (the reference's precision at --hidden-units 128 / 256):
     the persistent recurrence on v_mfma_f32_16x16x4_f32 equals the per-step
-    kernels up to fp32 summation order."""
+    kernels up to fp32 summation order (the backward by default; the forward
+    only with PDRNN_LSTM_PERSIST_F32_FWD=1, read once per process -- this
+    test covers the default)."""
     mod = _ext.require()
     assert mod.lstm_large_persist_mt(B, Hs, ndir, 2) > 0
     torch.manual_seed(B + T + cell + Hs)
