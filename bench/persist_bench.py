@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--cell", type=int, default=0)
     ap.add_argument("--hidden", type=int, default=1024)
     ap.add_argument("--dtype", choices=("bf16", "fp16", "fp32"), default="bf16")
+    ap.add_argument("--tiles", type=int, nargs="*", default=[0],
+                    help="per-step tile ids to time besides the automatic choice (lstm_large.hip TILE_CFGS_X)")
     a = ap.parse_args()
     from pytorch_distributed_rnn_amd import _ext
     mod = _ext.require()
@@ -53,7 +55,7 @@ def main():
            "persist_mt": mod.lstm_large_persist_mt(B, H, 1, code)}
     # tile -1: persistent when covered (PDRNN_LSTM_PERSIST=0 -> auto per-step
     # tile); tile 0: per-step 32x64 forward tiles, split-K backward
-    for name, t in (("auto", -1), ("per_step_tile0", 0)):
+    for name, t in [("auto", -1)] + [(f"per_step_tile{t}", t) for t in a.tiles]:
         fw = lambda: mod.lstm_large_fwd(xp, w, None, None, H, 0, t, a.cell)
         hseq, cseq, acts = fw()
         bw = lambda: mod.lstm_large_bwd(dout, None, None, wt, cseq, acts, None, H, 0, t, a.cell)

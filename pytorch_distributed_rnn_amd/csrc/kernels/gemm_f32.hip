@@ -37,7 +37,14 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int GF_BM = 128, GF_BK = 16, GF_THREADS = 256, GF_PAD = 16;
+constexpr int GF_BM = 128, GF_THREADS = 256, GF_PAD = 16;
+// k-tile depth: 32 for fp32 inputs with a k-major A (the weight-gradient
+// products G^T X: 8 MFMA k-steps between barriers, -4 % / -18 % on the fp32
+// motion model's dW shapes), 16 otherwise (a row-major A is transposed into
+// LDS element by element -- 32 made those shapes 8-31 % slower; 16-bit inputs
+// take one v_mfma_f32_16x16x16 per tile).  profiles/r4/h3/ vs profiles/r4/rd5/.
+template <int IN, bool AKM>
+constexpr int gf_bk() { return IN == 2 && AKM ? 32 : 16; }
 
 template <int IN>
 __device__ __forceinline__ float ld1(const void* p, int64_t i) {
@@ -72,20 +79,21 @@ __device__ __forceinline__ float4 quad(const void* p, int64_t ld, int r, int c, 
   return make_float4(v[0], v[1], v[2], v[3]);
 }
 
-template <int BN>
+template <int BN, int GF_BK>
 struct GfCfg {
   static constexpr int WN_WAVES = BN == 128 ? 2 : 1;
   static constexpr int WM_WAVES = 4 / WN_WAVES;
   static constexpr int WM = GF_BM / WM_WAVES, WN = BN / WN_WAVES;
   static constexpr int MI = WM / 16, NI = WN / 16;
-  static constexpr int A_QUADS = GF_BM * GF_BK / 4 / GF_THREADS;     // per thread (2)
+  static constexpr int A_QUADS = GF_BM * GF_BK / 4 / GF_THREADS;     // per thread (2 or 4)
   static constexpr int B_QUADS = (BN * GF_BK / 4 + GF_THREADS - 1) / GF_THREADS;
   static constexpr int LDA_S = GF_BM + GF_PAD, LDB_S = BN + GF_PAD;
 };
 
 template <int IN, bool AKM, bool BKM, int BN>
 __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p) {
-  using Cfg = GfCfg<BN>;
+  constexpr int GF_BK = gf_bk<IN, AKM>();
+  using Cfg = GfCfg<BN, GF_BK>;
   __shared__ __attribute__((aligned(16))) float As[2][GF_BK][Cfg::LDA_S];
   __shared__ __attribute__((aligned(16))) float Bs[2][GF_BK][Cfg::LDB_S];
 

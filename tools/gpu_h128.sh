@@ -12,7 +12,7 @@ for cell in lstm gru; do
   tail -1 gpurun_out/${tag}_bench_$cell.log | python tools/bench_line.py "H=128 fp32 $cell"
 done
 for cell in 0 1; do
-  timeout -k 10 120 python bench/persist_bench.py --hidden 128 --dtype fp32 --batch 1440 --seq 128 --cell $cell > gpurun_out/${tag}_persist_f32_cell$cell.json 2> gpurun_out/${tag}_persist_f32_cell$cell.err || { tail -20 gpurun_out/${tag}_persist_f32_cell$cell.err; exit 1; }
+  timeout -k 10 120 python bench/persist_bench.py --hidden 128 --dtype fp32 --batch 1440 --seq 128 --cell $cell --tiles 0 1 2 4 > gpurun_out/${tag}_persist_f32_cell$cell.json 2> gpurun_out/${tag}_persist_f32_cell$cell.err || { tail -20 gpurun_out/${tag}_persist_f32_cell$cell.err; exit 1; }
   cat gpurun_out/${tag}_persist_f32_cell$cell.json
 done
 bash tools/gpu_tables.sh ${tag}tb
