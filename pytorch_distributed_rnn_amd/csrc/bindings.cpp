@@ -893,6 +893,16 @@ Tensor persist_sticky_flag() {
   return sticky[dev];
 }
 
+// Row-owning fp32 recurrence at H = 128 (kernels/lstm_rows_f32.hip) instead of
+// the per-step / persistent kernels; PDRNN_LSTM_ROWS=0 turns it off (A/B).
+bool rows_f32_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("PDRNN_LSTM_ROWS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 // Per-step verification: true when a persistent launch on this device timed
 // out since the last check (synchronises); the flag is cleared, the timeout
 // counted, and the persistent path turned off for the process.
@@ -967,7 +977,9 @@ std::vector<Tensor> lstm_large_fwd(const Tensor& xp, const std::vector<Tensor>& 
     dd.acts = eptrm(acts, d * T * B * 4 * H);
   }
   hipStream_t st = cur_stream();
-  if (large_persist(a, ndir, false, dt, tile, o32, st) != kPersistOk) {
+  if (tile < 0 && rows_f32_on() && pdrnn_lstm_rows_f32_supported((int)H, dt)) {
+    HIP_LAUNCH_CHECK(pdrnn_lstm_rows_f32(&a, ndir, 0, st));
+  } else if (large_persist(a, ndir, false, dt, tile, o32, st) != kPersistOk) {
     for (int64_t s = 0; s < T; ++s) {
       a.step = (int)s;
       HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, ndir, 0, dt, (int)tile, st));
@@ -1040,6 +1052,10 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   }
   hipStream_t st = cur_stream();
   HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, ndir, dt, st));
+  if (tile < 0 && rows_f32_on() && pdrnn_lstm_rows_f32_supported((int)H, dt)) {
+    HIP_LAUNCH_CHECK(pdrnn_lstm_rows_f32(&a, ndir, 1, st));
+    return {dgates, dh0, dc0};
+  }
   const int pr = large_persist(a, ndir, true, dt, tile, o32, st);
   if (pr != kPersistOk) {
     // a failed launch may have advanced the dc carry: start the layer over

@@ -299,6 +299,11 @@ int pdrnn_lstm_large_bwd_pp(int B, int H, int ndir, int dtype);
 hipError_t pdrnn_lstm_large_step(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int tile,
                                  hipStream_t stream);
 hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir, int dtype, hipStream_t stream);
+// Row-owning fp32 recurrence (kernels/lstm_rows_f32.hip): one launch per layer
+// pass, 16 batch rows and all of W_hh per workgroup, no grid sync; H = 128,
+// fp32 storage.  The backward needs pdrnn_lstm_large_bwd_first first.
+int pdrnn_lstm_rows_f32_supported(int H, int dtype);
+hipError_t pdrnn_lstm_rows_f32(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, hipStream_t stream);
 // Persistent recurrence: all T steps of a layer in one cooperative launch with
 // W_hh register-resident.  persist_mt: rows-per-workgroup / 16 for this shape
 // (0 = not covered); counters: ndir * ceil(B / (16 mt)) zeroed ints; err: an
