@@ -15,4 +15,9 @@ for cell in 0 1; do
   timeout -k 10 120 python bench/persist_bench.py --hidden 128 --dtype fp32 --batch 1440 --seq 128 --cell $cell --tiles 0 1 2 4 > gpurun_out/${tag}_persist_f32_cell$cell.json 2> gpurun_out/${tag}_persist_f32_cell$cell.err || { tail -20 gpurun_out/${tag}_persist_f32_cell$cell.err; exit 1; }
   cat gpurun_out/${tag}_persist_f32_cell$cell.json
 done
+# A/B: two sequences per K-split forward workgroup at the headline batch
+timeout -k 10 180 python bench.py --steps 200 --warmup 20 > gpurun_out/${tag}_b1440_nbf1.log 2>&1 || { tail -20 gpurun_out/${tag}_b1440_nbf1.log; exit 1; }
+tail -1 gpurun_out/${tag}_b1440_nbf1.log | python tools/bench_line.py "B=1440 fwd NB=1"
+PDRNN_LSTM_NB_FWD=2 PDRNN_LSTM_SPLIT_FWD=2 timeout -k 10 180 python bench.py --steps 200 --warmup 20 > gpurun_out/${tag}_b1440_nbf2.log 2>&1 || { tail -20 gpurun_out/${tag}_b1440_nbf2.log; exit 1; }
+tail -1 gpurun_out/${tag}_b1440_nbf2.log | python tools/bench_line.py "B=1440 fwd NB=2"
 bash tools/gpu_tables.sh ${tag}tb
