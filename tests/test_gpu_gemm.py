@@ -190,9 +190,11 @@ def test_gemm_f32_segment_rowsum_bias_accumulate(splitk):
                                rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("rows,cols", [(184320, 512), (95, 7), (4096, 32)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("rows,cols", [(184320, 512), (95, 7), (4096, 32), (1000, 1024), (33, 512)])
 def test_col_sum_matches_fp64(dtype, rows, cols):
+    """cols % 512 == 0 with 16-bit input takes the 8-column-per-thread kernel
+    (the strided view below the 4-column one)."""
     mod = _mod()
     X = torch.randn(rows, cols, device="cuda").to(dtype)
     got = mod.col_sum(X)
