@@ -1515,6 +1515,36 @@ hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
 template <int H, int NB, bool SAVE>
 hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st);
 
+// GRU forward: NB sequences per workgroup (2 above one residency round: one
+// sequence per 4-wave workgroup holds ~150 VGPRs, 3 workgroups per CU); the
+// classifier head + CE epilogue of the fused training step (SAVE + head_w) is
+// shared with the LSTM.
+template <int H, int NB, bool SAVE>
+hipError_t launch_fwd_gs_gru(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
+  const int grid = (a->B + NB - 1) / NB;
+  const int block = a->NL * 4 * H;
+  const size_t lds = sizeof(float) * NB * a->NL * 2 * (2 * H);
+  const size_t xbytes = sizeof(float) * (size_t)NB * a->T * H;
+  const bool xl = xbytes <= (size_t)kXldsBytes;
+  if (a->head_w) {
+    if constexpr (SAVE) {
+      if (a->C > 16) return hipErrorInvalidValue;
+      if (xl) hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, NB, true, true, true, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+      else hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, NB, true, false, true, 1>), dim3(grid), dim3(block), lds, st, *a);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
+  if (xl)
+    hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, NB, SAVE, true, false, 1>), dim3(grid), dim3(block), lds + xbytes, st, *a);
+  else
+    hipLaunchKernelGGL((lstm_small_fwd_gs_kernel<H, NB, SAVE, false, false, 1>), dim3(grid), dim3(block), lds, st, *a);
+  return hipGetLastError();
+}
+
+template <int H, int NB, bool SAVE>
+hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st);
+
 // GRU forward: one sequence per workgroup; the classifier head + CE epilogue
 // of the fused training step (SAVE + head_w) is shared with the LSTM.
 template <int H, bool SAVE>
@@ -1694,7 +1724,10 @@ hipError_t dispatch_fwd(const PdrnnLstmSmallFwdArgs* a, int nb, int split, int s
   if (split == 1) {  // gate-split map (4 lanes per unit, one gate each)
     if (a->NL * 4 * H > 512) return hipErrorInvalidConfiguration;
 
-    if (a->cell == 1) return save ? launch_fwd_gs_gru<H, true>(a, st) : launch_fwd_gs_gru<H, false>(a, st);
+    if (a->cell == 1) {
+      if (nb == 2) return save ? launch_fwd_gs_gru<H, 2, true>(a, st) : launch_fwd_gs_gru<H, 2, false>(a, st);
+      return save ? launch_fwd_gs_gru<H, 1, true>(a, st) : launch_fwd_gs_gru<H, 1, false>(a, st);
+    }
     if (save) return nb == 2 ? launch_fwd_gs<H, 2, true>(a, st) : launch_fwd_gs<H, 1, true>(a, st);
     return nb == 2 ? launch_fwd_gs<H, 2, false>(a, st) : launch_fwd_gs<H, 1, false>(a, st);
   }

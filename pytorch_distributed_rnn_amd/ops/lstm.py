@@ -57,6 +57,22 @@ def small_launch_config(batch: int, hidden: int, num_layers: int = 2) -> Tuple[i
     return nb_fwd, sp_fwd, nb_bwd, sp_bwd  # split 0 = widest valid (chosen natively)
 
 
+def gru_fwd_nb(batch: int, hidden: int, device=None) -> int:
+    """Sequences per workgroup of the fused GRU step's gate-split forward: one
+    sequence per 4-wave workgroup holds ~150 VGPRs at H = 32, three
+    workgroups per CU; above that residency round two sequences share a
+    workgroup (one round instead of two, like the LSTM's K-split choice at
+    B > 1024).  PDRNN_LSTM_NB_FWD overrides."""
+    env = _env_int("PDRNN_LSTM_NB_FWD", 0)
+    if env in (1, 2):
+        return env
+    if hidden != 32 or not torch.cuda.is_available():
+        return 1
+    dev = device if device is not None else torch.cuda.current_device()
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    return 2 if batch > 3 * cus else 1
+
+
 def fused_bwd_nb(batch: int, hidden: int, num_layers: int) -> int:
     """Sequences per workgroup of the fused training step's backward.
 

@@ -328,13 +328,13 @@ class MotionTrainStep:
         return [fs["flat_p"], fs["exp_avg"], fs["exp_avg_sq"]], hp
 
     def __call__(self, features: Tensor, labels: Tensor, idx: Optional[Tensor]) -> Tensor:
-        from ..ops.lstm import fused_bwd_nb, small_launch_config
+        from ..ops.lstm import fused_bwd_nb, gru_fwd_nb, small_launch_config
         self.flat.attach_grads()
         batch = idx.numel() if idx is not None else features.shape[0]
         nb_fwd, sp_fwd, _, _ = small_launch_config(batch, self.H, self.NL)
         nb_bwd = fused_bwd_nb(batch, self.H, self.NL)
-        if self.gru:
-            nb_fwd, sp_fwd = 1, 1
+        if self.gru:  # gate-split forward only (1 or 2 sequences per workgroup)
+            nb_fwd, sp_fwd = gru_fwd_nb(batch, self.H, features.device), 1
         hw, hb = self.m.fc.weight, self.m.fc.bias  # the classifier head stays fp32
         if self.bf16:
             ws = self.weights  # rounded to bf16 in-kernel (round_bf16)
@@ -380,13 +380,13 @@ class MotionTrainStep:
         discarded: loads the kernels' code objects and sizes the allocator's
         workspace for this batch shape.  Parameters and optimizer state are not
         touched; the flat gradient (fully rewritten by every step) is zeroed."""
-        from ..ops.lstm import fused_bwd_nb, small_launch_config
+        from ..ops.lstm import fused_bwd_nb, gru_fwd_nb, small_launch_config
         self.flat.attach_grads()
         batch = idx.numel() if idx is not None else features.shape[0]
         nb_fwd, sp_fwd, _, _ = small_launch_config(batch, self.H, self.NL)
         nb_bwd = fused_bwd_nb(batch, self.H, self.NL)
-        if self.gru:
-            nb_fwd, sp_fwd = 1, 1
+        if self.gru:  # gate-split forward only (1 or 2 sequences per workgroup)
+            nb_fwd, sp_fwd = gru_fwd_nb(batch, self.H, features.device), 1
         if self.bf16:
             ws = self.weights  # rounded to bf16 in-kernel (round_bf16)
             if features.dtype != torch.bfloat16:

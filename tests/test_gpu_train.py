@@ -125,6 +125,30 @@ def test_fused_step_headline_batch_matches_autograd(nb, monkeypatch):
         assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
 
 
+def test_fused_gru_step_headline_batch_matches_autograd():
+    """GRU at B = 1440 and its short batch 1128: above one residency round
+    the gate-split forward takes two sequences per workgroup (ops/lstm.py
+    gru_fwd_nb) -- against the autograd path on the same kernels' math."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.ops.lstm import gru_fwd_nb
+    from pytorch_distributed_rnn_amd.train.trainer import Trainer
+    assert gru_fwd_nb(1440, 32) == 2
+    torch.manual_seed(3)
+    train, _, _ = synthetic_motion(n_train=2568, n_validation=2, n_test=2, seed=6)
+    m1 = MotionModel(9, 32, 2, 6, cell="gru")
+    m2 = copy.deepcopy(m1)
+    t1 = Trainer(m1, train, batch_size=1440, learning_rate=2.5e-3, device=torch.device("cuda"))
+    t2 = Trainer(m2, train, batch_size=1440, learning_rate=2.5e-3, device=torch.device("cuda"))
+    t2._fused = None
+    for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
+        s1, _ = t1.train_batch(x1)
+        s2, _ = t2.train_batch(x2)
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=2e-5, rtol=1e-4), k
+
+
 @pytest.mark.parametrize("cell,hidden,layers,seq,features", [
     ("lstm", 32, 2, 128, 9), ("lstm", 16, 1, 37, 9), ("lstm", 32, 3, 21, 5),
     ("lstm", 16, 2, 6, 16), ("gru", 32, 2, 128, 9), ("gru", 16, 2, 9, 3)])

@@ -20,4 +20,8 @@ timeout -k 10 180 python bench.py --steps 200 --warmup 20 > gpurun_out/${tag}_b1
 tail -1 gpurun_out/${tag}_b1440_nbf1.log | python tools/bench_line.py "B=1440 fwd NB=1"
 PDRNN_LSTM_NB_FWD=2 PDRNN_LSTM_SPLIT_FWD=2 timeout -k 10 180 python bench.py --steps 200 --warmup 20 > gpurun_out/${tag}_b1440_nbf2.log 2>&1 || { tail -20 gpurun_out/${tag}_b1440_nbf2.log; exit 1; }
 tail -1 gpurun_out/${tag}_b1440_nbf2.log | python tools/bench_line.py "B=1440 fwd NB=2"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread -k "gru" > gpurun_out/${tag}_gru_tests.log 2>&1 || { tail -40 gpurun_out/${tag}_gru_tests.log; exit 1; }
+tail -1 gpurun_out/${tag}_gru_tests.log
+timeout -k 10 180 python bench.py --cell gru --steps 200 --warmup 20 > gpurun_out/${tag}_gru1440.log 2>&1 || { tail -20 gpurun_out/${tag}_gru1440.log; exit 1; }
+tail -1 gpurun_out/${tag}_gru1440.log | python tools/bench_line.py "GRU B=1440"
 bash tools/gpu_tables.sh ${tag}tb
