@@ -34,7 +34,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-from .lstm_large import _tile, final_hidden, stack_layers
+from .lstm_large import _tile, final_hidden, mark_ready, run_recurrence, stack_layers
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
@@ -143,12 +143,20 @@ class _LargeGRULayer(torch.autograd.Function):
         mod = _ext.native(x.device)
         dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
         dhn_f = dhn.float().contiguous() if dhn is not None else None
-        dgates, dh0, _ = mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1)
+        dgates, dh0, _ = run_recurrence(
+            dhseq, lambda: mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1),
+            [dout, dhn_f, hs32, acts, h0f, *wt])
         grads: List[Optional[Tensor]] = []
         dx = None
         dx_pairs = []
         need_dx = ctx.needs_input_grad[0]
         x2 = x.reshape(T * B, I)
+        if need_dx and cdt == torch.float32:
+            # dX of both directions first (K segments): the layer below starts
+            # its recurrence beside this layer's dW GEMMs (lstm_large.run_recurrence)
+            Gx0 = dgates[0].view(T * B, 4 * H)[:, :3 * H]
+            seg = (dgates[1].view(T * B, 4 * H)[:, :3 * H], wih[1]) if ndir > 1 else None
+            dx = mark_ready(gemm_f32(Gx0, False, wih[0], True, pairs2=seg)[0].view(T, B, I))
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # [r | z | dpre_n | dpre_n r]
             Gx = G[:, :3 * H]                                        # x side: [r | z | dpre_n]
@@ -186,16 +194,11 @@ class _LargeGRULayer(torch.autograd.Function):
                 for dst, src in ((dwhh, dw4), (dbhh, cs)):
                     dst[:2 * H].copy_(src[:2 * H])
                     dst[2 * H:].copy_(src[3 * H:])
-            if not need_dx:
-                pass  # layer input without grad (e.g. the data): no dX GEMM
-            else:
+            if need_dx and cdt != torch.float32:
                 dx_pairs.append((Gx, wih[d]))
             grads += [dwih, dwhh, dbih if has_w[4 * d + 2] else None, dbhh if has_w[4 * d + 3] else None]
-        if dx_pairs and cdt == torch.float32:  # both directions in one launch (K segments)
-            dx = gemm_f32(dx_pairs[0][0], False, dx_pairs[0][1], True,
-                          pairs2=dx_pairs[1] if len(dx_pairs) > 1 else None)[0]
-        elif dx_pairs:
-            dx = mm_nk16(dx_pairs)  # both directions in one launch
+        if dx_pairs:
+            dx = mm_nk16(dx_pairs)  # 16-bit: both directions in one launch
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         return (dx.view(T, B, I) if dx is not None else None, dh0_out, None, *grads)
 

@@ -191,6 +191,60 @@ def _bias_cat(weights, ndir: int, hidden: int, device) -> Tensor:
     return t
 
 
+# ---------------------------------------------------------------------------
+# Cross-layer overlap in the fp32 backward: layer l's recurrence (90 of 256
+# CUs at the motion batch) needs only the layer above's dX, not its weight
+# gradients.  The layer above records an event right after its dX GEMM and
+# hangs it on the dX tensor; this layer's recurrence then runs on a
+# high-priority side stream that waits for that event only, while the main
+# stream is still busy with the layer above's dW GEMMs.  The main stream
+# joins the side stream before this layer's own GEMMs (and every gradient is
+# still returned through autograd on the main stream: DDP hooks unchanged).
+_SIDE = {}
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device=device, priority=-1)
+    return s
+
+
+def overlap_on() -> bool:
+    return os.environ.get("PDRNN_LARGE_OVERLAP", "1") != "0"
+
+
+def run_recurrence(dhseq: Optional[Tensor], fn, inputs: Sequence[Optional[Tensor]]):
+    """fn() -> tensors: the layer's backward recurrence, on the side stream
+    when the upstream gradient carries a ready event (see above), inline
+    otherwise."""
+    ev = getattr(dhseq, "_pdrnn_ready", None) if dhseq is not None else None
+    if ev is None or not overlap_on():
+        return fn()
+    main = torch.cuda.current_stream(dhseq.device)
+    side = _side_stream(dhseq.device)
+    side.wait_event(ev)
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in inputs:  # main-stream tensors read on the side stream
+        if t is not None:
+            t.record_stream(side)
+    for t in out:  # side-stream tensors read on the main stream
+        if t is not None:
+            t.record_stream(main)
+    main.wait_stream(side)
+    return out
+
+
+def mark_ready(dx: Optional[Tensor]) -> Optional[Tensor]:
+    """Record the event the layer below waits for (after this layer's dX)."""
+    if dx is not None and dx.is_cuda and overlap_on():
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dx.device))
+        dx._pdrnn_ready = ev
+    return dx
+
+
 def final_hidden(hseq: Tensor, last: Sequence[int], H: int) -> Tensor:
     """[ndir, B, H] final hidden states out of hseq [T, B, ndir*H]: one copy
     per direction into a fresh tensor (no ATen concatenation kernel)."""
@@ -265,7 +319,9 @@ class _LargeLSTMLayer(torch.autograd.Function):
         dhn_f = dhn.float().contiguous() if dhn is not None else None
         dcn_f = dcn.float().contiguous() if dcn is not None else None
         wt = list(whh)                                              # [H, 4H], gate-blocked
-        dgates, dh0, dc0 = mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile, 0)
+        dgates, dh0, dc0 = run_recurrence(
+            dhseq, lambda: mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile, 0),
+            [dout, dhn_f, dcn_f, cseq, acts, c0c, *wt])
         grads: List[Optional[Tensor]] = []
         dx = None
         need_dx = ctx.needs_input_grad[0]
@@ -276,8 +332,12 @@ class _LargeLSTMLayer(torch.autograd.Function):
         # (kernels/gemm_f32.hip): dW_hh over shifted views of the output
         # sequence with the initial-state pairing as a second K segment, dW_ih
         # with db as the row sums of dgates^T in the same pass, dX of both
-        # directions in one launch (K segments)
-        dx_pairs = []
+        # directions in one launch (K segments) -- first, so the layer below
+        # can start its recurrence beside this layer's dW (run_recurrence)
+        if need_dx:
+            Gd = [dgates[d].view(T * B, 4 * H) for d in range(ndir)]
+            dx = gemm_f32(Gd[0], False, wih[0], True, pairs2=(Gd[1], wih[1]) if ndir > 1 else None)[0]
+            dx = mark_ready(dx.view(T, B, I))
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
             hd = hseq[:, :, d * H:(d + 1) * H]                       # strided view, row stride ndir*H
@@ -294,13 +354,7 @@ class _LargeLSTMLayer(torch.autograd.Function):
             else:
                 dwhh = torch.zeros(4 * H, H, device=x.device, dtype=torch.float32)
             dwih, db = gemm_f32(G, True, x2, True, rowsum=True)
-            if need_dx:
-                dx_pairs.append((G, wih[d]))
             grads += [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
-        if dx_pairs:
-            dx = gemm_f32(dx_pairs[0][0], False, dx_pairs[0][1], True,
-                          pairs2=dx_pairs[1] if len(dx_pairs) > 1 else None)[0]
-        dx = dx.view(T, B, I) if dx is not None else None
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         dc0_out = dc0.to(c0_dtype) if has_c0 else None
         return (dx, dh0_out, dc0_out, None, *grads)
