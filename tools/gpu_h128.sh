@@ -11,6 +11,8 @@ for cell in lstm gru; do
   timeout -k 10 300 python bench.py --hidden 128 --cell $cell --steps 20 --warmup 5 > gpurun_out/${tag}_bench_$cell.log 2>&1 || { tail -20 gpurun_out/${tag}_bench_$cell.log; exit 1; }
   tail -1 gpurun_out/${tag}_bench_$cell.log | python tools/bench_line.py "H=128 fp32 $cell"
 done
+PDRNN_LARGE_OVERLAP=0 timeout -k 10 300 python bench.py --hidden 128 --steps 20 --warmup 5 > gpurun_out/${tag}_bench_lstm_noovl.log 2>&1 || { tail -20 gpurun_out/${tag}_bench_lstm_noovl.log; exit 1; }
+tail -1 gpurun_out/${tag}_bench_lstm_noovl.log | python tools/bench_line.py "H=128 fp32 lstm, no cross-layer overlap"
 for cell in 0 1; do
   timeout -k 10 120 python bench/persist_bench.py --hidden 128 --dtype fp32 --batch 1440 --seq 128 --cell $cell --tiles 0 1 2 4 > gpurun_out/${tag}_persist_f32_cell$cell.json 2> gpurun_out/${tag}_persist_f32_cell$cell.err || { tail -20 gpurun_out/${tag}_persist_f32_cell$cell.err; exit 1; }
   cat gpurun_out/${tag}_persist_f32_cell$cell.json
