@@ -236,18 +236,6 @@ def run_recurrence(dhseq: Optional[Tensor], fn, inputs: Sequence[Optional[Tensor
     return out
 
 
-_GEMM_SIDE = {}
-
-
-def gemm_side(device) -> "torch.cuda.Stream":
-    """A second stream for a layer's dW_ih GEMM beside its dW_hh GEMM (both
-    read the same dgates; each is memory- or latency-bound on its own)."""
-    s = _GEMM_SIDE.get(device)
-    if s is None:
-        s = _GEMM_SIDE[device] = torch.cuda.Stream(device=device)
-    return s
-
-
 def mark_ready(dx: Optional[Tensor]) -> Optional[Tensor]:
     """Record the event the layer below waits for (after this layer's dX)."""
     if dx is not None and dx.is_cuda and overlap_on():
@@ -350,17 +338,6 @@ class _LargeLSTMLayer(torch.autograd.Function):
             Gd = [dgates[d].view(T * B, 4 * H) for d in range(ndir)]
             dx = gemm_f32(Gd[0], False, wih[0], True, pairs2=(Gd[1], wih[1]) if ndir > 1 else None)[0]
             dx = mark_ready(dx.view(T, B, I))
-        conc = overlap_on()
-        if conc:  # dW_ih (+ db) of every direction on the second stream, dW_hh on this one
-            main, gs = torch.cuda.current_stream(x.device), gemm_side(x.device)
-            gs.wait_stream(main)
-            with torch.cuda.stream(gs):
-                wi = [gemm_f32(dgates[d].view(T * B, 4 * H), True, x2, True, rowsum=True) for d in range(ndir)]
-            for t in (dgates, x2):
-                t.record_stream(gs)
-            for dwih, db in wi:
-                dwih.record_stream(main)
-                db.record_stream(main)
         for d in range(ndir):
             G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
             hd = hseq[:, :, d * H:(d + 1) * H]                       # strided view, row stride ndir*H
@@ -376,10 +353,8 @@ class _LargeLSTMLayer(torch.autograd.Function):
                 dwhh = gemm_f32(seg2[0], True, seg2[1], True)[0]
             else:
                 dwhh = torch.zeros(4 * H, H, device=x.device, dtype=torch.float32)
-            dwih, db = wi[d] if conc else gemm_f32(G, True, x2, True, rowsum=True)
+            dwih, db = gemm_f32(G, True, x2, True, rowsum=True)
             grads += [dwih, dwhh, db if has_w[4 * d + 2] else None, db if has_w[4 * d + 3] else None]
-        if conc:
-            main.wait_stream(gs)
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
         dc0_out = dc0.to(c0_dtype) if has_c0 else None
         return (dx, dh0_out, dc0_out, None, *grads)
