@@ -41,3 +41,36 @@ def test_two_ranks_one_gpu_match_single_process(tmp_path, mode):
     mean = [(a + b) / 2 for a, b in zip(per[0], per[1])]
     for a, b in zip(mean, local):
         assert abs(a - b) < 1e-5, (mean, local)
+
+
+def test_two_rank_deferred_persist_verification(tmp_path):
+    """Multi-rank per-step verification of the persistent recurrence without a
+    host sync (train/lm.py settle, bindings.cpp persist_sticky_flag): rank 0's
+    first persistent launch is flagged as timed out; the MAX all-reduce of
+    the sticky flag makes BOTH ranks skip their Adam launches on the device
+    and re-run the skipped steps on the per-step kernels, so both ranks count
+    one fallback and end with the parameters of a run that never took the
+    persistent path (PDRNN_LSTM_PERSIST=0)."""
+    import json
+    worker = os.path.join(ROOT, "tests", "_lm_verify_worker.py")
+
+    def job(extra):
+        out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                   "--master-addr=127.0.0.1", f"--master-port={free_port()}", worker],
+                  cwd=str(tmp_path), env=_gpu_env(extra), timeout=150)
+        recs = [json.loads(line) for line in out.splitlines() if line.startswith("{\"rank\"")]
+        return {r["rank"]: r for r in recs}
+
+    got = job({"PDRNN_TEST_INJECT_RANK": "0"})
+    ref = job({"PDRNN_LSTM_PERSIST": "0"})
+    assert sorted(got) == [0, 1] and sorted(ref) == [0, 1]
+    for r in (0, 1):
+        assert got[r]["verify"] == 2, got[r]
+        assert got[r]["fallbacks"] == 1 and got[r]["disabled"], got[r]
+        assert ref[r]["fallbacks"] == 0, ref[r]
+    assert got[0]["checksum"] == got[1]["checksum"]
+    for r in (0, 1):
+        assert abs(got[r]["checksum"] - ref[r]["checksum"]) <= 1e-6 * ref[r]["abs"], (got[r], ref[r])
+        for a, b in zip(got[r]["losses"], ref[r]["losses"]):
+            assert abs(a - b) < 1e-4, (got[r]["losses"], ref[r]["losses"])
+
