@@ -26,6 +26,8 @@ def main(argv=None):
     ap.add_argument("--first", type=int, default=0, help="window = N anchor intervals from the --skip-th anchor")
     ap.add_argument("--end-skip", type=int, default=0,
                     help="with --first: the window ENDS this many anchors before the last one")
+    ap.add_argument("--sequence", type=int, default=0,
+                    help="also list the dispatches of the first N anchor intervals of the window, in order")
     ap.add_argument("--out")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
@@ -58,6 +60,10 @@ def main(argv=None):
         out.append(f"| `{short(name)}` | {n / steps:.2f} | {t / 1e3 / steps:.2f} |")
     tot = sum(t for _, t in agg.values())
     out.append(f"\nGPU kernel time {tot / 1e3 / steps:.2f} us/step, {sum(n for n, _ in agg.values()) / steps:.2f} dispatches/step")
+    if a.sequence:
+        first = [r for r in win if anchors[skip] <= r[1] < anchors[min(skip + a.sequence, len(anchors) - 1)]]
+        out += ["", "first window step, in dispatch order:", "", "| # | kernel | us |", "|---|---|---|"]
+        out += [f"| {i} | `{short(n)}` | {d / 1e3:.2f} |" for i, (n, _, d) in enumerate(first)]
     text = "\n".join(out)
     if a.out:
         with open(a.out, "w") as f:
