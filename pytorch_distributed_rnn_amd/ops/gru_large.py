@@ -198,9 +198,11 @@ class _LargeGRULayer(torch.autograd.Function):
                 dx_pairs.append((Gx, wih[d]))
             grads += [dwih, dwhh, dbih if has_w[4 * d + 2] else None, dbhh if has_w[4 * d + 3] else None]
         if dx_pairs:
-            dx = mm_nk16(dx_pairs)  # 16-bit: both directions in one launch
+            dx = mm_nk16(dx_pairs).view(T, B, I)  # 16-bit: both directions in one launch
         dh0_out = dh0.to(h0_dtype) if has_h0 else None
-        return (dx.view(T, B, I) if dx is not None else None, dh0_out, None, *grads)
+        # (the fp32 dx is returned as the very tensor mark_ready tagged: a view
+        # would drop the ready event the layer below waits for)
+        return (dx, dh0_out, None, *grads)
 
 
 def gru_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor], *, hidden: int,
