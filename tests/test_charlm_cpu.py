@@ -77,3 +77,34 @@ def test_lm_checkpoint_resume(tmp_path):
     assert state["epoch"] == 1 and "embedding.weight" in state["model_state"]
     run(args + ["--resume", str(ck), "local"], cwd=ROOT)
     assert (tmp_path / "charlm-epoch1.pt").exists()
+
+
+def test_lm_trainer_settle_is_a_no_op_on_cpu():
+    """The deferred persistent-path verification (train/lm.py settle) only
+    engages on a GPU in per-step verification mode; on the CPU a step returns
+    its loss directly and settle() has nothing to confirm."""
+    import torch
+    from pytorch_distributed_rnn_amd.data.charlm import CharCorpus
+    from pytorch_distributed_rnn_amd.models.charlm import CharLM
+    from pytorch_distributed_rnn_amd.train.lm import LMTrainer
+    torch.manual_seed(0)
+    corpus = CharCorpus.synthetic(20_000, seed=1)
+    tr = LMTrainer(CharLM(corpus.vocab_size, 16, 32, 1, 0.0, torch.float32), corpus, 4, 8, device=torch.device("cpu"),
+                   log_interval=0)
+    assert not tr._deferred_verify()
+    inp, tgt = next(iter(CharCorpus.segments(tr.streams, 8, 1)))
+    loss = tr.train_step(inp, tgt)
+    assert torch.isfinite(loss) and tr.settle() == 0 and tr._pending == []
+
+
+def test_gru_forward_sequences_per_workgroup_override(monkeypatch):
+    """ops/lstm.py gru_fwd_nb: PDRNN_LSTM_NB_FWD overrides the residency rule
+    (which needs a GPU to count CUs; 1 without one)."""
+    from pytorch_distributed_rnn_amd.ops.lstm import gru_fwd_nb
+    monkeypatch.setenv("PDRNN_LSTM_NB_FWD", "2")
+    assert gru_fwd_nb(100, 32) == 2
+    monkeypatch.delenv("PDRNN_LSTM_NB_FWD")
+    import torch
+    if not torch.cuda.is_available():
+        assert gru_fwd_nb(1440, 32) == 1
+    assert gru_fwd_nb(1440, 16) == 1
