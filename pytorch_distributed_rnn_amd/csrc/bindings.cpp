@@ -1068,6 +1068,103 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   return {dgates, dh0, dc0};
 }
 
+// Time ranges of a unidirectional fp32 H = 128 layer on the row-owning
+// kernels, into preallocated full-length tensors (the stacked-layer pipeline
+// of ops/lstm_large.py: layer l + 1 runs chunk c while layer l runs chunk
+// c + 1).  The state entering t0 > 0 is step t0 - 1 of the same tensors, so
+// chunked and whole-sequence runs do the same arithmetic.
+void check_rows_range(const Tensor& seq, int64_t width, int64_t T, int64_t B, const char* what) {
+  CHECK_HIP_TENSOR(seq);
+  TORCH_CHECK(seq.is_contiguous() && seq.scalar_type() == at::kFloat && seq.numel() == T * B * width, what,
+              ": contiguous fp32 [T, B, ", width, "]");
+}
+
+// xp: [t1 - t0, B, 4H] (bias included, gate-interleaved); hseq / cseq [T, B, H],
+// acts [T, B, 4H] written for t in [t0, t1)
+void lstm_rows_fwd_range(const Tensor& xp, const Tensor& w, const optional<Tensor>& h0, const optional<Tensor>& c0,
+                         const Tensor& hseq, const Tensor& cseq, const Tensor& acts, int64_t t0, int64_t t1,
+                         int64_t cell) {
+  CHECK_HIP_TENSOR(xp);
+  const c10::DeviceGuard guard(xp.device());
+  const int64_t H = w.size(1), T = hseq.size(0), B = hseq.size(1);
+  TORCH_CHECK(rows_f32_on() && pdrnn_lstm_rows_f32_supported((int)H, large_dtype(xp)), "row-owning fp32 kernels: H = 128");
+  TORCH_CHECK(cell == 0 || cell == 1, "cell: 0 = LSTM, 1 = GRU");
+  TORCH_CHECK(0 <= t0 && t0 < t1 && t1 <= T, "time range");
+  TORCH_CHECK(w.is_contiguous() && w.size(0) == 4 * H && w.scalar_type() == at::kFloat, "w: [4H, H] fp32");
+  check_rows_range(xp, 4 * H, t1 - t0, B, "xp");
+  check_rows_range(hseq, H, T, B, "hseq");
+  check_rows_range(cseq, H, T, B, "cseq");
+  check_rows_range(acts, 4 * H, T, B, "acts");
+  if (h0.has_value() && h0->defined()) check_rows_range(*h0, H, 1, B, "h0");
+  if (c0.has_value() && c0->defined()) check_rows_range(*c0, H, 1, B, "c0");
+  PdrnnLstmLargeStepArgs a{};
+  a.B = (int)B; a.H = (int)H; a.T = (int)(t1 - t0); a.cell = (int)cell;
+  PdrnnLstmLargeDir& d = a.dir[0];
+  float* hs = hseq.data_ptr<float>();
+  float* cs = cseq.data_ptr<float>();
+  d.w = w.data_ptr<float>();
+  d.xp = xp.data_ptr<float>(); d.xp_sb = 4 * H; d.xp_st = B * 4 * H;
+  d.h0 = t0 > 0 ? hs + (t0 - 1) * B * H : (h0.has_value() && h0->defined() ? h0->data_ptr<float>() : nullptr);
+  d.c0 = t0 > 0 ? cs + (t0 - 1) * B * H : (c0.has_value() && c0->defined() ? c0->data_ptr<float>() : nullptr);
+  d.hseq = hs + t0 * B * H; d.hseq_sb = H; d.hseq_st = B * H;
+  d.cseq = cs + t0 * B * H;
+  d.acts = acts.data_ptr<float>() + t0 * B * 4 * H;
+  HIP_LAUNCH_CHECK(pdrnn_lstm_rows_f32(&a, 1, 0, cur_stream()));
+}
+
+// Backward of [t0, t1) (run from the last range down): dout [t1 - t0, B, H]
+// (any row strides), dhn / dcn the gradients entering step t1 - 1 from above
+// (the final-state gradients, or dh / dc written by the range above); writes
+// dgates for [t0, t1) and the gradients leaving t0 into dh0 / dc0 [B, H]
+// (which may be the dhn / dcn buffers: the first-cell kernel reads them
+// before the recurrence overwrites them).  carry: [B, H] scratch.
+void lstm_rows_bwd_range(const optional<Tensor>& dout, const optional<Tensor>& dhn, const optional<Tensor>& dcn,
+                         const Tensor& wt, const Tensor& cseq, const Tensor& acts, const optional<Tensor>& c0,
+                         const Tensor& dgates, const Tensor& dh0, const Tensor& dc0, const Tensor& carry, int64_t t0,
+                         int64_t t1, int64_t cell) {
+  CHECK_HIP_TENSOR(acts);
+  const c10::DeviceGuard guard(acts.device());
+  const int64_t H = wt.size(0), T = cseq.size(0), B = cseq.size(1);
+  TORCH_CHECK(rows_f32_on() && pdrnn_lstm_rows_f32_supported((int)H, large_dtype(acts)), "row-owning fp32 kernels: H = 128");
+  TORCH_CHECK(cell == 0 || cell == 1, "cell: 0 = LSTM, 1 = GRU");
+  TORCH_CHECK(0 <= t0 && t0 < t1 && t1 <= T, "time range");
+  TORCH_CHECK(wt.is_contiguous() && wt.size(1) == 4 * H && wt.scalar_type() == at::kFloat, "wt: [H, 4H] fp32");
+  check_rows_range(cseq, H, T, B, "cseq");
+  check_rows_range(acts, 4 * H, T, B, "acts");
+  check_rows_range(dgates, 4 * H, T, B, "dgates");
+  check_rows_range(dh0, H, 1, B, "dh0");
+  check_rows_range(dc0, H, 1, B, "dc0");
+  check_rows_range(carry, H, 1, B, "carry");
+  if (dhn.has_value() && dhn->defined()) check_rows_range(*dhn, H, 1, B, "dhn");
+  if (dcn.has_value() && dcn->defined()) check_rows_range(*dcn, H, 1, B, "dcn");
+  if (c0.has_value() && c0->defined()) check_rows_range(*c0, H, 1, B, "c0");
+  const bool has_dout = dout.has_value() && dout->defined();
+  if (has_dout) {
+    TORCH_CHECK(dout->scalar_type() == at::kFloat && dout->dim() == 3 && dout->size(0) == t1 - t0 &&
+                dout->size(1) == B && dout->size(2) == H && dout->stride(2) == 1, "dout [t1 - t0, B, H] fp32");
+  }
+  PdrnnLstmLargeStepArgs a{};
+  a.B = (int)B; a.H = (int)H; a.T = (int)(t1 - t0); a.cell = (int)cell;
+  PdrnnLstmLargeDir& d = a.dir[0];
+  const float* cs = cseq.data_ptr<float>();
+  d.wt = wt.data_ptr<float>();
+  d.c0 = t0 > 0 ? cs + (t0 - 1) * B * H : (c0.has_value() && c0->defined() ? c0->data_ptr<float>() : nullptr);
+  d.cseq = const_cast<float*>(cs) + t0 * B * H;
+  d.acts = acts.data_ptr<float>() + t0 * B * 4 * H;
+  d.dgates = dgates.data_ptr<float>() + t0 * B * 4 * H;
+  if (has_dout) {
+    d.dout = dout->data_ptr<float>(); d.dout_sb = dout->stride(1); d.dout_st = dout->stride(0);
+  }
+  d.dhn = dhn.has_value() && dhn->defined() ? dhn->data_ptr<float>() : nullptr;
+  d.dcn = dcn.has_value() && dcn->defined() ? dcn->data_ptr<float>() : nullptr;
+  d.dc_carry = carry.data_ptr<float>();
+  d.dh0 = dh0.data_ptr<float>();
+  d.dc0 = dc0.data_ptr<float>();
+  hipStream_t st = cur_stream();
+  HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, 1, 2, st));
+  HIP_LAUNCH_CHECK(pdrnn_lstm_rows_f32(&a, 1, 1, st));
+}
+
 // Time-batched GEMM (kernels/gemm.hip).  A: a_kmajor ? [K, M] : [M, K];
 // B: b_kmajor ? [K, N] : [N, K] (unit stride along the last dim, any row
 // stride); optional second K segment A2 / B2 of the same layouts; output
@@ -1338,6 +1435,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
   m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
   m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });
+  m.def("lstm_rows_range_supported", [](int64_t H) { return rows_f32_on() && pdrnn_lstm_rows_f32_supported((int)H, 2) != 0; });
+  m.def("lstm_rows_fwd_range", &lstm_rows_fwd_range, "row-owning fp32 recurrence over steps [t0, t1) (preallocated outputs)");
+  m.def("lstm_rows_bwd_range", &lstm_rows_bwd_range, "row-owning fp32 BPTT over steps [t0, t1), last range first");
   m.def("set_persist_verify", [](int mode) { g_persist_verify = mode; },
         "0 off; 1 synchronise after every persistent-recurrence launch and re-run a timed-out layer on the "
         "per-step kernels; 2 per step: persist_step_check() before the optimizer update re-runs the step");

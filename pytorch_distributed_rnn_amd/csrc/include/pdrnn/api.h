@@ -304,7 +304,7 @@ hipError_t pdrnn_lstm_large_bwd_first(const PdrnnLstmLargeStepArgs* a, int ndir,
 // fp32 storage.  The backward needs pdrnn_lstm_large_bwd_first first.
 int pdrnn_lstm_rows_f32_supported(int H, int dtype);
 hipError_t pdrnn_lstm_rows_f32(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, hipStream_t stream);
-// Persistent recurrence: all T steps of a layer in one cooperative launch with
+// Persistent recurrence: all T steps of a layer in one launch (occupancy-checked, all workgroups co-resident) with
 // W_hh register-resident.  persist_mt: rows-per-workgroup / 16 for this shape
 // (0 = not covered); counters: ndir * ceil(B / (16 mt)) zeroed ints; err: an
 // int set to 1 if a grid-sync spin timed out (sticky, if not null: also set,

@@ -225,11 +225,13 @@ def _splitk_f32(dev, M: int, N: int, K: int) -> int:
 
 
 def gemm_f32(a: Tensor, a_kmajor: bool, b: Tensor, b_kmajor: bool, pairs2=None, bias: Optional[Tensor] = None,
-             rowsum: bool = False, out16: bool = False,
-             out: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+             rowsum: bool = False, out16: bool = False, out: Optional[Tensor] = None,
+             accumulate: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
     """C = op(a) op(b)^T (+ op(a2) op(b2)^T) (+ bias), fp32 products and
     accumulation on the matrix cores (kernels/gemm_f32.hip); ``rowsum``: also
-    the sums over K of op(a) (the bias gradient of a dW = G^T X product).
+    the sums over K of op(a) (the bias gradient of a dW = G^T X product);
+    ``accumulate``: C = out + ..., fp32 ``out`` (the row sums are not
+    accumulated).
     ``op``: a k-major operand is stored [K, rows].  Torch fallback without the
     extension (CPU)."""
     mod = _native_f32(a)
@@ -247,6 +249,7 @@ def gemm_f32(a: Tensor, a_kmajor: bool, b: Tensor, b_kmajor: bool, pairs2=None, 
             if sk > 1 and not out.is_contiguous():
                 kw["splitk"] = 1
             kw["out"] = out
+            kw["accumulate"] = accumulate
         c, rs = mod.gemm_f32(a, a_kmajor, b, b_kmajor, **kw)
         return c, (rs if rowsum else None)
     oa = (lambda t: t.t() if a_kmajor else t)
@@ -263,7 +266,7 @@ def gemm_f32(a: Tensor, a_kmajor: bool, b: Tensor, b_kmajor: bool, pairs2=None, 
             rs = rs + oa(pairs2[0]).float().sum(1)
     c = c.to(a.dtype) if out16 else c
     if out is not None:
-        out.copy_(c)
+        out.add_(c) if accumulate else out.copy_(c)
         c = out
     return c, rs
 

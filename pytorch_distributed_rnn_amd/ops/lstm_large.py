@@ -391,6 +391,203 @@ def _backward_gemms16(ctx, dgates, dh0, dc0, hseq, h0c, x2, wih):
     return (dx, dh0_out, dc0_out, None, *grads)
 
 
+# ---------------------------------------------------------------------------
+# Stacked-layer pipeline (fp32, one direction, H = 128 on the row-owning
+# kernels).  The sequence is cut into C time chunks and every layer runs on a
+# stream of its own (layer 0 on the caller's): layer l + 1 computes chunk c --
+# its input projection, then its recurrence -- while layer l computes chunk
+# c + 1, so the layers' recurrences (90 of 256 CUs each at the motion batch)
+# overlap instead of running one after the other.  The backward is the mirror
+# image: layer l's BPTT of chunk c starts as soon as the layer above has
+# produced dX for that chunk, and each layer's weight gradients follow its
+# recurrence on its stream (beside the recurrences of the layers below).
+# Chunk boundaries carry the state through the full-length tensors
+# (lstm_rows_fwd_range / lstm_rows_bwd_range), so the forward is
+# bit-identical to one whole-sequence launch per layer.
+#
+# One stream per layer, nothing more: with GPU_MAX_HW_QUEUES = 4 (HIP's
+# default) further streams share hardware queues, and an event wait on one of
+# them stalls the others (measured: separate projection and weight-gradient
+# streams made the step 25-70 % slower, profiles/r4/pipe/).
+_PIPE_STREAMS = {}
+
+
+def _pipe_stream(device, l: int) -> "torch.cuda.Stream":
+    if l == 0:
+        return torch.cuda.current_stream(device)
+    s = _PIPE_STREAMS.get((device, l))
+    if s is None:
+        s = _PIPE_STREAMS[(device, l)] = torch.cuda.Stream(device=device, priority=-1)
+    return s
+
+
+def pipeline_chunks(T: int) -> List[Tuple[int, int]]:
+    """[t0, t1) time chunks of the stacked-layer pipeline (PDRNN_LARGE_CHUNKS,
+    default 4)."""
+    try:
+        c = int(os.environ.get("PDRNN_LARGE_CHUNKS", "4"))
+    except ValueError:
+        c = 4
+    c = max(1, min(c, T))
+    return [(T * i // c, T * (i + 1) // c) for i in range(c)]
+
+
+def pipeline_ok(x: Tensor, hidden: int, num_layers: int, bidirectional: bool, dropout: float,
+                training: bool) -> bool:
+    """The stacked-layer pipeline covers unidirectional fp32 stacks of >= 2
+    layers at the row-owning kernels' H (PDRNN_LARGE_PIPE=0 turns it off)."""
+    if os.environ.get("PDRNN_LARGE_PIPE", "1") == "0" or _tile() >= 0:
+        return False
+    if x.dtype != torch.float32 or not x.is_cuda or bidirectional or num_layers < 2 or (dropout > 0 and training):
+        return False
+    mod = _ext.native(x.device)
+    return mod is not None and hasattr(mod, "lstm_rows_range_supported") and bool(mod.lstm_rows_range_supported(hidden))
+
+
+def _event(stream) -> "torch.cuda.Event":
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    return ev
+
+
+class _PipelinedLSTMStack(torch.autograd.Function):
+    """All layers of a unidirectional fp32 stack, chunk-pipelined (see above).
+    x: [T, B, I] fp32; h0 / c0: [L, B, H] or None; weights: nn.LSTM
+    ``_all_weights`` order, ``per`` (2 or 4) tensors per layer."""
+
+    @staticmethod
+    def forward(ctx, x, h0, c0, cfg, *weights):
+        H, L, per, chunks = cfg
+        T, B, I = x.shape
+        dev = x.device
+        f32 = torch.float32
+        mod = _ext.native(dev)
+        main = torch.cuda.current_stream(dev)
+        rec = [_pipe_stream(dev, l) for l in range(L)]
+        lw = [list(weights[l * per:(l + 1) * per]) + ([None, None] if per == 2 else []) for l in range(L)]
+        wih = [shadow(w[0], "i", f32, H) for w in lw]                 # [4H, I_l] gate-interleaved
+        whh = [shadow(w[1], "i", f32, H) for w in lw]
+        bias = [_bias_cat(w, 1, H, dev) for w in lw]
+        h0s = [h0[l].float().contiguous() if h0 is not None else None for l in range(L)]
+        c0s = [c0[l].float().contiguous() if c0 is not None else None for l in range(L)]
+        hseq = [x.new_empty(T, B, H) for _ in range(L)]
+        cseq = [x.new_empty(T, B, H) for _ in range(L)]
+        acts = [x.new_empty(T, B, 4 * H) for _ in range(L)]
+        xps = [gemm_f32(x.reshape(T * B, I), False, wih[0], False, bias=bias[0])[0].view(T, B, 4 * H)]
+        xps += [x.new_empty(T, B, 4 * H) for _ in range(1, L)]
+        side = rec[1:]
+        for s in side:
+            s.wait_stream(main)  # weights, shadows, buffers and layer 0's projection
+        done = [[None] * len(chunks) for _ in range(L)]
+        for ci, (t0, t1) in enumerate(chunks):
+            for l in range(L):
+                with torch.cuda.stream(rec[l]):
+                    if l > 0:  # this chunk's input projection: the layer below is done with it
+                        rec[l].wait_event(done[l - 1][ci])
+                        gemm_f32(hseq[l - 1][t0:t1].view(-1, H), False, wih[l], False, bias=bias[l],
+                                 out=xps[l][t0:t1].view(-1, 4 * H))
+                    mod.lstm_rows_fwd_range(xps[l][t0:t1], whh[l], h0s[l], c0s[l], hseq[l], cseq[l], acts[l],
+                                            t0, t1, 0)
+                    done[l][ci] = _event(rec[l])
+        for s in side:
+            main.wait_stream(s)
+        hn = x.new_empty(L, B, H)
+        cn = x.new_empty(L, B, H)
+        for l in range(L):
+            hn[l].copy_(hseq[l][T - 1])
+            cn[l].copy_(cseq[l][T - 1])
+        ctx.save_for_backward(x, *hseq, *cseq, *acts, *[shadow(w[0], "p", f32, H) for w in lw],
+                              *[shadow(w[1], "t", f32, H) for w in lw])
+        ctx.states = (h0s, c0s)
+        ctx.cfg = (H, L, per, chunks, [[w is not None for w in ws] for ws in lw],
+                   h0.dtype if h0 is not None else None, c0.dtype if c0 is not None else None)
+        return hseq[L - 1], hn, cn
+
+    @staticmethod
+    def backward(ctx, dhseq, dhn, dcn):
+        H, L, per, chunks, has_w, h0_dtype, c0_dtype = ctx.cfg
+        h0s, c0s = ctx.states
+        sv = ctx.saved_tensors
+        x = sv[0]
+        hseq, cseq, acts = sv[1:1 + L], sv[1 + L:1 + 2 * L], sv[1 + 2 * L:1 + 3 * L]
+        wp, wt = sv[1 + 3 * L:1 + 4 * L], sv[1 + 4 * L:1 + 5 * L]
+        T, B, I = x.shape
+        dev = x.device
+        mod = _ext.native(dev)
+        main = torch.cuda.current_stream(dev)
+        rec = [_pipe_stream(dev, l) for l in range(L)]
+        dgates = [x.new_empty(T, B, 4 * H) for _ in range(L)]
+        douts = [x.new_empty(T, B, H) for _ in range(L - 1)]
+        douts.append(dhseq.float().contiguous() if dhseq is not None else None)
+        dhb = [x.new_empty(B, H) for _ in range(L)]  # gradients leaving a chunk's first step
+        dcb = [x.new_empty(B, H) for _ in range(L)]
+        carry = [x.new_empty(B, H) for _ in range(L)]
+        dhn_l = [dhn[l].float().contiguous() if dhn is not None else None for l in range(L)]
+        dcn_l = [dcn[l].float().contiguous() if dcn is not None else None for l in range(L)]
+        ins = [x] + list(hseq[:-1])  # each layer's input sequence
+        dwih = [x.new_empty(4 * H, t.shape[2]) for t in ins]
+        dwhh = [x.new_empty(4 * H, H) for _ in range(L)]
+        db = [x.new_empty(4 * H) for _ in range(L)]
+        side = rec[1:]
+        for s in side:
+            s.wait_stream(main)
+        done = [[None] * len(chunks) for _ in range(L)]
+        last = len(chunks) - 1
+        for ci in range(last, -1, -1):
+            t0, t1 = chunks[ci]
+            for l in range(L - 1, -1, -1):
+                with torch.cuda.stream(rec[l]):
+                    if l < L - 1:  # this chunk's dout = dX of the layer above
+                        rec[l].wait_event(done[l + 1][ci])
+                        gemm_f32(dgates[l + 1][t0:t1].view(-1, 4 * H), False, wp[l + 1], True,
+                                 out=douts[l][t0:t1].view(-1, H))
+                    dout = douts[l][t0:t1] if douts[l] is not None else None
+                    mod.lstm_rows_bwd_range(dout, dhn_l[l] if ci == last else dhb[l],
+                                            dcn_l[l] if ci == last else dcb[l], wt[l], cseq[l], acts[l], c0s[l],
+                                            dgates[l], dhb[l], dcb[l], carry[l], t0, t1, 0)
+                    done[l][ci] = _event(rec[l])
+                    if ci == 0:  # the layer's recurrence is done: its weight gradients, on its stream
+                        _chunk_weight_grads(dwih[l], dwhh[l], db[l], dgates[l], hseq[l], h0s[l], ins[l], 0, T, True)
+        dx = None
+        if ctx.needs_input_grad[0]:  # (layer 0's stream is the caller's)
+            dx = gemm_f32(dgates[0].view(T * B, 4 * H), False, wp[0], True)[0].view(T, B, I)
+        for s in side:
+            main.wait_stream(s)
+        grads: List[Optional[Tensor]] = []
+        for l in range(L):
+            grads += [dwih[l], dwhh[l]]
+            if per == 4:
+                grads += [db[l] if has_w[l][2] else None, db[l] if has_w[l][3] else None]
+        dh0 = torch.stack(dhb).to(h0_dtype) if h0_dtype is not None else None
+        dc0 = torch.stack(dcb).to(c0_dtype) if c0_dtype is not None else None
+        return (dx, dh0, dc0, None, *grads)
+
+
+def _chunk_weight_grads(dwih: Tensor, dwhh: Tensor, db: Tensor, G3: Tensor, hd: Tensor, h0: Optional[Tensor],
+                        xin: Tensor, t0: int, t1: int, first: bool) -> None:
+    """Steps [t0, t1) of one unidirectional fp32 layer's dW_ih, dW_hh and db,
+    written (first chunk) or accumulated into the fp32 outputs: dW_hh pairs
+    dgates_t with h_{t-1} (h0 at t = 0), dW_ih dgates_t with the layer input,
+    db = the row sums of the dW_ih pass."""
+    H4 = G3.shape[2]
+    H = H4 // 4
+    lo = max(t0, 1)
+    seg0 = (G3[0], h0) if t0 == 0 and h0 is not None else None
+    if t1 > lo:
+        gemm_f32(G3[lo:t1].view(-1, H4), True, hd[lo - 1:t1 - 1].reshape(-1, H), True, pairs2=seg0, out=dwhh,
+                 accumulate=not first)
+    elif seg0 is not None:
+        gemm_f32(seg0[0], True, seg0[1], True, out=dwhh, accumulate=not first)
+    elif first:
+        dwhh.zero_()
+    _, rs = gemm_f32(G3[t0:t1].view(-1, H4), True, xin[t0:t1].reshape(-1, xin.shape[2]), True, rowsum=True,
+                     out=dwih, accumulate=not first)
+    if first:
+        db.copy_(rs)
+    else:
+        db.add_(rs)
+
+
 def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor],
                        c0: Optional[Tensor], *, hidden: int, num_layers: int, batch_first: bool,
                        bidirectional: bool = False, dropout: float = 0.0,
@@ -404,6 +601,10 @@ def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optio
     seq = x.transpose(0, 1) if batch_first else x
     seq = seq.contiguous()
     B = seq.shape[1]
+    if pipeline_ok(seq, hidden, num_layers, bidirectional, dropout, training):
+        out, hn, cn = _PipelinedLSTMStack.apply(seq, h0, c0, (hidden, num_layers, per, pipeline_chunks(seq.shape[0])),
+                                                *weights)
+        return (out.transpose(0, 1) if batch_first else out), hn, cn
     tile = _tile()
     hns, cns = [], []
     for l in range(num_layers):

@@ -28,6 +28,8 @@ def main(argv=None):
                     help="with --first: the window ENDS this many anchors before the last one")
     ap.add_argument("--sequence", type=int, default=0,
                     help="also list the dispatches of the first N anchor intervals of the window, in order")
+    ap.add_argument("--timeline", type=int, default=0,
+                    help="also list the first N anchor intervals as a timeline: start / end offsets and queue")
     ap.add_argument("--out")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
@@ -64,6 +66,18 @@ def main(argv=None):
         first = [r for r in win if anchors[skip] <= r[1] < anchors[min(skip + a.sequence, len(anchors) - 1)]]
         out += ["", "first window step, in dispatch order:", "", "| # | kernel | us |", "|---|---|---|"]
         out += [f"| {i} | `{short(n)}` | {d / 1e3:.2f} |" for i, (n, _, d) in enumerate(first)]
+    if a.timeline:
+        qc = next((q for q in ("queue_id", "stream_id") if q in cols), None)
+        trows = c.execute(f"select name, {t0c}, duration{', ' + qc if qc else ''} from kernels order by {t0c}").fetchall()
+        t_lo = anchors[skip]
+        t_hi = anchors[min(skip + a.timeline, len(anchors) - 1)]
+        out += ["", f"timeline of {a.timeline} window step(s) (us from the first anchor; queue = {qc}):", "",
+                "| start | end | us | queue | kernel |", "|---|---|---|---|---|"]
+        for r in trows:
+            if t_lo <= r[1] < t_hi:
+                q = r[3] if qc else "-"
+                out.append(f"| {(r[1] - t_lo) / 1e3:.1f} | {(r[1] + r[2] - t_lo) / 1e3:.1f} | {r[2] / 1e3:.1f} | {q} | "
+                           f"`{short(r[0])}` |")
     text = "\n".join(out)
     if a.out:
         with open(a.out, "w") as f:
