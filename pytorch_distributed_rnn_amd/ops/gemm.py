@@ -226,12 +226,12 @@ def _splitk_f32(dev, M: int, N: int, K: int) -> int:
 
 def gemm_f32(a: Tensor, a_kmajor: bool, b: Tensor, b_kmajor: bool, pairs2=None, bias: Optional[Tensor] = None,
              rowsum: bool = False, out16: bool = False, out: Optional[Tensor] = None,
-             accumulate: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
+             accumulate: bool = False, splitk: Optional[int] = None) -> Tuple[Tensor, Optional[Tensor]]:
     """C = op(a) op(b)^T (+ op(a2) op(b2)^T) (+ bias), fp32 products and
     accumulation on the matrix cores (kernels/gemm_f32.hip); ``rowsum``: also
     the sums over K of op(a) (the bias gradient of a dW = G^T X product);
     ``accumulate``: C = out + ..., fp32 ``out`` (the row sums are not
-    accumulated).
+    accumulated); ``splitk``: K slices instead of the occupancy heuristic.
     ``op``: a k-major operand is stored [K, rows].  Torch fallback without the
     extension (CPU)."""
     mod = _native_f32(a)
@@ -241,7 +241,7 @@ def gemm_f32(a: Tensor, a_kmajor: bool, b: Tensor, b_kmajor: bool, pairs2=None, 
         N = b.shape[1] if b_kmajor else b.shape[0]
         K = (a.shape[0] if a_kmajor else a.shape[1]) + ((pairs2[0].shape[0] if a_kmajor else pairs2[0].shape[1])
                                                          if pairs2 else 0)
-        sk = 1 if (bias is not None or out16) else _splitk_f32(a.device, M, N, K)
+        sk = 1 if (bias is not None or out16) else (splitk or _splitk_f32(a.device, M, N, K))
         kw = dict(bias=bias, rowsum=rowsum, out16=out16, splitk=sk)
         if pairs2:
             kw.update(A2=pairs2[0], B2=pairs2[1])

@@ -423,11 +423,12 @@ def _pipe_stream(device, l: int) -> "torch.cuda.Stream":
 
 def pipeline_chunks(T: int) -> List[Tuple[int, int]]:
     """[t0, t1) time chunks of the stacked-layer pipeline (PDRNN_LARGE_CHUNKS,
-    default 4)."""
+    default 3: at T = 128 4.54-4.57 ms/step against 4.69-4.79 with 2, 4 or 5
+    chunks and 4.92 with 6, profiles/r4/pipe/p6_*)."""
     try:
-        c = int(os.environ.get("PDRNN_LARGE_CHUNKS", "4"))
+        c = int(os.environ.get("PDRNN_LARGE_CHUNKS", "3"))
     except ValueError:
-        c = 4
+        c = 3
     c = max(1, min(c, T))
     return [(T * i // c, T * (i + 1) // c) for i in range(c)]
 
@@ -539,8 +540,10 @@ class _PipelinedLSTMStack(torch.autograd.Function):
                 with torch.cuda.stream(rec[l]):
                     if l < L - 1:  # this chunk's dout = dX of the layer above
                         rec[l].wait_event(done[l + 1][ci])
+                        # (one K slice: split-K partials and their sum beside the
+                        # recurrences cost more than they recover, profiles/r4/pipe/p6_*)
                         gemm_f32(dgates[l + 1][t0:t1].view(-1, 4 * H), False, wp[l + 1], True,
-                                 out=douts[l][t0:t1].view(-1, H))
+                                 out=douts[l][t0:t1].view(-1, H), splitk=1)
                     dout = douts[l][t0:t1] if douts[l] is not None else None
                     mod.lstm_rows_bwd_range(dout, dhn_l[l] if ci == last else dhb[l],
                                             dcn_l[l] if ci == last else dcb[l], wt[l], cseq[l], acts[l], c0s[l],
