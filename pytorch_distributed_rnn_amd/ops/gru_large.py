@@ -34,7 +34,8 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-from .lstm_large import _tile, final_hidden, mark_ready, run_recurrence, stack_layers
+from .lstm_large import (_tile, final_hidden, mark_ready, pipeline_backward, pipeline_chunks, pipeline_forward,
+                         pipeline_join, pipeline_ok, pipeline_streams, run_recurrence, stack_layers)
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
@@ -205,6 +206,123 @@ class _LargeGRULayer(torch.autograd.Function):
         return (dx, dh0_out, None, *grads)
 
 
+class _PipelinedGRUStack(torch.autograd.Function):
+    """All layers of a unidirectional fp32 GRU stack (H = 128, row-owning
+    kernels), chunk-pipelined like the LSTM's (ops/lstm_large.py, stacked-layer
+    pipeline): layer l + 1 runs chunk c while layer l runs chunk c + 1.
+    h0: [L, B, H] or None; weights: ``nn.GRU`` order, ``per`` per layer."""
+
+    @staticmethod
+    def forward(ctx, x, h0, cfg, *weights):
+        H, L, per, chunks = cfg
+        T, B, I = x.shape
+        dev = x.device
+        mod = _ext.native(dev)
+        lw = [list(weights[l * per:(l + 1) * per]) + ([None, None] if per == 2 else []) for l in range(L)]
+        # per layer: (W_ih [3H, I_l], projection stack, W_hh4, its interleaved form, W_hh4^T, folded bias)
+        sh = [_gru_shadows(lw[l], 1, H, I if l == 0 else H, torch.float32, dev) for l in range(L)]
+        h0s = [h0[l].float().contiguous() if h0 is not None else None for l in range(L)]
+        hseq = [x.new_empty(T, B, H) for _ in range(L)]
+        hs32 = [x.new_empty(T, B, H) for _ in range(L)]
+        acts = [x.new_empty(T, B, 4 * H) for _ in range(L)]
+        xps = [gemm_f32(x.reshape(T * B, I), False, sh[0][1], False, bias=sh[0][5])[0].view(T, B, 4 * H)]
+        xps += [x.new_empty(T, B, 4 * H) for _ in range(1, L)]
+        rec = pipeline_streams(dev, L)
+
+        def project(l, t0, t1):
+            gemm_f32(hseq[l - 1][t0:t1].view(-1, H), False, sh[l][1], False, bias=sh[l][5],
+                     out=xps[l][t0:t1].view(-1, 4 * H))
+
+        def recur(l, t0, t1):  # (the GRU's fp32 hidden state rides in the c0 / cseq slot)
+            mod.lstm_rows_fwd_range(xps[l][t0:t1], sh[l][3][0], h0s[l], h0s[l], hseq[l], hs32[l], acts[l], t0, t1, 1)
+
+        pipeline_forward(rec, chunks, project, recur)
+        pipeline_join(rec)
+        hn = x.new_empty(L, B, H)
+        for l in range(L):
+            hn[l].copy_(hseq[l][T - 1])
+        ctx.save_for_backward(x, *hseq, *hs32, *acts, *[t[0][0] for t in sh], *[t[4][0] for t in sh])
+        ctx.states = h0s
+        ctx.cfg = (H, L, per, chunks, [[w is not None for w in ws] for ws in lw], h0.dtype if h0 is not None else None)
+        return hseq[L - 1], hn
+
+    @staticmethod
+    def backward(ctx, dhseq, dhn):
+        H, L, per, chunks, has_w, h0_dtype = ctx.cfg
+        h0s = ctx.states
+        sv = ctx.saved_tensors
+        x = sv[0]
+        hseq, hs32, acts = sv[1:1 + L], sv[1 + L:1 + 2 * L], sv[1 + 2 * L:1 + 3 * L]
+        wih, wt = sv[1 + 3 * L:1 + 4 * L], sv[1 + 4 * L:1 + 5 * L]
+        T, B, I = x.shape
+        dev = x.device
+        mod = _ext.native(dev)
+        dgates = [x.new_empty(T, B, 4 * H) for _ in range(L)]
+        douts = [x.new_empty(T, B, H) for _ in range(L - 1)]
+        douts.append(dhseq.float().contiguous() if dhseq is not None else None)
+        dhb = [x.new_empty(B, H) for _ in range(L)]  # gradient leaving a chunk's first step
+        dcb = [x.new_empty(B, H) for _ in range(L)]  # (unused by the GRU cell)
+        carry = [x.new_empty(B, H) for _ in range(L)]
+        dhn_l = [dhn[l].float().contiguous() if dhn is not None else None for l in range(L)]
+        ins = [x] + list(hseq[:-1])
+        dwih = [x.new_empty(3 * H, t.shape[2]) for t in ins]
+        dwhh = [x.new_empty(3 * H, H) for _ in range(L)]
+        dbih = [x.new_empty(3 * H) for _ in range(L)]
+        dbhh = [x.new_empty(3 * H) for _ in range(L)]
+        rec = pipeline_streams(dev, L)
+
+        def project(l, t0, t1):  # dX of the layer above: its [r | z | dpre_n] block times W_ih
+            gemm_f32(dgates[l + 1][t0:t1].view(-1, 4 * H)[:, :3 * H], False, wih[l + 1], True,
+                     out=douts[l][t0:t1].view(-1, H), splitk=1)
+
+        def recur(l, first, t0, t1):
+            dout = douts[l][t0:t1] if douts[l] is not None else None
+            mod.lstm_rows_bwd_range(dout, dhn_l[l] if first else dhb[l], None, wt[l], hs32[l], acts[l], h0s[l],
+                                    dgates[l], dhb[l], dcb[l], carry[l], t0, t1, 1)
+
+        def finish(l):
+            _gru_weight_grads(dwih[l], dwhh[l], dbih[l], dbhh[l], dgates[l], hseq[l], h0s[l], ins[l])
+
+        pipeline_backward(rec, chunks, project, recur, finish)
+        dx = None
+        if ctx.needs_input_grad[0]:  # (layer 0's stream is the caller's)
+            dx = gemm_f32(dgates[0].view(T * B, 4 * H)[:, :3 * H], False, wih[0], True)[0].view(T, B, I)
+        pipeline_join(rec)
+        grads: List[Optional[Tensor]] = []
+        for l in range(L):
+            grads += [dwih[l], dwhh[l]]
+            if per == 4:
+                grads += [dbih[l] if has_w[l][2] else None, dbhh[l] if has_w[l][3] else None]
+        dh0 = torch.stack(dhb).to(h0_dtype) if h0_dtype is not None else None
+        return (dx, dh0, None, *grads)
+
+
+def _gru_weight_grads(dwih: Tensor, dwhh: Tensor, dbih: Tensor, dbhh: Tensor, G3: Tensor, hd: Tensor,
+                      h0: Optional[Tensor], xin: Tensor) -> None:
+    """One unidirectional fp32 GRU layer's dW_ih, dW_hh, b_ih and b_hh
+    gradients into the given fp32 tensors (the d = 0 case of
+    _LargeGRULayer.backward): the [r | z] and n_h gate blocks of dW_hh over
+    shifted views of the output sequence with h0 as a second K segment, db_ih
+    as the row sums of the dW_ih pass."""
+    T, B, H4 = G3.shape
+    H = H4 // 4
+    G = G3.view(T * B, H4)
+    g0, Gs = G[:B], G[B:]
+    hs = hd[:-1].reshape((T - 1) * B, H)
+    for cols, rows in ((slice(0, 2 * H), slice(0, 2 * H)), (slice(3 * H, 4 * H), slice(2 * H, 3 * H))):
+        seg2 = (g0[:, cols], h0) if h0 is not None else None
+        if T > 1:
+            gemm_f32(Gs[:, cols], True, hs, True, pairs2=seg2, out=dwhh[rows])
+        elif seg2 is not None:
+            gemm_f32(seg2[0], True, seg2[1], True, out=dwhh[rows])
+        else:
+            dwhh[rows].zero_()
+    _, rs = gemm_f32(G[:, :3 * H], True, xin.reshape(T * B, -1), True, rowsum=True, out=dwih)
+    dbih.copy_(rs)
+    dbhh[:2 * H].copy_(rs[:2 * H])
+    dbhh[2 * H:].copy_(col_sum(G[:, 3 * H:]))
+
+
 def gru_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor], *, hidden: int,
                       num_layers: int, batch_first: bool, bidirectional: bool = False, dropout: float = 0.0,
                       training: bool = False) -> Tuple[Tensor, Tensor]:
@@ -215,6 +333,9 @@ def gru_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Option
     ndir = 2 if bidirectional else 1
     per = len(weights) // (num_layers * ndir)
     seq = (x.transpose(0, 1) if batch_first else x).contiguous()
+    if pipeline_ok(seq, hidden, num_layers, bidirectional, dropout, training):
+        out, hn = _PipelinedGRUStack.apply(seq, h0, (hidden, num_layers, per, pipeline_chunks(seq.shape[0])), *weights)
+        return (out.transpose(0, 1) if batch_first else out), hn
     tile = _tile()
     hns = []
     for l in range(num_layers):

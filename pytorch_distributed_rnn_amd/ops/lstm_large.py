@@ -451,6 +451,60 @@ def _event(stream) -> "torch.cuda.Event":
     return ev
 
 
+def pipeline_streams(device, L: int) -> List["torch.cuda.Stream"]:
+    """One stream per layer (layer 0: the caller's); the side streams first
+    wait for everything the caller has queued (weights, shadows, buffers)."""
+    main = torch.cuda.current_stream(device)
+    streams = [_pipe_stream(device, l) for l in range(L)]
+    for s in streams[1:]:
+        s.wait_stream(main)
+    return streams
+
+
+def pipeline_join(streams) -> None:
+    main = streams[0]
+    for s in streams[1:]:
+        main.wait_stream(s)
+
+
+def pipeline_forward(streams, chunks, project, recur) -> None:
+    """Issue the stacked-layer forward: for every chunk and layer,
+    ``project(l, t0, t1)`` (l > 0, once the layer below has finished the
+    chunk) then ``recur(l, t0, t1)``, on layer l's stream."""
+    L = len(streams)
+    done = [[None] * len(chunks) for _ in range(L)]
+    for ci, (t0, t1) in enumerate(chunks):
+        for l in range(L):
+            with torch.cuda.stream(streams[l]):
+                if l > 0:
+                    streams[l].wait_event(done[l - 1][ci])
+                    project(l, t0, t1)
+                recur(l, t0, t1)
+                done[l][ci] = _event(streams[l])
+
+
+def pipeline_backward(streams, chunks, project, recur, finish) -> None:
+    """Issue the stacked-layer backward, last chunk first: ``project(l, t0,
+    t1)`` (dX of layer l + 1 for the chunk, once that layer has finished it),
+    ``recur(l, first, t0, t1)`` (first: the chunk that starts the layer's
+    BPTT), and after a layer's last chunk ``finish(l)`` (its weight
+    gradients), on layer l's stream."""
+    L = len(streams)
+    done = [[None] * len(chunks) for _ in range(L)]
+    last = len(chunks) - 1
+    for ci in range(last, -1, -1):
+        t0, t1 = chunks[ci]
+        for l in range(L - 1, -1, -1):
+            with torch.cuda.stream(streams[l]):
+                if l < L - 1:
+                    streams[l].wait_event(done[l + 1][ci])
+                    project(l, t0, t1)
+                recur(l, ci == last, t0, t1)
+                done[l][ci] = _event(streams[l])
+                if ci == 0:
+                    finish(l)
+
+
 class _PipelinedLSTMStack(torch.autograd.Function):
     """All layers of a unidirectional fp32 stack, chunk-pipelined (see above).
     x: [T, B, I] fp32; h0 / c0: [L, B, H] or None; weights: nn.LSTM
@@ -463,8 +517,6 @@ class _PipelinedLSTMStack(torch.autograd.Function):
         dev = x.device
         f32 = torch.float32
         mod = _ext.native(dev)
-        main = torch.cuda.current_stream(dev)
-        rec = [_pipe_stream(dev, l) for l in range(L)]
         lw = [list(weights[l * per:(l + 1) * per]) + ([None, None] if per == 2 else []) for l in range(L)]
         wih = [shadow(w[0], "i", f32, H) for w in lw]                 # [4H, I_l] gate-interleaved
         whh = [shadow(w[1], "i", f32, H) for w in lw]
@@ -476,22 +528,17 @@ class _PipelinedLSTMStack(torch.autograd.Function):
         acts = [x.new_empty(T, B, 4 * H) for _ in range(L)]
         xps = [gemm_f32(x.reshape(T * B, I), False, wih[0], False, bias=bias[0])[0].view(T, B, 4 * H)]
         xps += [x.new_empty(T, B, 4 * H) for _ in range(1, L)]
-        side = rec[1:]
-        for s in side:
-            s.wait_stream(main)  # weights, shadows, buffers and layer 0's projection
-        done = [[None] * len(chunks) for _ in range(L)]
-        for ci, (t0, t1) in enumerate(chunks):
-            for l in range(L):
-                with torch.cuda.stream(rec[l]):
-                    if l > 0:  # this chunk's input projection: the layer below is done with it
-                        rec[l].wait_event(done[l - 1][ci])
-                        gemm_f32(hseq[l - 1][t0:t1].view(-1, H), False, wih[l], False, bias=bias[l],
-                                 out=xps[l][t0:t1].view(-1, 4 * H))
-                    mod.lstm_rows_fwd_range(xps[l][t0:t1], whh[l], h0s[l], c0s[l], hseq[l], cseq[l], acts[l],
-                                            t0, t1, 0)
-                    done[l][ci] = _event(rec[l])
-        for s in side:
-            main.wait_stream(s)
+        rec = pipeline_streams(dev, L)
+
+        def project(l, t0, t1):  # this chunk's input projection
+            gemm_f32(hseq[l - 1][t0:t1].view(-1, H), False, wih[l], False, bias=bias[l],
+                     out=xps[l][t0:t1].view(-1, 4 * H))
+
+        def recur(l, t0, t1):
+            mod.lstm_rows_fwd_range(xps[l][t0:t1], whh[l], h0s[l], c0s[l], hseq[l], cseq[l], acts[l], t0, t1, 0)
+
+        pipeline_forward(rec, chunks, project, recur)
+        pipeline_join(rec)
         hn = x.new_empty(L, B, H)
         cn = x.new_empty(L, B, H)
         for l in range(L):
@@ -515,8 +562,6 @@ class _PipelinedLSTMStack(torch.autograd.Function):
         T, B, I = x.shape
         dev = x.device
         mod = _ext.native(dev)
-        main = torch.cuda.current_stream(dev)
-        rec = [_pipe_stream(dev, l) for l in range(L)]
         dgates = [x.new_empty(T, B, 4 * H) for _ in range(L)]
         douts = [x.new_empty(T, B, H) for _ in range(L - 1)]
         douts.append(dhseq.float().contiguous() if dhseq is not None else None)
@@ -529,33 +574,27 @@ class _PipelinedLSTMStack(torch.autograd.Function):
         dwih = [x.new_empty(4 * H, t.shape[2]) for t in ins]
         dwhh = [x.new_empty(4 * H, H) for _ in range(L)]
         db = [x.new_empty(4 * H) for _ in range(L)]
-        side = rec[1:]
-        for s in side:
-            s.wait_stream(main)
-        done = [[None] * len(chunks) for _ in range(L)]
-        last = len(chunks) - 1
-        for ci in range(last, -1, -1):
-            t0, t1 = chunks[ci]
-            for l in range(L - 1, -1, -1):
-                with torch.cuda.stream(rec[l]):
-                    if l < L - 1:  # this chunk's dout = dX of the layer above
-                        rec[l].wait_event(done[l + 1][ci])
-                        # (one K slice: split-K partials and their sum beside the
-                        # recurrences cost more than they recover, profiles/r4/pipe/p6_*)
-                        gemm_f32(dgates[l + 1][t0:t1].view(-1, 4 * H), False, wp[l + 1], True,
-                                 out=douts[l][t0:t1].view(-1, H), splitk=1)
-                    dout = douts[l][t0:t1] if douts[l] is not None else None
-                    mod.lstm_rows_bwd_range(dout, dhn_l[l] if ci == last else dhb[l],
-                                            dcn_l[l] if ci == last else dcb[l], wt[l], cseq[l], acts[l], c0s[l],
-                                            dgates[l], dhb[l], dcb[l], carry[l], t0, t1, 0)
-                    done[l][ci] = _event(rec[l])
-                    if ci == 0:  # the layer's recurrence is done: its weight gradients, on its stream
-                        _chunk_weight_grads(dwih[l], dwhh[l], db[l], dgates[l], hseq[l], h0s[l], ins[l], 0, T, True)
+        rec = pipeline_streams(dev, L)
+
+        def project(l, t0, t1):  # this chunk's dout = dX of the layer above
+            # (one K slice: split-K partials and their sum beside the
+            # recurrences cost more than they recover, profiles/r4/pipe/p6_*)
+            gemm_f32(dgates[l + 1][t0:t1].view(-1, 4 * H), False, wp[l + 1], True, out=douts[l][t0:t1].view(-1, H),
+                     splitk=1)
+
+        def recur(l, first, t0, t1):
+            dout = douts[l][t0:t1] if douts[l] is not None else None
+            mod.lstm_rows_bwd_range(dout, dhn_l[l] if first else dhb[l], dcn_l[l] if first else dcb[l], wt[l],
+                                    cseq[l], acts[l], c0s[l], dgates[l], dhb[l], dcb[l], carry[l], t0, t1, 0)
+
+        def finish(l):  # the layer's recurrence is done: its weight gradients, on its stream
+            _chunk_weight_grads(dwih[l], dwhh[l], db[l], dgates[l], hseq[l], h0s[l], ins[l], 0, T, True)
+
+        pipeline_backward(rec, chunks, project, recur, finish)
         dx = None
         if ctx.needs_input_grad[0]:  # (layer 0's stream is the caller's)
             dx = gemm_f32(dgates[0].view(T * B, 4 * H), False, wp[0], True)[0].view(T, B, I)
-        for s in side:
-            main.wait_stream(s)
+        pipeline_join(rec)
         grads: List[Optional[Tensor]] = []
         for l in range(L):
             grads += [dwih[l], dwhh[l]]

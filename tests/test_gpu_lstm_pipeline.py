@@ -67,12 +67,13 @@ def test_pipeline_matches_whole_sequence_and_fp64(L, chunks, B, T, I, bias, stat
         assert _rel(pipe[k], ref[k]) < 1e-4, k
 
 
-def test_pipeline_runs_beside_the_default_stream():
-    """Two training steps through the motion model at H = 128: the per-layer
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+def test_pipeline_runs_beside_the_default_stream(cell):
+    """Three training steps through the motion model at H = 128: the per-layer
     streams join the caller's stream (no stale reads across steps)."""
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     torch.manual_seed(3)
-    model = MotionModel(9, 128, 2, 6).cuda()
+    model = MotionModel(9, 128, 2, 6, cell=cell).cuda()
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     x = torch.randn(64, 32, 9, device="cuda")
     y = torch.randint(0, 6, (64,), device="cuda")
@@ -84,7 +85,7 @@ def test_pipeline_runs_beside_the_default_stream():
         opt.step()
         losses.append(float(loss))
     torch.manual_seed(3)
-    ref = MotionModel(9, 128, 2, 6).cuda()
+    ref = MotionModel(9, 128, 2, 6, cell=cell).cuda()
     import os
     os.environ["PDRNN_LARGE_PIPE"] = "0"
     try:
@@ -100,3 +101,49 @@ def test_pipeline_runs_beside_the_default_stream():
         del os.environ["PDRNN_LARGE_PIPE"]
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 1e-5 * max(1.0, abs(b))
+
+
+def _run_gru(m, x, h0, g):
+    for p in m.parameters():
+        p.grad = None
+    xa = x.clone().requires_grad_(True)
+    h0a = h0.clone().requires_grad_(True) if h0 is not None else None
+    out, hn = m(xa, h0a)
+    ((out * g).sum() + 0.7 * hn.sum()).backward()
+    res = {"out": out, "hn": hn, "dx": xa.grad}
+    if h0 is not None:
+        res["dh0"] = h0a.grad
+    res.update({n: p.grad.clone() for n, p in m.named_parameters()})
+    return res
+
+
+@pytest.mark.parametrize("L,chunks,B,T,I,bias,state", [(2, 3, 40, 16, 9, True, False), (3, 5, 17, 7, 128, False, True),
+                                                       (2, 1, 16, 5, 9, True, True), (2, 12, 20, 12, 9, True, True)])
+def test_gru_pipeline_matches_whole_sequence_and_fp64(L, chunks, B, T, I, bias, state, monkeypatch):
+    from pytorch_distributed_rnn_amd.models.rnn import GRU
+    from pytorch_distributed_rnn_amd.ops import gru_large
+    torch.manual_seed(8)
+    H = 128
+    m = GRU(I, H, L, batch_first=True, bias=bias).cuda()
+    x = torch.randn(B, T, I, device="cuda")
+    h0 = torch.randn(L, B, H, device="cuda") if state else None
+    g = torch.randn(B, T, H, device="cuda")
+    monkeypatch.setenv("PDRNN_LARGE_CHUNKS", str(chunks))
+    calls = []
+    orig = gru_large._PipelinedGRUStack.apply
+    monkeypatch.setattr(gru_large._PipelinedGRUStack, "apply", lambda *a: calls.append(1) or orig(*a))
+    pipe = _run_gru(m, x, h0, g)
+    assert calls, "the pipelined GRU stack did not run"
+    monkeypatch.setenv("PDRNN_LARGE_PIPE", "0")
+    whole = _run_gru(m, x, h0, g)
+    assert len(calls) == 1
+    ref_m = torch.nn.GRU(I, H, L, batch_first=True, bias=bias).double().cuda()
+    with torch.no_grad():
+        for (_, p), (_, q) in zip(m.named_parameters(), ref_m.named_parameters()):
+            q.copy_(p.double())
+    ref = _run_gru(ref_m, x.double(), h0.double() if state else None, g.double())
+    for k in pipe:
+        if k in ("out", "hn"):
+            assert torch.equal(pipe[k], whole[k]), k
+        assert _rel(pipe[k], whole[k]) < 1e-5, k
+        assert _rel(pipe[k], ref[k]) < 1e-4, k

@@ -1,4 +1,4 @@
-# fp32 --hidden 128 stacked-layer pipeline: tests, then a bench A/B (one gpurun call):
+# fp32 --hidden 128 stacked-layer pipeline (CELL=gru for the GRU): tests, then a bench A/B (one gpurun call):
 #   bash tools/gpu_pipe.sh TAG "ENV1=... ENV2=..." ...   (the first run is the default)
 set -e
 export TMPDIR=/tmp
