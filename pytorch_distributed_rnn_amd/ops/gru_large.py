@@ -113,6 +113,7 @@ class _LargeGRULayer(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, h0, cfg, *weights):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero fill (lstm_large.run_recurrence)
         H, ndir, tile = cfg
         cdt = x.dtype
         T, B, I = x.shape
@@ -142,11 +143,13 @@ class _LargeGRULayer(torch.autograd.Function):
         cdt = x.dtype
         T, B, I = x.shape
         mod = _ext.native(x.device)
-        dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
-        dhn_f = dhn.float().contiguous() if dhn is not None else None
-        dgates, dh0, _ = run_recurrence(
-            dhseq, lambda: mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1),
-            [dout, dhn_f, hs32, acts, h0f, *wt])
+
+        def bptt():
+            dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
+            dhn_f = dhn.float().contiguous() if dhn is not None else None
+            return mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1)
+
+        dgates, dh0, _ = run_recurrence(dhseq, bptt, [dhseq, dhn, hs32, acts, h0f, *wt])
         grads: List[Optional[Tensor]] = []
         dx = None
         dx_pairs = []
@@ -214,6 +217,7 @@ class _PipelinedGRUStack(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, h0, cfg, *weights):
+        ctx.set_materialize_grads(False)
         H, L, per, chunks = cfg
         T, B, I = x.shape
         dev = x.device

@@ -217,8 +217,17 @@ def overlap_on() -> bool:
 def run_recurrence(dhseq: Optional[Tensor], fn, inputs: Sequence[Optional[Tensor]]):
     """fn() -> tensors: the layer's backward recurrence, on the side stream
     when the upstream gradient carries a ready event (see above), inline
-    otherwise."""
+    otherwise.  ``inputs``: the tensors fn reads, as autograd delivered them;
+    fn converts them itself, so any conversion kernel runs on the side stream
+    after the event.  The event covers the main stream up to the dX GEMM
+    only, so the layer's Function must not let autograd materialise zero
+    gradients (``ctx.set_materialize_grads(False)``): such a zero fill is
+    queued on the main stream after the event, and the side stream read it
+    before it ran (uninitialised dc carry: wrong gradients one run in a few,
+    tools/pipe_determinism.py)."""
     ev = getattr(dhseq, "_pdrnn_ready", None) if dhseq is not None else None
+    if ev is not None and getattr(dhseq, "_pdrnn_ready_version", None) != dhseq._version:
+        ev = None  # written after the event (e.g. an in-place gradient accumulation)
     if ev is None or not overlap_on():
         return fn()
     main = torch.cuda.current_stream(dhseq.device)
@@ -242,6 +251,7 @@ def mark_ready(dx: Optional[Tensor]) -> Optional[Tensor]:
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dx.device))
         dx._pdrnn_ready = ev
+        dx._pdrnn_ready_version = dx._version
     return dx
 
 
@@ -274,6 +284,7 @@ class _LargeLSTMLayer(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, h0, c0, cfg, *weights):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero fill (run_recurrence)
         hidden, ndir, tile = cfg
         cdt = x.dtype
         T, B, I = x.shape
@@ -315,13 +326,15 @@ class _LargeLSTMLayer(torch.autograd.Function):
         cdt = x.dtype
         T, B, I = x.shape
         mod = _ext.native(x.device)
-        dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
-        dhn_f = dhn.float().contiguous() if dhn is not None else None
-        dcn_f = dcn.float().contiguous() if dcn is not None else None
         wt = list(whh)                                              # [H, 4H], gate-blocked
-        dgates, dh0, dc0 = run_recurrence(
-            dhseq, lambda: mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile, 0),
-            [dout, dhn_f, dcn_f, cseq, acts, c0c, *wt])
+
+        def bptt():
+            dout = dhseq.to(cdt).contiguous() if dhseq is not None else None
+            dhn_f = dhn.float().contiguous() if dhn is not None else None
+            dcn_f = dcn.float().contiguous() if dcn is not None else None
+            return mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile, 0)
+
+        dgates, dh0, dc0 = run_recurrence(dhseq, bptt, [dhseq, dhn, dcn, cseq, acts, c0c, *wt])
         grads: List[Optional[Tensor]] = []
         dx = None
         need_dx = ctx.needs_input_grad[0]
@@ -512,6 +525,7 @@ class _PipelinedLSTMStack(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, h0, c0, cfg, *weights):
+        ctx.set_materialize_grads(False)
         H, L, per, chunks = cfg
         T, B, I = x.shape
         dev = x.device

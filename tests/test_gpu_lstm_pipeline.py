@@ -70,11 +70,13 @@ def test_pipeline_matches_whole_sequence_and_fp64(L, chunks, B, T, I, bias, stat
 @pytest.mark.parametrize("cell", ["lstm", "gru"])
 def test_pipeline_runs_beside_the_default_stream(cell):
     """Three training steps through the motion model at H = 128: the per-layer
-    streams join the caller's stream (no stale reads across steps)."""
+    streams join the caller's stream (no stale reads across steps).  SGD, not
+    Adam: Adam's first steps are ~lr * sign(g), so gradients that agree to
+    1e-6 can still move a near-zero-gradient weight in opposite directions."""
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     torch.manual_seed(3)
     model = MotionModel(9, 128, 2, 6, cell=cell).cuda()
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    opt = torch.optim.SGD(model.parameters(), lr=0.5)
     x = torch.randn(64, 32, 9, device="cuda")
     y = torch.randint(0, 6, (64,), device="cuda")
     losses = []
@@ -89,7 +91,7 @@ def test_pipeline_runs_beside_the_default_stream(cell):
     import os
     os.environ["PDRNN_LARGE_PIPE"] = "0"
     try:
-        opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+        opt = torch.optim.SGD(ref.parameters(), lr=0.5)
         ref_losses = []
         for _ in range(3):
             opt.zero_grad()
@@ -101,6 +103,7 @@ def test_pipeline_runs_beside_the_default_stream(cell):
         del os.environ["PDRNN_LARGE_PIPE"]
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 1e-5 * max(1.0, abs(b))
+    assert losses[-1] < losses[0]
 
 
 def _run_gru(m, x, h0, g):
@@ -147,3 +150,31 @@ def test_gru_pipeline_matches_whole_sequence_and_fp64(L, chunks, B, T, I, bias, 
             assert torch.equal(pipe[k], whole[k]), k
         assert _rel(pipe[k], whole[k]) < 1e-5, k
         assert _rel(pipe[k], ref[k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
+def test_layer_by_layer_overlap_matches_serial(cell, monkeypatch):
+    """The layer-by-layer path's cross-layer backward overlap (the layer
+    below's BPTT on a side stream after the layer above's dX event) gives the
+    serial path's gradients bit for bit, run after run.  The motion model
+    leaves the LSTM's cell-state output unused: before its Functions stopped
+    materialising zero gradients, that zero fill was queued on the main stream
+    after the event and the side stream sometimes read it first."""
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.setenv("PDRNN_LARGE_PIPE", "0")
+    torch.manual_seed(5)
+    model = MotionModel(9, 128, 2, 6, cell=cell).cuda()
+    x = torch.randn(96, 40, 9, device="cuda")
+    y = torch.randint(0, 6, (96,), device="cuda")
+
+    def grads():
+        model.zero_grad()
+        torch.nn.functional.cross_entropy(model(x), y).backward()
+        return [p.grad.clone() for p in model.parameters()]
+
+    monkeypatch.setenv("PDRNN_LARGE_OVERLAP", "0")
+    ref = grads()
+    monkeypatch.setenv("PDRNN_LARGE_OVERLAP", "1")
+    for _ in range(4):
+        for a, b in zip(grads(), ref):
+            assert torch.equal(a, b)
