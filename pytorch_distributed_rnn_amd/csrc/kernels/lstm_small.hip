@@ -1592,9 +1592,6 @@ hipError_t launch_fwd_gs(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Lanes per hidden unit of the unit-group backward: 8 when the workgroup still
-// fits (NL*H*8 <= 512; shorter per-lane row slices), else 4.
-// PDRNN_LSTM_BWD_L=4|8 overrides (sweeps).
 // lanes per hidden unit of the unit-group backward: 8 at H = 64 (row slices
 // of 32), else 4
 template <int H>
