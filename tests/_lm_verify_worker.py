@@ -34,9 +34,12 @@ def main():
     tr.settle()
     torch.cuda.synchronize()
     flat = torch.cat([p.detach().double().reshape(-1) for p in tr.inner.parameters()])
-    print(json.dumps({"rank": tr.rank, "verify": mod.persist_verify_mode(), "fallbacks": mod.persist_fallbacks(),
+    rec = json.dumps({"rank": tr.rank, "verify": mod.persist_verify_mode(), "fallbacks": mod.persist_fallbacks(),
                       "disabled": bool(mod.persist_disabled()), "checksum": float(flat.sum()),
-                      "abs": float(flat.abs().sum()), "losses": [float(x) for x in losses]}), flush=True)
+                      "abs": float(flat.abs().sum()), "losses": [float(x) for x in losses]})
+    # one file per rank: the ranks' stdout lines interleave under torch.distributed.run
+    with open(f"verify_rank{tr.rank}.json", "w") as f:
+        f.write(rec + "\n")
     env.shutdown()
 
 

@@ -29,12 +29,15 @@ def _gpu_env(extra=None):
     return env
 
 
-@pytest.mark.parametrize("mode", ["distributed", "horovod"])
-def test_two_ranks_one_gpu_match_single_process(tmp_path, mode):
-    local = batch_losses(run([sys.executable, MAIN] + COMMON + ["local"], cwd=str(tmp_path), env=_gpu_env(),
+@pytest.mark.parametrize("mode,hidden", [("distributed", 32), ("horovod", 32), ("distributed", 128)])
+def test_two_ranks_one_gpu_match_single_process(tmp_path, mode, hidden):
+    """hidden 128: the fp32 large-H path (row-owning kernels, stacked-layer
+    chunk pipeline on per-layer streams) under the DDP gradient hooks."""
+    common = COMMON + ["--hidden-units", str(hidden)]
+    local = batch_losses(run([sys.executable, MAIN] + common + ["local"], cwd=str(tmp_path), env=_gpu_env(),
                              timeout=110))[0]
     out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-               "--master-addr=127.0.0.1", f"--master-port={free_port()}", MAIN] + COMMON + [mode],
+               "--master-addr=127.0.0.1", f"--master-port={free_port()}", MAIN] + common + [mode],
               cwd=str(tmp_path), env=_gpu_env({"PDRNN_BACKEND": "gloo"}), timeout=110)
     per = batch_losses(out)
     assert sorted(per) == [0, 1] and len(per[0]) == len(local) == 2
@@ -55,10 +58,13 @@ def test_two_rank_deferred_persist_verification(tmp_path):
     worker = os.path.join(ROOT, "tests", "_lm_verify_worker.py")
 
     def job(extra):
-        out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                   "--master-addr=127.0.0.1", f"--master-port={free_port()}", worker],
-                  cwd=str(tmp_path), env=_gpu_env(extra), timeout=150)
-        recs = [json.loads(line) for line in out.splitlines() if line.startswith("{\"rank\"")]
+        for r in (0, 1):
+            (tmp_path / f"verify_rank{r}.json").unlink(missing_ok=True)
+        run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+             "--master-addr=127.0.0.1", f"--master-port={free_port()}", worker],
+            cwd=str(tmp_path), env=_gpu_env(extra), timeout=150)
+        recs = [json.loads((tmp_path / f"verify_rank{r}.json").read_text()) for r in (0, 1)
+                if (tmp_path / f"verify_rank{r}.json").exists()]
         return {r["rank"]: r for r in recs}
 
     got = job({"PDRNN_TEST_INJECT_RANK": "0"})
