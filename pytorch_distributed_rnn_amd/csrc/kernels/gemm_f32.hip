@@ -79,6 +79,23 @@ __device__ __forceinline__ float4 quad(const void* p, int64_t ld, int r, int c, 
   return make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// the same without bounds checks (a tile known to be in range, vec layout)
+template <int IN>
+__device__ __forceinline__ float4 quad_nb(const void* p, int64_t i) {
+  if constexpr (IN == 2) {
+    return *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p) + i);
+    if constexpr (IN == 0) {
+      return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                         __uint_as_float(u.y & 0xffff0000u));
+    } else {
+      const __half2 h0 = __builtin_bit_cast(__half2, u.x), h1 = __builtin_bit_cast(__half2, u.y);
+      return make_float4(__low2float(h0), __high2float(h0), __low2float(h1), __high2float(h1));
+    }
+  }
+}
+
 template <int BN, int GF_BK>
 struct GfCfg {
   static constexpr int WN_WAVES = BN == 128 ? 2 : 1;
@@ -131,6 +148,33 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
       if (q < BN * GF_BK / 4) {
         if constexpr (BKM) xb[j] = quad<IN>(B, ldb, k0 + q / (BN / 4), n0 + (q % (BN / 4)) * 4, K, p.N, vec);
         else xb[j] = quad<IN>(B, ldb, n0 + q / (GF_BK / 4), k0 + (q % (GF_BK / 4)) * 4, p.N, K, vec);
+      }
+    }
+  };
+  // the same for a tile known to be in range (vec layout): straight-line
+  // vector loads.  Run from a loop of its own: with the bounds-checked loads
+  // in the same loop, the divergent branches around them made the compiler
+  // join register copies of the loaded values -- and wait for every load
+  // (s_waitcnt vmcnt(0)) -- before the MFMAs, so the next tile's loads never
+  // overlapped them (profiles/r4/gemm_probe/)
+  auto load_fast = [&](int t, float4 (&xa)[Cfg::A_QUADS], float4 (&xb)[Cfg::B_QUADS]) {
+    const bool s2 = t >= nt1;
+    const void* A = s2 ? p.A2 : p.A;
+    const void* B = s2 ? p.B2 : p.B;
+    const int64_t lda = s2 ? p.lda2 : p.lda, ldb = s2 ? p.ldb2 : p.ldb;
+    const int k0 = (s2 ? t - nt1 : t) * GF_BK;
+#pragma unroll
+    for (int j = 0; j < Cfg::A_QUADS; ++j) {
+      const int q = tid + j * GF_THREADS;
+      if constexpr (AKM) xa[j] = quad_nb<IN>(A, (int64_t)(k0 + q / (GF_BM / 4)) * lda + m0 + (q % (GF_BM / 4)) * 4);
+      else xa[j] = quad_nb<IN>(A, (int64_t)(m0 + q / (GF_BK / 4)) * lda + k0 + (q % (GF_BK / 4)) * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < Cfg::B_QUADS; ++j) {
+      const int q = tid + j * GF_THREADS;
+      if ((BN * GF_BK / 4) % GF_THREADS == 0 || q < BN * GF_BK / 4) {  // (compile-time true when B tiles evenly)
+        if constexpr (BKM) xb[j] = quad_nb<IN>(B, (int64_t)(k0 + q / (BN / 4)) * ldb + n0 + (q % (BN / 4)) * 4);
+        else xb[j] = quad_nb<IN>(B, (int64_t)(n0 + q / (GF_BK / 4)) * ldb + k0 + (q % (GF_BK / 4)) * 4);
       }
     }
   };
@@ -242,13 +286,24 @@ __global__ void __launch_bounds__(GF_THREADS) gemm_f32_kernel(PdrnnGemmF32Args p
     store(0, ra, rb);
   }
   __syncthreads();
-  for (int t = t_begin; t < t_end; ++t) {
-    const bool more = t + 1 < t_end;
-    if (more) load(t + 1, ra, rb);  // in flight during the MFMAs below
-    compute(buf);
-    if (more) store(buf ^ 1, ra, rb);
-    __syncthreads();
-    buf ^= 1;
+  if (vec && m0 + GF_BM <= p.M && n0 + BN <= p.N && p.K % GF_BK == 0 && p.K2 % GF_BK == 0) {
+    for (int t = t_begin; t < t_end; ++t) {  // every tile in range
+      const bool more = t + 1 < t_end;
+      if (more) load_fast(t + 1, ra, rb);  // in flight during the MFMAs below
+      compute(buf);
+      if (more) store(buf ^ 1, ra, rb);
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    for (int t = t_begin; t < t_end; ++t) {
+      const bool more = t + 1 < t_end;
+      if (more) load(t + 1, ra, rb);
+      compute(buf);
+      if (more) store(buf ^ 1, ra, rb);
+      __syncthreads();
+      buf ^= 1;
+    }
   }
 
   // ---- epilogue: lane holds rows 4 fk + r, column fr of every 16 x 16 tile
