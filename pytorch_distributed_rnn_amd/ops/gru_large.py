@@ -34,8 +34,8 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-from .lstm_large import (_tile, final_hidden, mark_ready, pipeline_backward, pipeline_chunks, pipeline_forward,
-                         pipeline_join, pipeline_ok, pipeline_streams, run_recurrence, stack_layers)
+from .lstm_large import (_tile, final_hidden, mark_ready, padded_cols, pipeline_backward, pipeline_chunks,
+                         pipeline_forward, pipeline_join, pipeline_ok, pipeline_streams, run_recurrence, stack_layers)
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
@@ -321,7 +321,12 @@ def _gru_weight_grads(dwih: Tensor, dwhh: Tensor, dbih: Tensor, dbhh: Tensor, G3
             gemm_f32(seg2[0], True, seg2[1], True, out=dwhh[rows])
         else:
             dwhh[rows].zero_()
-    _, rs = gemm_f32(G[:, :3 * H], True, xin.reshape(T * B, -1), True, rowsum=True, out=dwih)
+    x2 = xin.reshape(T * B, -1)
+    if x2.shape[1] % 32:  # narrow input: whole, aligned column tiles (lstm_large.padded_cols)
+        c, rs = gemm_f32(G[:, :3 * H], True, padded_cols(x2), True, rowsum=True)
+        dwih.copy_(c[:, :x2.shape[1]])
+    else:
+        _, rs = gemm_f32(G[:, :3 * H], True, x2, True, rowsum=True, out=dwih)
     dbih.copy_(rs)
     dbhh[:2 * H].copy_(rs[:2 * H])
     dbhh[2 * H:].copy_(col_sum(G[:, 3 * H:]))

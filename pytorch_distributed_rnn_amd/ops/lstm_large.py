@@ -619,6 +619,18 @@ class _PipelinedLSTMStack(torch.autograd.Function):
         return (dx, dh0, dc0, None, *grads)
 
 
+def padded_cols(x2: Tensor, mult: int = 32) -> Tensor:
+    """x2 [K, n] zero-padded to a multiple of ``mult`` columns (one copy).  A
+    weight-gradient GEMM against a narrow, unaligned input (the motion model's
+    9 features: rows of 36 bytes) runs gemm_f32's bounds-checked loop, whose
+    loads do not overlap its MFMAs; padded, every tile is whole and aligned
+    (layer 0's dW_ih 214 -> ~90 us at the motion batch, profiles/r4/gemm_probe/)."""
+    n = x2.shape[1]
+    out = x2.new_zeros(x2.shape[0], -(-n // mult) * mult)
+    out[:, :n].copy_(x2)
+    return out
+
+
 def _chunk_weight_grads(dwih: Tensor, dwhh: Tensor, db: Tensor, G3: Tensor, hd: Tensor, h0: Optional[Tensor],
                         xin: Tensor, t0: int, t1: int, first: bool) -> None:
     """Steps [t0, t1) of one unidirectional fp32 layer's dW_ih, dW_hh and db,
@@ -636,8 +648,12 @@ def _chunk_weight_grads(dwih: Tensor, dwhh: Tensor, db: Tensor, G3: Tensor, hd: 
         gemm_f32(seg0[0], True, seg0[1], True, out=dwhh, accumulate=not first)
     elif first:
         dwhh.zero_()
-    _, rs = gemm_f32(G3[t0:t1].view(-1, H4), True, xin[t0:t1].reshape(-1, xin.shape[2]), True, rowsum=True,
-                     out=dwih, accumulate=not first)
+    x2 = xin[t0:t1].reshape(-1, xin.shape[2])
+    if x2.shape[1] % 32:  # narrow input (motion: 9 features): whole, aligned column tiles
+        c, rs = gemm_f32(G3[t0:t1].view(-1, H4), True, padded_cols(x2), True, rowsum=True)
+        dwih.copy_(c[:, :x2.shape[1]]) if first else dwih.add_(c[:, :x2.shape[1]])
+    else:
+        _, rs = gemm_f32(G3[t0:t1].view(-1, H4), True, x2, True, rowsum=True, out=dwih, accumulate=not first)
     if first:
         db.copy_(rs)
     else:
