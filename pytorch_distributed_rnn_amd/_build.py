@@ -24,6 +24,11 @@ Usage::
     python -m pytorch_distributed_rnn_amd._build          # incremental
     PDRNN_DEBUG_BUILD=1 python -m pytorch_distributed_rnn_amd._build   # -O1 -g + device asserts
     python -m pytorch_distributed_rnn_amd._build --clean  # full rebuild
+    PDRNN_SANITIZE=address,undefined python -m pytorch_distributed_rnn_amd._build
+        # host runtime (comm.cpp, reducer.cpp, bindings) under ASan + UBSan (or
+        # PDRNN_SANITIZE=thread: TSan) into build_native_san_<flavour>/; load it
+        # with PDRNN_EXT_SO=<that .so> and the sanitizer runtime preloaded
+        # (tools/sanitize_host.sh).  Device code is built as usual.
 """
 from __future__ import annotations
 
@@ -48,7 +53,18 @@ def _ext_suffix() -> str:
     return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 
+def sanitize_flavour() -> str:
+    return os.environ.get("PDRNN_SANITIZE", "").strip()
+
+
+def _san_dir() -> Path:
+    tag = sanitize_flavour().replace(",", "_")
+    return PKG_DIR / f"build_native_san_{tag}"
+
+
 def ext_path() -> Path:
+    if sanitize_flavour():
+        return _san_dir() / ("_C" + _ext_suffix())
     return PKG_DIR / ("_C" + _ext_suffix())
 
 
@@ -95,15 +111,19 @@ def build(verbose: bool = False, clean: bool = False, jobs: int | None = None) -
     """Compile every HIP kernel for gfx950 plus the host runtime; link ``_C``."""
     inc, torch_lib, abi = _torch_paths()
     kernels, runtime, headers = _sources()
-    if clean and BUILD_DIR.exists():
-        shutil.rmtree(BUILD_DIR)
-    BUILD_DIR.mkdir(exist_ok=True)
+    san = sanitize_flavour()
+    build_dir = _san_dir() if san else BUILD_DIR
+    if clean and build_dir.exists():
+        shutil.rmtree(build_dir)
+    build_dir.mkdir(exist_ok=True)
     hipcc = ROCM / "bin" / "hipcc"
     py_inc = sysconfig.get_paths()["include"]
     common_inc = [f"-I{CSRC / 'include'}"]
     debug = os.environ.get("PDRNN_DEBUG_BUILD", "0") == "1"
     hip_opt = ["-O1", "-g", "-DPDRNN_DEBUG=1"] if debug else ["-O3"]
     host_opt = ["-O0", "-g", "-DPDRNN_DEBUG=1"] if debug else ["-O2"]
+    if san:  # the host TUs only (g++): device code has no sanitizer on this pool
+        host_opt = ["-O1", "-g", f"-fsanitize={san}", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"]
     hip_flags = [
         "-c", *hip_opt, "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
         "-munsafe-fp-atomics", "-Wno-unused-result", *common_inc,
@@ -120,11 +140,11 @@ def build(verbose: bool = False, clean: bool = False, jobs: int | None = None) -
 
     jobs_list = []
     for src in kernels:
-        obj = BUILD_DIR / (src.stem + ".hip.o")
+        obj = BUILD_DIR / (src.stem + ".hip.o")  # device code: shared with the plain build
         sig = _digest([src], hdr_sig + " ".join(hip_flags))
         jobs_list.append((src, obj, sig, [hipcc, *hip_flags, src, "-o", obj]))
     for src in runtime:
-        obj = BUILD_DIR / (src.stem + ".cpp.o")
+        obj = build_dir / (src.stem + ".cpp.o")
         sig = _digest([src], hdr_sig + " ".join(host_flags))
         jobs_list.append((src, obj, sig, ["g++", *host_flags, src, "-o", obj]))
 

@@ -31,6 +31,17 @@ def _try_import():
         return _C
     _TRIED = True
     try:
+        so = os.environ.get("PDRNN_EXT_SO")
+        if so:
+            # an alternative build of the extension (e.g. the sanitizer build of
+            # _build.py, PDRNN_SANITIZE): loaded under the same module name
+            import importlib.util
+            import sys
+            spec = importlib.util.spec_from_file_location("pytorch_distributed_rnn_amd._C", so)
+            _C = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+            sys.modules["pytorch_distributed_rnn_amd._C"] = _C
+            return _C
         _C = importlib.import_module("pytorch_distributed_rnn_amd._C")
     except BaseException as e:  # noqa: BLE001 - report any loader failure verbatim
         _IMPORT_ERROR = e

@@ -23,6 +23,12 @@ bool stamps_enabled() {
   static const bool on = std::getenv("PDRNN_LSTM_STAMPS") != nullptr;
   return on;
 }
+// PDRNN_SW=0: the fused motion step runs the gate-split / K-split kernel family
+// instead of the sequence-in-wave kernels (A/B); read per call (tests flip it)
+bool sw_enabled() {
+  const char* e = std::getenv("PDRNN_SW");
+  return !(e && e[0] == '0');
+}
 void report_stamps(const char* what, const Tensor& st, int iters) {
   // [grid, 8]: loop start / end shader cycles, loop start / end real time,
   // workgroup entry / exit real time (100 MHz; entry/exit 0 when not stamped)
@@ -457,19 +463,25 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   if (nb_bwd <= 0 || cell == 1) nb_bwd = 1;  // the GRU backward is single-sequence
   const int gridb = pdrnn_lstm_small_bwd_grid((int)H, (int)NL, (int)T, (int)B, (int)nb_bwd, (int)split_bwd);
   TORCH_CHECK(gridb > 0, "unsupported backward tile nb=", nb_bwd);
+  // Sequence-in-wave kernels (lstm_sw.hip: a sequence's recurrence never
+  // leaves its wave) for the motion shape; PDRNN_SW=0 keeps the gate-split /
+  // K-split family below (A/B).  Weight gradients deferred to lstm_small_dw.
+  const bool sw = sw_enabled() && pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, (int)cell) == 1 &&
+                  pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T) != 0 && T <= 640;
+  const int sw_mode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B) : -1;
   // Above one residency round the BPTT defers its weight gradients: the
   // recurrence writes the gate gradients (into `act`, in place) and the
   // matrix-core kernel lstm_small_dw forms dW / db over all B*T rows, one slab
   // row per K chunk (see pdrnn_lstm_small_bwd_dwout).  One round or less keeps
   // the one-launch step (register-resident dW, no extra launch).
   const int dw_mode = pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T);
-  const bool dwout = nb_bwd == 1 && split_bwd == 1 && ((gridb < B && dw_mode == 1) || dw_mode == 2);
+  const bool dwout = sw || (nb_bwd == 1 && split_bwd == 1 && ((gridb < B && dw_mode == 1) || dw_mode == 2));
   // deferred dW: sequences per BPTT workgroup, and whether those workgroups
   // form the dW of their own tile (one slab row per tile) or a separate
   // matrix-core launch does it over fixed K chunks
   const int nb_dw = dwout ? pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B) : (int)nb_bwd;
   // (one slab row per tile: above ~1k tiles the reduction's slab read outweighs the saved dW pass)
-  const bool dw_fused = dwout && (B + nb_dw - 1) / nb_dw <= 1024 &&
+  const bool dw_fused = !sw && dwout && (B + nb_dw - 1) / nb_dw <= 1024 &&
                         pdrnn_lstm_small_bwd_dw_ok((int)H, (int)NL, (int)T, (int)B, (int)I, nb_dw) == 1;
   const int slab_rows = dw_fused ? (int)((B + nb_dw - 1) / nb_dw)
                                  : dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
@@ -499,10 +511,17 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   f.B = (int)B; f.T = (int)T; f.I = (int)I; f.NL = (int)NL; f.cell = (int)cell;
   f.w_bf16 = round_bf16 ? 1 : 0;
   hipStream_t st = cur_stream();
+  // deferred dW: the fp32 copy of the gathered layer-0 input rows (written by
+  // the sequence-in-wave forward, or by the gate-split deferred-dW backward)
+  const int64_t xg_ld = (I + 3) / 4 * 4;
+  Tensor xg;
+  if (dwout) xg = at::empty({(B * T + 16) * xg_ld + 256}, opts);  // + one DMA job past the last 16-row stage
+  if (sw) { f.xg_out = xg.data_ptr<float>(); f.xg_ld = (int)xg_ld; }
+  const int sw_nb = sw_mode == 1 ? 2 : 1;
   Tensor st_f, st_b;
   if (stamps_enabled()) {
-    st_f = at::zeros({(B + nb_fwd - 1) / nb_fwd, 8}, opts.dtype(at::kLong));
-    st_b = at::zeros({gridb, 8}, opts.dtype(at::kLong));
+    st_f = at::zeros({sw ? (B + sw_nb - 1) / sw_nb : (B + nb_fwd - 1) / nb_fwd, 8}, opts.dtype(at::kLong));
+    st_b = at::zeros({sw ? (B + sw_nb - 1) / sw_nb : gridb, 8}, opts.dtype(at::kLong));
     f.stamps = reinterpret_cast<uint64_t*>(st_f.data_ptr<int64_t>());
   }
   // latency regime (one sequence per workgroup in both passes): forward,
@@ -510,7 +529,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const bool one_launch = !dwout && !st_f.defined() &&
       pdrnn_lstm_small_step_ok((int)H, (int)NL, (int)B, (int)nb_fwd, (int)split_fwd, (int)nb_bwd, (int)split_bwd,
                                gridb) == 1;
-  if (!one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
+  if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_fwd(&f, sw_mode, st));
+  else if (!one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
 
   PdrnnLstmSmallBwdArgs bk{};
   bk.prio = prio_env();
@@ -526,18 +546,16 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.B = (int)B; bk.T = (int)T; bk.I = (int)I; bk.NL = (int)NL; bk.cell = (int)cell;
   bk.w_bf16 = f.w_bf16;
   int grid_dw = gridb;
-  Tensor xg;
   if (dwout) {
-    grid_dw = dw_fused ? slab_rows : pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb_dw);
+    grid_dw = sw ? (int)((B + sw_nb - 1) / sw_nb)
+                 : dw_fused ? slab_rows : pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb_dw);
     TORCH_CHECK(grid_dw > 0, "deferred-dW backward: no resident grid");
-    if (st_f.defined()) {
+    if (st_f.defined() && !sw) {
       st_b = at::zeros({grid_dw, 8}, opts.dtype(at::kLong));
       bk.stamps = reinterpret_cast<uint64_t*>(st_b.data_ptr<int64_t>());
     }
     bk.dg_out = f.act;  // in place: each row lane overwrites the activation it has consumed
     bk.dg_st = 5 * H;
-    const int64_t xg_ld = (I + 3) / 4 * 4;
-    xg = at::empty({(B * T + 16) * xg_ld + 256}, opts);  // + one DMA job past the last 16-row stage
     bk.xg_out = xg.data_ptr<float>();
     bk.xg_ld = (int)xg_ld;
   }
@@ -553,16 +571,20 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     }
     dw.B = (int)B; dw.T = (int)T; dw.I = (int)I; dw.NL = (int)NL; dw.chunks = slab_rows;
   }
-  if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
+  if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_bwd(&bk, sw_mode, st));
+  else if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
   else if (dw_fused) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dw(&bk, &dw, (int)H, nb_dw, st));
   else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, nb_dw, st));
   else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
   if (dwout && !dw_fused) HIP_LAUNCH_CHECK(pdrnn_lstm_small_dw(&dw, (int)H, st));
   if (st_f.defined()) {
-    report_stamps("fwd(head step)", st_f, (int)(T + NL - 1));
-    report_stamps(dw_fused ? "bwd(head step, lean, own-tile dW)" : dwout ? "bwd(head step, lean, deferred dW)"
-                                                                    : "bwd(head step, lean)", st_b,
-                  (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_dw - 1) / ((int64_t)grid_dw * nb_dw)));
+    const int bw_iters = sw ? (int)(T + NL - 1)
+                            : (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_dw - 1) / ((int64_t)grid_dw * nb_dw));
+    report_stamps(sw ? "fwd(head step, seq-in-wave)" : "fwd(head step)", st_f, (int)(T + NL - 1));
+    report_stamps(sw ? "bwd(head step, seq-in-wave, deferred dW)"
+                     : dw_fused ? "bwd(head step, lean, own-tile dW)"
+                                : dwout ? "bwd(head step, lean, deferred dW)" : "bwd(head step, lean)",
+                  st_b, bw_iters);
   }
 
   // one-pass reduction of the slabs into the flat gradient (+ batch statistics),
@@ -746,7 +768,8 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 // PDRNN_LSTM_PERSIST != 0.  A grid-sync spin that times out (bounded at 2 s
 // in the kernel: co-residency lost, e.g. to RCCL kernels on the comm stream)
 // leaves that launch's outputs invalid.
-//   * verify on (set_persist_verify(true) -- the multi-rank trainers do it --
+//   * verify on (set_persist_verify(1) -- parallel/comm.py get_comm does it for every
+//     multi-rank GPU job --
 //     or PDRNN_LSTM_PERSIST_VERIFY=1): the host synchronises after the launch
 //     and reads its error flag; on a timeout it warns, clears the sticky flag
 //     and returns kPersistFailed, and the caller re-runs the layer on the
@@ -756,8 +779,9 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
 //     synchronisation; a sticky per-device flag is copied to pinned memory
 //     after every launch and checked at the next one (fails loudly one call
 //     later), and by persist_check() at epoch end.
-//   * verify per step (set_persist_verify(2) -- the multi-rank trainers do
-//     it): no synchronisation at all; a timed-out launch leaves the sticky
+//   * verify per step (set_persist_verify(2) -- only the LM trainer, which
+//     carries the skip word and re-runs skipped steps, switches to it:
+//     parallel/comm.py use_step_verification): no synchronisation at all; a timed-out launch leaves the sticky
 //     flag set, the step's later persistent launches run per step, the
 //     trainer all-reduces the flag on the stream and hands it to the Adam
 //     launch as its skip word (persist_sticky_flag), reads its pinned copy
@@ -795,34 +819,41 @@ int* pinned_word() {
 }
 std::vector<int*>& persist_sticky_host() { static auto& v = *new std::vector<int*>(64, nullptr); return v; }
 
-int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int dt, int64_t tile,
-                  const at::TensorOptions& opts, hipStream_t st) {
+// Row tiles of the persistent recurrence for this launch, or 0 when the
+// per-step kernels run it (PDRNN_LSTM_PERSIST=0, an explicit tile, the path
+// turned off after a timeout, the fp32 forward, or a shape it does not cover).
+int large_persist_plan(int B, int H, int ndir, bool backward, int dt, int64_t tile) {
   static const int env = [] {
     const char* e = std::getenv("PDRNN_LSTM_PERSIST");
     return e ? std::atoi(e) : 1;
   }();
-  static const bool check = [] {
-    const char* e = std::getenv("PDRNN_LSTM_PERSIST_CHECK");
-    return e && std::atoi(e) != 0;
-  }();
-  const int mode = 0;  // kernel mode bits: 16 = test hook (persist_inject_timeouts)
-  if (env == 0 || tile >= 0 || g_persist_disabled.load()) return kPersistNotRun;
+  if (env == 0 || tile >= 0 || g_persist_disabled.load()) return 0;
   // fp32 storage: the persistent backward only -- the persistent forward ran
   // 8.3 us per step against 7.1 for the per-step kernels at the fp32 motion
   // model's H = 128, B = 1440 (its K = H is too short to pay for the 8-wave
   // K split's LDS reduction; the backward's K = 4H is not: 8.6 vs 11.7 us;
   // profiles/r4/h2/h2_persist_f32_cell*.json)
-  static const bool f32_fwd = [] {
-    const char* e = std::getenv("PDRNN_LSTM_PERSIST_F32_FWD");  // A/B: the fp32 persistent forward
-    return e && std::atoi(e) != 0;
-  }();
-  if (dt == 2 && !backward && !f32_fwd) return kPersistNotRun;
+  if (dt == 2 && !backward) return 0;
   int dev = 0;
   TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
   int cus = 0;
   TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
-  const int mt = pdrnn_lstm_large_persist_mt(a.B, a.H, ndir, dt, cus);
+  // multi-rank: leave the CUs RCCL's kernels may take (comm.cpp, maxCTAs), so
+  // a bucket all-reduce resident first never keeps the grid from co-residency
+  return pdrnn_lstm_large_persist_mt(B, H, ndir, dt, cus - pdrnn::rccl_cta_reserve());
+}
+
+int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int dt, int64_t tile,
+                  const at::TensorOptions& opts, hipStream_t st) {
+  static const bool check = [] {
+    const char* e = std::getenv("PDRNN_LSTM_PERSIST_CHECK");
+    return e && std::atoi(e) != 0;
+  }();
+  const int mode = 0;  // kernel mode bits: 16 = test hook (persist_inject_timeouts)
+  const int mt = large_persist_plan(a.B, a.H, ndir, backward, dt, tile);
   if (mt == 0) return kPersistNotRun;
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
   const int nmb = (a.B + 16 * mt - 1) / (16 * mt);
   std::vector<Tensor>& sticky = persist_sticky();
   std::vector<int*>& sticky_host = persist_sticky_host();
@@ -1179,6 +1210,8 @@ Tensor gemm16(const Tensor& A, bool a_kmajor, const Tensor& B, bool b_kmajor, co
   const int dt = dtype_code(A);
   TORCH_CHECK(dtype_code(B) == dt && A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1,
               "gemm16: 2-D 16-bit operands of one dtype with unit inner stride");
+  TORCH_CHECK(!accumulate || (out.has_value() && out->defined()),
+              "gemm16: accumulate=True needs the output tensor to accumulate into");
   const int64_t M = a_kmajor ? A.size(1) : A.size(0), K = a_kmajor ? A.size(0) : A.size(1);
   const int64_t N = b_kmajor ? B.size(1) : B.size(0);
   TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == K, "gemm16: K mismatch");
@@ -1268,6 +1301,8 @@ std::vector<Tensor> gemm_f32(const Tensor& A, bool a_kmajor, const Tensor& B, bo
   const int dt = any_dtype(A);
   TORCH_CHECK(any_dtype(B) == dt && A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1,
               "gemm_f32: 2-D operands of one dtype with unit inner stride");
+  TORCH_CHECK(!accumulate || (out.has_value() && out->defined()),
+              "gemm_f32: accumulate=True needs the output tensor to accumulate into");
   const int64_t M = a_kmajor ? A.size(1) : A.size(0), K = a_kmajor ? A.size(0) : A.size(1);
   const int64_t N = b_kmajor ? B.size(1) : B.size(0);
   TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == K, "gemm_f32: K mismatch");
@@ -1406,6 +1441,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return py::make_tuple(nb, pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb),
                           pdrnn_lstm_small_bwd_dw_ok((int)H, (int)NL, (int)T, (int)B, 9, nb) == 1);
   }, "(sequences per workgroup, grid, own-tile dW) of the deferred-dW backward for this shape (9 inputs)");
+  m.def("lstm_sw_ok", [](int64_t H, int64_t I, int64_t NL) { return pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, 0) == 1; },
+        "the sequence-in-wave kernels (lstm_sw.hip) cover this LSTM stack in the fused train step");
+  m.def("lstm_sw_mode", [](int64_t NL, int64_t B) { return pdrnn_lstm_sw_mode((int)NL, (int)B); },
+        "wave map of the sequence-in-wave kernels for B sequences (0/1: a wave per 1/2 sequences, 2/3: a wave "
+        "per layer of 1/2 sequences)");
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });
@@ -1433,6 +1473,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("decoupled"), py::arg("maximize"), py::arg("lr_t") = py::none(), py::arg("step_t") = py::none(),
         py::arg("ticket") = py::none(), py::arg("skip") = py::none());
   m.def("lstm_large_fwd", &lstm_large_fwd, "large-H LSTM layer forward (MFMA step kernels, both directions)");
+  m.def("rccl_max_ctas", []() { return pdrnn::rccl_max_ctas(); },
+        "workgroup cap of the native RCCL communicators' kernels (PDRNN_RCCL_MAX_CTAS)");
+  m.def("rccl_cta_reserve", []() { return pdrnn::rccl_cta_reserve(); },
+        "CUs a persistent recurrence leaves free for RCCL in this process");
+  m.def("lstm_large_bwd_persistent",
+        [](int64_t B, int64_t H, int64_t ndir, int64_t dtype, int64_t tile) {
+          // the backward recurrence lstm_large_bwd would run as one grid-synced
+          // persistent launch (dtype 0 bf16, 1 fp16, 2 fp32): such a launch must
+          // not share the GPU with side-stream GEMMs (ops/lstm_large.py run_recurrence)
+          if (tile < 0 && dtype == 2 && rows_f32_on() && pdrnn_lstm_rows_f32_supported((int)H, 2)) return false;
+          return large_persist_plan((int)B, (int)H, (int)ndir, true, (int)dtype, tile) != 0;
+        },
+        "1 when lstm_large_bwd's recurrence would take the grid-synced persistent path");
   m.def("lstm_large_bwd", &lstm_large_bwd, "large-H LSTM layer BPTT (MFMA step kernels) -> dgates, dh0, dc0");
   m.def("lstm_large_supported", [](int64_t H) { return pdrnn_lstm_large_supported((int)H) != 0; });
   m.def("lstm_rows_range_supported", [](int64_t H) { return rows_f32_on() && pdrnn_lstm_rows_f32_supported((int)H, 2) != 0; });
@@ -1469,7 +1522,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     int dev = 0, cus = 0;
     TORCH_CHECK(hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess);
-    return pdrnn_lstm_large_persist_mt((int)B, (int)H, (int)ndir, (int)dtype, cus);
+    return pdrnn_lstm_large_persist_mt((int)B, (int)H, (int)ndir, (int)dtype, cus - pdrnn::rccl_cta_reserve());
   }, "persistent large-H recurrence: rows-per-workgroup / 16 for this shape on the current device (0 = not covered)");
   m.def("gemm_nt", &gemm_nt, "C = A Bt^T (bf16/fp16 in, f32 out) on the MFMA tile core", py::arg("A"),
         py::arg("Bt"), py::arg("tile") = -1);

@@ -56,6 +56,10 @@ typedef struct {
   int x_bf16;                // x holds bf16 values (read once into LDS; requires the LDS-resident x path)
   int prio;                  // lower the waves' issue priority as the recurrence progresses (see prio_by_progress)
   int w_bf16;                // round the fp32 W_ih / W_hh to bf16 as they are loaded (bf16 models: no cast pass)
+  // sequence-in-wave forward (lstm_sw.hip): the staged, widened layer-0 input
+  // rows [B*T][xg_ld] for the deferred-dW kernel (NULL: not written)
+  float* xg_out;
+  int xg_ld;
 } PdrnnLstmSmallFwdArgs;
 
 typedef struct {
@@ -158,6 +162,30 @@ int pdrnn_lstm_small_step_ok(int H, int NL, int B, int nb_fwd, int split_fwd, in
                              int gridb);
 hipError_t pdrnn_lstm_small_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBwdArgs* b, int H,
                                  hipStream_t stream);
+
+// ----------------------------------------------------------------------------
+// Sequence-in-wave LSTM stack (kernels/lstm_sw.hip): H = 32, 1 or 2 layers,
+// input size <= 12, lean training contract (zero initial state, loss through
+// the fused head on h_T).  A sequence's whole recurrence lives in ONE wave
+// (mode 0: one sequence per wave, mode 1: two), or in one wave per layer of a
+// 2-layer stack (mode 2), so h_t never crosses a workgroup barrier inside a
+// layer.  The forward writes act / hseq / xg_out like the gate-split forward
+// plus the head's slab rows; the backward writes the gate gradients over the
+// activations (dg_out = act, dg_st = 5H) for pdrnn_lstm_small_dw.
+// ----------------------------------------------------------------------------
+int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell);
+// mode for a batch of B sequences (PDRNN_SW_MODE overrides): 0, 1 or 2
+int pdrnn_lstm_sw_mode(int NL, int B);
+hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode, hipStream_t stream);
+hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode, hipStream_t stream);
+
+// bf16 matrix-core recurrence (kernels/lstm_mb.hip) for bf16 models: same
+// shapes and contracts as the sequence-in-wave kernels, 16 sequences per
+// workgroup, the recurrent products on v_mfma_f32_16x16x32_bf16 (h_t, x_t and
+// the gate gradients rounded to bf16 as operands, fp32 accumulation / state).
+int pdrnn_lstm_mb_ok(int H, int I, int NL, int cell, int T);
+hipError_t pdrnn_lstm_mb_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t stream);
+hipError_t pdrnn_lstm_mb_bwd(const PdrnnLstmSmallBwdArgs* a, hipStream_t stream);
 
 // Column sums of a [rows, P] fp32 slab into out[P] (out = beta*out + sum).
 // Two deterministic passes through `work` ([split, P] floats, split <= 64).

@@ -80,6 +80,12 @@ constexpr int kWatchdogExit = 86;
 // before the call returns -- A/B switch for overlap / stream-ordering bugs.
 bool serialize_comm();
 
+// CU budget of RCCL's kernels (PDRNN_RCCL_MAX_CTAS) and the CUs a persistent
+// grid must leave free in this process (0 until a multi-rank RCCL
+// communicator exists)
+int rccl_max_ctas();
+int rccl_cta_reserve();
+
 std::shared_ptr<Comm> make_rccl_comm(const std::string& uid, int rank, int world, int device, bool high_priority,
                                      double timeout_s);
 std::shared_ptr<Comm> make_pg_comm(const pybind11::object& process_group);

@@ -1,0 +1,781 @@
+// Sequence-in-wave LSTM stack (H = 32, 1-2 layers), forward and lean BPTT,
+// fp32, gfx950.  The motion model's recurrence (reference: nn.LSTM in
+// src/motion/model.py:9,14, trained by src/motion/trainer/base.py:111,116).
+//
+// Why a second small-H family (docs/DESIGN.md §2b): the gate-split kernels of
+// lstm_small.hip spread one sequence over 4 waves (a layer = 128 lanes, one
+// gate row each), so every step broadcasts the 64-float operand vector from
+// LDS to all 4 waves (16 ds_read_b128 per lane, the LDS serialises the four
+// waves' reads: ~276 of 966 cycles at B = 180) and crosses an s_barrier
+// (~216 cycles).  Here a sequence never leaves its wave:
+//
+//  * lane = (unit u = lane >> 1, K half s = lane & 1).  A lane holds the four
+//    gate rows q*H + u of [W_ih | W_hh] over ITS half of the operand vector
+//    (layer >= 1: s = 0 the input h^{l-1}_t, s = 1 the own h_{t-1}; layer 0:
+//    s = 0 x_t (12 columns, zero-padded) + h[0, 12), s = 1 h[12, 32)), as k
+//    pairs for v_pk_fma_f32.  Half the operand vector per lane: 8 (layer 1) /
+//    6 (layer 0) ds_read_b128 per step, the two halves' addresses on disjoint
+//    banks.  One DPP swap adds the partner's partial sums.
+//  * lane s = 0 activates i, g and lane s = 1 f, o (rows pre-scaled by
+//    -log2 e, x2 for g: sigma = 1 / (1 + 2^z), tanh(g) = 2 sigma(2g) - 1); two
+//    DPP swaps give both lanes all four gates; both update c, h.
+//  * h_t goes to a per-wave LDS slot and is read back by the same wave next
+//    step: LDS operations of one wave execute in order, so no barrier and no
+//    waitcnt beyond the reads' own.  Mode 2 runs each layer of a 2-layer
+//    stack in its own wave (one barrier per step, h^0 handed over through
+//    parity slots) for the latency regime.
+//  * BPTT, per layer: lane (u, s) owns column u of W_hh (and W_ih for
+//    layers >= 1: the input gradient feeding the layer below) over gate rows
+//    [64 s, 64 s + 64); the row phase makes the lane's two pre-activation gate
+//    gradients (s = 0: i, f; s = 1: g, o) from the saved activations, writes
+//    them to LDS and over the activation slots (deferred dW, lstm_small_dw.hip),
+//    and the column phase reads its 64 rows back (16 ds_read_b128) for
+//    W^T dz; one DPP swap completes the sums.  Layer 1's input gradient
+//    stays in registers for layer 0's next step (mode 2: LDS parity slots).
+//  * Whole sequences per wave, so the grid is B / NB waves, at most one wave
+//    per SIMD (~300-400 VGPRs: every weight in registers).
+#include "pdrnn/api.h"
+#include "pdrnn/common.h"
+#include "pdrnn/motion_head.h"
+
+#include <cstdlib>
+
+namespace pdrnn {
+namespace {
+
+constexpr int kH = 32;
+constexpr float kA = -1.4426950408889634f;  // -log2(e): rows pre-scaled so sigma(z) = 1 / (1 + 2^acc)
+constexpr int kHB = 36;                     // h slot: 32 values + a zero chunk (layer 0, s = 1, chunk 5)
+constexpr int kXS = 12;                     // staged x row: I <= 12 columns, zero-padded
+constexpr int kDZ = 4 * kH + 4;             // dz vector, rows >= 64 shifted by 4 floats (bank spread)
+constexpr uint32_t kOOR = 0x80000000u;      // buffer offset past the range: the store is dropped
+
+// bf16 models: fp32 masters rounded to bf16 as they load (round to nearest even)
+PDRNN_DEVICE float wround(float v, int w_bf16) { return w_bf16 ? (float)(__bf16)v : v; }
+PDRNN_DEVICE float sig2(float z) { return fast_rcp(1.f + __builtin_amdgcn_exp2f(z)); }
+PDRNN_DEVICE float tanh_c(float c) { return fmaf(sig2(c * (2.f * kA)), 2.f, -1.f); }
+PDRNN_DEVICE float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+PDRNN_DEVICE pdrnn_f2 lo2(float4 v) { return pdrnn_f2{v.x, v.y}; }
+PDRNN_DEVICE pdrnn_f2 hi2(float4 v) { return pdrnn_f2{v.z, v.w}; }
+PDRNN_DEVICE pdrnn_f2 pfma(pdrnn_f2 a, pdrnn_f2 b, pdrnn_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+PDRNN_DEVICE void bstore(float v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, so, 0);
+}
+PDRNN_DEVICE int dz_slot(int r) { return r + (r >= 2 * kH ? 4 : 0); }
+// sum of this lane's value and its K-half partner's (lanes 2u, 2u + 1)
+PDRNN_DEVICE float pair_sum(float v) { return v + dpp_swap1(v); }
+
+template <int NB>
+PDRNN_DEVICE int pick(const int (&v)[NB], int n) {
+  if constexpr (NB == 1) return v[0];
+  else return n == 0 ? v[0] : v[1];
+}
+
+// ---------------------------------------------------------------------------
+// Forward
+// ---------------------------------------------------------------------------
+// this lane's four gate rows over NC float4 chunks of its operand half, k pairs
+template <int NC>
+struct FwdW {
+  pdrnn_f2 w[4][2 * NC];
+  float bias[4];
+};
+
+// Column of chunk c, element e (-1: zero) -- see the file comment.
+PDRNN_DEVICE int fwd_col(int l, int s, int c, int e, int Iin, bool& from_ih) {
+  if (l == 0) {
+    if (s == 0) {
+      if (c < 3) { from_ih = true; const int k = 4 * c + e; return k < Iin ? k : -1; }
+      from_ih = false; return 4 * (c - 3) + e;
+    }
+    from_ih = false; return c < 5 ? 12 + 4 * c + e : -1;
+  }
+  from_ih = s == 0;
+  return 4 * c + e;
+}
+
+template <int NC>
+PDRNN_DEVICE FwdW<NC> load_fwd_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, int s) {
+  FwdW<NC> W;
+  const int Iin = l == 0 ? a.I : kH;
+  const float* wih = a.w_ih[l];
+  const float* whh = a.w_hh[l];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = q * kH + u;
+    const float sc = kA * (q == 2 ? 2.f : 1.f);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bool ih = false;
+        const int k = fwd_col(l, s, c, e, Iin, ih);
+        float x = 0.f;
+        if (k >= 0) x = ih ? wih[(int64_t)r * Iin + k] : whh[(int64_t)r * kH + k];
+        v[e] = wround(x, a.w_bf16) * sc;
+      }
+      W.w[q][2 * c] = pdrnn_f2{v[0], v[1]};
+      W.w[q][2 * c + 1] = pdrnn_f2{v[2], v[3]};
+    }
+    W.bias[q] = ((a.b_ih[l] ? wround(a.b_ih[l][r], a.w_bf16) : 0.f) +
+                 (a.b_hh[l] ? wround(a.b_hh[l][r], a.w_bf16) : 0.f)) * sc;
+  }
+  return W;
+}
+
+template <int NC>
+PDRNN_DEVICE void fwd_dot(const FwdW<NC>& W, const float4 (&v)[NC], float (&p)[4]) {
+  pdrnn_f2 acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[q] = pfma(W.w[q][2 * c], lo2(v[c]), acc[q]);
+      acc[q] = pfma(W.w[q][2 * c + 1], hi2(v[c]), acc[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = acc[q].x + acc[q].y;
+}
+
+struct Cell {
+  float a0, a1, c, h;
+};
+// partial sums of both K halves -> this lane's two activations (s = 0: i, g;
+// s = 1: f, o) and the unit's new c, h (on both lanes)
+PDRNN_DEVICE Cell fwd_cell(const float (&p)[4], const float (&bias)[4], float c, bool odd) {
+  float tot[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tot[q] = pair_sum(p[q]) + bias[q];
+  const float z0 = odd ? tot[1] : tot[0];
+  const float z1 = odd ? tot[3] : tot[2];
+  const float a0 = sig2(z0);
+  const float s1 = sig2(z1);
+  const float a1 = odd ? s1 : fmaf(s1, 2.f, -1.f);
+  const float b0 = dpp_swap1(a0), b1 = dpp_swap1(a1);
+  const float ig = odd ? b0 : a0, fg = odd ? a0 : b0;
+  const float gg = odd ? b1 : a1, og = odd ? a1 : b1;
+  Cell r;
+  r.a0 = a0;
+  r.a1 = a1;
+  r.c = fmaf(fg, c, ig * gg);
+  r.h = og * tanh_c(r.c);
+  return r;
+}
+
+template <int NL, int NB>
+PDRNN_DEVICE constexpr int fwd_lds_floats_hb() { return NB * NL * 2 * kHB; }
+
+// NL = 1 or 2.  MODE 0/1: one wave runs all layers of NB = 1 / 2 sequences.
+// MODE 2/3 (NL = 2): wave l runs layer l of NB = 1 / 2 sequences, one
+// barrier per step (layer 0's h_t handed over through parity slots).
+template <int NL, int MODE>
+__global__ void __launch_bounds__(MODE >= 2 ? 64 * NL : 64) lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
+  constexpr int NB = (MODE & 1) ? 2 : 1;
+  constexpr bool SPLIT = MODE >= 2;
+  static_assert(NL == 1 || NL == 2, "one or two layers");
+  static_assert(!SPLIT || NL == 2, "layer-split mode needs two layers");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int lane = tid & 63;
+  const int wv = SPLIT ? __builtin_amdgcn_readfirstlane(tid >> 6) : 0;
+  const int u = lane >> 1;
+  const bool odd = (lane & 1) != 0;
+  const int B = a.B, T = a.T, I = a.I;
+  const int bbase = blockIdx.x * NB;
+  float* hb = smem;
+  float* xs = smem + fwd_lds_floats_hb<NL, NB>();
+  auto hbuf = [&](int n, int l, int p) { return hb + ((n * NL + l) * 2 + p) * kHB; };
+
+  int bidx[NB], bsrc[NB];
+  bool valid[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const int b = bbase + n;
+    valid[n] = b < B;
+    bidx[n] = valid[n] ? b : B - 1;  // an empty slot recomputes the last sequence, stores nothing
+    bsrc[n] = a.idx ? (int)a.idx[bidx[n]] : bidx[n];
+  }
+
+  // ---- prologue: zero the h slots (h_{-1} = 0, pad chunks), stage x ------
+  for (int e = tid; e < fwd_lds_floats_hb<NL, NB>(); e += nthr) hb[e] = 0.f;
+  {
+    const int per = T * kXS, tot = NB * per;
+    const int xg_ld = a.xg_ld;
+    for (int e0 = tid; e0 < tot; e0 += 4 * nthr) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = min(e0 + r * nthr, tot - 1);
+        const int n = e / per, rem = e - n * per;
+        const int t = rem / kXS, k = rem - t * kXS;
+        const float x = ldx(a.x, (int64_t)pick<NB>(bsrc, n) * a.x_sb + (int64_t)t * a.x_st + min(k, I - 1), a.x_bf16);
+        v[r] = k < I ? x : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = e0 + r * nthr;
+        if (e < tot) {
+          const int n = e / per, rem = e - n * per;
+          const int t = rem / kXS, k = rem - t * kXS;
+          xs[e] = v[r];
+          if (a.xg_out && k < xg_ld && (n == 0 ? valid[0] : valid[NB - 1]))
+            a.xg_out[((int64_t)pick<NB>(bidx, n) * T + t) * xg_ld + k] = v[r];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
+  const __amdgpu_buffer_rsrc_t r_h = uniform_rsrc(a.hseq);
+  const uint32_t s_ = odd ? 1u : 0u;
+  const uint32_t vo_a0 = (s_ * kH + u) * 4, vo_a1 = ((2 + s_) * kH + u) * 4, vo_c = (4 * kH + u) * 4, vo_h = u * 4;
+  uint32_t vmask[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) vmask[n] = valid[n] ? 0u : kOOR;
+  // byte offset of row (l, b, t) in act (5H floats per row) and hseq (H)
+  auto row = [&](int l, int n, int t) -> uint32_t {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(((l * B + pick<NB>(bidx, n)) * T + t)));
+  };
+
+  uint64_t st0 = 0, sr0 = 0;
+  if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
+
+  // state: c and the last committed h per (layer, sequence)
+  float cst[NL][NB], hst[NL][NB];
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) { cst[l][n] = 0.f; hst[l][n] = 0.f; }
+
+  // Layer 0 at time t (active unless t == T) / layer 1 at time t (active
+  // unless t < 0), for all NB sequences, split into the operand reads and the
+  // rest: a caller running both layers issues both layers' reads first (their
+  // LDS order against the other layer's h write would otherwise serialise
+  // the two independent chains).
+  auto rd0 = [&](int t, float4 (&v)[NB][6]) {
+    const int tc = min(t, T - 1);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const float* hp = hbuf(n, 0, (t - 1) & 1);
+      const float* pa = odd ? hp + 12 : xs + (n * T + tc) * kXS;
+      const float* pb = odd ? hp + 24 : hp;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[n][c] = ld4(pa + 4 * c);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[n][3 + c] = ld4(pb + 4 * c);
+    }
+  };
+  auto rd1 = [&](int t, float4 (&v)[NB][8]) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const float* pc = odd ? hbuf(n, 1, (t - 1) & 1) : hbuf(n, 0, t & 1);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[n][c] = ld4(pc + 4 * c);
+    }
+  };
+  auto commit = [&](int l, int n, int t, bool act, const Cell& r) {
+    cst[l][n] = act ? r.c : cst[l][n];
+    hst[l][n] = act ? r.h : hst[l][n];
+    hbuf(n, l, t & 1)[u] = hst[l][n];
+    const uint32_t rw = row(l, n, min(max(t, 0), T - 1));
+    const uint32_t m = act ? vmask[n] : kOOR;
+    bstore(r.a0, r_act, vo_a0 | m, rw * (5 * kH * 4));
+    bstore(r.a1, r_act, vo_a1 | m, rw * (5 * kH * 4));
+    bstore(r.c, r_act, vo_c | m, rw * (5 * kH * 4));
+    bstore(r.h, r_h, vo_h | m, rw * (kH * 4));
+  };
+  auto cmp0 = [&](const FwdW<6>& W, int t, const float4 (&v)[NB][6]) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      float p[4];
+      fwd_dot<6>(W, v[n], p);
+      commit(0, n, t, t < T, fwd_cell(p, W.bias, cst[0][n], odd));
+    }
+  };
+  auto cmp1 = [&](const FwdW<8>& W, int t, const float4 (&v)[NB][8]) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      float p[4];
+      fwd_dot<8>(W, v[n], p);
+      commit(NL - 1, n, t, t >= 0, fwd_cell(p, W.bias, cst[NL - 1][n], odd));
+    }
+  };
+
+  if constexpr (NL == 1) {
+    const FwdW<6> W0 = load_fwd_w<6>(a, 0, u, odd ? 1 : 0);
+    for (int t = 0; t < T; ++t) {
+      float4 v0[NB][6];
+      rd0(t, v0);
+      cmp0(W0, t, v0);
+    }
+  } else if constexpr (!SPLIT) {
+    const FwdW<6> W0 = load_fwd_w<6>(a, 0, u, odd ? 1 : 0);
+    const FwdW<8> W1 = load_fwd_w<8>(a, 1, u, odd ? 1 : 0);
+    // layer 0 at t = it, layer 1 at t = it - 1: both read h^0_{it-1}
+    for (int it = 0; it <= T; ++it) {
+      float4 v0[NB][6], v1[NB][8];
+      rd0(it, v0);
+      rd1(it - 1, v1);
+      cmp0(W0, it, v0);
+      cmp1(W1, it - 1, v1);
+    }
+  } else {
+    if (wv == 0) {
+      const FwdW<6> W0 = load_fwd_w<6>(a, 0, u, odd ? 1 : 0);
+      for (int it = 0; it <= T; ++it) {
+        if (it < T) {
+          float4 v0[NB][6];
+          rd0(it, v0);
+          cmp0(W0, it, v0);
+        }
+        lds_barrier();
+      }
+    } else {
+      const FwdW<8> W1 = load_fwd_w<8>(a, 1, u, odd ? 1 : 0);
+      for (int it = 0; it <= T; ++it) {
+        if (it > 0) {
+          float4 v1[NB][8];
+          rd1(it - 1, v1);
+          cmp1(W1, it - 1, v1);
+        }
+        lds_barrier();
+      }
+    }
+  }
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+  }
+
+  // ---- epilogue: h_n / c_n, then the fused head on the top layer's h_T ----
+  const bool top_wave = !SPLIT || wv == NL - 1;
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    if (!valid[n]) continue;
+    const int b = bbase + n;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      if (SPLIT && l != wv) continue;
+      if (!odd && a.hn) a.hn[((int64_t)l * B + b) * kH + u] = hst[l][n];
+      if (!odd && a.cn) a.cn[((int64_t)l * B + b) * kH + u] = cst[l][n];
+    }
+    if (a.head_w && top_wave) motion_head(a, b, hst[NL - 1][n], u, odd);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward (lean contract: zero initial state, dL/dh_T of the top layer only,
+// weight gradients deferred to pdrnn_lstm_small_dw)
+// ---------------------------------------------------------------------------
+struct Ops {
+  float i, f, g, o, c, cp;
+};
+
+// column u of W_hh (and W_ih) over rows [64 s, 64 s + 64), row pairs
+struct BwdCol {
+  pdrnn_f2 w[32];
+};
+PDRNN_DEVICE BwdCol load_bwd_col(const float* w, int ld, int col, bool live, int u, int s, int wbf) {
+  BwdCol W;
+  (void)u;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const int r = 64 * s + 2 * j;
+    const float x0 = w[(int64_t)r * ld + col], x1 = w[(int64_t)(r + 1) * ld + col];
+    W.w[j] = live ? pdrnn_f2{wround(x0, wbf), wround(x1, wbf)} : pdrnn_f2{0.f, 0.f};
+  }
+  return W;
+}
+
+// gate gradients of this lane (d0: i | g, d1: f | o) from the saved
+// activations; dc carries dL/dc_t into step t - 1
+PDRNN_DEVICE void row_phase(const Ops& o, float dht, float& dc, bool odd, bool has_prev, float& d0, float& d1) {
+  const float cp = has_prev ? o.cp : 0.f;
+  const float tc = tanh_c(o.c);
+  const float dcp = fmaf(dht * o.o, fmaf(-tc, tc, 1.f), dc);
+  const float X = odd ? o.i : o.g;
+  const float Y = odd ? fmaf(-o.g, o.g, 1.f) : fmaf(-o.i, o.i, o.i);
+  d0 = dcp * X * Y;
+  const float P = odd ? dht : dcp;
+  const float Q = odd ? tc : cp;
+  const float R = odd ? fmaf(-o.o, o.o, o.o) : fmaf(-o.f, o.f, o.f);
+  d1 = P * Q * R;
+  dc = dcp * o.f;
+}
+
+PDRNN_DEVICE float col_dot(const BwdCol& W, const float4 (&g)[16]) {
+  pdrnn_f2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    a0 = pfma(W.w[2 * c], lo2(g[c]), a0);
+    a1 = pfma(W.w[2 * c + 1], hi2(g[c]), a1);
+  }
+  const pdrnn_f2 s = a0 + a1;
+  return pair_sum(s.x + s.y);
+}
+
+template <int NL, int MODE>
+__global__ void __launch_bounds__(MODE >= 2 ? 64 * NL : 64) lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
+  constexpr int NB = (MODE & 1) ? 2 : 1;
+  constexpr bool SPLIT = MODE >= 2;
+  static_assert(NL == 1 || NL == 2, "one or two layers");
+  static_assert(!SPLIT || NL == 2, "layer-split mode needs two layers");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = SPLIT ? __builtin_amdgcn_readfirstlane(tid >> 6) : 0;
+  const int u = lane >> 1;
+  const int s = lane & 1;
+  const bool odd = s != 0;
+  const int B = a.B, T = a.T;
+  const int bbase = blockIdx.x * NB;
+  float* dzb = smem;                          // [NB][NL][2][kDZ]
+  float* dxb = smem + NB * NL * 2 * kDZ;      // [NB][2][32] (mode 2: layer 1 -> layer 0)
+  auto dzbuf = [&](int n, int l, int p) { return dzb + ((n * NL + l) * 2 + p) * kDZ; };
+
+  int bidx[NB];
+  bool valid[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const int b = bbase + n;
+    valid[n] = b < B;
+    bidx[n] = valid[n] ? b : B - 1;
+  }
+  uint32_t vmask[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) vmask[n] = valid[n] ? 0u : kOOR;
+
+  // the dW kernel streams whole 16-row stages: the 16 padding rows behind the
+  // last layer's gate gradients must hold finite values
+  if (blockIdx.x == 0) {
+    float* pad = a.dg_out + (int64_t)NL * B * T * a.dg_st;
+    for (int e = tid; e < 16 * a.dg_st; e += blockDim.x) pad[e] = 0.f;
+  }
+
+  const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
+  const __amdgpu_buffer_rsrc_t r_dg = uniform_rsrc(a.dg_out);
+  const uint32_t st_act = 5 * kH * 4, st_dg = (uint32_t)a.dg_st * 4;
+  const uint32_t vo_i = u * 4, vo_f = (kH + u) * 4, vo_g = (2 * kH + u) * 4, vo_o = (3 * kH + u) * 4;
+  const uint32_t vo_c = (4 * kH + u) * 4;
+  const uint32_t vo_d0 = (2 * s * kH + u) * 4, vo_d1 = ((2 * s + 1) * kH + u) * 4;
+  const int slot0 = dz_slot(2 * s * kH + u), slot1 = dz_slot((2 * s + 1) * kH + u);
+  const int colbase = dz_slot(64 * s);
+
+  auto rowidx = [&](int l, int n, int t) -> uint32_t {
+    return __builtin_amdgcn_readfirstlane((uint32_t)((l * B + pick<NB>(bidx, n)) * T + t));
+  };
+  // branch-free operand loads of layer l, step t (clamped; masked at use)
+  auto load_ops = [&](int l, int n, int t) {
+    const int tc = min(max(t, 0), T - 1);
+    const uint32_t ra = rowidx(l, n, tc) * st_act;
+    const uint32_t rp = __builtin_amdgcn_readfirstlane(tc > 0 ? ra - st_act : ra);
+    Ops o;
+    o.i = bload(r_act, vo_i, ra);
+    o.f = bload(r_act, vo_f, ra);
+    o.g = bload(r_act, vo_g, ra);
+    o.o = bload(r_act, vo_o, ra);
+    o.c = bload(r_act, vo_c, ra);
+    o.cp = bload(r_act, vo_c, rp);
+    return o;
+  };
+
+  // per (layer, sequence) state
+  float dhrec[NL][NB], dc[NL][NB], dx1[NB];
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) { dhrec[l][n] = 0.f; dc[l][n] = 0.f; }
+  float dhtop[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    dx1[n] = 0.f;
+    dhtop[n] = a.dhn[(int64_t)bidx[n] * kH + u];
+  }
+  if (SPLIT) {
+    for (int e = tid; e < NB * 2 * 32; e += blockDim.x) dxb[e] = 0.f;
+  }
+
+  uint64_t st0 = 0, sr0 = 0;
+  if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
+
+  // Iteration `it`: the top layer at t = T-1-it, layer 0 (of a 2-layer stack)
+  // at t = T-it (lag 1: its dh input is layer 1's input gradient of step t).
+  // The body is branch-free (inactive steps compute on clamped operands and
+  // their stores are dropped): a branch join would make the waitcnt pass wait
+  // for the prefetches of the next two iterations.
+  const int iters = T + NL - 1;
+
+  // layer-generic pieces
+  auto rows = [&](int l, int n, int t, const Ops& o, float dh_in, bool act) {
+    float d0, d1, dcn = dc[l][n];
+    row_phase(o, dhrec[l][n] + dh_in, dcn, odd, t > 0, d0, d1);
+    dc[l][n] = act ? dcn : dc[l][n];
+    float* zb = dzbuf(n, l, t & 1);
+    zb[slot0] = d0;
+    zb[slot1] = d1;
+    const uint32_t so = rowidx(l, n, min(max(t, 0), T - 1)) * st_dg;
+    const uint32_t m = act ? vmask[n] : kOOR;
+    bstore(d0, r_dg, vo_d0 | m, so);
+    bstore(d1, r_dg, vo_d1 | m, so);
+  };
+  auto read_dz = [&](int l, int n, int t, float4 (&g)[16]) {
+    const float* zb = dzbuf(n, l, t & 1) + colbase;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) g[c] = ld4(zb + 4 * c);
+  };
+
+  if constexpr (NL == 1) {
+    const BwdCol Whh = load_bwd_col(a.w_hh[0], kH, u, true, u, s, a.w_bf16);
+    Ops opA[NB], opB[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) opA[n] = load_ops(0, n, T - 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) opB[n] = load_ops(0, n, T - 2);
+    __builtin_amdgcn_sched_barrier(0);
+    auto body = [&](int it, Ops (&op)[NB]) {
+      const int t = T - 1 - it;
+      const bool act = t >= 0;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) rows(0, n, t, op[n], it == 0 ? dhtop[n] : 0.f, act);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        float4 g[16];
+        read_dz(0, n, t, g);
+        const float v = col_dot(Whh, g);
+        dhrec[0][n] = act ? v : dhrec[0][n];
+      }
+#pragma unroll
+      for (int n = 0; n < NB; ++n) op[n] = load_ops(0, n, t - 2);
+    };
+    int it = 0;
+    for (; it + 1 < iters; it += 2) {
+      body(it, opA);
+      body(it + 1, opB);
+    }
+    if (it < iters) body(it, opA);
+  } else if constexpr (!SPLIT) {
+    const BwdCol Whh1 = load_bwd_col(a.w_hh[1], kH, u, true, u, s, a.w_bf16);
+    const BwdCol Wih1 = load_bwd_col(a.w_ih[1], kH, u, true, u, s, a.w_bf16);
+    const BwdCol Whh0 = load_bwd_col(a.w_hh[0], kH, u, true, u, s, a.w_bf16);
+    Ops opA[2][NB], opB[2][NB];
+    // issue order pinned (A's loads, then B's, each layer 1 then layer 0): the
+    // loop's counted vmcnt waits are the max over its entry edges
+#pragma unroll
+    for (int n = 0; n < NB; ++n) { opA[1][n] = load_ops(1, n, T - 1); opA[0][n] = load_ops(0, n, T); }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) { opB[1][n] = load_ops(1, n, T - 2); opB[0][n] = load_ops(0, n, T - 1); }
+    __builtin_amdgcn_sched_barrier(0);
+    auto body = [&](int it, Ops (&op)[2][NB]) {
+      const int t1 = T - 1 - it, t0 = T - it;
+      const bool act1 = t1 >= 0, act0 = t0 < T;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        rows(1, n, t1, op[1][n], it == 0 ? dhtop[n] : 0.f, act1);
+        rows(0, n, t0, op[0][n], dx1[n], act0);
+      }
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        float4 g1[16], g0[16];
+        read_dz(1, n, t1, g1);
+        read_dz(0, n, t0, g0);
+        const float vh1 = col_dot(Whh1, g1);
+        const float vx1 = col_dot(Wih1, g1);
+        const float vh0 = col_dot(Whh0, g0);
+        dhrec[1][n] = act1 ? vh1 : dhrec[1][n];
+        dx1[n] = act1 ? vx1 : 0.f;
+        dhrec[0][n] = act0 ? vh0 : dhrec[0][n];
+      }
+#pragma unroll
+      for (int n = 0; n < NB; ++n) { op[1][n] = load_ops(1, n, t1 - 2); op[0][n] = load_ops(0, n, t0 - 2); }
+    };
+    int it = 0;
+    for (; it + 1 < iters; it += 2) {
+      body(it, opA);
+      body(it + 1, opB);
+    }
+    if (it < iters) body(it, opA);
+  } else {
+    // modes 2/3: wave 1 = layer 1 (t = T-1-it), wave 0 = layer 0 (t = T-it),
+    // one barrier per iteration; layer 1's input gradient of step t reaches
+    // layer 0 through dxb[n][t & 1]
+    if (wv == 1) {
+      const BwdCol Whh1 = load_bwd_col(a.w_hh[1], kH, u, true, u, s, a.w_bf16);
+      const BwdCol Wih1 = load_bwd_col(a.w_ih[1], kH, u, true, u, s, a.w_bf16);
+      Ops opA[NB], opB[NB];
+#pragma unroll
+      for (int n = 0; n < NB; ++n) opA[n] = load_ops(1, n, T - 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) opB[n] = load_ops(1, n, T - 2);
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      auto body = [&](int it, Ops (&op)[NB]) {
+        const int t = T - 1 - it;
+        const bool act = t >= 0;
+#pragma unroll
+        for (int n = 0; n < NB; ++n) rows(1, n, t, op[n], it == 0 ? dhtop[n] : 0.f, act);
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          float4 g[16];
+          read_dz(1, n, t, g);
+          const float vh = col_dot(Whh1, g);
+          const float vx = col_dot(Wih1, g);
+          dhrec[1][n] = act ? vh : dhrec[1][n];
+          if (!odd) dxb[(n * 2 + (t & 1)) * 32 + u] = act ? vx : 0.f;
+          // one sequence's 64-float dz slice in registers at a time (two
+          // would push the wave past 256 VGPRs: one wave per SIMD)
+          if (NB > 1) __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int n = 0; n < NB; ++n) op[n] = load_ops(1, n, t - 2);
+        lds_barrier();
+      };
+      int it = 0;
+      for (; it + 1 < iters; it += 2) {
+        body(it, opA);
+        body(it + 1, opB);
+      }
+      if (it < iters) body(it, opA);
+    } else {
+      const BwdCol Whh0 = load_bwd_col(a.w_hh[0], kH, u, true, u, s, a.w_bf16);
+      Ops opA[NB], opB[NB];
+#pragma unroll
+      for (int n = 0; n < NB; ++n) opA[n] = load_ops(0, n, T);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) opB[n] = load_ops(0, n, T - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      auto body = [&](int it, Ops (&op)[NB]) {
+        const int t = T - it;
+        const bool act = t < T;
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          const float dxin = dxb[(n * 2 + (t & 1)) * 32 + u];  // layer 1's step-t input gradient
+          rows(0, n, t, op[n], act ? dxin : 0.f, act);
+        }
+#pragma unroll
+        for (int n = 0; n < NB; ++n) {
+          float4 g[16];
+          read_dz(0, n, t, g);
+          const float vh = col_dot(Whh0, g);
+          dhrec[0][n] = act ? vh : dhrec[0][n];
+          if (NB > 1) __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int n = 0; n < NB; ++n) op[n] = load_ops(0, n, t - 2);
+        lds_barrier();
+      };
+      int it = 0;
+      for (; it + 1 < iters; it += 2) {
+        body(it, opA);
+        body(it + 1, opB);
+      }
+      if (it < iters) body(it, opA);
+    }
+  }
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+  }
+}
+
+// ---- host side -------------------------------------------------------------
+int sw_cus() {
+  static thread_local int c_dev = -1, c_val = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != c_dev) {
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    c_dev = dev;
+    c_val = cus > 0 ? cus : 1;
+  }
+  return c_val;
+}
+
+size_t fwd_lds(int NL, int nb, int T) { return sizeof(float) * ((size_t)nb * NL * 2 * kHB + (size_t)nb * T * kXS); }
+size_t bwd_lds(int NL, int nb) { return sizeof(float) * ((size_t)nb * NL * 2 * kDZ + (size_t)nb * 2 * 32); }
+int mode_nb(int mode) { return (mode & 1) ? 2 : 1; }
+
+template <int NL, int MODE>
+hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
+  constexpr int NB = (MODE & 1) ? 2 : 1;
+  const int grid = (a->B + NB - 1) / NB;
+  const int block = MODE >= 2 ? 64 * NL : 64;
+  hipLaunchKernelGGL((lstm_sw_fwd_kernel<NL, MODE>), dim3(grid), dim3(block), fwd_lds(NL, NB, a->T), st, *a);
+  return hipGetLastError();
+}
+template <int NL, int MODE>
+hipError_t launch_bwd(const PdrnnLstmSmallBwdArgs* a, hipStream_t st) {
+  constexpr int NB = (MODE & 1) ? 2 : 1;
+  const int grid = (a->B + NB - 1) / NB;
+  const int block = MODE >= 2 ? 64 * NL : 64;
+  hipLaunchKernelGGL((lstm_sw_bwd_kernel<NL, MODE>), dim3(grid), dim3(block), bwd_lds(NL, NB), st, *a);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace pdrnn
+
+using namespace pdrnn;
+
+extern "C" int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell) {
+  return (H == kH && I >= 1 && I <= kXS && (NL == 1 || NL == 2) && cell == 0) ? 1 : 0;
+}
+
+// Two-layer stacks: one wave per layer (mode 2), two sequences per wave above
+// one resident round (mode 3: B = 1152 / 1440).  One layer: one wave per
+// sequence (mode 0), two above one wave per SIMD (mode 1).
+extern "C" int pdrnn_lstm_sw_mode(int NL, int B) {
+  const char* e = getenv("PDRNN_SW_MODE");
+  if (e && *e) {
+    const int m = atoi(e);
+    if (m >= 0 && m <= 3 && (m < 2 || NL == 2)) return m;
+  }
+  const int simds = 4 * sw_cus();
+  if (NL == 2) return 2 * B <= 2 * simds ? 2 : 3;  // split waves hold <= 256 VGPRs: 2 per SIMD
+  return B <= simds ? 0 : 1;
+}
+
+extern "C" hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode, hipStream_t st) {
+  if (!pdrnn_lstm_sw_ok(kH, a->I, a->NL, a->cell) || a->h0 || a->c0) return hipErrorInvalidValue;
+  if (!a->act || !a->hseq || a->B <= 0 || a->T <= 0) return hipErrorInvalidValue;
+  if (a->head_w && (a->C > 16 || a->C < 1 || !a->labels || !a->slab || !a->dh_top)) return hipErrorInvalidValue;
+  if (a->xg_out && (a->xg_ld < a->I || a->xg_ld > kXS)) return hipErrorInvalidValue;
+  if (fwd_lds(a->NL, mode_nb(mode), a->T) > 64 * 1024) return hipErrorInvalidConfiguration;
+  if (a->NL == 1) {
+    if (mode == 0) return launch_fwd<1, 0>(a, st);
+    if (mode == 1) return launch_fwd<1, 1>(a, st);
+    return hipErrorInvalidValue;
+  }
+  if (mode == 0) return launch_fwd<2, 0>(a, st);
+  if (mode == 1) return launch_fwd<2, 1>(a, st);
+  if (mode == 2) return launch_fwd<2, 2>(a, st);
+  if (mode == 3) return launch_fwd<2, 3>(a, st);
+  return hipErrorInvalidValue;
+}
+
+extern "C" hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode, hipStream_t st) {
+  if (!pdrnn_lstm_sw_ok(kH, a->I, a->NL, a->cell)) return hipErrorInvalidValue;
+  if (a->h0 || a->c0 || a->dout || a->dcn || a->dx || a->dh0 || a->dc0 || !a->dhn || !a->dhn_top_only)
+    return hipErrorInvalidValue;  // lean contract only
+  if (!a->act || !a->dg_out || a->dg_st < 4 * kH || a->B <= 0 || a->T <= 0) return hipErrorInvalidValue;
+  if (a->NL == 1) {
+    if (mode == 0) return launch_bwd<1, 0>(a, st);
+    if (mode == 1) return launch_bwd<1, 1>(a, st);
+    return hipErrorInvalidValue;
+  }
+  if (mode == 0) return launch_bwd<2, 0>(a, st);
+  if (mode == 1) return launch_bwd<2, 1>(a, st);
+  if (mode == 2) return launch_bwd<2, 2>(a, st);
+  if (mode == 3) return launch_bwd<2, 3>(a, st);
+  return hipErrorInvalidValue;
+}

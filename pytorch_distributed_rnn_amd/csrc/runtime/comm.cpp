@@ -100,6 +100,25 @@ double env_double(const char* name, double dflt) {
 
 using Clock = std::chrono::steady_clock;
 
+// PDRNN_RCCL_MAX_CTAS (default 8; 0 = RCCL's own choice): workgroups an RCCL
+// collective of our communicators may occupy.  The motion all-reduce (56.6 KB)
+// is latency-bound and needs few; a 32 MiB char-LM bucket over 7 xGMI peers
+// still gets 8 channels.
+std::atomic<int> g_cta_reserve{0};
+
+}  // namespace
+
+int rccl_max_ctas() {
+  static const int v = [] {
+    const char* e = std::getenv("PDRNN_RCCL_MAX_CTAS");
+    return e && *e ? std::max(0, std::atoi(e)) : 8;
+  }();
+  return v;
+}
+int rccl_cta_reserve() { return g_cta_reserve.load(); }
+
+namespace {
+
 class RcclComm final : public Comm {
  public:
   RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority, double timeout_s)
@@ -115,7 +134,19 @@ class RcclComm final : public Comm {
     HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
     // every peer has just joined the torch.distributed rendezvous that carried
     // the unique id, so a blocking init cannot wait on a dead rank for long
-    NCCL_CHECK(ncclCommInitRank(&comm_, world_, id, rank_));
+    // Cap the CUs RCCL's kernels may take (config.maxCTAs): a bucket
+    // all-reduce runs beside the grid-synced persistent recurrences of the
+    // large-H layers, which need all their workgroups co-resident.  The
+    // persistent planner leaves that many CUs free in every multi-rank
+    // process (rccl_cta_reserve, bindings.cpp large_persist_plan), so an
+    // all-reduce already resident can never keep a persistent grid waiting.
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    const int max_ctas = rccl_max_ctas();
+    if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+    NCCL_CHECK(ncclCommInitRankConfig(&comm_, world_, id, rank_, &cfg));
+    // (a forced one-rank collective rehearses the multi-rank overlap on one GPU)
+    if ((world_ > 1 || env_flag("PDRNN_FORCE_COLLECTIVE", false)) && max_ctas > 0)
+      g_cta_reserve.store(std::max(g_cta_reserve.load(), max_ctas));
     exit_on_abort_ = env_flag("PDRNN_COMM_WATCHDOG_EXIT", true);
     grace_s_ = env_double("PDRNN_COMM_WATCHDOG_GRACE_S", 5.0);
     poll_ms_ = std::max(1.0, env_double("PDRNN_COMM_WATCHDOG_POLL_MS", 100.0));

@@ -81,10 +81,14 @@ class GradReducer {
       const int64_t cap = std::max<int64_t>(buckets_idx_.empty() ? first_bucket_cap_bytes : bucket_cap_bytes, 1);
       const int64_t bytes = p.numel() * p.element_size();
       const int64_t grp = groups.empty() ? 0 : groups[i];
-      if (bytes > cap && p.numel() > 1) {
+      // a parameter is split by the regular cap, never by the (smaller)
+      // first-bucket cap: a large weight right behind the small head bias
+      // would otherwise become ceil(bytes / 1 MiB) latency-bound messages
+      const int64_t split_cap = std::max<int64_t>(bucket_cap_bytes, 1);
+      if (bytes > split_cap && p.numel() > 1) {
         close();
         // equal chunks rounded up to 4 KiB, issued from the parameter's end
-        const int64_t k = (bytes + cap - 1) / cap;
+        const int64_t k = (bytes + split_cap - 1) / split_cap;
         const int64_t align = std::max<int64_t>(4096 / p.element_size(), 1);
         const int64_t len = ((p.numel() + k - 1) / k + align - 1) / align * align;
         for (int64_t c = (p.numel() + len - 1) / len - 1; c >= 0; --c) {

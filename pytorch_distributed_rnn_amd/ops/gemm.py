@@ -207,7 +207,9 @@ def _native_f32(t: Tensor):
 
 
 def _unit_inner(t: Tensor) -> bool:
-    return t.dim() == 2 and (t.stride(1) == 1 or t.shape[1] == 1) and t.stride(0) >= 1
+    # the native binding requires a unit inner stride (a [K, 1] view with any
+    # other stride would be rejected there instead of taking the torch path)
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= 1
 
 
 def _splitk_f32(dev, M: int, N: int, K: int) -> int:

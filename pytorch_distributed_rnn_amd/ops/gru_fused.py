@@ -53,10 +53,20 @@ def _zeros(like: Tensor, n: int) -> Tensor:
     return z[:n]
 
 
-def _pack(weights: Sequence[Optional[Tensor]], num_layers: int, hidden: int, like: Tensor) -> List[Tensor]:
+def packed_numel(weights: Sequence[Optional[Tensor]], num_layers: int, hidden: int) -> int:
+    """Elements of the 4-block stacks of all layers (the ``out`` buffer of _pack)."""
+    H = hidden
+    return sum(4 * H * int(weights[4 * l].shape[1]) + 4 * H * H + 8 * H for l in range(num_layers))
+
+
+def _pack(weights: Sequence[Optional[Tensor]], num_layers: int, hidden: int, like: Tensor,
+          out: Optional[Tensor] = None) -> List[Tensor]:
     """All layers' 4-block stacks as views of ONE buffer built by a single
     batched cat launch (the zero blocks are slices of a cached zero vector),
-    instead of a cat + zero fill per tensor per step."""
+    instead of a cat + zero fill per tensor per step.  ``out``: a persistent
+    buffer of ``packed_numel`` elements the cat writes into -- no allocation,
+    so the fused step can capture it in a HIP graph and every replay re-packs
+    the current parameters."""
     H = hidden
     pieces: List[Tensor] = []
     shapes: List[Tuple[int, ...]] = []
@@ -71,15 +81,15 @@ def _pack(weights: Sequence[Optional[Tensor]], num_layers: int, hidden: int, lik
                        w_hh[:2 * H].reshape(-1), _zeros(like, H * H), w_hh[2 * H:].reshape(-1),
                        b_ih, zb, b_hh[:2 * H], zb, b_hh[2 * H:]]
             shapes += [(4 * H, I), (4 * H, H), (4 * H,), (4 * H,)]
-        flat = torch.cat(pieces)
-    out, off = [], 0
+        flat = torch.cat(pieces) if out is None else torch.cat(pieces, out=out)
+    views, off = [], 0
     for s in shapes:
         n = 1
         for d in s:
             n *= d
-        out.append(flat[off:off + n].view(s))
+        views.append(flat[off:off + n].view(s))
         off += n
-    return out
+    return views
 
 
 def _unpack_index(hidden: int, in_dims: Tuple[int, ...], device: torch.device) -> Tensor:

@@ -149,7 +149,9 @@ class _LargeGRULayer(torch.autograd.Function):
             dhn_f = dhn.float().contiguous() if dhn is not None else None
             return mod.lstm_large_bwd(dout, dhn_f, None, wt, hs32, acts, h0f, H, rev_mask, tile, 1)
 
-        dgates, dh0, _ = run_recurrence(dhseq, bptt, [dhseq, dhn, hs32, acts, h0f, *wt])
+        persistent = bool(getattr(mod, "lstm_large_bwd_persistent", lambda *a: True)(
+            B, H, ndir, {torch.bfloat16: 0, torch.float16: 1}.get(cdt, 2), tile))
+        dgates, dh0, _ = run_recurrence(dhseq, bptt, [dhseq, dhn, hs32, acts, h0f, *wt], persistent)
         grads: List[Optional[Tensor]] = []
         dx = None
         dx_pairs = []

@@ -214,7 +214,7 @@ def overlap_on() -> bool:
     return os.environ.get("PDRNN_LARGE_OVERLAP", "1") != "0"
 
 
-def run_recurrence(dhseq: Optional[Tensor], fn, inputs: Sequence[Optional[Tensor]]):
+def run_recurrence(dhseq: Optional[Tensor], fn, inputs: Sequence[Optional[Tensor]], persistent: bool = False):
     """fn() -> tensors: the layer's backward recurrence, on the side stream
     when the upstream gradient carries a ready event (see above), inline
     otherwise.  ``inputs``: the tensors fn reads, as autograd delivered them;
@@ -224,7 +224,11 @@ def run_recurrence(dhseq: Optional[Tensor], fn, inputs: Sequence[Optional[Tensor
     gradients (``ctx.set_materialize_grads(False)``): such a zero fill is
     queued on the main stream after the event, and the side stream read it
     before it ran (uninitialised dc carry: wrong gradients one run in a few,
-    tools/pipe_determinism.py)."""
+    tools/pipe_determinism.py).  ``persistent``: the recurrence is one
+    grid-synced persistent launch, whose co-residency is checked against an
+    idle device only -- it runs inline, never beside the side-stream GEMMs."""
+    if persistent:
+        return fn()
     ev = getattr(dhseq, "_pdrnn_ready", None) if dhseq is not None else None
     if ev is not None and getattr(dhseq, "_pdrnn_ready_version", None) != dhseq._version:
         ev = None  # written after the event (e.g. an in-place gradient accumulation)
@@ -334,7 +338,9 @@ class _LargeLSTMLayer(torch.autograd.Function):
             dcn_f = dcn.float().contiguous() if dcn is not None else None
             return mod.lstm_large_bwd(dout, dhn_f, dcn_f, wt, cseq, acts, c0c, H, rev_mask, tile, 0)
 
-        dgates, dh0, dc0 = run_recurrence(dhseq, bptt, [dhseq, dhn, dcn, cseq, acts, c0c, *wt])
+        persistent = bool(getattr(mod, "lstm_large_bwd_persistent", lambda *a: True)(
+            B, H, ndir, {torch.bfloat16: 0, torch.float16: 1}.get(cdt, 2), tile))
+        dgates, dh0, dc0 = run_recurrence(dhseq, bptt, [dhseq, dhn, dcn, cseq, acts, c0c, *wt], persistent)
         grads: List[Optional[Tensor]] = []
         dx = None
         need_dx = ctx.needs_input_grad[0]

@@ -140,13 +140,32 @@ def get_comm(group=None, prefer_native: bool = True):
     if mod is not None and torch.cuda.is_available() and dist.get_world_size(g) > 1 \
             and hasattr(mod, "set_persist_verify"):
         # collectives now run beside the compute stream: a persistent
-        # recurrence can lose co-residency to them, so every step is verified
-        # before its optimizer update and re-run after a timeout (per-step
-        # mode: bindings.cpp large_persist / persist_step_check, train/lm.py);
-        # PDRNN_LSTM_PERSIST_VERIFY=1 selects the per-launch check instead
-        if os.environ.get("PDRNN_LSTM_PERSIST_VERIFY") is None:
-            mod.set_persist_verify(2)
+        # recurrence can lose co-residency to them, so every persistent launch
+        # is verified (host-synchronised) and a timed-out layer re-run on the
+        # per-step kernels before anything uses its result (mode 1, bindings.cpp
+        # large_persist).  The LM trainer, which also carries the skip word to
+        # Adam and re-runs skipped steps (train/lm.py settle), upgrades its
+        # process to the sync-free per-step mode 2 (use_step_verification).
+        if os.environ.get("PDRNN_LSTM_PERSIST_VERIFY") is None and mod.persist_verify_mode() != 2:
+            mod.set_persist_verify(1)
     return comm
+
+
+def use_step_verification() -> bool:
+    """Switch this multi-rank GPU process to per-step persistent-path
+    verification (mode 2: no host sync per launch; a timed-out step's
+    optimizer update is skipped on the device and the step re-run).  Only a
+    trainer that passes the sticky flag to its optimizer as the skip word and
+    re-runs skipped steps may call this (``LMTrainer``); every other trainer
+    keeps mode 1, where a timed-out layer is re-run inside its own launch
+    sequence before the gradient is used.  Returns True when mode 2 is on."""
+    mod = _ext.extension()
+    if mod is None or not torch.cuda.is_available() or not hasattr(mod, "set_persist_verify"):
+        return False
+    if os.environ.get("PDRNN_LSTM_PERSIST_VERIFY") is not None:
+        return mod.persist_verify_mode() == 2
+    mod.set_persist_verify(2)
+    return True
 
 
 def close_comms() -> None:

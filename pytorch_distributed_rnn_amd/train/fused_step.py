@@ -74,9 +74,9 @@ class MotionTrainStep:
     """Callable running one fused training step; returns [loss, n, correct].
 
     Single process (no gradient sync): the optimizer step is fused into the
-    tail of the gradient reduction (``adam_partials`` kernel), so one step
-    is four launches: forward+head+CE, BPTT, reduction pass 1, reduction
-    pass 2 + Adam.
+    one-pass gradient reduction (``slab_reduce_adam`` kernel), so one step is
+    four launches: forward+head+CE, BPTT, the matrix-core weight gradients
+    (deferred dW) and the reduction + Adam.
 
     With gradient sync (multi-GPU) the step is forward+BPTT+reductions, the
     inline RCCL all-reduce and the flat Adam.  ``cuda_graph=True`` (or
@@ -148,6 +148,25 @@ class MotionTrainStep:
         self.cuda_graph = bool(cuda_graph)
         self._graph = None       # last replayed synced step (torch.cuda.CUDAGraph = hipGraph)
         self._graphs = {}        # configuration key -> captured step
+        self._gru_buf = None     # GRU: persistent [r|z|n_x|n_h] packing buffer (graph-capturable)
+
+    def _operands(self, features: Tensor):
+        """(weights as the kernels read them, features, cell code): the bf16
+        model's fp32 masters (rounded in-kernel) with bf16 inputs, the GRU's
+        4-block packing written into a persistent buffer (one captured cat
+        kernel: no allocation, so the packed step graph-replays), else the
+        parameters themselves."""
+        if self.bf16:
+            if features.dtype != torch.bfloat16:
+                features = features.to(torch.bfloat16)
+            return self.weights, features, 0
+        if self.gru:
+            from ..ops.gru_fused import _pack, packed_numel
+            if self._gru_buf is None:
+                self._gru_buf = torch.empty(packed_numel(self.weights, self.NL, self.H), dtype=self.flat.data.dtype,
+                                            device=self.flat.data.device)
+            return _pack(self.weights, self.NL, self.H, self.flat.data, out=self._gru_buf), features, 1
+        return self.weights, features, 0
 
     def run_steps(self, features: Tensor, labels: Tensor, idx_list) -> Optional[list]:
         """Consecutive training steps (an epoch's batches, the short last one
@@ -158,9 +177,9 @@ class MotionTrainStep:
         host copy sits between the steps: the batch indices of all steps reach
         the graph's static buffer in one copy before the replay.  Returns each
         step's statistics row, or None when this configuration runs per step
-        (no gradient sync / no graph replay, bf16 or GRU packing, host-gathered
-        batches, the first two calls of a configuration)."""
-        if self.grad_sync is None or not self.cuda_graph or self.gru:
+        (no gradient sync / no graph replay, host-gathered batches, the first
+        two calls of a configuration)."""
+        if self.grad_sync is None or not self.cuda_graph:
             return None
         if not idx_list or any(i is None for i in idx_list):
             return None
@@ -231,6 +250,9 @@ class MotionTrainStep:
         cfgs = []
         for b in sizes:
             nb_fwd, sp_fwd, _, _ = small_launch_config(b, self.H, self.NL)
+            if self.gru:
+                from ..ops.lstm import gru_fwd_nb
+                nb_fwd, sp_fwd = gru_fwd_nb(b, self.H, features.device), 1
             cfgs.append(((nb_fwd, sp_fwd), fused_bwd_nb(b, self.H, self.NL)))
         key = ("epoch", features.data_ptr(), tuple(features.shape), features.dtype, labels.data_ptr(),
                labels.numel(), tuple(sizes), idx_dtype, tuple(cfgs), lr, b1, b2, eps, wd, dec,
@@ -244,7 +266,7 @@ class MotionTrainStep:
         capture -- then the capture itself, which runs nothing.  Parameters
         and optimizer state are untouched; the flat gradient (rewritten by
         every step) is left zeroed.  True when the graph is ready."""
-        if self.grad_sync is None or not self.cuda_graph or self.gru or not sizes:
+        if self.grad_sync is None or not self.cuda_graph or not sizes:
             return False
         adam = self._flat_adam_peek()
         if adam is None:
@@ -289,9 +311,10 @@ class MotionTrainStep:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for view, ((nb, sp), nb_bwd) in zip(views, cfgs):
-                self.mod.lstm_head_train_step(features, view, labels, self.weights, hw, hb, self.flat.grad, self.ring,
-                                              self.H, self.NL, sp, 0, nb, nb_bwd, None, None, 0, None, ent["step"],
-                                              ent["slot_off"], round_bf16=self.bf16)
+                ws, feats, cell = self._operands(features)  # GRU: re-packed from the updated parameters
+                self.mod.lstm_head_train_step(feats, view, labels, ws, hw, hb, self.flat.grad, self.ring,
+                                              self.H, self.NL, sp, 0, nb, nb_bwd, None, None, cell, self.colmap,
+                                              ent["step"], ent["slot_off"], round_bf16=self.bf16)
                 self.grad_sync()
                 self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step + 1.0, 1.0, bool(dec),
                                    False, None, ent["step"], ent["ticket"])
@@ -336,29 +359,20 @@ class MotionTrainStep:
         if self.gru:  # gate-split forward only (1 or 2 sequences per workgroup)
             nb_fwd, sp_fwd = gru_fwd_nb(batch, self.H, features.device), 1
         hw, hb = self.m.fc.weight, self.m.fc.bias  # the classifier head stays fp32
-        if self.bf16:
-            ws = self.weights  # rounded to bf16 in-kernel (round_bf16)
-            if features.dtype != torch.bfloat16:
-                features = features.to(torch.bfloat16)
-        elif self.gru:
-            from ..ops.gru_fused import _pack
-            ws = _pack(self.weights, self.NL, self.H, self.flat.data)
-        else:
-            ws = self.weights
-        cell = 1 if self.gru else 0
         slot = self._slot
         stats = self.ring[slot]
         self._slot = (self._slot + 1) % self.RING
         adam = self._flat_adam()
+        if self.grad_sync is not None and adam is not None and self.cuda_graph:
+            if self._graph_step(features, labels, idx, (nb_fwd, sp_fwd), nb_bwd, adam, stats, slot):
+                return stats
+        ws, features, cell = self._operands(features)
         if adam is not None and self.grad_sync is None:
             with trace_range("pdrnn.fwd_bwd_adam"):
                 self.mod.lstm_head_train_step(features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H,
                                               self.NL, sp_fwd, 0, nb_fwd, nb_bwd, adam[0], adam[1], cell, self.colmap,
                                               round_bf16=self.bf16)
             return stats
-        if self.grad_sync is not None and adam is not None and self.cuda_graph:
-            if self._graph_step(features, labels, idx, ws, (nb_fwd, sp_fwd), nb_bwd, adam, stats, slot):
-                return stats
         with trace_range("pdrnn.fwd_bwd"):
             self.mod.lstm_head_train_step(
                 features, idx, labels, ws, hw, hb, self.flat.grad, stats, self.H, self.NL, sp_fwd, 0, nb_fwd, nb_bwd,
@@ -387,15 +401,7 @@ class MotionTrainStep:
         nb_bwd = fused_bwd_nb(batch, self.H, self.NL)
         if self.gru:  # gate-split forward only (1 or 2 sequences per workgroup)
             nb_fwd, sp_fwd = gru_fwd_nb(batch, self.H, features.device), 1
-        if self.bf16:
-            ws = self.weights  # rounded to bf16 in-kernel (round_bf16)
-            if features.dtype != torch.bfloat16:
-                features = features.to(torch.bfloat16)
-        elif self.gru:
-            from ..ops.gru_fused import _pack
-            ws = _pack(self.weights, self.NL, self.H, self.flat.data)
-        else:
-            ws = self.weights
+        ws, features, cell = self._operands(features)
         stats = torch.zeros(3, dtype=torch.float32, device=self.flat.grad.device)
         # the single-process step folds Adam into its reduction: warm THAT
         # kernel variant too (its first launch pays the code-object load), on
@@ -408,7 +414,7 @@ class MotionTrainStep:
                 adam_bufs = [p.clone(), m.clone(), v.clone()]
         self.mod.lstm_head_train_step(features, idx, labels, ws, self.m.fc.weight, self.m.fc.bias, self.flat.grad,
                                       stats, self.H, self.NL, sp_fwd, 0, nb_fwd, nb_bwd, adam_bufs, adam_hp,
-                                      1 if self.gru else 0, self.colmap, round_bf16=self.bf16)
+                                      cell, self.colmap, round_bf16=self.bf16)
         self.flat.grad.zero_()
 
     def _flat_adam_peek(self):
@@ -428,14 +434,12 @@ class MotionTrainStep:
     # an epoch alternate: no re-capture every epoch)
     _GRAPHS_MAX = 4
 
-    def _graph_step(self, features: Tensor, labels: Tensor, idx: Optional[Tensor], ws, nb_fwd,
+    def _graph_step(self, features: Tensor, labels: Tensor, idx: Optional[Tensor], nb_fwd,
                     nb_bwd: int, adam, stats: Tensor, slot: int) -> bool:
         """Run the synced step as a graph replay.  False: run it eagerly --
-        the GRU (its per-step weight packing allocates), and the first two
-        steps of a configuration, so that RCCL's lazy connection setup and the
-        kernels' first-use allocations happen outside the capture."""
-        if self.gru:
-            return False  # per-step weight packing allocates
+        the first two steps of a configuration, so that RCCL's lazy connection
+        setup and the kernels' first-use allocations happen outside the
+        capture (the GRU's packing writes a persistent buffer: captured too)."""
         if idx is None:
             return False  # host-gathered batches change pointers every step
         (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
@@ -454,7 +458,7 @@ class MotionTrainStep:
             if ent["eager"] <= 2:
                 return False
             try:
-                self._capture(ent, features, labels, idx, ws, nb_fwd, nb_bwd, adam, slot)
+                self._capture(ent, features, labels, idx, nb_fwd, nb_bwd, adam, slot)
             except Exception as exc:  # capture unsupported here: stay eager for good
                 import warnings
                 warnings.warn(f"HIP graph capture of the synced step failed ({exc!r}); running eagerly")
@@ -481,7 +485,7 @@ class MotionTrainStep:
             stats.copy_(self.ring[row], non_blocking=True)
         return True
 
-    def _capture(self, ent: dict, features: Tensor, labels: Tensor, idx: Tensor, ws, nb_fwd, nb_bwd: int, adam,
+    def _capture(self, ent: dict, features: Tensor, labels: Tensor, idx: Tensor, nb_fwd, nb_bwd: int, adam,
                  slot: int):
         (p, m, v), (lr, b1, b2, eps, wd, step, dec) = adam
         dev = self.flat.grad.device
@@ -497,9 +501,10 @@ class MotionTrainStep:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             nb, sp = nb_fwd  # (sequences per forward workgroup, forward lanes per unit)
-            self.mod.lstm_head_train_step(features, ent["idx"], labels, ws, hw, hb, self.flat.grad, self.ring,
-                                          self.H, self.NL, sp, 0, nb, nb_bwd, None, None, 0, None, ent["step"],
-                                          ent["slot_off"], round_bf16=self.bf16)
+            ws, feats, cell = self._operands(features)  # GRU: the re-pack is part of the graph
+            self.mod.lstm_head_train_step(feats, ent["idx"], labels, ws, hw, hb, self.flat.grad, self.ring,
+                                          self.H, self.NL, sp, 0, nb, nb_bwd, None, None, cell, self.colmap,
+                                          ent["step"], ent["slot_off"], round_bf16=self.bf16)
             self.grad_sync()
             self.mod.adam_flat(p, self.flat.grad, m, v, None, lr, b1, b2, eps, wd, step, 1.0, bool(dec), False,
                                None, ent["step"], ent["ticket"])

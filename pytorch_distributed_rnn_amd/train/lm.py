@@ -55,6 +55,12 @@ class LMTrainer:
                       if distributed and (self.world > 1 or force_ddp) else self.inner)
         self.flat = next(iter(self.inner._pdrnn_flat.values()))
         self.optimizer = FusedAdam(self.inner.parameters(), lr=learning_rate)
+        if distributed and self.world > 1 and device.type == "cuda":
+            # this trainer carries the sticky persistent-timeout flag to Adam as
+            # its skip word and re-runs skipped steps (settle): the sync-free
+            # per-step verification mode is safe here, not in the motion trainers
+            from ..parallel.comm import use_step_verification
+            use_step_verification()
         self.seq_len = seq_len
         self.grad_clip = grad_clip
         self.log_interval = log_interval

@@ -232,6 +232,31 @@ def test_ddp_splits_oversized_parameter_across_buckets(tmp_path):
     assert out["err"] < 1e-6, out["err"]
 
 
+def test_ddp_split_uses_regular_cap_behind_first_bucket(tmp_path):
+    """a large weight right behind the small head parameters (the
+    first bucket still open) is split by the regular bucket cap, not by the
+    1 MiB first-bucket cap: 16 MiB at a 4 MiB cap = 4 slices, not 16."""
+    script = tmp_path / "split1.py"
+    script.write_text(
+        "import json, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch\n"
+        "from pytorch_distributed_rnn_amd.parallel import env\n"
+        "from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel\n"
+        "from pytorch_distributed_rnn_amd.utils.flat import flatten_module\n"
+        "env.init_distributed('gloo')\n"
+        "m = torch.nn.Sequential(torch.nn.Linear(1024, 4096), torch.nn.Linear(4096, 4))\n"
+        "flatten_module(m)\n"
+        "d = DistributedDataParallel(m, bucket_cap_mb=4, first_bucket_cap_mb=1)\n"
+        "lay = d.bucket_layout()\n"
+        "if env.get_rank() == 0:\n"
+        "    open('split1.json', 'w').write(json.dumps([b['names'] for b in lay]))\n"
+        "env.shutdown()\n")
+    torchrun([str(script)], nproc=2, cwd=str(tmp_path), timeout=300)
+    names = json.loads((tmp_path / "split1.json").read_text())
+    assert sum(1 for n in names if n == ["0.weight"]) == 4, names
+
+
 def test_allreduce_sweep_tool_world2(tmp_path):
     """bench/allreduce_sweep.py (the bucket-cap measurement) at world 2 on gloo:
     one JSON line per message size from rank 0."""

@@ -233,7 +233,7 @@ def _epoch_of(step, feats, labels, idx_list):
     return [r.clone() for r in res], replayed
 
 
-@pytest.mark.parametrize("mode", ["ddp", "horovod", "ddp-bf16"])
+@pytest.mark.parametrize("mode", ["ddp", "horovod", "ddp-bf16", "ddp-gru"])
 def test_epoch_graph_replay_matches_local(rccl_group, mode):
     """every step of an epoch (4 full batches + the short
     last one, indices as consecutive views of one tensor like the loader's)
@@ -254,7 +254,10 @@ def test_epoch_graph_replay_matches_local(rccl_group, mode):
     feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
     if bf16:
         feats = feats.to(torch.bfloat16)
-    m1 = MotionModel(9, 32, 2, 6, compute_dtype=torch.bfloat16 if bf16 else torch.float32).cuda()
+    # GRU: the packed [r|z|n_x|n_h] weights are re-packed
+    # into a persistent buffer inside the graph (no per-step allocation)
+    m1 = MotionModel(9, 32, 2, 6, cell="gru" if mode.endswith("gru") else "lstm",
+                     compute_dtype=torch.bfloat16 if bf16 else torch.float32).cuda()
     m2 = copy.deepcopy(m1)
     flatten_module(m2)
     o2 = FusedAdam(m2.parameters(), lr=2.5e-3)

@@ -65,8 +65,8 @@ def test_persistent_fp32_matches_per_step(cell, Hs, B, T, ndir, rev):
     on v_mfma_f32_16x16x4_f32 equals the per-step kernels up to fp32
     summation order: at H = 128 the row-owning recurrence
     (kernels/lstm_rows_f32.hip, forward and backward), at H = 256 the
-    persistent backward (the fp32 persistent forward only with
-    PDRNN_LSTM_PERSIST_F32_FWD=1, read once per process)."""
+    persistent backward (the fp32 forward runs the per-step kernels: its
+    persistent form was slower and is not offered)."""
     mod = _ext.require()
     assert Hs == 128 or mod.lstm_large_persist_mt(B, Hs, ndir, 2) > 0
     torch.manual_seed(B + T + cell + Hs)

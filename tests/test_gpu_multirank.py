@@ -80,3 +80,35 @@ def test_two_rank_deferred_persist_verification(tmp_path):
         for a, b in zip(got[r]["losses"], ref[r]["losses"]):
             assert abs(a - b) < 1e-4, (got[r]["losses"], ref[r]["losses"])
 
+
+
+def test_two_rank_motion_persist_verification(tmp_path):
+    """the motion DDP trainer does not carry the LM
+    trainer's skip word, so multi-rank jobs keep per-launch verification
+    (mode 1): a timed-out persistent backward (fp32 H = 256) is re-run on the
+    per-step kernels before its gradient is all-reduced.  Rank 0's first
+    persistent launch is flagged as timed out; both ranks end with the
+    parameters of a run that never took the persistent path."""
+    import json
+    worker = os.path.join(ROOT, "tests", "_motion_verify_worker.py")
+
+    def job(extra):
+        for r in (0, 1):
+            (tmp_path / f"mverify_rank{r}.json").unlink(missing_ok=True)
+        run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+             "--master-addr=127.0.0.1", f"--master-port={free_port()}", worker],
+            cwd=str(tmp_path), env=_gpu_env(extra), timeout=150)
+        recs = [json.loads((tmp_path / f"mverify_rank{r}.json").read_text()) for r in (0, 1)
+                if (tmp_path / f"mverify_rank{r}.json").exists()]
+        return {r["rank"]: r for r in recs}
+
+    got = job({"PDRNN_TEST_INJECT_RANK": "0"})
+    ref = job({"PDRNN_LSTM_PERSIST": "0"})
+    assert sorted(got) == [0, 1] and sorted(ref) == [0, 1]
+    assert got[0]["verify"] == 1 and got[1]["verify"] == 1, got
+    assert got[0]["fallbacks"] == 1 and got[1]["fallbacks"] == 0, got
+    assert got[0]["checksum"] == got[1]["checksum"]
+    for r in (0, 1):
+        assert abs(got[r]["checksum"] - ref[r]["checksum"]) <= 1e-5 * ref[r]["abs"], (got[r], ref[r])
+        for a, b in zip(got[r]["losses"], ref[r]["losses"]):
+            assert abs(a - b) < 1e-4, (got[r]["losses"], ref[r]["losses"])

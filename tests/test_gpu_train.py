@@ -239,6 +239,7 @@ def test_headline_batch_gradients_match_fp64(B, nb, fused, monkeypatch):
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     monkeypatch.delenv("PDRNN_LSTM_DWOUT", raising=False)
+    monkeypatch.setenv("PDRNN_SW", "0")  # the gate-split / K-split family (sequence-in-wave: test below)
     monkeypatch.setenv("PDRNN_DWOUT_NB", nb)
     monkeypatch.setenv("PDRNN_BWD_DW_FUSED", fused)
     mod = _ext.native(torch.device("cuda", 0))
@@ -253,6 +254,63 @@ def test_headline_batch_gradients_match_fp64(B, nb, fused, monkeypatch):
     for (k, r), g in zip(ref.named_parameters(), grads):
         scale = r.grad.abs().max().item()
         assert (g - r.grad).abs().max().item() <= 2e-6 * scale + 1e-12, k
+
+
+def _fp64_check(m0, train, B, tol=2e-6):
+    grads, x, y = _fused_grads(copy.deepcopy(m0), train, B)
+    ref = copy.deepcopy(m0).cuda().double()
+    torch.nn.functional.cross_entropy(ref(x.double()), y).backward()
+    for (k, r), g in zip(ref.named_parameters(), grads):
+        scale = r.grad.abs().max().item()
+        assert (g - r.grad).abs().max().item() <= tol * scale + 1e-12, k
+
+
+@pytest.mark.parametrize("B,layers,mode", [(1440, 2, ""), (1152, 2, ""), (720, 2, ""), (360, 2, ""), (180, 2, ""),
+                                           (144, 2, ""), (97, 2, ""), (1440, 2, "2"), (180, 2, "3"),
+                                           (180, 1, ""), (1440, 1, ""), (180, 2, "0")])
+def test_seq_in_wave_step_gradients_match_fp64(B, layers, mode, monkeypatch):
+    """The sequence-in-wave step (kernels/lstm_sw.hip: each sequence's
+    recurrence inside one wave, or one wave per layer; deferred matrix-core
+    dW; one-pass reduction) at every per-rank batch of the 1/2/4/8-GPU
+    strong-scaling runs (1440 / 720 / 360 / 180, and the epoch's short last
+    batches 1152 / 144), an odd batch (a half-empty two-sequence wave), each
+    wave map forced once, and the single-layer config-2 shape: gradients
+    before Adam against fp64 torch autograd on the same weights and batch."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.delenv("PDRNN_SW", raising=False)
+    if mode:
+        monkeypatch.setenv("PDRNN_SW_MODE", mode)
+    else:
+        monkeypatch.delenv("PDRNN_SW_MODE", raising=False)
+    mod = _ext.native(torch.device("cuda", 0))
+    assert mod.lstm_sw_ok(32, 9, layers)
+    torch.manual_seed(13 + B)
+    train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=14)
+    _fp64_check(MotionModel(9, 32, layers, 6), train, B)
+
+
+@pytest.mark.parametrize("cell,B", [("gru", 180), ("gru", 144), ("lstm", 180), ("lstm", 144)])
+def test_one_launch_gradients_match_fp64(cell, B, monkeypatch):
+    """the one-launch step kernel (lstm_small_step_gs_kernel,
+    forward + head/CE + register-dW BPTT per workgroup) at the 8-GPU epoch's
+    per-rank batches against fp64 autograd: the GRU's path, and the LSTM's
+    with the sequence-in-wave kernels switched off (PDRNN_SW=0)."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.ops.lstm import fused_bwd_nb, small_launch_config
+    monkeypatch.setenv("PDRNN_SW", "0")
+    monkeypatch.delenv("PDRNN_LSTM_DWOUT", raising=False)
+    mod = _ext.native(torch.device("cuda", 0))
+    nb_f, sp_f, _, sp_b = small_launch_config(B, 32, 2)
+    if cell == "gru":
+        nb_f, sp_f = 1, 1
+    assert mod.lstm_small_step_one_launch(32, 2, 128, B, nb_f, sp_f, fused_bwd_nb(B, 32, 2), sp_b)
+    torch.manual_seed(21 + B)
+    train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=22)
+    _fp64_check(MotionModel(9, 32, 2, 6, cell=cell), train, B)
 
 
 def test_deferred_dw_pairs_sequences_at_headline_batch(monkeypatch):
