@@ -10,15 +10,19 @@ OUT=pytorch_distributed_rnn_amd/build_native/probe
 if [ "$1" = build ]; then
   mkdir -p $OUT
   FL="-O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics -Ipytorch_distributed_rnn_amd/csrc/include ${PROBE_FLAGS}"
-  for f in lstm_sw lstm_mb lstm_small lstm_small_dw; do
-    if [ ! -f $OUT/$f.o ] || [ $K/$f.hip -nt $OUT/$f.o ] || [ -n "$PROBE_FLAGS" ]; then
-      /opt/rocm/bin/hipcc -c $FL $K/$f.hip -o $OUT/$f.o 2>/dev/null &
+  # the two kernel files under study always rebuild (PROBE_FLAGS diagnostics);
+  # the gate-split family only when its source changed
+  for f in lstm_sw lstm_mb; do /opt/rocm/bin/hipcc -c $FL $K/$f.hip -o $OUT/$f.o 2>/dev/null & done
+  for f in lstm_small lstm_small_dw; do
+    if [ ! -f $OUT/$f.o ] || [ $K/$f.hip -nt $OUT/$f.o ]; then
+      /opt/rocm/bin/hipcc -c -O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics \
+        -Ipytorch_distributed_rnn_amd/csrc/include $K/$f.hip -o $OUT/$f.o 2>/dev/null &
     fi
   done
   /opt/rocm/bin/hipcc -c $FL bench/sw_probe.cpp -o $OUT/sw_probe.o 2>/dev/null &
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 $OUT/*.o -o $OUT/sw_probe
-  echo built $OUT/sw_probe
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 $OUT/*.o -o $OUT/${PROBE_NAME:-sw_probe}
+  echo built $OUT/${PROBE_NAME:-sw_probe}
   exit 0
 fi
 tag=${2:-sw}

@@ -15,7 +15,9 @@ Policy (so that GPU runs never silently fall back to eager PyTorch):
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 from typing import Optional
 
 import torch
@@ -35,8 +37,6 @@ def _try_import():
         if so:
             # an alternative build of the extension (e.g. the sanitizer build of
             # _build.py, PDRNN_SANITIZE): loaded under the same module name
-            import importlib.util
-            import sys
             spec = importlib.util.spec_from_file_location("pytorch_distributed_rnn_amd._C", so)
             _C = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(_C)

@@ -468,7 +468,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   // K-split family below (A/B).  Weight gradients deferred to lstm_small_dw.
   const bool sw = sw_enabled() && pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, (int)cell) == 1 &&
                   pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T) != 0 && T <= 640;
-  const int sw_mode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B) : -1;
+  const int sw_fmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 0) : -1;
+  const int sw_bmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 1) : -1;
   // Above one residency round the BPTT defers its weight gradients: the
   // recurrence writes the gate gradients (into `act`, in place) and the
   // matrix-core kernel lstm_small_dw forms dW / db over all B*T rows, one slab
@@ -517,11 +518,12 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   Tensor xg;
   if (dwout) xg = at::empty({(B * T + 16) * xg_ld + 256}, opts);  // + one DMA job past the last 16-row stage
   if (sw) { f.xg_out = xg.data_ptr<float>(); f.xg_ld = (int)xg_ld; }
-  const int sw_nb = sw_mode == 1 ? 2 : 1;
+  // sequences per sequence-in-wave workgroup: two in the odd modes
+  const int sw_fnb = sw_fmode & 1 ? 2 : 1, sw_bnb = sw_bmode & 1 ? 2 : 1;
   Tensor st_f, st_b;
   if (stamps_enabled()) {
-    st_f = at::zeros({sw ? (B + sw_nb - 1) / sw_nb : (B + nb_fwd - 1) / nb_fwd, 8}, opts.dtype(at::kLong));
-    st_b = at::zeros({sw ? (B + sw_nb - 1) / sw_nb : gridb, 8}, opts.dtype(at::kLong));
+    st_f = at::zeros({sw ? (B + sw_fnb - 1) / sw_fnb : (B + nb_fwd - 1) / nb_fwd, 8}, opts.dtype(at::kLong));
+    st_b = at::zeros({sw ? (B + sw_bnb - 1) / sw_bnb : gridb, 8}, opts.dtype(at::kLong));
     f.stamps = reinterpret_cast<uint64_t*>(st_f.data_ptr<int64_t>());
   }
   // latency regime (one sequence per workgroup in both passes): forward,
@@ -529,7 +531,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const bool one_launch = !dwout && !st_f.defined() &&
       pdrnn_lstm_small_step_ok((int)H, (int)NL, (int)B, (int)nb_fwd, (int)split_fwd, (int)nb_bwd, (int)split_bwd,
                                gridb) == 1;
-  if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_fwd(&f, sw_mode, st));
+  if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_fwd(&f, sw_fmode, st));
   else if (!one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
 
   PdrnnLstmSmallBwdArgs bk{};
@@ -547,7 +549,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   bk.w_bf16 = f.w_bf16;
   int grid_dw = gridb;
   if (dwout) {
-    grid_dw = sw ? (int)((B + sw_nb - 1) / sw_nb)
+    grid_dw = sw ? (int)((B + sw_bnb - 1) / sw_bnb)
                  : dw_fused ? slab_rows : pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb_dw);
     TORCH_CHECK(grid_dw > 0, "deferred-dW backward: no resident grid");
     if (st_f.defined() && !sw) {
@@ -571,7 +573,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     }
     dw.B = (int)B; dw.T = (int)T; dw.I = (int)I; dw.NL = (int)NL; dw.chunks = slab_rows;
   }
-  if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_bwd(&bk, sw_mode, st));
+  if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_bwd(&bk, sw_bmode, st));
   else if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
   else if (dw_fused) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dw(&bk, &dw, (int)H, nb_dw, st));
   else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, nb_dw, st));
@@ -1443,9 +1445,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "(sequences per workgroup, grid, own-tile dW) of the deferred-dW backward for this shape (9 inputs)");
   m.def("lstm_sw_ok", [](int64_t H, int64_t I, int64_t NL) { return pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, 0) == 1; },
         "the sequence-in-wave kernels (lstm_sw.hip) cover this LSTM stack in the fused train step");
-  m.def("lstm_sw_mode", [](int64_t NL, int64_t B) { return pdrnn_lstm_sw_mode((int)NL, (int)B); },
+  m.def("lstm_sw_mode", [](int64_t NL, int64_t B, bool backward) { return pdrnn_lstm_sw_mode((int)NL, (int)B, backward ? 1 : 0); },
         "wave map of the sequence-in-wave kernels for B sequences (0/1: a wave per 1/2 sequences, 2/3: a wave "
-        "per layer of 1/2 sequences)");
+        "per layer of 1/2 sequences, 4/5: pipelined waves per layer)",
+        py::arg("NL"), py::arg("B"), py::arg("backward") = false);
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;
   });

@@ -175,7 +175,7 @@ hipError_t pdrnn_lstm_small_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstm
 // ----------------------------------------------------------------------------
 int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell);
 // mode for a batch of B sequences (PDRNN_SW_MODE overrides): 0, 1 or 2
-int pdrnn_lstm_sw_mode(int NL, int B);
+int pdrnn_lstm_sw_mode(int NL, int B, int backward);
 hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode, hipStream_t stream);
 hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode, hipStream_t stream);
 

@@ -99,3 +99,27 @@ def test_dropped_rank_fails_survivors_fast(tmp_path):
     for r in (0, 2):
         assert codes[r] != 0, f"survivor rank {r} exited 0:\n{outs[r][-2000:]}"
     assert elapsed < timeout_s * 4 + 60, elapsed
+
+
+def test_extension_loads_when_built(monkeypatch):
+    """The in-tree extension imports through the loader (both the default
+    module path and the PDRNN_EXT_SO alternative-build path): a loader error
+    would otherwise silently put every CPU host-runtime test on the Python
+    twins and every GPU run on the loud 'failed to load' path."""
+    import glob
+    import os
+
+    from pytorch_distributed_rnn_amd import _ext
+    pkg = os.path.dirname(_ext.__file__)
+    built = glob.glob(os.path.join(pkg, "_C*.so"))
+    if not built:
+        pytest.skip("extension not built in this tree")
+    for so in (None, built[0]):
+        if so:
+            monkeypatch.setenv("PDRNN_EXT_SO", so)
+        else:
+            monkeypatch.delenv("PDRNN_EXT_SO", raising=False)
+        monkeypatch.setattr(_ext, "_TRIED", False)
+        monkeypatch.setattr(_ext, "_C", None)
+        assert _ext.extension() is not None, repr(_ext._IMPORT_ERROR)
+        assert hasattr(_ext.extension(), "GradReducer")

@@ -288,12 +288,14 @@ def test_epoch_graph_replay_matches_local(rccl_group, mode):
         b = [s2(feats, labels, i).clone() for i in idx_list]
         outs.append((a, b))
     assert replays == 3, "the epoch was never replayed from a graph"
-    for a, b in outs:
-        for x, y in zip(a, b):
-            torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
     # bf16: the synced step reduces dW in another order than the local step;
     # fp32-level gradient differences flip bf16 roundings of the weights inside
-    # the kernels and Adam carries them over 25 steps (~1 % of one lr step)
+    # the kernels and Adam carries them over 25 steps (~1 % of one lr step),
+    # which moves the later losses by ~1e-5 relative
+    ltol = dict(rtol=1e-4, atol=1e-5) if bf16 else dict(rtol=1e-5, atol=1e-6)
+    for a, b in outs:
+        for x, y in zip(a, b):
+            torch.testing.assert_close(x, y, **ltol)
     ptol = dict(rtol=1e-3, atol=1e-4) if bf16 else dict(rtol=1e-5, atol=1e-6)
     for p, q in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(p, q, **ptol)

@@ -267,6 +267,7 @@ def _fp64_check(m0, train, B, tol=2e-6):
 
 @pytest.mark.parametrize("B,layers,mode", [(1440, 2, ""), (1152, 2, ""), (720, 2, ""), (360, 2, ""), (180, 2, ""),
                                            (144, 2, ""), (97, 2, ""), (1440, 2, "2"), (180, 2, "3"),
+                                           (180, 2, "4"), (97, 2, "5"), (720, 2, "2/4"), (1152, 2, "3/2"),
                                            (180, 1, ""), (1440, 1, ""), (180, 2, "0")])
 def test_seq_in_wave_step_gradients_match_fp64(B, layers, mode, monkeypatch):
     """The sequence-in-wave step (kernels/lstm_sw.hip: each sequence's
@@ -280,10 +281,12 @@ def test_seq_in_wave_step_gradients_match_fp64(B, layers, mode, monkeypatch):
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     monkeypatch.delenv("PDRNN_SW", raising=False)
-    if mode:
-        monkeypatch.setenv("PDRNN_SW_MODE", mode)
-    else:
-        monkeypatch.delenv("PDRNN_SW_MODE", raising=False)
+    fm, _, bm = mode.partition("/")  # "F/B": forward and backward maps forced apart
+    for var, val in (("PDRNN_SW_MODE", fm), ("PDRNN_SW_BWD_MODE", bm)):
+        if val:
+            monkeypatch.setenv(var, val)
+        else:
+            monkeypatch.delenv(var, raising=False)
     mod = _ext.native(torch.device("cuda", 0))
     assert mod.lstm_sw_ok(32, 9, layers)
     torch.manual_seed(13 + B)
