@@ -12,7 +12,9 @@ if [ "$1" = build ]; then
   FL="-O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics -Ipytorch_distributed_rnn_amd/csrc/include ${PROBE_FLAGS}"
   # the two kernel files under study always rebuild (PROBE_FLAGS diagnostics);
   # the gate-split family only when its source changed
-  for f in lstm_sw lstm_mb; do /opt/rocm/bin/hipcc -c $FL $K/$f.hip -o $OUT/$f.o 2>/dev/null & done
+  # SW_SRC: an alternative lstm_sw.hip (A/B against another revision)
+  /opt/rocm/bin/hipcc -c $FL ${SW_SRC:-$K/lstm_sw.hip} -o $OUT/lstm_sw.o 2>/dev/null &
+  /opt/rocm/bin/hipcc -c $FL $K/lstm_mb.hip -o $OUT/lstm_mb.o 2>/dev/null &
   for f in lstm_small lstm_small_dw; do
     if [ ! -f $OUT/$f.o ] || [ $K/$f.hip -nt $OUT/$f.o ]; then
       /opt/rocm/bin/hipcc -c -O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics \

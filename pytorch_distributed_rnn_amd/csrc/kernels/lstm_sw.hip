@@ -74,11 +74,17 @@ PDRNN_DEVICE int pick(const int (&v)[NB], int n) {
 // ---------------------------------------------------------------------------
 // Forward
 // ---------------------------------------------------------------------------
-// this lane's four gate rows over NC float4 chunks of its operand half, k pairs
+// This lane's four gate rows over NC float4 chunks of its operand half, k
+// pairs, in the order (m0, x0, m1, x1): m0 / m1 are the gates this lane
+// activates (s = 0: i, g; s = 1: f, o) and x0 / x1 the ones its partner
+// activates.  After the loop the sum of w[0] is this lane's own partial of
+// m0 and the sum of w[1] the partial its partner needs (and likewise for
+// m1): one DPP add per gate finishes the K-split sum, with no select.  The
+// biases of m0 / m1 seed their accumulators.
 template <int NC>
 struct FwdW {
   pdrnn_f2 w[4][2 * NC];
-  float bias[4];
+  float bias[2];
 };
 
 // Column of chunk c, element e (-1: zero) -- see the file comment.
@@ -100,8 +106,10 @@ PDRNN_DEVICE FwdW<NC> load_fwd_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, i
   const int Iin = l == 0 ? a.I : kH;
   const float* wih = a.w_ih[l];
   const float* whh = a.w_hh[l];
+  const int gq[4] = {s, 1 - s, 2 + s, 3 - s};  // (m0, x0, m1, x1)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int j = 0; j < 4; ++j) {
+    const int q = gq[j];
     const int r = q * kH + u;
     const float sc = kA * (q == 2 ? 2.f : 1.f);
 #pragma unroll
@@ -115,55 +123,54 @@ PDRNN_DEVICE FwdW<NC> load_fwd_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, i
         if (k >= 0) x = ih ? wih[(int64_t)r * Iin + k] : whh[(int64_t)r * kH + k];
         v[e] = wround(x, a.w_bf16) * sc;
       }
-      W.w[q][2 * c] = pdrnn_f2{v[0], v[1]};
-      W.w[q][2 * c + 1] = pdrnn_f2{v[2], v[3]};
+      W.w[j][2 * c] = pdrnn_f2{v[0], v[1]};
+      W.w[j][2 * c + 1] = pdrnn_f2{v[2], v[3]};
     }
-    W.bias[q] = ((a.b_ih[l] ? wround(a.b_ih[l][r], a.w_bf16) : 0.f) +
-                 (a.b_hh[l] ? wround(a.b_hh[l][r], a.w_bf16) : 0.f)) * sc;
+    if (!(j & 1))
+      W.bias[j >> 1] = ((a.b_ih[l] ? wround(a.b_ih[l][r], a.w_bf16) : 0.f) +
+                        (a.b_hh[l] ? wround(a.b_hh[l][r], a.w_bf16) : 0.f)) * sc;
   }
   return W;
 }
 
+// p[0] / p[2]: own partials of m0 / m1 (+ bias), p[1] / p[3]: the partner's
 template <int NC>
 PDRNN_DEVICE void fwd_dot(const FwdW<NC>& W, const float4 (&v)[NC], float (&p)[4]) {
-  pdrnn_f2 acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+  pdrnn_f2 acc[4] = {{W.bias[0], 0.f}, {0.f, 0.f}, {W.bias[1], 0.f}, {0.f, 0.f}};
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      acc[q] = pfma(W.w[q][2 * c], lo2(v[c]), acc[q]);
-      acc[q] = pfma(W.w[q][2 * c + 1], hi2(v[c]), acc[q]);
+    for (int j = 0; j < 4; ++j) {
+      acc[j] = pfma(W.w[j][2 * c], lo2(v[c]), acc[j]);
+      acc[j] = pfma(W.w[j][2 * c + 1], hi2(v[c]), acc[j]);
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) p[q] = acc[q].x + acc[q].y;
+  for (int j = 0; j < 4; ++j) p[j] = acc[j].x + acc[j].y;
 }
 
 struct Cell {
   float a0, a1, c, h;
 };
-// partial sums of both K halves -> this lane's two activations (s = 0: i, g;
-// s = 1: f, o) and the unit's new c, h (on both lanes)
-PDRNN_DEVICE Cell fwd_cell(const float (&p)[4], const float (&bias)[4], float c, bool odd) {
-  float tot[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) tot[q] = pair_sum(p[q]) + bias[q];
-  const float z0 = odd ? tot[1] : tot[0];
-  const float z1 = odd ? tot[3] : tot[2];
-  const float a0 = sig2(z0);
-  const float s1 = sig2(z1);
-  const float a1 = odd ? s1 : fmaf(s1, 2.f, -1.f);
-  const float b0 = dpp_swap1(a0), b1 = dpp_swap1(a1);
-  const float ig = odd ? b0 : a0, fg = odd ? a0 : b0;
-  const float gg = odd ? b1 : a1, og = odd ? a1 : b1;
+// DPP quad_perm [1, 1, 3, 3]: both lanes of a pair read the odd lane
+PDRNN_DEVICE float from_odd(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xF5, 0xF, 0xF, false));
+}
+// The K-split sums -> this lane's two activations (s = 0: i, g; s = 1: f, o;
+// `gk` = {2, -1} on even lanes: tanh(g) = 2 sigma(2g) - 1, {1, 0} on odd) and
+// the unit's new c, h on both lanes: c = f c + i g is the sum of one product
+// per lane (odd: f c, even: i g), h = o tanh(c) with o read from the odd lane.
+PDRNN_DEVICE Cell fwd_cell(const float (&p)[4], pdrnn_f2 gk, float c, bool odd) {
+  const float z0 = p[0] + dpp_swap1(p[1]);
+  const float z1 = p[2] + dpp_swap1(p[3]);
   Cell r;
-  r.a0 = a0;
-  r.a1 = a1;
-  r.c = fmaf(fg, c, ig * gg);
-  r.h = og * tanh_c(r.c);
+  r.a0 = sig2(z0);
+  r.a1 = fmaf(sig2(z1), gk.x, gk.y);
+  const float term = r.a0 * (odd ? c : r.a1);
+  r.c = term + dpp_swap1(term);
+  r.h = from_odd(r.a1) * tanh_c(r.c);
   return r;
 }
-
 template <int NL, int NB>
 PDRNN_DEVICE constexpr int fwd_lds_floats_hb() { return NB * NL * 2 * kHB; }
 
@@ -173,7 +180,7 @@ PDRNN_DEVICE constexpr int fwd_lds_floats_hb() { return NB * NL * 2 * kHB; }
 // mode 2 holds <= 168 VGPRs: three waves per SIMD, so B = 1440 (2880 layer
 // waves on 1024 SIMDs) is one residency round with every SIMD loaded evenly
 template <int NL, int MODE>
-__global__ void __launch_bounds__(MODE >= 2 ? 64 * NL : 64) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 3 : 1)))
+__global__ void __launch_bounds__(MODE >= 2 ? 64 * NL : 64) __attribute__((amdgpu_waves_per_eu(MODE == 6 ? 3 : 1)))
 lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   constexpr int NB = (MODE & 1) ? 2 : 1;
   constexpr bool SPLIT = MODE >= 2;
@@ -291,12 +298,13 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
     bstore(r.c, r_act, vo_c | m, rw * (5 * kH * 4));
     bstore(r.h, r_h, vo_h | m, rw * (kH * 4));
   };
+  const pdrnn_f2 gk = odd ? pdrnn_f2{1.f, 0.f} : pdrnn_f2{2.f, -1.f};
   auto cmp0 = [&](const FwdW<6>& W, int t, const float4 (&v)[NB][6]) {
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
       float p[4];
       fwd_dot<6>(W, v[n], p);
-      commit(0, n, t, t < T, fwd_cell(p, W.bias, cst[0][n], odd));
+      commit(0, n, t, t < T, fwd_cell(p, gk, cst[0][n], odd));
     }
   };
   auto cmp1 = [&](const FwdW<8>& W, int t, const float4 (&v)[NB][8]) {
@@ -304,7 +312,7 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
     for (int n = 0; n < NB; ++n) {
       float p[4];
       fwd_dot<8>(W, v[n], p);
-      commit(NL - 1, n, t, t >= 0, fwd_cell(p, W.bias, cst[NL - 1][n], odd));
+      commit(NL - 1, n, t, t >= 0, fwd_cell(p, gk, cst[NL - 1][n], odd));
     }
   };
 
@@ -327,12 +335,17 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
       cmp1(W1, it - 1, v1);
     }
   } else {
+    // mode 2: every operand read of the step in flight before the first
+    // FMA (one LDS latency per step); mode 6 (the same map at <= 168 VGPRs,
+    // three waves per SIMD for B > one wave per SIMD) leaves the reads to the
+    // scheduler, which pairs them to stay within its registers
     if (wv == 0) {
       const FwdW<6> W0 = load_fwd_w<6>(a, 0, u, odd ? 1 : 0);
       for (int it = 0; it <= T; ++it) {
         if (it < T) {
           float4 v0[NB][6];
           rd0(it, v0);
+          if constexpr (MODE != 6) __builtin_amdgcn_sched_barrier(0);
           cmp0(W0, it, v0);
         }
         lds_barrier();
@@ -343,6 +356,7 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
         if (it > 0) {
           float4 v1[NB][8];
           rd1(it - 1, v1);
+          if constexpr (MODE != 6) __builtin_amdgcn_sched_barrier(0);
           cmp1(W1, it - 1, v1);
         }
         lds_barrier();
@@ -693,455 +707,6 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Pipelined wave map (modes 4 / 5, two layers): the input projections leave
-// the recurrences' critical path.  Per workgroup (NB sequences), four waves
-// linked by LDS rings instead of barriers:
-//   wave 0: xp0_t = W_ih0 x_t + b0            (no recurrence: runs ahead)
-//   wave 1: layer-0 recurrence on xp0_t        -> h0_t
-//   wave 2: xp1_t = W_ih1 h0_t + b1           (runs as soon as h0_t exists)
-//   wave 3: layer-1 recurrence on xp1_t        -> h1_t, the head
-// A recurrence wave's step is W_hh h_{t-1} only: lane (u, s) holds the four
-// gate rows of unit u over h columns [16 s, 16 s + 16) (32 packed FMAs) plus
-// the unit's four projections (one ds_read_b128).  A projection wave's lane L
-// owns gate-interleaved rows 2L, 2L + 1 (projections stored [u][q]).
-// Ring hand-off: the producer writes a slot, then bumps its LDS counter; the
-// consumer polls the counter, reads the slot, then bumps its own consumed
-// counter, which the producer polls before overwriting.  One wave's LDS
-// operations execute in order, so the counter write lands after the data
-// write and a read issued after the poll sees it; the compiler is kept from
-// reordering across them by memory clobbers.  Every poll loop is bounded.
-// ---------------------------------------------------------------------------
-constexpr int kR = 8;  // ring slots
-
-PDRNN_DEVICE int ring_peek(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-PDRNN_DEVICE void ring_post(int* p, int v) {
-  asm volatile("" ::: "memory");
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-#ifndef SW_STAMPS
-#define SW_STAMPS 0  // diagnostic builds: cycles spent in ring waits (bench/sw_probe.sh, PROBE_FLAGS)
-#endif
-PDRNN_DEVICE void ring_wait(const int* p, int v, uint64_t* waited = nullptr) {
-  uint64_t t0 = 0;
-  if (SW_STAMPS && waited) t0 = stamp_cycles();
-  for (int n = 0; n < (1 << 24); ++n) {  // bounded: ~0.5 s of s_sleep at worst
-    if (__builtin_amdgcn_readfirstlane(ring_peek(p)) >= v) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");
-  if (SW_STAMPS && waited) *waited += stamp_cycles() - t0;
-}
-
-// counters: produced / consumed for each ring
-enum { kCXp0 = 0, kDXp0, kCH0, kDH0, kCXp1, kDXp1, kNCtr = 8 };
-
-template <int NB>
-struct SwpLds {
-  static constexpr int xs = 0;                        // [NB][T][kXS] (size depends on T: placed last)
-  static constexpr int xp0 = 0;                       // [NB][kR][4H]
-  static constexpr int h0 = xp0 + NB * kR * 4 * kH;   // [NB][kR][H]
-  static constexpr int xp1 = h0 + NB * kR * kH;       // [NB][kR][4H]
-  static constexpr int h1 = xp1 + NB * kR * 4 * kH;   // [NB][2][H]
-  static constexpr int ctr = h1 + NB * 2 * kH;        // kNCtr ints
-  static constexpr int xsb = ctr + kNCtr;             // x staging
-};
-
-// four gate rows of unit u over h columns [16 s, 16 s + 16), pre-scaled
-struct RecW {
-  pdrnn_f2 w[4][8];
-};
-PDRNN_DEVICE RecW load_rec_w(const float* whh, int u, int s, int wbf) {
-  RecW W;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float sc = kA * (q == 2 ? 2.f : 1.f);
-    const float* p = whh + (int64_t)(q * kH + u) * kH + 16 * s;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) W.w[q][j] = pdrnn_f2{wround(p[2 * j], wbf) * sc, wround(p[2 * j + 1], wbf) * sc};
-  }
-  return W;
-}
-// gate-interleaved rows 2L, 2L + 1 (unit L >> 1, gates 2 (L & 1) + {0, 1}) of
-// a [4H, K] input weight, pre-scaled, K zero-padded to KP
-template <int KP>
-struct ProjW {
-  pdrnn_f2 w[2][KP / 2];
-  float bias[2];
-};
-template <int KP>
-PDRNN_DEVICE ProjW<KP> load_proj_w(const float* wih, int K, const float* bih, const float* bhh, int L, int wbf) {
-  ProjW<KP> W;
-  const int u = L >> 1;
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int q = 2 * (L & 1) + e;
-    const int r = q * kH + u;
-    const float sc = kA * (q == 2 ? 2.f : 1.f);
-#pragma unroll
-    for (int j = 0; j < KP / 2; ++j) {
-      const int k0 = 2 * j, k1 = 2 * j + 1;
-      const float v0 = wih[(int64_t)r * K + min(k0, K - 1)], v1 = wih[(int64_t)r * K + min(k1, K - 1)];
-      W.w[e][j] = pdrnn_f2{k0 < K ? wround(v0, wbf) * sc : 0.f, k1 < K ? wround(v1, wbf) * sc : 0.f};
-    }
-    W.bias[e] = ((bih ? wround(bih[r], wbf) : 0.f) + (bhh ? wround(bhh[r], wbf) : 0.f)) * sc;
-  }
-  return W;
-}
-// projections of rows 2L, 2L + 1 from an LDS operand vector of KP floats
-template <int KP>
-PDRNN_DEVICE pdrnn_f2 proj_dot(const ProjW<KP>& W, const float* v) {
-  pdrnn_f2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
-  float4 x[KP / 4];
-#pragma unroll
-  for (int c = 0; c < KP / 4; ++c) x[c] = ld4(v + 4 * c);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int c = 0; c < KP / 4; ++c) {
-    a0 = pfma(W.w[0][2 * c], lo2(x[c]), a0);
-    a0 = pfma(W.w[0][2 * c + 1], hi2(x[c]), a0);
-    a1 = pfma(W.w[1][2 * c], lo2(x[c]), a1);
-    a1 = pfma(W.w[1][2 * c + 1], hi2(x[c]), a1);
-  }
-  return pdrnn_f2{a0.x + a0.y + W.bias[0], a1.x + a1.y + W.bias[1]};
-}
-
-template <int NB>
-__global__ void __launch_bounds__(256) lstm_swp_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
-  using Lay = SwpLds<NB>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int u = lane >> 1, s = lane & 1;
-  const bool odd = s != 0;
-  const int B = a.B, T = a.T, I = a.I;
-  const int bbase = blockIdx.x * NB;
-  int* ctr = reinterpret_cast<int*>(smem + Lay::ctr);
-  float* xs = smem + Lay::xsb;
-  auto xp0 = [&](int n, int t) { return smem + Lay::xp0 + (n * kR + (t & (kR - 1))) * 4 * kH; };
-  auto h0s = [&](int n, int t) { return smem + Lay::h0 + (n * kR + (t & (kR - 1))) * kH; };
-  auto xp1 = [&](int n, int t) { return smem + Lay::xp1 + (n * kR + (t & (kR - 1))) * 4 * kH; };
-  auto h1s = [&](int n, int t) { return smem + Lay::h1 + (n * 2 + (t & 1)) * kH; };
-
-  int bidx[NB], bsrc[NB];
-  bool valid[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    const int b = bbase + n;
-    valid[n] = b < B;
-    bidx[n] = valid[n] ? b : B - 1;
-    bsrc[n] = a.idx ? (int)a.idx[bidx[n]] : bidx[n];
-  }
-  for (int e = tid; e < Lay::xsb; e += 256) smem[e] = 0.f;  // rings (h_{-1} = 0) and counters
-  {
-    const int per = T * kXS, tot = NB * per;
-    for (int e0 = tid; e0 < tot; e0 += 4 * 256) {
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int e = min(e0 + r * 256, tot - 1);
-        const int n = e / per, rem = e - n * per;
-        const int t = rem / kXS, k = rem - t * kXS;
-        const float x = ldx(a.x, (int64_t)pick<NB>(bsrc, n) * a.x_sb + (int64_t)t * a.x_st + min(k, I - 1), a.x_bf16);
-        v[r] = k < I ? x : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int e = e0 + r * 256;
-        if (e < tot) {
-          const int n = e / per, rem = e - n * per;
-          const int t = rem / kXS, k = rem - t * kXS;
-          xs[e] = v[r];
-          if (a.xg_out && k < a.xg_ld && (n == 0 ? valid[0] : valid[NB - 1]))
-            a.xg_out[((int64_t)pick<NB>(bidx, n) * T + t) * a.xg_ld + k] = v[r];
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  uint64_t st0 = 0, sr0 = 0;
-  if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
-
-  if (wv == 0 || wv == 2) {
-    // ---- projection waves --------------------------------------------------
-    const bool l1 = wv == 2;
-    const int cP = l1 ? kCXp1 : kCXp0, dP = l1 ? kDXp1 : kDXp0;
-    if (!l1) {
-      const ProjW<kXS> W = load_proj_w<kXS>(a.w_ih[0], I, a.b_ih[0], a.b_hh[0], lane, a.w_bf16);
-      for (int t = 0; t < T; ++t) {
-        ring_wait(ctr + dP, t - kR + 1);  // slot t % R consumed by the recurrence wave
-#pragma unroll
-        for (int n = 0; n < NB; ++n) {
-          const pdrnn_f2 v = proj_dot<kXS>(W, xs + (n * T + t) * kXS);
-          *reinterpret_cast<pdrnn_f2*>(xp0(n, t) + 2 * lane) = v;
-        }
-        ring_post(ctr + cP, t + 1);
-      }
-    } else {
-      const ProjW<kH> W = load_proj_w<kH>(a.w_ih[1], kH, a.b_ih[1], a.b_hh[1], lane, a.w_bf16);
-      for (int t = 0; t < T; ++t) {
-        ring_wait(ctr + kCH0, t + 1);     // h0_t written
-        ring_wait(ctr + dP, t - kR + 1);  // xp1 slot free
-        pdrnn_f2 v[NB];
-#pragma unroll
-        for (int n = 0; n < NB; ++n) v[n] = proj_dot<kH>(W, h0s(n, t));
-        ring_post(ctr + kDH0, t + 1);     // h0_t read (the reads were issued before this write)
-#pragma unroll
-        for (int n = 0; n < NB; ++n) *reinterpret_cast<pdrnn_f2*>(xp1(n, t) + 2 * lane) = v[n];
-        ring_post(ctr + cP, t + 1);
-      }
-    }
-    return;
-  }
-
-  // ---- recurrence waves (1: layer 0, 3: layer 1) ----------------------------
-  const int l = wv == 1 ? 0 : 1;
-  const RecW W = load_rec_w(a.w_hh[l], u, s, a.w_bf16);
-  const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
-  const __amdgpu_buffer_rsrc_t r_h = uniform_rsrc(a.hseq);
-  const uint32_t vo_a0 = (s * kH + u) * 4, vo_a1 = ((2 + s) * kH + u) * 4, vo_c = (4 * kH + u) * 4, vo_h = u * 4;
-  uint32_t vmask[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) vmask[n] = valid[n] ? 0u : kOOR;
-  const int cIn = l == 0 ? kCXp0 : kCXp1, dIn = l == 0 ? kDXp0 : kDXp1;
-  float cst[NB], hst[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) { cst[n] = 0.f; hst[n] = 0.f; }
-  uint64_t waited = 0;
-  const uint64_t lt0 = SW_STAMPS ? stamp_cycles() : 0;
-  for (int t = 0; t < T; ++t) {
-    ring_wait(ctr + cIn, t + 1, &waited);
-    if (l == 0) ring_wait(ctr + kDH0, t - kR + 1, &waited);  // h0 slot t % R read by the projection wave
-    float4 xq[NB], hv[NB][4];
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      xq[n] = ld4((l == 0 ? xp0(n, t) : xp1(n, t)) + 4 * u);
-      const float* hp = (l == 0 ? h0s(n, t - 1) : h1s(n, t - 1)) + 16 * s;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) hv[n][c] = ld4(hp + 4 * c);
-    }
-    ring_post(ctr + dIn, t + 1);
-    // every read of the step in flight before the first use: one LDS latency
-    // per step (left alone, the scheduler pairs them and waits three times)
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      pdrnn_f2 acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          acc[q] = pfma(W.w[q][2 * c], lo2(hv[n][c]), acc[q]);
-          acc[q] = pfma(W.w[q][2 * c + 1], hi2(hv[n][c]), acc[q]);
-        }
-      float p[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) p[q] = acc[q].x + acc[q].y;
-      const float xb[4] = {xq[n].x, xq[n].y, xq[n].z, xq[n].w};
-      const Cell r = fwd_cell(p, xb, cst[n], odd);
-      cst[n] = r.c;
-      hst[n] = r.h;
-      (l == 0 ? h0s(n, t) : h1s(n, t))[u] = r.h;
-      const uint32_t rw = __builtin_amdgcn_readfirstlane((uint32_t)((l * B + pick<NB>(bidx, n)) * T + t));
-#if !(SW_STAMPS & 2)  // ablation: no global stores (timing only)
-      bstore(r.a0, r_act, vo_a0 | vmask[n], rw * (5 * kH * 4));
-      bstore(r.a1, r_act, vo_a1 | vmask[n], rw * (5 * kH * 4));
-      bstore(r.c, r_act, vo_c | vmask[n], rw * (5 * kH * 4));
-      bstore(r.h, r_h, vo_h | vmask[n], rw * (kH * 4));
-#endif
-    }
-    if (l == 0) ring_post(ctr + kCH0, t + 1);
-  }
-  if (a.stamps && tid == 64 * 3) {
-    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
-    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
-  }
-  if (SW_STAMPS && a.stamps && lane == 0) {  // [4 + 2 l]: loop cycles, [5 + 2 l]: of which ring waits
-    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
-    st[4 + 2 * l] = stamp_cycles() - lt0;
-    st[5 + 2 * l] = waited;
-  }
-#pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    if (!valid[n]) continue;
-    const int b = bbase + n;
-    if (!odd && a.hn) a.hn[((int64_t)l * B + b) * kH + u] = hst[n];
-    if (!odd && a.cn) a.cn[((int64_t)l * B + b) * kH + u] = cst[n];
-    if (l == 1 && a.head_w) motion_head(a, b, hst[n], u, odd);
-  }
-}
-
-// Pipelined BPTT (modes 4 / 5, two layers), three waves per workgroup:
-//   wave 1: layer-1 recurrence (row phase + dh = W_hh1^T dz1)  -> dz1 ring
-//   wave 2: layer-1 input gradient dx1 = W_ih1^T dz1            -> dx1 ring
-//   wave 0: layer-0 recurrence on dh = W_hh0^T dz0 + dx1
-// so each recurrence's step carries one 64-row column product per lane.
-enum { kCDz1 = 0, kDDz1, kCDx1, kDDx1 };
-
-template <int NB>
-struct SwpBwdLds {
-  static constexpr int dz1 = 0;                        // [NB][kR][kDZ]
-  static constexpr int dx1 = dz1 + NB * kR * kDZ;      // [NB][kR][H]
-  static constexpr int dz0 = dx1 + NB * kR * kH;       // [NB][2][kDZ]
-  static constexpr int ctr = dz0 + NB * 2 * kDZ;       // kNCtr ints
-  static constexpr int total = ctr + kNCtr;
-};
-
-template <int NB>
-__global__ void __launch_bounds__(192) lstm_swp_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
-  using Lay = SwpBwdLds<NB>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int u = lane >> 1, s = lane & 1;
-  const bool odd = s != 0;
-  const int B = a.B, T = a.T;
-  const int bbase = blockIdx.x * NB;
-  int* ctr = reinterpret_cast<int*>(smem + Lay::ctr);
-  auto dz1s = [&](int n, int i) { return smem + Lay::dz1 + (n * kR + (i & (kR - 1))) * kDZ; };
-  auto dx1s = [&](int n, int i) { return smem + Lay::dx1 + (n * kR + (i & (kR - 1))) * kH; };
-  auto dz0s = [&](int n, int i) { return smem + Lay::dz0 + (n * 2 + (i & 1)) * kDZ; };
-
-  int bidx[NB];
-  bool valid[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    const int b = bbase + n;
-    valid[n] = b < B;
-    bidx[n] = valid[n] ? b : B - 1;
-  }
-  uint32_t vmask[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) vmask[n] = valid[n] ? 0u : kOOR;
-  if (blockIdx.x == 0) {  // the dW kernel's 16 padding rows behind the last layer
-    float* pad = a.dg_out + (int64_t)2 * B * T * a.dg_st;
-    for (int e = tid; e < 16 * a.dg_st; e += 192) pad[e] = 0.f;
-  }
-  for (int e = tid; e < Lay::total; e += 192) smem[e] = 0.f;
-  __syncthreads();
-
-  const int colbase = dz_slot(64 * s);
-  if (wv == 2) {
-    // ---- layer-1 input gradient -------------------------------------------
-    const BwdCol Wih1 = load_bwd_col(a.w_ih[1], kH, u, true, u, s, a.w_bf16);
-    for (int i = 0; i < T; ++i) {
-      ring_wait(ctr + kCDz1, i + 1);
-      ring_wait(ctr + kDDx1, i - kR + 1);
-      float4 g[NB][16];
-#pragma unroll
-      for (int n = 0; n < NB; ++n)
-#pragma unroll
-        for (int c = 0; c < 16; ++c) g[n][c] = ld4(dz1s(n, i) + colbase + 4 * c);
-      ring_post(ctr + kDDz1, i + 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) {
-        const float vx = col_dot(Wih1, g[n]);
-        dx1s(n, i)[u] = vx;
-      }
-      ring_post(ctr + kCDx1, i + 1);
-    }
-    return;
-  }
-
-  // ---- recurrence waves: 1 = layer 1 (top), 0 = layer 0 --------------------
-  const int l = wv == 1 ? 1 : 0;
-  const bool top = l == 1;
-  const BwdCol Whh = load_bwd_col(a.w_hh[l], kH, u, true, u, s, a.w_bf16);
-  const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
-  const __amdgpu_buffer_rsrc_t r_dg = uniform_rsrc(a.dg_out);
-  const uint32_t st_act = 5 * kH * 4, st_dg = (uint32_t)a.dg_st * 4;
-  const uint32_t vo_i = u * 4, vo_f = (kH + u) * 4, vo_g = (2 * kH + u) * 4, vo_o = (3 * kH + u) * 4;
-  const uint32_t vo_c = (4 * kH + u) * 4;
-  const uint32_t vo_d0 = (2 * s * kH + u) * 4, vo_d1 = ((2 * s + 1) * kH + u) * 4;
-  const int slot0 = dz_slot(2 * s * kH + u), slot1 = dz_slot((2 * s + 1) * kH + u);
-  auto rowidx = [&](int n, int t) -> uint32_t {
-    return __builtin_amdgcn_readfirstlane((uint32_t)((l * B + pick<NB>(bidx, n)) * T + t));
-  };
-  auto load_ops = [&](int n, int t) {
-    const int tc = min(max(t, 0), T - 1);
-    const uint32_t ra = rowidx(n, tc) * st_act;
-    const uint32_t rp = __builtin_amdgcn_readfirstlane(tc > 0 ? ra - st_act : ra);
-    Ops o;
-    o.i = bload(r_act, vo_i, ra);
-    o.f = bload(r_act, vo_f, ra);
-    o.g = bload(r_act, vo_g, ra);
-    o.o = bload(r_act, vo_o, ra);
-    o.c = bload(r_act, vo_c, ra);
-    o.cp = bload(r_act, vo_c, rp);
-    return o;
-  };
-  float dhrec[NB], dc[NB], dhtop[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    dhrec[n] = 0.f;
-    dc[n] = 0.f;
-    dhtop[n] = top ? a.dhn[(int64_t)bidx[n] * kH + u] : 0.f;
-  }
-  Ops opA[NB], opB[NB];
-#pragma unroll
-  for (int n = 0; n < NB; ++n) opA[n] = load_ops(n, T - 1);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int n = 0; n < NB; ++n) opB[n] = load_ops(n, T - 2);
-  __builtin_amdgcn_sched_barrier(0);
-  uint64_t st0 = 0, sr0 = 0;
-  if (a.stamps && tid == 64) { st0 = stamp_cycles(); sr0 = stamp_real(); }
-
-  // step i works on t = T-1-i (both layers: layer 0 consumes dx1 of the same t)
-  auto body = [&](int i, Ops (&op)[NB]) {
-    const int t = T - 1 - i;
-    float dxin[NB];
-    if (top) {
-      ring_wait(ctr + kDDz1, i - kR + 1);  // dz1 slot i % R read by the input-gradient wave
-#pragma unroll
-      for (int n = 0; n < NB; ++n) dxin[n] = i == 0 ? dhtop[n] : 0.f;
-    } else {
-      ring_wait(ctr + kCDx1, i + 1);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) dxin[n] = dx1s(n, i)[u];
-      ring_post(ctr + kDDx1, i + 1);
-    }
-    float* zb[NB];
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      zb[n] = top ? dz1s(n, i) : dz0s(n, i);
-      float d0, d1, dcn = dc[n];
-      row_phase(op[n], dhrec[n] + dxin[n], dcn, odd, t > 0, d0, d1);
-      dc[n] = dcn;
-      zb[n][slot0] = d0;
-      zb[n][slot1] = d1;
-      const uint32_t so = rowidx(n, t) * st_dg;
-      bstore(d0, r_dg, vo_d0 | vmask[n], so);
-      bstore(d1, r_dg, vo_d1 | vmask[n], so);
-    }
-    if (top) ring_post(ctr + kCDz1, i + 1);
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      float4 g[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) g[c] = ld4(zb[n] + colbase + 4 * c);
-      __builtin_amdgcn_sched_barrier(0);
-      dhrec[n] = col_dot(Whh, g);
-    }
-#pragma unroll
-    for (int n = 0; n < NB; ++n) op[n] = load_ops(n, t - 2);
-  };
-  int i = 0;
-  for (; i + 1 < T; i += 2) {
-    body(i, opA);
-    body(i + 1, opB);
-  }
-  if (i < T) body(i, opA);
-  if (a.stamps && tid == 64) {
-    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
-    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
-  }
-}
-
 // ---- host side -------------------------------------------------------------
 int sw_cus() {
   static thread_local int c_dev = -1, c_val = 0;
@@ -1182,34 +747,26 @@ hipError_t launch_bwd(const PdrnnLstmSmallBwdArgs* a, hipStream_t st) {
 
 using namespace pdrnn;
 
-namespace pdrnn {
-namespace {
-size_t swp_fwd_lds(int nb, int T) {
-  const int xsb = nb == 2 ? SwpLds<2>::xsb : SwpLds<1>::xsb;
-  return sizeof(float) * ((size_t)xsb + (size_t)nb * T * kXS);
-}
-size_t swp_bwd_lds(int nb) { return sizeof(float) * (size_t)(nb == 2 ? SwpBwdLds<2>::total : SwpBwdLds<1>::total); }
-}  // namespace
-}  // namespace pdrnn
 
 extern "C" int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell) {
   return (H == kH && I >= 1 && I <= kXS && (NL == 1 || NL == 2) && cell == 0) ? 1 : 0;
 }
 
-// Measured (bench/sw_probe.cpp, profiles/r5/sw): two-layer stacks run the
-// forward one wave per layer (mode 2, three waves per SIMD) at every B; the
-// backward one wave per layer up to one wave per SIMD and two sequences per
-// wave (mode 3) above.  One layer: one wave per sequence (mode 0), two above
-// one wave per SIMD (mode 1).  PDRNN_SW_MODE / PDRNN_SW_BWD_MODE override.
+// Measured (bench/sw_probe.cpp, profiles/r5/sw): two-layer stacks run one
+// wave per layer up to one wave per SIMD (mode 2); above, the forward keeps
+// that map at three waves per SIMD (mode 6) and the backward takes two
+// sequences per wave (mode 3).  One layer: one wave per sequence (mode 0),
+// two above one wave per SIMD (mode 1).  PDRNN_SW_MODE / PDRNN_SW_BWD_MODE
+// override.
 extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
   const char* e = getenv(backward ? "PDRNN_SW_BWD_MODE" : "PDRNN_SW_MODE");
   if (!(e && *e) && backward) e = getenv("PDRNN_SW_MODE");
   if (e && *e) {
     const int m = atoi(e);
-    if (m >= 0 && m <= 5 && (m < 2 || NL == 2)) return m;
+    if (m >= 0 && m <= 6 && m != 4 && m != 5 && (m < 2 || NL == 2) && (m != 6 || !backward)) return m;
   }
   const int simds = 4 * sw_cus();
-  if (NL == 2) return !backward || B <= simds ? 2 : 3;
+  if (NL == 2) return B <= simds ? 2 : backward ? 3 : 6;
   return B <= simds ? 0 : 1;
 }
 
@@ -1228,22 +785,7 @@ extern "C" hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode
   if (mode == 1) return launch_fwd<2, 1>(a, st);
   if (mode == 2) return launch_fwd<2, 2>(a, st);
   if (mode == 3) return launch_fwd<2, 3>(a, st);
-  if (mode == 4 || mode == 5) {
-    const int nb = mode == 5 ? 2 : 1;
-    const size_t lds = swp_fwd_lds(nb, a->T);
-    if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-    const int grid = (a->B + nb - 1) / nb;
-    if (mode == 4) {
-      if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)lstm_swp_fwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lstm_swp_fwd_kernel<1>), dim3(grid), dim3(256), lds, st, *a);
-    } else {
-      if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)lstm_swp_fwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((lstm_swp_fwd_kernel<2>), dim3(grid), dim3(256), lds, st, *a);
-    }
-    return hipGetLastError();
-  }
+  if (mode == 6) return launch_fwd<2, 6>(a, st);
   return hipErrorInvalidValue;
 }
 
@@ -1261,12 +803,5 @@ extern "C" hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode
   if (mode == 1) return launch_bwd<2, 1>(a, st);
   if (mode == 2) return launch_bwd<2, 2>(a, st);
   if (mode == 3) return launch_bwd<2, 3>(a, st);
-  if (mode == 4 || mode == 5) {
-    const int nb = mode == 5 ? 2 : 1;
-    const int grid = (a->B + nb - 1) / nb;
-    if (mode == 4) hipLaunchKernelGGL((lstm_swp_bwd_kernel<1>), dim3(grid), dim3(192), swp_bwd_lds(1), st, *a);
-    else hipLaunchKernelGGL((lstm_swp_bwd_kernel<2>), dim3(grid), dim3(192), swp_bwd_lds(2), st, *a);
-    return hipGetLastError();
-  }
   return hipErrorInvalidValue;
 }
