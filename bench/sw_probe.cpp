@@ -212,10 +212,10 @@ int main(int argc, char** argv) {
   }
   float* dhw = (float*)up(hw.data(), hw.size() * 4);
   float* dhb = (float*)up(hb.data(), hb.size() * 4);
-  const size_t n_act = (size_t)NL * B * T * 5 * H + 16 * 5 * H;
-  const size_t n_h = H + (size_t)NL * B * T * H + 16 * H;
+  const size_t n_act = (size_t)NL * B * T * 5 * H + PDRNN_DW_PAD_ROWS * 5 * H;
+  const size_t n_h = H + (size_t)NL * B * T * H + PDRNN_DW_PAD_ROWS * H;
   const int xg_ld = 12;
-  const size_t n_xg = ((size_t)B * T + 16) * xg_ld + 256;
+  const size_t n_xg = ((size_t)B * T + PDRNN_DW_PAD_ROWS) * xg_ld + 256;
   const int PH = C * H + C + 3;
   float *act, *hbuf, *xg, *hslab, *dhtop, *hn, *cn;
   CK(hipMalloc(&act, n_act * 4)); CK(hipMalloc(&hbuf, n_h * 4)); CK(hipMalloc(&xg, n_xg * 4));
@@ -307,6 +307,18 @@ int main(int argc, char** argv) {
     const double e_act = maxrel(h_act, RR.act, rows, 5 * H, 5 * H, 5 * H);
     const double e_h = maxrel(hseq_only, RR.hseq, rows, H, H, H);
     const double e_dht = maxrel(h_dht, RR.dhtop, B, H, H, H);
+    if (getenv("PROBE_DUMP") && e_act > tol) {  // first mismatching activations: (l, b, t, slot)
+      int shown = 0;
+      for (size_t r = 0; r < rows && shown < 12; ++r)
+        for (int k = 0; k < 5 * H && shown < 12; ++k) {
+          const double ref = RR.act[r * 5 * H + k], got = h_act[r * 5 * H + k];
+          if (std::fabs(got - ref) > 0.1) {
+            printf("  act l=%zu b=%zu t=%zu slot=%d got %.4f ref %.4f\n", r / ((size_t)B * T), (r / T) % B, r % T, k,
+                   got, ref);
+            ++shown;
+          }
+        }
+    }
     run_bwd();
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(h_act.data(), act, n_act * 4, hipMemcpyDeviceToHost));

@@ -448,9 +448,10 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const int64_t PH = P_head + 3;              // + [loss, count, correct]
   auto opts = x.options().dtype(at::kFloat);
   // hseq / act with the deferred-dW kernel's padding (one h row in front,
-  // 16 rows behind: it streams whole 16-row stages without clamps)
-  Tensor hseq_buf = at::empty({H + NL * B * T * H + 16 * H}, opts);
-  Tensor act = at::empty({NL * B * T * 5 * H + 16 * 5 * H}, opts);
+  // PDRNN_DW_PAD_ROWS rows behind: it streams whole stages without clamps)
+  constexpr int64_t PADR = PDRNN_DW_PAD_ROWS;
+  Tensor hseq_buf = at::empty({H + NL * B * T * H + PADR * H}, opts);
+  Tensor act = at::empty({NL * B * T * 5 * H + PADR * 5 * H}, opts);
   Tensor hn = at::empty({NL, B, H}, opts), cn = at::empty({NL, B, H}, opts);
   Tensor dh_top = at::empty({B, H}, opts);
   Tensor head_slab = at::empty({B, PH}, opts);
@@ -477,15 +478,10 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   // the one-launch step (register-resident dW, no extra launch).
   const int dw_mode = pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T);
   const bool dwout = sw || (nb_bwd == 1 && split_bwd == 1 && ((gridb < B && dw_mode == 1) || dw_mode == 2));
-  // deferred dW: sequences per BPTT workgroup, and whether those workgroups
-  // form the dW of their own tile (one slab row per tile) or a separate
-  // matrix-core launch does it over fixed K chunks
+  // deferred dW: sequences per BPTT workgroup; the matrix-core launch forms
+  // dW over fixed K chunks, one slab row each
   const int nb_dw = dwout ? pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B) : (int)nb_bwd;
-  // (one slab row per tile: above ~1k tiles the reduction's slab read outweighs the saved dW pass)
-  const bool dw_fused = !sw && dwout && (B + nb_dw - 1) / nb_dw <= 1024 &&
-                        pdrnn_lstm_small_bwd_dw_ok((int)H, (int)NL, (int)T, (int)B, (int)I, nb_dw) == 1;
-  const int slab_rows = dw_fused ? (int)((B + nb_dw - 1) / nb_dw)
-                                 : dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
+  const int slab_rows = dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
   Tensor slab = at::empty({slab_rows, L.P}, opts);
 
   PdrnnLstmSmallFwdArgs f{};
@@ -516,7 +512,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   // the sequence-in-wave forward, or by the gate-split deferred-dW backward)
   const int64_t xg_ld = (I + 3) / 4 * 4;
   Tensor xg;
-  if (dwout) xg = at::empty({(B * T + 16) * xg_ld + 256}, opts);  // + one DMA job past the last 16-row stage
+  if (dwout) xg = at::empty({(B * T + PADR) * xg_ld + 256}, opts);  // + one DMA job past the last stage
   if (sw) { f.xg_out = xg.data_ptr<float>(); f.xg_ld = (int)xg_ld; }
   // sequences per sequence-in-wave workgroup: two in the odd modes
   const int sw_fnb = sw_fmode & 1 ? 2 : 1, sw_bnb = sw_bmode & 1 ? 2 : 1;
@@ -550,7 +546,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   int grid_dw = gridb;
   if (dwout) {
     grid_dw = sw ? (int)((B + sw_bnb - 1) / sw_bnb)
-                 : dw_fused ? slab_rows : pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb_dw);
+                 : pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb_dw);
     TORCH_CHECK(grid_dw > 0, "deferred-dW backward: no resident grid");
     if (st_f.defined() && !sw) {
       st_b = at::zeros({grid_dw, 8}, opts.dtype(at::kLong));
@@ -575,17 +571,15 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   }
   if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_bwd(&bk, sw_bmode, st));
   else if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
-  else if (dw_fused) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dw(&bk, &dw, (int)H, nb_dw, st));
   else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, nb_dw, st));
   else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
-  if (dwout && !dw_fused) HIP_LAUNCH_CHECK(pdrnn_lstm_small_dw(&dw, (int)H, st));
+  if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_dw(&dw, (int)H, st));
   if (st_f.defined()) {
     const int bw_iters = sw ? (int)(T + NL - 1)
                             : (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_dw - 1) / ((int64_t)grid_dw * nb_dw));
     report_stamps(sw ? "fwd(head step, seq-in-wave)" : "fwd(head step)", st_f, (int)(T + NL - 1));
     report_stamps(sw ? "bwd(head step, seq-in-wave, deferred dW)"
-                     : dw_fused ? "bwd(head step, lean, own-tile dW)"
-                                : dwout ? "bwd(head step, lean, deferred dW)" : "bwd(head step, lean)",
+                     : dwout ? "bwd(head step, lean, deferred dW)" : "bwd(head step, lean)",
                   st_b, bw_iters);
   }
 
@@ -1440,14 +1434,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "the fused training step defers the weight gradients to the matrix-core dW kernel for this shape");
   m.def("lstm_small_dwout_geometry", [](int64_t H, int64_t NL, int64_t T, int64_t B) {
     const int nb = pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B);
-    return py::make_tuple(nb, pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb),
-                          pdrnn_lstm_small_bwd_dw_ok((int)H, (int)NL, (int)T, (int)B, 9, nb) == 1);
-  }, "(sequences per workgroup, grid, own-tile dW) of the deferred-dW backward for this shape (9 inputs)");
+    return py::make_tuple(nb, pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb));
+  }, "(sequences per workgroup, grid) of the deferred-dW backward for this shape");
   m.def("lstm_sw_ok", [](int64_t H, int64_t I, int64_t NL) { return pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, 0) == 1; },
         "the sequence-in-wave kernels (lstm_sw.hip) cover this LSTM stack in the fused train step");
   m.def("lstm_sw_mode", [](int64_t NL, int64_t B, bool backward) { return pdrnn_lstm_sw_mode((int)NL, (int)B, backward ? 1 : 0); },
         "wave map of the sequence-in-wave kernels for B sequences (0/1: a wave per 1/2 sequences, 2/3: a wave "
-        "per layer of 1/2 sequences, 4/5: pipelined waves per layer)",
+        "per layer of 1/2 sequences, 6: mode 2 at three waves per SIMD, forward only)",
         py::arg("NL"), py::arg("B"), py::arg("backward") = false);
   m.def("lstm_small_supported", [](int64_t H, int64_t I, int64_t NL) {
     return pdrnn_lstm_small_supported((int)H, (int)I, (int)NL) != 0;

@@ -94,8 +94,8 @@ typedef struct {
   // (layer l, row b, step t) to dg_out + ((l*B + b)*T + t)*dg_st + [0, 4H)
   // instead (dg_out may be `act` itself, dg_st = 5H: each lane overwrites the
   // activation slot it has just consumed); pdrnn_lstm_small_dw then forms
-  // dW_ih, dW_hh and the biases on the matrix cores.  dg_out must have 16
-  // padding rows behind the last layer (the kernel zeroes them).
+  // dW_ih, dW_hh and the biases on the matrix cores.  dg_out must have
+  // PDRNN_DW_PAD_ROWS padding rows behind the last layer (the kernel zeroes them).
   float* dg_out;
   int64_t dg_st;
   float* xg_out;             // DWOUT: [B*T][xg_ld] fp32 copy of the (gathered, widened) layer-0 input
@@ -112,9 +112,12 @@ typedef struct {
 // split over `chunks` contiguous (b, t) row ranges: chunk c writes slab row c
 // (columns in the stack's flat parameter layout), reduced afterwards by
 // pdrnn_slab_reduce_adam.
-// Padding contract (the kernel streams whole 16-row stages without clamps):
-// hseq readable from row -1 of layer 0 (H floats before it) through 16 rows
-// past the last layer; dg and xg readable through 16 rows past their end.
+// Padding contract (the kernel streams whole stages of up to
+// PDRNN_DW_PAD_ROWS rows without clamps): hseq readable from row -1 of layer
+// 0 (H floats before it) through PDRNN_DW_PAD_ROWS rows past the last layer;
+// dg and xg readable through PDRNN_DW_PAD_ROWS rows past their end (dg: those
+// rows finite -- the BPTT zeroes them).
+#define PDRNN_DW_PAD_ROWS 32
 typedef struct {
   const float* xg;           // layer-0 input rows [B*T][xg_ld] fp32 (the BPTT's xg_out), xg_ld = I rounded up to 4
   int xg_ld;
@@ -138,11 +141,6 @@ hipError_t pdrnn_lstm_small_dw(const PdrnnLstmSmallDwArgs* a, int H, hipStream_t
 // nb = sequences per workgroup (1 or 2: pdrnn_lstm_small_bwd_dwout_nb).
 hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int grid, int nb, hipStream_t stream);
 int pdrnn_lstm_small_bwd_dwout_nb(int H, int NL, int T, int B);
-// Deferred-dW BPTT whose workgroups (one per nb-sequence tile, grid = tiles)
-// then form the weight gradients of their own rows: d->chunks = tiles slab rows.
-int pdrnn_lstm_small_bwd_dw_ok(int H, int NL, int T, int B, int I, int nb);
-hipError_t pdrnn_lstm_small_bwd_dw(const PdrnnLstmSmallBwdArgs* a, const PdrnnLstmSmallDwArgs* d, int H, int nb,
-                                   hipStream_t stream);
 int pdrnn_lstm_small_bwd_dwout_grid(int H, int NL, int T, int B, int nb);
 
 // Query the launch geometry chosen for (H, B): returns grid size (number of slab rows).

@@ -13,13 +13,20 @@ namespace pdrnn {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kDwRows = 16;    // (b,t) rows per pipeline stage = 4 MFMA K steps (fixed: the row cursor assumes it)
+// (b,t) rows per pipeline stage (4 per MFMA K step).  32-row stages (twice
+// the MFMA work per barrier) measured no faster at H = 32: 67-69 vs 68 us at
+// B = 1440, 16.5 vs 14.1 at B = 180 (profiles/r5/sw/sw13_dw32.log) -- the
+// kernel sits near both its HBM (~280 MB a step) and its MFMA floor at ~50 %
+// of each (profiles/r5/pmc/dw_b1440.md).
+template <int H>
+constexpr int dw_rows() { return 16; }
+static_assert(dw_rows<32>() <= PDRNN_DW_PAD_ROWS, "dW stages read past the padding");
 
 template <int H>
 constexpr int dw_stages() { return H >= 64 ? 3 : 4; }
-// LDS floats per stage: gate gradients [16][4H] | h_{t-1} rows [16][H] | input rows [16][H]
+// LDS floats per stage: gate gradients [RW][4H] | h_{t-1} rows [RW][H] | input rows [RW][H]
 template <int H>
-constexpr int dw_stage_floats() { return kDwRows * 6 * H; }
+constexpr int dw_stage_floats() { return dw_rows<H>() * 6 * H; }
 
 template <int N>
 __device__ __forceinline__ void dw_wait_vm() {
@@ -70,8 +77,9 @@ __device__ __forceinline__ void lstm_small_dw_range(const PdrnnLstmSmallDwArgs& 
   constexpr int MT = 4 * G;   // virtual 16-row m-tiles
   constexpr int R = dw_stages<H>();
   constexpr int SF = dw_stage_floats<H>();
-  constexpr int OFF_BH = kDwRows * 4 * H, OFF_BIN = kDwRows * 5 * H;
-  constexpr int JA = H / 4, JH = H / 16;
+  constexpr int RW = dw_rows<H>();
+  constexpr int OFF_BH = RW * 4 * H, OFF_BIN = RW * 5 * H;
+  constexpr int JA = RW * H / 64, JH = RW * H / 256;
   constexpr int MAXJ = 8;  // jobs per wave and stage, upper bound (launcher-checked)
   // ONE dynamic LDS array (a second __shared__ object makes hipcc drain vmcnt
   // before ds_reads): the R stage slots
@@ -86,7 +94,7 @@ __device__ __forceinline__ void lstm_small_dw_range(const PdrnnLstmSmallDwArgs& 
   const int NW = NI + H / 16;
   const int64_t BT = (int64_t)B * T;
   const int nst = st1 - st0;
-  const int JX = X0 ? (kDwRows * IP + 255) / 256 : JH;
+  const int JX = X0 ? (RW * IP + 255) / 256 : JH;
   const int J = JA + JH + JX;
   const int JPW = (J + NW - 1) / NW;  // wave-uniform; (R - 2) * JPW <= 16, JPW <= MAXJ
   const bool active = w < NW && nst > 0;  // idle waves of the narrower layer only join barriers
@@ -97,7 +105,7 @@ __device__ __forceinline__ void lstm_small_dw_range(const PdrnnLstmSmallDwArgs& 
   int64_t jstride[MAXJ];
   int jdst[MAXJ];
   {
-    const int64_t k0 = (int64_t)st0 * kDwRows;
+    const int64_t k0 = (int64_t)st0 * RW;
     const float* dg_l = a.dg + (int64_t)l * BT * a.dg_st;
     const float* h_own = a.hseq + (int64_t)l * BT * H;
     const float* h_below = a.hseq + (int64_t)(l > 0 ? l - 1 : 0) * BT * H;
@@ -111,22 +119,22 @@ __device__ __forceinline__ void lstm_small_dw_range(const PdrnnLstmSmallDwArgs& 
       if (j < JA) {  // gate-gradient rows
         constexpr int RPJ = 64 / H;
         src = dg_l + (k0 + j * RPJ + lane / H) * a.dg_st + (lane % H) * 4;
-        stride = kDwRows * a.dg_st;
+        stride = RW * a.dg_st;
         dst = j * 256;
-      } else if (j < JA + JH) {  // h_{t-1}: h rows k0-1 .. k0+14 (row -1 is front padding)
+      } else if (j < JA + JH) {  // h_{t-1}: h rows k0-1 .. k0+RW-2 (row -1 is front padding)
         const int jj = j - JA;
         src = h_own + (k0 - 1) * H + (jj * 64 + lane) * 4;
-        stride = kDwRows * H;
+        stride = RW * H;
         dst = OFF_BH + jj * 256;
-      } else if (!X0) {  // layer below's h rows k0 .. k0+15
+      } else if (!X0) {  // layer below's h rows k0 .. k0+RW-1
         const int jj = j - JA - JH;
         src = h_below + k0 * H + (jj * 64 + lane) * 4;
-        stride = kDwRows * H;
+        stride = RW * H;
         dst = OFF_BIN + jj * 256;
-      } else {  // x rows k0 .. k0+15 (row stride IP)
+      } else {  // x rows k0 .. k0+RW-1 (row stride IP)
         const int jj = j - JA - JH;
         src = a.xg + k0 * IP + (jj * 64 + lane) * 4;
-        stride = kDwRows * IP;
+        stride = RW * IP;
         dst = OFF_BIN + jj * 256;
       }
       jsrc[q] = reinterpret_cast<const char*>(src);
@@ -164,7 +172,7 @@ __device__ __forceinline__ void lstm_small_dw_range(const PdrnnLstmSmallDwArgs& 
     for (int p = 0; p < R - 1; ++p)
       if (p < nst) issue(p, p);
   }
-  int t0 = (int)(((int64_t)st0 * kDwRows + kk) % T);  // t of this lane's first row in the stage
+  int t0 = (int)(((int64_t)st0 * RW + kk) % T);  // t of this lane's first row in the stage
   for (int s = 0; s < nst; ++s) {
     // retire this wave's DMAs of stage s (up to R-2 later stages stay in
     // flight), then a barrier: every wave's DMAs of stage s have landed, and
@@ -174,14 +182,15 @@ __device__ __forceinline__ void lstm_small_dw_range(const PdrnnLstmSmallDwArgs& 
     if (active && s + R - 1 < nst) issue(s + R - 1, (s + R - 1) % R);
     if (!active) continue;
     const float* sA = lds + (s % R) * SF;
-    const int64_t k0 = (int64_t)(st0 + s) * kDwRows;
-    // the stage's fragments first (all 4 K steps: one LDS latency per stage),
-    // then its 4 x 4G MFMAs back to back
-    f32x4 av[4][G];
-    float bv[4];
+    const int64_t k0 = (int64_t)(st0 + s) * RW;
+    // the stage's fragments first (all RW / 4 K steps: one LDS latency per
+    // stage), then its RW / 4 x 4G MFMAs back to back
+    constexpr int KS = RW / 4;
+    f32x4 av[KS][G];
+    float bv[KS];
     int t = t0;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       const int r = 4 * ks + kk;
 #pragma unroll
       for (int g = 0; g < G; ++g) av[ks][g] = *reinterpret_cast<const f32x4*>(sA + r * 4 * H + 64 * g + 4 * i);
@@ -196,9 +205,9 @@ __device__ __forceinline__ void lstm_small_dw_range(const PdrnnLstmSmallDwArgs& 
       t += 4;
       t = t >= T ? t - T : t;
     }
-    t0 = t;  // 4 K steps x 4 rows = one 16-row stage: the next stage starts here
+    t0 = t;  // KS K steps x 4 rows = one stage: the next stage starts here
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         acc[4 * g + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ks][g].x, bv[ks], acc[4 * g + 0], 0, 0, 0);
@@ -209,7 +218,7 @@ __device__ __forceinline__ void lstm_small_dw_range(const PdrnnLstmSmallDwArgs& 
     }
     if (db_wave) {  // wave-uniform branch, no loads inside
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         const float am = k0 + 4 * ks + kk < k_end ? 1.f : 0.f;
 #pragma unroll
         for (int g = 0; g < G; ++g) {

@@ -1461,8 +1461,16 @@ hipError_t persist_launch(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwa
     const size_t lds = (size_t)PS_WAVES * MT * 16 * (PS_NU + 4) * 4;
     return persist_go(lstm_large_persist_bwd_kernel<DT, CELL, KSB, MT>, grid, lds, st, *a, sy, &occ_bwd);
   }
-  const size_t lds = (size_t)PS_WAVES * MT * 16 * (4 * PS_NU + 4) * 4;
-  return persist_go(lstm_large_persist_fwd_kernel<DT, CELL, KSF, MT>, grid, lds, st, *a, sy, &occ_fwd);
+  if constexpr (DT::EPC != 8) {
+    // fp32: no persistent forward (8.3 vs 7.1 us a step for the per-step
+    // kernels at H = 128, profiles/r4/h2/h2_persist_f32_cell*.json; the
+    // planner never asks for it, bindings.cpp large_persist_plan)
+    (void)occ_fwd;
+    return hipErrorInvalidValue;
+  } else {
+    const size_t lds = (size_t)PS_WAVES * MT * 16 * (4 * PS_NU + 4) * 4;
+    return persist_go(lstm_large_persist_fwd_kernel<DT, CELL, KSF, MT>, grid, lds, st, *a, sy, &occ_fwd);
+  }
 }
 
 // 16-bit storage: H = 1024 (forward K-steps per wave H/256 = 4, backward

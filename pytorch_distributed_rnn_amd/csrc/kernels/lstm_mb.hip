@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(256 * NL) lstm_mb_bwd_kernel(PdrnnLstmSmallBwd
   for (int e = tid; e < (2 * NL * 4 + 2 * 4) * PT; e += 256 * NL) smem[e] = 0.f;
   if (blockIdx.x == 0) {
     float* pad = a.dg_out + (int64_t)NL * B * T * a.dg_st;
-    for (int e = tid; e < 16 * a.dg_st; e += 256 * NL) pad[e] = 0.f;
+    for (int e = tid; e < PDRNN_DW_PAD_ROWS * a.dg_st; e += 256 * NL) pad[e] = 0.f;
   }
 
   // A fragments: W^T for this wave's K-step.  M-tile mt row i = lane & 15 is

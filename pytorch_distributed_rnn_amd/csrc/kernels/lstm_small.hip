@@ -28,7 +28,6 @@
 //    layers are load-balanced in the pipeline and there is one code path.
 #include "pdrnn/api.h"
 #include "pdrnn/common.h"
-#include "pdrnn/small_dw.h"
 
 #include <cstring>
 
@@ -1302,12 +1301,12 @@ __device__ __forceinline__ void lstm_small_bwd_gs_body(const PdrnnLstmSmallBwdAr
 
   // ---------------- epilogue: this workgroup's partial dW / db ----------
   if constexpr (DWOUT) {
-    // the dW kernel streams whole 16-row stages: the 16 padding rows behind
-    // the last layer's gate gradients must hold finite values (masked
+    // the dW kernel streams whole stages: the PDRNN_DW_PAD_ROWS padding rows
+    // behind the last layer's gate gradients must hold finite values (masked
     // operands are multiplied by zero there, and NaN * 0 = NaN)
     if (blockIdx.x == 0) {
       float* pad = a.dg_out + (int64_t)NL * B * T * a.dg_st;
-      for (int e = threadIdx.x; e < 16 * a.dg_st; e += blockDim.x) pad[e] = 0.f;
+      for (int e = threadIdx.x; e < PDRNN_DW_PAD_ROWS * a.dg_st; e += blockDim.x) pad[e] = 0.f;
     }
     return;
   }
@@ -1350,39 +1349,6 @@ template <int H, int L, int NB, bool XLDS, int CELL>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB > 1 ? 3 : 1)))
 lstm_small_bwd_dwout_kernel(PdrnnLstmSmallBwdArgs a) {
   lstm_small_bwd_gs_body<H, L, NB, XLDS, true, CELL, true>(a);
-}
-
-// Deferred-dW BPTT whose workgroups then form the weight gradients of their
-// OWN sequences: one workgroup per batch tile (grid = tiles, no persistence),
-// the tile's gate gradients / inputs are still L2-hot, and the matrix-core
-// reduction (pdrnn/small_dw.h) of the early-finishing workgroups runs beside
-// the recurrences still in flight on the same CUs -- the BPTT's exit spread
-// and the separate dW launch (and its HBM re-read of the gate gradients)
-// leave the critical path.  Slab row = tile.  Requires NB * T % 16 == 0 (a
-// tile's rows are whole 16-row stages of the dW pipeline).  Opt-in: at B =
-// 1440 the early finishers' dW did not overlap the recurrences enough to beat
-// the separate launch (bwd+dW 229 us vs 158 + 68; see pdrnn_lstm_small_bwd_dw_ok).
-template <int H, int L, int NB, int CELL>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NB > 1 ? 3 : 1)))
-lstm_small_bwd_dw_kernel(PdrnnLstmSmallBwdArgs a, PdrnnLstmSmallDwArgs d) {
-  lstm_small_bwd_gs_body<H, L, NB, true, true, CELL, true>(a);
-  // this workgroup's gate gradients and gathered x rows (buffer stores of
-  // every wave) must be in L2 before the DMA reads them, and this CU's L1 may
-  // still hold the activation lines those stores overwrote: drain, barrier,
-  // invalidate the L1 (same-CU hand-off: the bytes are this workgroup's own)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  asm volatile("buffer_inv sc0" ::: "memory");
-  const int64_t BT = (int64_t)d.B * d.T;
-  const int64_t k0 = (int64_t)blockIdx.x * NB * d.T;
-  const int64_t k_end = min(k0 + (int64_t)NB * d.T, BT);
-  const int st0 = (int)(k0 / kDwRows);
-  const int st1 = (int)((k_end + kDwRows - 1) / kDwRows);
-  lstm_small_dw_range<H, true, true>(d, 0, st0, st1, k_end, blockIdx.x);
-  for (int l = 1; l < d.NL; ++l) {
-    __syncthreads();  // the previous layer's LDS ring is still being read
-    lstm_small_dw_range<H, false, true>(d, l, st0, st1, k_end, blockIdx.x);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1885,27 +1851,6 @@ hipError_t launch_bwd_dwout_nb(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, i
   return hipGetLastError();
 }
 
-template <int H, int NB>
-hipError_t launch_bwd_dw_nb(const PdrnnLstmSmallBwdArgs* a, const PdrnnLstmSmallDwArgs* d, hipStream_t st) {
-  constexpr int L = dwout_lanes<H>();
-  const int block = a->NL * H * L;
-  const size_t lds_b = bwd_gs_lds<H, NB>(a->NL) + bwd_gs_xbytes<H, NB>(a->T);
-  const size_t lds_d = sizeof(float) * (size_t)dw_stages<H>() * dw_stage_floats<H>();
-  if (bwd_gs_xbytes<H, NB>(a->T) > (size_t)kXldsBytes || !a->xg_out) return hipErrorInvalidConfiguration;
-  // the dW half runs one wave per 16-column tile of [in | h] on this block
-  const int nw0 = (a->I + 15) / 16 + H / 16, nw1 = 2 * (H / 16);
-  if (nw0 * 64 > block || (a->NL > 1 && nw1 * 64 > block)) return hipErrorInvalidConfiguration;
-  const int jobs0 = H / 4 + H / 16 + (16 * d->xg_ld + 255) / 256, jobs1 = H / 4 + 2 * (H / 16);
-  const int jpw0 = (jobs0 + nw0 - 1) / nw0, jpw1 = (jobs1 + nw1 - 1) / nw1;
-  constexpr int ahead = dw_stages<H>() - 2;
-  if (ahead * jpw0 > 16 || ahead * jpw1 > 16 || jpw0 > 8 || jpw1 > 8) return hipErrorInvalidConfiguration;
-  const int grid = (a->B + NB - 1) / NB;
-  const size_t lds = lds_b > lds_d ? lds_b : lds_d;
-  if (a->cell == 1) hipLaunchKernelGGL((lstm_small_bwd_dw_kernel<H, L, NB, 1>), dim3(grid), dim3(block), lds, st, *a, *d);
-  else hipLaunchKernelGGL((lstm_small_bwd_dw_kernel<H, L, NB, 0>), dim3(grid), dim3(block), lds, st, *a, *d);
-  return hipGetLastError();
-}
-
 template <int H>
 hipError_t launch_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int grid, int nb) {
   constexpr int L = dwout_lanes<H>();
@@ -1964,37 +1909,6 @@ hipError_t pdrnn_lstm_small_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, int H, int
     case 16: return pdrnn::launch_bwd_dwout<16>(a, stream, grid, nb);
     case 32: return pdrnn::launch_bwd_dwout<32>(a, stream, grid, nb);
     case 64: return pdrnn::launch_bwd_dwout<64>(a, stream, grid, nb);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// 1 when the BPTT + own-tile dW kernel covers this shape: the deferred-dW
-// BPTT at nb sequences per workgroup with whole 16-row dW stages per tile.
-// PDRNN_BWD_DW_FUSED=0 keeps the separate dW launch (A/B measurements).
-int pdrnn_lstm_small_bwd_dw_ok(int H, int NL, int T, int B, int I, int nb) {
-  // opt-in (PDRNN_BWD_DW_FUSED=1): measured no faster than the separate dW
-  // launch at B = 1440 -- the dW MFMAs run after most recurrences have ended
-  // instead of beside them (0.383 vs 0.376 ms/step, profiles/r4/fz2_*)
-  const char* e = getenv("PDRNN_BWD_DW_FUSED");  // per call: tests flip it in-process
-  if (!e || e[0] != '1') return 0;
-  if ((H != 16 && H != 32) || (nb != 1 && nb != 2) || NL < 1 || NL > PDRNN_MAX_LAYERS || I < 1 || I > H) return 0;
-  const int block = NL * H * 4;  // dwout_lanes = 4 for H <= 32
-  if (block > 512 || (nb * T) % pdrnn::kDwRows != 0 || B < 1) return 0;
-  // the dW half: one wave per 16-column tile of [in | h] (layer 0) / [h_below | h]
-  const int nw0 = (I + 15) / 16 + H / 16, nw1 = 2 * (H / 16);
-  return (nw0 * 64 <= block && (NL == 1 || nw1 * 64 <= block)) ? 1 : 0;
-}
-
-hipError_t pdrnn_lstm_small_bwd_dw(const PdrnnLstmSmallBwdArgs* a, const PdrnnLstmSmallDwArgs* d, int H, int nb,
-                                   hipStream_t stream) {
-  if (!pdrnn_lstm_small_bwd_dw_ok(H, a->NL, a->T, a->B, a->I, nb)) return hipErrorInvalidConfiguration;
-  if (!pdrnn::bwd_lean(a) || !a->dg_out || a->dg_st < 4 * H || d->chunks != (a->B + nb - 1) / nb ||
-      d->B != a->B || d->T != a->T || d->NL != a->NL || d->I != a->I || d->xg_ld % 4 != 0 || d->I > H)
-    return hipErrorInvalidValue;
-  if (a->x_bf16 && (size_t)a->T * H * sizeof(float) * nb > (size_t)pdrnn::kXldsBytes) return hipErrorInvalidConfiguration;
-  switch (H) {
-    case 16: return nb == 2 ? pdrnn::launch_bwd_dw_nb<16, 2>(a, d, stream) : pdrnn::launch_bwd_dw_nb<16, 1>(a, d, stream);
-    case 32: return nb == 2 ? pdrnn::launch_bwd_dw_nb<32, 2>(a, d, stream) : pdrnn::launch_bwd_dw_nb<32, 1>(a, d, stream);
     default: return hipErrorInvalidValue;
   }
 }

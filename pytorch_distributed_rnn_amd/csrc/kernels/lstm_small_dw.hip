@@ -27,7 +27,7 @@
 //   * db: the first h_prev wave also sums its A fragments on the VALU (free
 //     beside the MFMAs) and reduces them over the 4 row lanes at the end.
 //   * Operands reach LDS by DMA (global_load_lds, no VGPR staging): a ring
-//     of 16-row stages, two stages in flight past the one being consumed,
+//     of 32-row stages (16 at H = 64), stages in flight past the one being consumed,
 //     retired by a counted vmcnt + raw barrier (a __syncthreads() would drain
 //     the ring); every wave issues an equal share of a stage's DMA jobs.
 // Chunk c writes its partial sums to slab row c; pdrnn_slab_reduce_adam sums
@@ -43,10 +43,11 @@ namespace {
 template <int H>
 __global__ void __launch_bounds__(512) lstm_small_dw_kernel(PdrnnLstmSmallDwArgs a) {
   const int64_t BT = (int64_t)a.B * a.T;
-  const int nstage_all = (int)((BT + kDwRows - 1) / kDwRows);
+  constexpr int RW = dw_rows<H>();
+  const int nstage_all = (int)((BT + RW - 1) / RW);
   const int st0 = (int)((int64_t)nstage_all * blockIdx.x / a.chunks);
   const int st1 = (int)((int64_t)nstage_all * (blockIdx.x + 1) / a.chunks);
-  const int64_t k_end = min((int64_t)st1 * kDwRows, BT);
+  const int64_t k_end = min((int64_t)st1 * RW, BT);
   if (blockIdx.y == 0) lstm_small_dw_range<H, true>(a, 0, st0, st1, k_end, blockIdx.x);
   else lstm_small_dw_range<H, false>(a, blockIdx.y, st0, st1, k_end, blockIdx.x);
 }
@@ -54,11 +55,14 @@ template <int H>
 hipError_t launch_dw(const PdrnnLstmSmallDwArgs* a, hipStream_t st) {
   const size_t lds = sizeof(float) * (size_t)dw_stages<H>() * dw_stage_floats<H>();
   const int nw0 = (a->I + 15) / 16 + H / 16, nw1 = 2 * (H / 16);
-  const int jobs0 = H / 4 + H / 16 + (16 * a->xg_ld + 255) / 256, jobs1 = H / 4 + 2 * (H / 16);
+  constexpr int RW = dw_rows<H>();
+  const int jobs0 = RW * H / 64 + RW * H / 256 + (RW * a->xg_ld + 255) / 256, jobs1 = RW * H / 64 + 2 * (RW * H / 256);
   const int jpw0 = (jobs0 + nw0 - 1) / nw0, jpw1 = (jobs1 + nw1 - 1) / nw1;
   constexpr int ahead = dw_stages<H>() - 2;  // stages each wave keeps in flight past the one it waits for
   if (ahead * jpw0 > 16 || ahead * jpw1 > 16 || jpw0 > 8 || jpw1 > 8) return hipErrorInvalidConfiguration;
   const int nw = a->NL > 1 && nw1 > nw0 ? nw1 : nw0;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)lstm_small_dw_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((lstm_small_dw_kernel<H>), dim3((unsigned)a->chunks, (unsigned)a->NL), dim3(64 * nw), lds, st, *a);
   return hipGetLastError();
 }
@@ -69,8 +73,9 @@ hipError_t launch_dw(const PdrnnLstmSmallDwArgs* a, hipStream_t st) {
 extern "C" {
 
 int pdrnn_lstm_small_dw_chunks(int H, int NL, int B, int T) {
-  (void)H; (void)NL;
-  const int64_t stages = ((int64_t)B * T + pdrnn::kDwRows - 1) / pdrnn::kDwRows;
+  (void)NL;
+  const int rw = H >= 64 ? pdrnn::dw_rows<64>() : pdrnn::dw_rows<32>();
+  const int64_t stages = ((int64_t)B * T + rw - 1) / rw;
   int64_t c = 256;
   if (c > stages / 4) c = stages / 4;  // at least 4 stages per chunk (amortise the pipeline fill)
   if (c < 1) c = 1;

@@ -470,11 +470,11 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
 #pragma unroll
   for (int n = 0; n < NB; ++n) vmask[n] = valid[n] ? 0u : kOOR;
 
-  // the dW kernel streams whole 16-row stages: the 16 padding rows behind the
-  // last layer's gate gradients must hold finite values
+  // the dW kernel streams whole stages: the PDRNN_DW_PAD_ROWS padding rows
+  // behind the last layer's gate gradients must hold finite values
   if (blockIdx.x == 0) {
     float* pad = a.dg_out + (int64_t)NL * B * T * a.dg_st;
-    for (int e = tid; e < 16 * a.dg_st; e += blockDim.x) pad[e] = 0.f;
+    for (int e = tid; e < PDRNN_DW_PAD_ROWS * a.dg_st; e += blockDim.x) pad[e] = 0.f;
   }
 
   const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);

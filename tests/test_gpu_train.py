@@ -152,8 +152,7 @@ def test_fused_gru_step_headline_batch_matches_autograd():
 @pytest.mark.parametrize("cell,hidden,layers,seq,features", [
     ("lstm", 32, 2, 128, 9), ("lstm", 16, 1, 37, 9), ("lstm", 32, 3, 21, 5),
     ("lstm", 16, 2, 6, 16), ("gru", 32, 2, 128, 9), ("gru", 16, 2, 9, 3)])
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_deferred_dw_backward_matches_autograd(cell, hidden, layers, seq, features, fused, monkeypatch):
+def test_deferred_dw_backward_matches_autograd(cell, hidden, layers, seq, features, monkeypatch):
     """The BPTT with the weight gradients deferred to the matrix-core kernel
     (lstm_small_dw.hip) -- forced at B = 96 so that every shape runs it; 382
     samples leave a last batch of 94 (with odd T: B*T not a multiple of the
@@ -163,7 +162,6 @@ def test_deferred_dw_backward_matches_autograd(cell, hidden, layers, seq, featur
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     monkeypatch.setenv("PDRNN_LSTM_DWOUT", "force")
-    monkeypatch.setenv("PDRNN_BWD_DW_FUSED", fused)
     assert _ext.native(torch.device("cuda")).lstm_small_step_deferred_dw(hidden, layers, seq, 96)
     torch.manual_seed(3)
     train, _, _ = synthetic_motion(n_train=382, n_validation=2, n_test=2, seq_length=seq, num_features=features,
@@ -225,15 +223,13 @@ def test_deferred_dw_gradients_match_fp64(cell, hidden, layers, seq, monkeypatch
         assert (g - r.grad).abs().max().item() <= 2e-6 * scale + 1e-12, k
 
 
-@pytest.mark.parametrize("B,nb,fused", [(1440, "2", "1"), (1152, "2", "1"), (1440, "1", "1"), (1440, "2", "0"),
-                                        (1440, "1", "0")])
-def test_headline_batch_gradients_match_fp64(B, nb, fused, monkeypatch):
+@pytest.mark.parametrize("B,nb", [(1440, "2"), (1152, "2"), (1440, "1")])
+def test_headline_batch_gradients_match_fp64(B, nb, monkeypatch):
     """The headline step at the epoch's two batch sizes (1440 and the short
     last 1152 of a 6912-sequence epoch): gradients of the fused HIP step
     (deferred-dW BPTT with one or two sequences per workgroup; the weight
-    gradients formed by the BPTT workgroups over their own tile, or by the
-    separate matrix-core launch over 256 K chunks; the one-pass slab
-    reduction) before Adam against fp64 torch autograd on the same weights
+    gradients formed by the matrix-core launch over 256 K chunks; the
+    one-pass slab reduction) before Adam against fp64 torch autograd on the same weights
     and batch -- an oracle independent of the HIP kernels."""
     from pytorch_distributed_rnn_amd import _ext
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
@@ -241,10 +237,8 @@ def test_headline_batch_gradients_match_fp64(B, nb, fused, monkeypatch):
     monkeypatch.delenv("PDRNN_LSTM_DWOUT", raising=False)
     monkeypatch.setenv("PDRNN_SW", "0")  # the gate-split / K-split family (sequence-in-wave: test below)
     monkeypatch.setenv("PDRNN_DWOUT_NB", nb)
-    monkeypatch.setenv("PDRNN_BWD_DW_FUSED", fused)
     mod = _ext.native(torch.device("cuda", 0))
     assert mod.lstm_small_step_deferred_dw(32, 2, 128, B)
-    assert mod.lstm_small_dwout_geometry(32, 2, 128, B)[2] == (fused == "1")
     torch.manual_seed(11)
     train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=12)
     m0 = MotionModel(9, 32, 2, 6)
@@ -322,10 +316,9 @@ def test_deferred_dw_pairs_sequences_at_headline_batch(monkeypatch):
     from pytorch_distributed_rnn_amd import _ext
     monkeypatch.delenv("PDRNN_DWOUT_NB", raising=False)
     mod = _ext.native(torch.device("cuda", 0))
-    monkeypatch.delenv("PDRNN_BWD_DW_FUSED", raising=False)
     for B in (1440, 1152):
-        nb, grid, fused = mod.lstm_small_dwout_geometry(32, 2, 128, B)
-        assert (nb, grid, fused) == (2, B // 2, False), (B, nb, grid, fused)
+        nb, grid = mod.lstm_small_dwout_geometry(32, 2, 128, B)
+        assert (nb, grid) == (2, B // 2), (B, nb, grid)
 
 
 def test_deferred_dw_selected_above_one_round(monkeypatch):
