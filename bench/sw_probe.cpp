@@ -264,8 +264,8 @@ int main(int argc, char** argv) {
   uint64_t* stamps = nullptr;
   const bool want_stamps = getenv("SW_STAMPS") != nullptr;
   if (want_stamps) {
-    CK(hipMalloc(&stamps, (size_t)B * 8 * 8));
-    CK(hipMemset(stamps, 0, (size_t)B * 8 * 8));
+    CK(hipMalloc(&stamps, (size_t)B * 8 * 8 + 4096));  // + the MB_DEBUG dump area
+    CK(hipMemset(stamps, 0, (size_t)B * 8 * 8 + 4096));
     f.stamps = stamps;
   }
   hipStream_t st;
@@ -307,6 +307,35 @@ int main(int argc, char** argv) {
     const double e_act = maxrel(h_act, RR.act, rows, 5 * H, 5 * H, 5 * H);
     const double e_h = maxrel(hseq_only, RR.hseq, rows, H, H, H);
     const double e_dht = maxrel(h_dht, RR.dhtop, B, H, H, H);
+    if (getenv("PROBE_DUMP") && mb && want_stamps) {  // MB_DEBUG build: the h image of step 0, tile 0
+      std::vector<uint32_t> d(256), wa(256);
+      CK(hipMemcpy(d.data(), reinterpret_cast<uint32_t*>(stamps) + 256, 1024, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(wa.data(), reinterpret_cast<uint32_t*>(stamps) + 512, 1024, hipMemcpyDeviceToHost));
+      int badw = 0;
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t wv = wa[lane * 4 + j / 2];
+          const uint32_t bits = (j & 1 ? wv >> 16 : wv & 0xFFFF) << 16;
+          float got;
+          std::memcpy(&got, &bits, 4);
+          const int ai = lane & 15, row = (ai & 3) * H + 8 * (ai >> 2) + 0, k = 8 * (lane >> 4) + j;
+          const float ref = whh[0][row * H + k];
+          if (std::fabs(got - ref) > 0.01f && badw++ < 6) printf("  W_hh frag lane %d j %d got %.4f ref %.4f\n", lane, j, got, ref);
+        }
+      printf("  W_hh A fragment (wave 0, m-tile 0): %d of 512 off\n", badw);
+      int bad = 0;
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t wv = d[lane * 4 + j / 2];
+          const uint32_t bits = (j & 1 ? wv >> 16 : wv & 0xFFFF) << 16;
+          float got;
+          std::memcpy(&got, &bits, 4);
+          const int n = lane & 15, u = 8 * (lane >> 4) + j;
+          const double ref = RR.hseq[((size_t)n * T + 0) * H + u];
+          if (std::fabs(got - ref) > 0.02 && bad++ < 8) printf("  img n=%d u=%d got %.4f ref %.4f\n", n, u, got, ref);
+        }
+      printf("  h image step 0: %d of 512 off\n", bad);
+    }
     if (getenv("PROBE_DUMP") && e_act > tol) {  // first mismatching activations: (l, b, t, slot)
       int shown = 0;
       for (size_t r = 0; r < rows && shown < 12; ++r)

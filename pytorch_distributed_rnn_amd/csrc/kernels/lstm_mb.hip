@@ -16,8 +16,11 @@
 //    permutation also makes the h a lane produces (units 8 (l>>4) + mt) the
 //    B-operand slice (k = 8 (l>>4) .. +7) of its column: the four waves of the
 //    tile (two M-tiles each) meet in one LDS image of h_t per step (one 4-byte
-//    write and one 16-byte read per lane, one barrier).  x_t enters through a
-//    v_mfma_f32_16x16x16_bf16 per M-tile from an LDS-staged bf16 image.
+//    write and one 16-byte read per lane, one barrier).  x_t enters through one
+//    more v_mfma_f32_16x16x32_bf16 per M-tile (K = 16 staged columns + 16
+//    zeros) from an LDS-staged bf16 image: one MFMA shape in every accumulate
+//    chain (a 16x16x16 result chained into a 16x16x32 as SrcC came out
+//    corrupted, run-to-run different, at t >= 1: profiles/r5/sw/mb9_dump.log).
 //  * backward, layer l: four waves, wave s owns K-step s of the gate rows
 //    (units 8 s .. 8 s + 7): lane l computes the pre-activation gate
 //    gradients of units 8 s + 2 (l>>4) + {0, 1} for sequence l&15 -- exactly
@@ -43,10 +46,8 @@ constexpr int kXK = 16;                     // staged x columns (I <= 16, zero-p
 constexpr float kL2E = 1.4426950408889634f;
 constexpr uint32_t kOOR = 0x80000000u;      // buffer offset past the range: the store is dropped
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 PDRNN_DEVICE uint32_t bfb(float v) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v); }
 PDRNN_DEVICE uint32_t pk(float a, float b) { return bfb(a) | (bfb(b) << 16); }
@@ -56,10 +57,6 @@ PDRNN_DEVICE float tnh(float z) { return fmaf(sgm(2.f * z), 2.f, -1.f); }
 PDRNN_DEVICE f32x4 mfma32(u32x4 a, u32x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
                                                  0, 0);
-}
-PDRNN_DEVICE f32x4 mfma16(u32x2 a, u32x2 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c, 0,
-                                                   0, 0);
 }
 PDRNN_DEVICE void bst(float v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, so, 0);
@@ -129,8 +126,9 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
   // ---- weights: A fragments of this wave's two M-tiles ----------------------
   // A row i = lane & 15 of M-tile mt: unit 8 (i >> 2) + mt, gate i & 3
   const int ai = lane & 15, ak = lane >> 4;
-  u32x2 ax[2];
-  u32x4 ah0[2], aih1[2], ahh1[2];
+  // (W_ih of layer 0 as a K = 32 operand: k < 16 the staged x columns, k >= 16
+  // zero -- one MFMA shape for the whole accumulate chain)
+  u32x4 ax[2], ah0[2], aih1[2], ahh1[2];
   float bias[NL][2][4];
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
@@ -138,14 +136,14 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
     const int row = (ai & 3) * kH + 8 * (ai >> 2) + mt;
     {
       const float* p = a.w_ih[0] + (int64_t)row * I;
-      float v[4];
+      float v[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = 4 * ak + j;
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * ak + j;
         const float x = p[min(k, I - 1)];
         v[j] = k < I ? x : 0.f;
       }
-      ax[m] = u32x2{pk(v[0], v[1]), pk(v[2], v[3])};
+      ax[m] = u32x4{pk(v[0], v[1]), pk(v[2], v[3]), pk(v[4], v[5]), pk(v[6], v[7])};
     }
     ah0[m] = wrow8(a.w_hh[0], kH, row, 8 * ak);
     if constexpr (NL == 2) {
@@ -209,8 +207,11 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
   auto bfrag = [&](int l, int t) {  // B operand: h_t of units 8g .. 8g+7, sequence n
     return *reinterpret_cast<const u32x4*>(hbuf(l, t & 1) + n * kH + 8 * g);
   };
+  // x_t as the K = 32 B operand: lanes g < 2 hold staged columns 8g .. 8g+7
+  const u32x4 zx = {0u, 0u, 0u, 0u};
   auto xfrag = [&](int t) {
-    return *reinterpret_cast<const u32x2*>(xs + (min(t, T - 1) * kN + n) * kXK + 4 * g);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(xs + (min(t, T - 1) * kN + n) * kXK + 8 * (g & 1));
+    return g < 2 ? v : zx;
   };
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 
@@ -218,12 +219,19 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
   for (int it = 0; it < iters; ++it) {
     const int t0 = it, t1 = it - 1;
     const u32x4 bh0 = bfrag(0, t0 - 1);
-    const u32x2 bx = xfrag(t0);
+#ifdef MB_DEBUG
+    if (it == 1 && blockIdx.x == 0 && w == 0 && a.stamps) {  // the step-0 h image as read (probe dump)
+      uint32_t* dbg = reinterpret_cast<uint32_t*>(a.stamps) + 256;  // past the stamps of workgroup 0
+      for (int j = 0; j < 4; ++j) dbg[lane * 4 + j] = bh0[j];
+      for (int j = 0; j < 4; ++j) dbg[256 + lane * 4 + j] = ah0[0][j];
+    }
+#endif
+    const u32x4 bx = xfrag(t0);
     u32x4 bh1;
     if constexpr (NL == 2) bh1 = bfrag(1, t1 - 1);
     f32x4 acc0[2], acc1[2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) acc0[m] = mfma32(ah0[m], bh0, mfma16(ax[m], bx, z4));
+    for (int m = 0; m < 2; ++m) acc0[m] = mfma32(ah0[m], bh0, mfma32(ax[m], bx, z4));
     if constexpr (NL == 2) {
 #pragma unroll
       for (int m = 0; m < 2; ++m) acc1[m] = mfma32(ahh1[m], bh1, mfma32(aih1[m], bh0, z4));
