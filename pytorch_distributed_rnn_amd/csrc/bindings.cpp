@@ -735,12 +735,24 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
   if (g.scalar_type() == at::kBFloat16) dt = 0;
   else if (g.scalar_type() == at::kHalf) dt = 1;
   else g = g.to(at::kFloat);
-  Tensor flat = idx.contiguous().view({-1});
-  flat = at::where(flat < 0, flat + num_embeddings, flat);
-  auto sorted = at::sort(flat, /*stable=*/true, /*dim=*/0, /*descending=*/false);
-  Tensor vals = std::get<0>(sorted), perm = std::get<1>(sorted).contiguous();
-  Tensor bounds = at::arange(num_embeddings + 1, flat.options());
-  Tensor offsets = at::searchsorted(vals, bounds).contiguous();
+  Tensor flat = idx.contiguous().view({-1}).to(at::kLong);
+  Tensor perm, offsets;
+  if (num_embeddings <= 16384 && flat.numel() < ((int64_t)1 << 31)) {
+    // in-tree stable counting sort (kernels/embedding.hip)
+    perm = at::empty({flat.numel()}, flat.options());
+    offsets = at::empty({num_embeddings + 1}, flat.options());
+    Tensor scratch = at::empty({std::max<int64_t>(pdrnn_embedding_sort_scratch(flat.numel(), num_embeddings), 1)},
+                               flat.options().dtype(at::kInt));
+    HIP_LAUNCH_CHECK(pdrnn_embedding_sort(flat.data_ptr<int64_t>(), flat.numel(), num_embeddings,
+                                          scratch.data_ptr<int>(), perm.data_ptr<int64_t>(),
+                                          offsets.data_ptr<int64_t>(), cur_stream()));
+  } else {  // large vocabularies: library stable sort + bucket bounds
+    flat = at::where(flat < 0, flat + num_embeddings, flat);
+    auto sorted = at::sort(flat, /*stable=*/true, /*dim=*/0, /*descending=*/false);
+    Tensor vals = std::get<0>(sorted);
+    perm = std::get<1>(sorted).contiguous();
+    offsets = at::searchsorted(vals, at::arange(num_embeddings + 1, flat.options())).contiguous();
+  }
   Tensor dw = at::empty({num_embeddings, dim}, dout.options().dtype(at::kFloat));
   // small vocabulary, many contributions per row: split each row's list
   const int64_t per_row = g.size(0) / std::max<int64_t>(num_embeddings, 1);
@@ -1093,6 +1105,139 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
     }
   }
   return {dgates, dh0, dc0};
+}
+
+// ---------------------------------------------------------------------------
+// Step ranges of a unidirectional 16-bit layer on the persistent kernels, into
+// preallocated full-length tensors (ops/lstm_large.py _PipelinedLSTMStack16:
+// layer l + 1 runs chunk c while layer l runs chunk c + 1, each grid planned
+// for half the CUs so two co-reside).  `sync` (int32 [large_persist_sync_len])
+// is zeroed before a layer's first range and carries the per-step counters
+// across its ranges.  A grid that cannot launch runs the range on the
+// per-step kernels; a grid-sync timeout sets the device's sticky flag (the
+// trainers' persistent-path checks).  Returns true when the persistent kernel ran.
+int64_t large_persist_sync_len(int64_t B, int64_t mt) { return (B + 16 * mt - 1) / (16 * mt) + 4; }
+
+int* persist_sticky_ptr(const at::TensorOptions& opts) {
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
+  TORCH_CHECK(dev >= 0 && dev < 64, "device index");
+  std::vector<Tensor>& sticky = persist_sticky();
+  if (!sticky[dev].defined()) {
+    sticky[dev] = at::zeros({1}, opts.dtype(at::kInt));
+    persist_sticky_host()[dev] = pinned_word();
+  }
+  return sticky[dev].data_ptr<int>();
+}
+
+bool lstm_large_fwd_range(const Tensor& xp, const Tensor& w, const optional<Tensor>& h0, const optional<Tensor>& c0,
+                          const Tensor& hseq, const Tensor& cseq, const Tensor& acts, int64_t H, int64_t s0,
+                          int64_t s1, const Tensor& sync, int64_t mt) {
+  CHECK_HIP_TENSOR(xp);
+  const c10::DeviceGuard guard(xp.device());
+  const int dt = large_dtype(xp);
+  TORCH_CHECK(dt != 2, "16-bit storage");
+  const int64_t T = xp.size(0), B = xp.size(1);
+  TORCH_CHECK(xp.is_contiguous() && xp.size(2) == 4 * H, "xp [T, B, 4H] contiguous");
+  TORCH_CHECK(w.is_contiguous() && w.size(0) == 4 * H && w.size(1) == H && large_dtype(w) == dt, "w [4H, H]");
+  TORCH_CHECK(hseq.is_contiguous() && hseq.numel() == T * B * H && large_dtype(hseq) == dt, "hseq [T, B, H]");
+  TORCH_CHECK(cseq.is_contiguous() && cseq.numel() == T * B * H && cseq.scalar_type() == at::kFloat, "cseq f32");
+  TORCH_CHECK(acts.is_contiguous() && acts.numel() == T * B * 4 * H && large_dtype(acts) == dt, "acts");
+  TORCH_CHECK(0 <= s0 && s0 < s1 && s1 <= T, "step range");
+  TORCH_CHECK(sync.is_contiguous() && sync.scalar_type() == at::kInt && sync.numel() >= large_persist_sync_len(B, mt),
+              "sync int32");
+  const bool has_h0 = h0.has_value() && h0->defined(), has_c0 = c0.has_value() && c0->defined();
+  if (has_h0) TORCH_CHECK(h0->is_contiguous() && large_dtype(*h0) == dt && h0->numel() == B * H, "h0 [1, B, H]");
+  if (has_c0) TORCH_CHECK(c0->is_contiguous() && c0->scalar_type() == at::kFloat && c0->numel() == B * H, "c0");
+  PdrnnLstmLargeStepArgs a{};
+  a.B = (int)B; a.H = (int)H; a.T = (int)T;
+  a.s0 = (int)s0; a.s1 = (int)s1;
+  PdrnnLstmLargeDir& d = a.dir[0];
+  d.w = eptr(w);
+  d.xp = eptr(xp); d.xp_sb = 4 * H; d.xp_st = B * 4 * H;
+  d.h0 = has_h0 ? eptr(*h0) : nullptr;
+  d.c0 = has_c0 ? c0->data_ptr<float>() : nullptr;
+  d.hseq = eptrm(hseq); d.hseq_sb = H; d.hseq_st = B * H;
+  d.cseq = cseq.data_ptr<float>();
+  d.acts = eptrm(acts);
+  hipStream_t st = cur_stream();
+  int* cnt = sync.data_ptr<int>();
+  const int nmb = (int)((B + 16 * mt - 1) / (16 * mt));
+  if (mt >= 1 && !g_persist_disabled.load() &&
+      pdrnn_lstm_large_persist(&a, 1, 0, dt, (int)mt, cnt, cnt + nmb, persist_sticky_ptr(xp.options()), 0, st) ==
+          hipSuccess)
+    return true;
+  (void)hipGetLastError();
+  for (int64_t s = s0; s < s1; ++s) {
+    a.step = (int)s;
+    HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, 1, 0, dt, -1, st));
+  }
+  return false;
+}
+
+bool lstm_large_bwd_range(const optional<Tensor>& dout, const optional<Tensor>& dhn, const optional<Tensor>& dcn,
+                          const Tensor& wt, const Tensor& cseq, const Tensor& acts, const optional<Tensor>& c0,
+                          const Tensor& dgates, const Tensor& carry, const Tensor& dh0, const Tensor& dc0, int64_t H,
+                          int64_t s0, int64_t s1, const Tensor& sync, int64_t mt) {
+  CHECK_HIP_TENSOR(acts);
+  const c10::DeviceGuard guard(acts.device());
+  const int dt = large_dtype(acts);
+  TORCH_CHECK(dt != 2, "16-bit storage");
+  TORCH_CHECK(acts.is_contiguous() && acts.dim() == 4 && acts.size(0) == 1 && acts.size(3) == 4 * H, "acts [1, T, B, 4H]");
+  const int64_t T = acts.size(1), B = acts.size(2);
+  TORCH_CHECK(wt.is_contiguous() && wt.size(0) == H && wt.size(1) == 4 * H && large_dtype(wt) == dt, "wt [H, 4H]");
+  TORCH_CHECK(cseq.is_contiguous() && cseq.numel() == T * B * H && cseq.scalar_type() == at::kFloat, "cseq f32");
+  TORCH_CHECK(dgates.is_contiguous() && dgates.numel() == T * B * 4 * H && large_dtype(dgates) == dt, "dgates");
+  for (const Tensor* t : {&carry, &dh0, &dc0})
+    TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kFloat && t->numel() == B * H, "carry / dh0 / dc0 f32");
+  TORCH_CHECK(0 <= s0 && s0 < s1 && s1 <= T, "step range");
+  TORCH_CHECK(sync.is_contiguous() && sync.scalar_type() == at::kInt && sync.numel() >= large_persist_sync_len(B, mt),
+              "sync int32");
+  const bool has_dout = dout.has_value() && dout->defined();
+  if (has_dout) TORCH_CHECK(dout->is_contiguous() && large_dtype(*dout) == dt && dout->numel() == T * B * H, "dout");
+  auto f32p = [&](const optional<Tensor>& t) -> const float* {
+    if (!(t.has_value() && t->defined())) return nullptr;
+    TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kFloat && t->numel() == B * H, "f32 [1, B, H] state");
+    return t->data_ptr<float>();
+  };
+  PdrnnLstmLargeStepArgs a{};
+  a.B = (int)B; a.H = (int)H; a.T = (int)T;
+  a.s0 = (int)s0; a.s1 = (int)s1;
+  PdrnnLstmLargeDir& d = a.dir[0];
+  d.wt = eptr(wt);
+  d.c0 = f32p(c0);
+  d.cseq = cseq.data_ptr<float>();
+  d.acts = eptrm(acts);
+  d.dgates = eptrm(dgates);
+  if (has_dout) { d.dout = eptr(*dout); d.dout_sb = H; d.dout_st = B * H; }
+  d.dhn = f32p(dhn);
+  d.dcn = f32p(dcn);
+  d.dc_carry = carry.data_ptr<float>();
+  d.dh0 = dh0.data_ptr<float>();
+  d.dc0 = dc0.data_ptr<float>();
+  int big = 0;
+  a.splitk = pdrnn_lstm_large_bwd_splitk((int)B, (int)H, 1, &big);
+  a.splitk_big = big;
+  a.bwd_pp = a.splitk == 1 ? pdrnn_lstm_large_bwd_pp((int)B, (int)H, 1, dt) : 0;
+  Tensor ws;
+  if (a.splitk > 1 || a.bwd_pp) {
+    ws = at::empty({a.splitk, 2, B, H}, acts.options().dtype(at::kFloat));
+    a.ws = ws.data_ptr<float>();
+  }
+  hipStream_t st = cur_stream();
+  if (s0 == 0) HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, 1, dt, st));
+  int* cnt = sync.data_ptr<int>();
+  const int nmb = (int)((B + 16 * mt - 1) / (16 * mt));
+  if (mt >= 1 && !g_persist_disabled.load() &&
+      pdrnn_lstm_large_persist(&a, 1, 1, dt, (int)mt, cnt, cnt + nmb, persist_sticky_ptr(acts.options()), 0, st) ==
+          hipSuccess)
+    return true;
+  (void)hipGetLastError();
+  for (int64_t s = s0; s < s1; ++s) {
+    a.step = (int)s;
+    HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, 1, 1, dt, -1, st));
+  }
+  return false;
 }
 
 // Time ranges of a unidirectional fp32 H = 128 layer on the row-owning
@@ -1533,7 +1678,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     a.c_16bit = out16; a.ldc = N; a.A2 = a.B2 = K2 ? (const void*)1 : nullptr;
     return M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && pdrnn_gemm_supported(&a) != 0;
   });
+  m.def("large_persist_sync_len", &large_persist_sync_len, "int32 words of a step-range sync buffer (B, mt)");
+  m.def("large_persist_mt", [](int64_t B, int64_t H, int64_t ndir, int64_t dtype, int64_t cus) {
+    return g_persist_disabled.load() ? 0 : pdrnn_lstm_large_persist_mt((int)B, (int)H, (int)ndir, (int)dtype, (int)cus);
+  }, "row tiles of the persistent recurrence for a grid of at most `cus` workgroups (0: not covered / turned off)");
+  m.def("lstm_large_fwd_range", &lstm_large_fwd_range, "persistent forward over processing steps [s0, s1)");
+  m.def("lstm_large_bwd_range", &lstm_large_bwd_range, "persistent BPTT over processing steps [s0, s1)");
   m.def("embedding_fwd", &embedding_fwd, py::arg("weight"), py::arg("idx"), py::arg("out_dtype") = py::none());
+  m.def("embedding_sort", [](const Tensor& idx, int64_t V) {
+    CHECK_HIP_TENSOR(idx);
+    const c10::DeviceGuard guard(idx.device());
+    Tensor flat = idx.contiguous().view({-1}).to(at::kLong);
+    Tensor perm = at::empty({flat.numel()}, flat.options()), offsets = at::empty({V + 1}, flat.options());
+    Tensor scratch = at::empty({std::max<int64_t>(pdrnn_embedding_sort_scratch(flat.numel(), V), 1)},
+                               flat.options().dtype(at::kInt));
+    HIP_LAUNCH_CHECK(pdrnn_embedding_sort(flat.data_ptr<int64_t>(), flat.numel(), V, scratch.data_ptr<int>(),
+                                          perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), cur_stream()));
+    return py::make_tuple(perm, offsets);
+  }, "stable in-tree counting sort of indices by row (V <= 16384): (perm, row offsets)");
   m.def("embedding_bwd", &embedding_bwd);
   m.attr("offload_arch") = "gfx950";
   pdrnn::register_runtime(m);

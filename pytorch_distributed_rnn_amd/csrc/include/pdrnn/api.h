@@ -269,6 +269,11 @@ hipError_t pdrnn_embedding_fwd16(const float* weight, const int64_t* idx, uint16
 // dout_dtype: 0 bf16, 1 fp16, 2 fp32
 // Small-vocabulary form: each row's contribution list split into `pieces`
 // equal parts (partials: [V][pieces][dim] fp32 scratch), summed in order.
+// Stable in-tree sort of n indices by row (V <= 16384): perm [n], offsets
+// [V + 1] (int64), scratch int32 [pdrnn_embedding_sort_scratch(n, V)].
+int64_t pdrnn_embedding_sort_scratch(int64_t n, int64_t V);
+hipError_t pdrnn_embedding_sort(const int64_t* idx, int64_t n, int64_t V, int* scratch, int64_t* perm,
+                                int64_t* offsets, hipStream_t stream);
 hipError_t pdrnn_embedding_bwd_pieces(const void* dout, int dout_dtype, const int64_t* perm, const int64_t* offsets,
                                      float* partials, int pieces, float* dweight, int64_t num_embeddings, int64_t dim,
                                      int64_t padding_idx, hipStream_t stream);
@@ -315,6 +320,11 @@ typedef struct {
   int bwd_pp;              // backward: ping-pong GEMM into ws, then the cell kernel (needs ws, splitk = 1)
   int cell;                // 0 = LSTM; 1 = GRU packed as [r|z|n_x|n_h] (cseq = fp32 h, acts = r,z,n,n_h)
   float* ws;               // backward split-K partials [splitk][2][B][H] fp32
+  // persistent kernels: processing-order steps [s0, s1) of the T-step layer
+  // (s1 = 0: all of them).  A range after the first resumes from the state the
+  // earlier range left in hseq / cseq (forward) or dgates / dc_carry
+  // (backward); the sync counters carry over (zeroed before the first range).
+  int s0, s1;
 } PdrnnLstmLargeStepArgs;
 
 int pdrnn_lstm_large_supported(int H);

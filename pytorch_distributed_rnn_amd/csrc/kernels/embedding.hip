@@ -172,6 +172,89 @@ __global__ void __launch_bounds__(256) emb_bwd_pieces_sum_kernel(const float* __
   dw[e] = acc;
 }
 
+// ---- stable counting sort of the indices by vocabulary row (in-tree) ------
+// Replaces a library radix / merge sort + searchsorted: the vocabulary is
+// small (char-LM: 256), so a histogram per index block, one scan over
+// (row, block) and a stable scatter give the same perm / offsets as a stable
+// sort, deterministically and in three small launches.
+constexpr int kSortTile = 256;     // indices per scatter sub-tile (= block size)
+constexpr int kSortChunk = 4096;   // indices per histogram / scatter block
+
+__device__ __forceinline__ int64_t wrap_idx(int64_t v, int64_t V) { return v < 0 ? v + V : v; }
+
+// blockcounts[b][v] = occurrences of v in indices [b * chunk, (b + 1) * chunk)
+__global__ void __launch_bounds__(256) emb_count_kernel(const int64_t* __restrict__ idx, int64_t n, int V,
+                                                        int* __restrict__ bcount) {
+  extern __shared__ int hist[];
+  for (int v = threadIdx.x; v < V; v += blockDim.x) hist[v] = 0;
+  __syncthreads();
+  const int64_t j0 = (int64_t)blockIdx.x * kSortChunk, j1 = min(j0 + kSortChunk, n);
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+    const int64_t v = wrap_idx(idx[j], V);
+    PDRNN_DEVICE_ASSERT(v >= 0 && v < V);
+    atomicAdd(&hist[v], 1);
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < V; v += blockDim.x) bcount[(int64_t)blockIdx.x * V + v] = hist[v];
+}
+
+// one workgroup: base[b][v] = offsets[v] + sum_{b' < b} bcount[b'][v];
+// offsets[v] = sum_{v' < v} total[v'] (offsets[V] = n)
+__global__ void __launch_bounds__(1024) emb_scan_kernel(int* __restrict__ bcount, int nb, int V,
+                                                        int64_t* __restrict__ offsets) {
+  extern __shared__ int tot[];  // [V] totals, then exclusive offsets
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    int run = 0;
+    for (int b = 0; b < nb; ++b) {
+      const int c = bcount[(int64_t)b * V + v];
+      bcount[(int64_t)b * V + v] = run;
+      run += c;
+    }
+    tot[v] = run;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // V <= 16384: a serial scan of the totals is a few microseconds
+    int run = 0;
+    for (int v = 0; v < V; ++v) {
+      const int c = tot[v];
+      tot[v] = run;
+      run += c;
+    }
+    offsets[V] = run;
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    offsets[v] = tot[v];
+    for (int b = 0; b < nb; ++b) bcount[(int64_t)b * V + v] += tot[v];
+  }
+}
+
+// perm[base[b][v] + (rank of j among the earlier indices of v in block b)] = j
+__global__ void __launch_bounds__(kSortTile) emb_scatter_kernel(const int64_t* __restrict__ idx, int64_t n, int V,
+                                                                const int* __restrict__ base,
+                                                                int64_t* __restrict__ perm) {
+  extern __shared__ int sh[];  // [V] running count of this block, [kSortTile] the tile's rows
+  int* cnt = sh;
+  int* tile = sh + V;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) cnt[v] = 0;
+  const int64_t j0 = (int64_t)blockIdx.x * kSortChunk, j1 = min(j0 + kSortChunk, n);
+  const int* bb = base + (int64_t)blockIdx.x * V;
+  for (int64_t t0 = j0; t0 < j1; t0 += kSortTile) {
+    const int64_t j = t0 + threadIdx.x;
+    const int v = j < j1 ? (int)wrap_idx(idx[j], V) : -1;
+    __syncthreads();  // the previous tile's counts are in, its rows read
+    tile[threadIdx.x] = v;
+    __syncthreads();
+    if (v >= 0) {
+      int rank = 0;
+      for (int k = 0; k < (int)threadIdx.x; ++k) rank += tile[k] == v;
+      perm[bb[v] + cnt[v] + rank] = j;
+    }
+    __syncthreads();  // every thread has read cnt[] for this tile
+    if (v >= 0) atomicAdd(&cnt[v], 1);
+  }
+}
+
 int blocks_for(int64_t rows) {
   int64_t b = (rows + 3) / 4;  // 4 waves per block, one row per wave
   if (b < 1) b = 1;
@@ -241,6 +324,29 @@ hipError_t pdrnn_embedding_bwd_pieces(const void* dout, int dout_dtype, const in
   const int64_t n = num_embeddings * dim;
   hipLaunchKernelGGL(pdrnn::emb_bwd_pieces_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                      partials, dweight, num_embeddings, dim, pieces, padding_idx);
+  return hipGetLastError();
+}
+
+// Stable sort of n indices by row into perm (int64 [n]) and the row
+// offsets (int64 [V + 1]); scratch: int32 [ceil(n / 4096) * V].  V <= 16384.
+int64_t pdrnn_embedding_sort_scratch(int64_t n, int64_t V) {
+  return ((n + pdrnn::kSortChunk - 1) / pdrnn::kSortChunk) * V;
+}
+hipError_t pdrnn_embedding_sort(const int64_t* idx, int64_t n, int64_t V, int* scratch, int64_t* perm,
+                                int64_t* offsets, hipStream_t stream) {
+  if (V < 1 || V > 16384 || n < 0 || n >= (int64_t)1 << 31) return hipErrorInvalidValue;
+  const int nb = (int)((n + pdrnn::kSortChunk - 1) / pdrnn::kSortChunk);
+  if (nb == 0) {
+    hipLaunchKernelGGL(pdrnn::emb_scan_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)V, stream, scratch, 0,
+                       (int)V, offsets);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(pdrnn::emb_count_kernel, dim3(nb), dim3(256), sizeof(int) * (size_t)V, stream, idx, n, (int)V,
+                     scratch);
+  hipLaunchKernelGGL(pdrnn::emb_scan_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)V, stream, scratch, nb,
+                     (int)V, offsets);
+  hipLaunchKernelGGL(pdrnn::emb_scatter_kernel, dim3(nb), dim3(pdrnn::kSortTile),
+                     sizeof(int) * ((size_t)V + pdrnn::kSortTile), stream, idx, n, (int)V, scratch, perm);
   return hipGetLastError();
 }
 

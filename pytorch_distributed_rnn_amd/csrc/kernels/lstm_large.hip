@@ -1152,10 +1152,16 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
   int brow[MT];
   float cst[MT];   // cell state (LSTM c / GRU h), fp32, register-resident
   Quad<S> xpn[MT];  // next step's 4 gate pre-activations
+  // step range of this launch (a later range resumes from c_{t0 - 1} in cseq
+  // and h_{t0 - 1} in hseq)
+  const int S0 = args.s1 > 0 ? args.s0 : 0, S1 = args.s1 > 0 ? args.s1 : T;
+  const int t_first = rev ? T - 1 - S0 : S0;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     brow[mt] = min(mb * 16 * MT + mt * 16 + er, B - 1);
-    cst[mt] = d.c0 ? d.c0[(int64_t)brow[mt] * H + u] : 0.f;
+    const int tp0 = rev ? t_first + 1 : t_first - 1;
+    cst[mt] = S0 > 0 ? d.cseq[(int64_t)tp0 * B * H + (int64_t)brow[mt] * H + u]
+                     : (d.c0 ? d.c0[(int64_t)brow[mt] * H + u] : 0.f);
   }
   auto load_xp = [&](int t) {
 #pragma unroll
@@ -1163,9 +1169,9 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
       xpn[mt] = *reinterpret_cast<const Quad<S>*>(static_cast<const S*>(d.xp) + (int64_t)t * d.xp_st +
                                                 (int64_t)brow[mt] * d.xp_sb + 4 * u);
   };
-  load_xp(rev ? T - 1 : 0);
+  load_xp(t_first);
 
-  for (int s = 0; s < T; ++s) {
+  for (int s = S0; s < S1; ++s) {
     const int t = rev ? T - 1 - s : s;
     const int tp = rev ? t + 1 : t - 1;
     const bool first = s == 0;
@@ -1173,7 +1179,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) xcur[mt] = xpn[mt];
     PS_STAMP(0)
-    if (!first && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err, sync.sticky);
+    if (s > S0 && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err, sync.sticky);
     PS_STAMP(1)
 
     f32x4 acc[MT][CT];
@@ -1243,7 +1249,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
     if (s + 1 < T) ps_arrive(cnt, sync.mode);
     else __syncthreads();  // (LDS reuse only; nothing waits for the last step)
     PS_STAMP(5)
-    if (s + 1 < T) load_xp(rev ? t - 1 : t + 1);
+    if (s + 1 < S1) load_xp(rev ? t - 1 : t + 1);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int b = mb * 16 * MT + mt * 16 + er;
@@ -1322,12 +1328,15 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
       nsp[mt] = has_prev ? d.cseq[(int64_t)tpp * B * H + bu] : (d.c0 ? d.c0[bu] : 0.f);
     }
   };
+  // step range of this launch: a later range resumes from dgates_t (written
+  // by the earlier range's last step) and the carry it left in dc_carry
+  const int S0 = args.s1 > 0 ? args.s0 : 0, S1 = args.s1 > 0 ? args.s1 : T;
   {
-    const int t0 = rev ? 0 : T - 1, tn0 = rev ? t0 + 1 : t0 - 1;
+    const int t0 = rev ? S0 : T - 1 - S0, tn0 = rev ? t0 + 1 : t0 - 1;
     if (rev ? tn0 < T : tn0 >= 0) load_ops(tn0);
   }
 
-  for (int s = 0; s < T; ++s) {
+  for (int s = S0; s < S1; ++s) {
     const int t = rev ? s : T - 1 - s;
     const int tn = rev ? t + 1 : t - 1;
     const bool cell = rev ? tn < T : tn >= 0;
@@ -1337,7 +1346,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
     for (int mt = 0; mt < MT; ++mt) { od[mt] = nd[mt]; ocur[mt] = ncur[mt]; osp[mt] = nsp[mt]; oact[mt] = nact[mt]; }
     // dgates_t of the whole batch block: written by every column block (the
     // first one by the separate first-step kernel, ordered by the launch)
-    if (s > 0 && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err, sync.sticky);
+    if (s > S0 && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err, sync.sticky);
     f32x4 acc[MT][CT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -1419,7 +1428,14 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_bwd_kernel(Pdrn
     if (s + 1 < T) {
       ps_arrive(cnt, sync.mode);
       const int tn2 = rev ? tn + 1 : tn - 1;  // cell-backward step of s + 1
-      if (rev ? tn2 < T : tn2 >= 0) load_ops(tn2);
+      if (s + 1 < S1 && (rev ? tn2 < T : tn2 >= 0)) load_ops(tn2);
+    }
+  }
+  if (S1 < T) {  // the next range's carry
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int b = mb * 16 * MT + mt * 16 + er;
+      if (b < B) d.dc_carry[(int64_t)b * H + u] = carry[mt];
     }
   }
 }

@@ -203,3 +203,30 @@ def test_shadow_weights_follow_optimizer_steps():
     for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
         torch.testing.assert_close(p, q, rtol=0, atol=0, msg=k)
     assert any(hasattr(p, "_pdrnn_shadow") for p in m1.parameters())
+
+
+@pytest.mark.parametrize("V,N", [(256, 65536), (300, 5000), (16384, 70001), (7, 0), (5, 3)])
+def test_embedding_sort_matches_stable_sort(V, N):
+    """The in-tree counting sort behind the embedding backward (no library
+    sort kernels) equals torch's stable sort: same permutation (ties in index
+    order) and the same row offsets, negative indices wrapped."""
+    mod = _ext.require()
+    torch.manual_seed(9)
+    idx = torch.randint(-V, V, (N,), device="cuda")
+    perm, off = mod.embedding_sort(idx, V)
+    flat = torch.where(idx < 0, idx + V, idx)
+    vals, ref_perm = torch.sort(flat, stable=True)
+    assert torch.equal(perm, ref_perm)
+    assert torch.equal(off, torch.searchsorted(vals, torch.arange(V + 1, device="cuda")))
+
+
+def test_embedding_bwd_large_vocab_uses_library_sort():
+    """Above 16384 rows the backward keeps the library sort: still equal to index_add."""
+    mod = _ext.require()
+    torch.manual_seed(10)
+    V, D, N = 20000, 64, 3000
+    idx = torch.randint(0, V, (N,), device="cuda")
+    g = torch.randn(N, D, device="cuda")
+    dw = mod.embedding_bwd(g, idx, V, -1)
+    ref = torch.zeros(V, D, device="cuda").index_add_(0, idx, g)
+    torch.testing.assert_close(dw, ref, rtol=1e-5, atol=1e-5)
