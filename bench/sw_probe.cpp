@@ -232,7 +232,7 @@ int main(int argc, char** argv) {
   }
   const int chunks = pdrnn_lstm_small_dw_chunks(H, NL, B, T);
   float* slab;
-  CK(hipMalloc(&slab, (size_t)std::max(chunks, 1) * P * 4));
+  CK(hipMalloc(&slab, (size_t)std::max(std::max(chunks, 1), B) * P * 4));  // (mode 4: one row per sequence)
 
   PdrnnLstmSmallFwdArgs f{};
   f.x = dx; f.idx = didx; f.x_sb = (int64_t)T * I; f.x_st = I;
@@ -288,7 +288,7 @@ int main(int argc, char** argv) {
     auto run_fwd = [&]() {
       if (old) CK(pdrnn_lstm_small_fwd(&f, H, nb_old_f, sp_old_f, 1, st));
       else if (mb) CK(pdrnn_lstm_mb_fwd(&f, st));
-      else CK(pdrnn_lstm_sw_fwd(&f, mode, st));
+      else CK(pdrnn_lstm_sw_fwd(&f, mode == 4 ? 2 : mode, st));  // 4: backward-only map
     };
     auto run_bwd = [&]() {
       if (old) CK(pdrnn_lstm_small_bwd_dwout(&bk, H, grid_old_b, nb_old_b, st));
@@ -351,15 +351,35 @@ int main(int argc, char** argv) {
     run_bwd();
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(h_act.data(), act, n_act * 4, hipMemcpyDeviceToHost));
-    const double e_dz = maxrel(h_act, RR.dz, rows, 5 * H, 4 * H, 4 * H);
+    const double e_dz = mode == 4 ? 0.0 : maxrel(h_act, RR.dz, rows, 5 * H, 4 * H, 4 * H);  // (4: no dz stores)
+    // the summed weight gradients (slab rows), against the first mode's
+    {
+      int nrows = B;
+      if (mode != 4) {
+        CK(pdrnn_lstm_small_dw(&dw, H, st));
+        nrows = chunks;
+      }
+      CK(hipStreamSynchronize(st));
+      std::vector<float> hs((size_t)nrows * P);
+      CK(hipMemcpy(hs.data(), slab, hs.size() * 4, hipMemcpyDeviceToHost));
+      std::vector<double> sum(P, 0.0);
+      for (int r = 0; r < nrows; ++r)
+        for (int64_t k = 0; k < P; ++k) sum[k] += hs[(size_t)r * P + k];
+      static std::vector<double> first;
+      if (first.empty()) first = sum;
+      double mx = 0, err = 0;
+      for (int64_t k = 0; k < P; ++k) { mx = std::max(mx, std::fabs(first[k])); err = std::max(err, std::fabs(sum[k] - first[k])); }
+      printf("  dW sum vs first mode: max rel %.2e\n", mx > 0 ? err / mx : err);
+    }
     // timing
-    for (int w = 0; w < 3; ++w) { run_fwd(); run_bwd(); CK(pdrnn_lstm_small_dw(&dw, H, st)); }
+    for (int w = 0; w < 3; ++w) { run_fwd(); run_bwd(); if (mode != 4) CK(pdrnn_lstm_small_dw(&dw, H, st)); }
     CK(hipEventRecord(e0, st));
     for (int r = 0; r < reps; ++r) run_fwd();
     CK(hipEventRecord(e1, st));
     for (int r = 0; r < reps; ++r) run_bwd();
     CK(hipEventRecord(e2, st));
-    for (int r = 0; r < reps; ++r) CK(pdrnn_lstm_small_dw(&dw, H, st));
+    for (int r = 0; r < reps; ++r)
+      if (mode != 4) CK(pdrnn_lstm_small_dw(&dw, H, st));
     CK(hipEventRecord(e3, st));
     CK(hipEventSynchronize(e3));
     float tf = 0, tb = 0, tw = 0;

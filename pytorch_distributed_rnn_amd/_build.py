@@ -107,6 +107,13 @@ def _run(cmd, verbose):
     return r
 
 
+# per-file device flags.  lstm_sw: the backward's weight-gradient waves
+# (mode 4) keep their MFMA accumulators in VGPRs -- in AGPRs they would be
+# allocated beside the BPTT waves' VGPRs (one kernel, one register budget)
+# and the workgroup would drop to one wave per SIMD.
+_FILE_FLAGS = {"lstm_sw": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def build(verbose: bool = False, clean: bool = False, jobs: int | None = None) -> Path:
     """Compile every HIP kernel for gfx950 plus the host runtime; link ``_C``."""
     inc, torch_lib, abi = _torch_paths()
@@ -141,8 +148,9 @@ def build(verbose: bool = False, clean: bool = False, jobs: int | None = None) -
     jobs_list = []
     for src in kernels:
         obj = BUILD_DIR / (src.stem + ".hip.o")  # device code: shared with the plain build
-        sig = _digest([src], hdr_sig + " ".join(hip_flags))
-        jobs_list.append((src, obj, sig, [hipcc, *hip_flags, src, "-o", obj]))
+        flags = hip_flags + _FILE_FLAGS.get(src.stem, [])
+        sig = _digest([src], hdr_sig + " ".join(flags))
+        jobs_list.append((src, obj, sig, [hipcc, *flags, src, "-o", obj]))
     for src in runtime:
         obj = build_dir / (src.stem + ".cpp.o")
         sig = _digest([src], hdr_sig + " ".join(host_flags))

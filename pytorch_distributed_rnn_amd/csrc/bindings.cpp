@@ -470,7 +470,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const bool sw = sw_enabled() && pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, (int)cell) == 1 &&
                   pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T) != 0 && T <= 640;
   const int sw_fmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 0) : -1;
-  const int sw_bmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 1) : -1;
+  int sw_bmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 1) : -1;
+  if (sw_bmode == 4 && T % 4) sw_bmode = 2;  // register dW: whole 4-step K steps
   // Above one residency round the BPTT defers its weight gradients: the
   // recurrence writes the gate gradients (into `act`, in place) and the
   // matrix-core kernel lstm_small_dw forms dW / db over all B*T rows, one slab
@@ -481,7 +482,10 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   // deferred dW: sequences per BPTT workgroup; the matrix-core launch forms
   // dW over fixed K chunks, one slab row each
   const int nb_dw = dwout ? pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B) : (int)nb_bwd;
-  const int slab_rows = dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
+  // (sequence-in-wave mode 4: the BPTT waves form dW on the matrix cores, one
+  // slab row per sequence, no dW launch)
+  const bool sw_rdw = sw && sw_bmode == 4;
+  const int slab_rows = sw_rdw ? (int)B : dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
   Tensor slab = at::empty({slab_rows, L.P}, opts);
 
   PdrnnLstmSmallFwdArgs f{};
@@ -573,7 +577,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   else if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
   else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, nb_dw, st));
   else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
-  if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_dw(&dw, (int)H, st));
+  if (dwout && !sw_rdw) HIP_LAUNCH_CHECK(pdrnn_lstm_small_dw(&dw, (int)H, st));
   if (st_f.defined()) {
     const int bw_iters = sw ? (int)(T + NL - 1)
                             : (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_dw - 1) / ((int64_t)grid_dw * nb_dw));

@@ -39,9 +39,12 @@
 #include "pdrnn/motion_head.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace pdrnn {
 namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kH = 32;
 constexpr float kA = -1.4426950408889634f;  // -log2(e): rows pre-scaled so sigma(z) = 1 / (1 + 2^acc)
@@ -438,10 +441,14 @@ PDRNN_DEVICE float col_dot(const BwdCol& W, const float4 (&g)[16]) {
 // (no occupancy target: at 168 VGPRs the split backward spills, and it only
 // runs at B <= one wave per SIMD)
 template <int NL, int MODE>
-__global__ void __launch_bounds__(MODE >= 2 ? 64 * NL : 64)
+__global__ void __launch_bounds__(MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64)
 lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
   constexpr int NB = (MODE & 1) ? 2 : 1;
   constexpr bool SPLIT = MODE >= 2;
+  // mode 4: the mode-2 map plus two waves that accumulate the weight
+  // gradients on the matrix cores (no gate-gradient stores, no dW launch)
+  constexpr bool DWACC = MODE == 4;
+  constexpr int ZR = DWACC ? 8 : 2;  // dz slots per (sequence, layer): a ring that holds a dW K step
   static_assert(NL == 1 || NL == 2, "one or two layers");
   static_assert(!SPLIT || NL == 2, "layer-split mode needs two layers");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -454,9 +461,9 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
   const bool odd = s != 0;
   const int B = a.B, T = a.T;
   const int bbase = blockIdx.x * NB;
-  float* dzb = smem;                          // [NB][NL][2][kDZ]
-  float* dxb = smem + NB * NL * 2 * kDZ;      // [NB][2][32] (mode 2: layer 1 -> layer 0)
-  auto dzbuf = [&](int n, int l, int p) { return dzb + ((n * NL + l) * 2 + p) * kDZ; };
+  float* dzb = smem;                          // [NB][NL][ZR][kDZ]
+  float* dxb = smem + NB * NL * ZR * kDZ;     // [NB][2][32] (modes 2/3: layer 1 -> layer 0)
+  auto dzbuf = [&](int n, int l, int t) { return dzb + ((n * NL + l) * ZR + (t & (ZR - 1))) * kDZ; };
 
   int bidx[NB];
   bool valid[NB];
@@ -472,7 +479,7 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
 
   // the dW kernel streams whole stages: the PDRNN_DW_PAD_ROWS padding rows
   // behind the last layer's gate gradients must hold finite values
-  if (blockIdx.x == 0) {
+  if (!DWACC && blockIdx.x == 0) {
     float* pad = a.dg_out + (int64_t)NL * B * T * a.dg_st;
     for (int e = tid; e < PDRNN_DW_PAD_ROWS * a.dg_st; e += blockDim.x) pad[e] = 0.f;
   }
@@ -530,21 +537,158 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
   // for the prefetches of the next two iterations.
   const int iters = T + NL - 1;
 
+  // DWACC: the weight gradients on the matrix cores of two extra waves of the
+  // workgroup (wave 2: layer 0, wave 3: layer 1), so the BPTT waves never
+  // wait on a busy matrix core.  dW_hh / dW_ih of a layer are 16x16 C tiles
+  // of v_mfma_f32_16x16x4_f32 (M = 128 gate rows in 8 tiles, N = 32 columns
+  // in 2, K = 4 consecutive time steps).  A K step's A operands (the layer's
+  // dz from the 8-slot LDS ring) are captured in the iteration after its
+  // last step is written; its 32 MFMAs issue a quarter (two m-tiles) per
+  // iteration.  The B operands (h_{t-1} and the layer input, no recurrence
+  // dependency) are loaded one group ahead.  The BPTT waves keep their two
+  // gate rows' bias sums in registers.
+  float dbs[2] = {0.f, 0.f};
+  const int xld = a.xg_ld;
+  // B operands of the K step over times t .. t+3 (lane: time t + (lane >> 4),
+  // column lane & 15 of each 16-column tile)
+  auto dw_loadb = [&](int l, int t, float (&bv)[4]) {
+    const int tk = t + (lane >> 4), c = lane & 15;
+    const int64_t b = bidx[0];
+    const float* hown = a.hseq + ((int64_t)(l * B + b) * T + max(tk - 1, 0)) * kH;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) bv[nt] = tk > 0 ? hown[16 * nt + c] : 0.f;
+    if (l > 0) {
+      const float* hin = a.hseq + ((int64_t)((l - 1) * B + b) * T + tk) * kH;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) bv[2 + nt] = hin[16 * nt + c];
+    } else {
+      bv[2] = c < xld ? a.xg_out[((int64_t)b * T + tk) * xld + c] : 0.f;
+      bv[3] = 0.f;
+    }
+  };
+  // the dW wave of layer L (compile time); its iteration `it` is the BPTT
+  // waves' iteration (one barrier each)
+  auto dw_wave = [&](auto lc) {
+    constexpr int L = decltype(lc)::value;
+    constexpr int NI = L > 0 ? 2 : 1;  // input column tiles (layer 0: I <= 16)
+    f32x4 ahh[8][2], aih[8][NI];
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) ahh[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int nt = 0; nt < NI; ++nt) aih[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float pav[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f}, bnext[4];
+    dw_loadb(L, T - 4, bnext);
+    // (branch-free: before the first K step is complete the A operands are
+    // zeros; a branch would put the accumulators through copies at its joins)
+    auto capture = [&](int g, bool live) {
+      const float* zb = dzbuf(0, L, g + (lane >> 4));
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const float z = zb[dz_slot(16 * mt + (lane & 15))];
+        pav[mt] = live ? z : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pb[k] = bnext[k];
+      dw_loadb(L, max(g - 4, 0), bnext);
+    };
+    auto quarter = [&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        constexpr int m0 = 2 * q;
+        const int mt = m0 + j;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          ahh[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pav[mt], pb[nt], ahh[mt][nt], 0, 0, 0);
+#pragma unroll
+        for (int nt = 0; nt < NI; ++nt)
+          aih[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pav[mt], pb[2 + nt], aih[mt][nt], 0, 0, 0);
+      }
+    };
+    using Q0 = std::integral_constant<int, 0>;
+    using Q1 = std::integral_constant<int, 1>;
+    using Q2 = std::integral_constant<int, 2>;
+    using Q3 = std::integral_constant<int, 3>;
+    // T % 4 == 0.  Layer 1's group g (times g .. g+3) is complete after
+    // iteration T-1-g, layer 0's after T-g: capture at it = T-g (layer 1) or
+    // T-g+1 (layer 0), i.e. at it % 4 == LAG, then one quarter per iteration.
+    constexpr int LAG = 1 - L;
+    auto pos = [&](int it, auto pc) {
+      constexpr int p = decltype(pc)::value;
+      constexpr int q = (p - LAG + 4) & 3;
+      if constexpr (q == 0) capture(T - it + LAG, it >= 4 + LAG);
+      quarter(std::integral_constant<int, q>{});
+      __builtin_amdgcn_sched_barrier(0);  // (a quarter per iteration, not clumped)
+      lds_barrier();
+    };
+    __syncthreads();
+    const int iters = T + 1;
+    int it = 0;
+    for (; it + 3 < iters; it += 4) {
+      pos(it, Q0{});
+      pos(it + 1, Q1{});
+      pos(it + 2, Q2{});
+      pos(it + 3, Q3{});
+    }
+    pos(it, Q0{});  // it = T
+    // (after the last barrier every dz is in the ring)
+    if constexpr (L == 1) {
+      quarter(Q1{}); quarter(Q2{}); quarter(Q3{});
+    } else {
+      capture(0, true);
+      quarter(Q0{}); quarter(Q1{}); quarter(Q2{}); quarter(Q3{});
+    }
+    // this workgroup's slab row (an empty slot recomputed sequence B - 1: its
+    // row must still be written, as zeros, since the reduction sums every row)
+    float* srow = a.slab + (int64_t)blockIdx.x * a.P;
+    const int Iin = L == 0 ? a.I : kH;
+    const int c = lane & 15, r4 = 4 * (lane >> 4);
+    const float keep = valid[0] ? 1.f : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * mt + r4 + r;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) srow[a.off_whh[L] + (int64_t)row * kH + 16 * nt + c] = keep * ahh[mt][nt][r];
+#pragma unroll
+        for (int nt = 0; nt < NI; ++nt) {
+          const int col = 16 * nt + c;
+          if (col < Iin) srow[a.off_wih[L] + (int64_t)row * Iin + col] = keep * aih[mt][nt][r];
+        }
+      }
+  };
+  auto db_store = [&](int l) {
+    float* srow = a.slab + (int64_t)blockIdx.x * a.P;
+    const float d0 = valid[0] ? dbs[0] : 0.f, d1 = valid[0] ? dbs[1] : 0.f;
+    const int r0 = 2 * s * kH + u, r1 = r0 + kH;
+    if (a.off_bih[l] >= 0) { srow[a.off_bih[l] + r0] = d0; srow[a.off_bih[l] + r1] = d1; }
+    if (a.off_bhh[l] >= 0) { srow[a.off_bhh[l] + r0] = d0; srow[a.off_bhh[l] + r1] = d1; }
+  };
+
   // layer-generic pieces
   auto rows = [&](int l, int n, int t, const Ops& o, float dh_in, bool act) {
     float d0, d1, dcn = dc[l][n];
     row_phase(o, dhrec[l][n] + dh_in, dcn, odd, t > 0, d0, d1);
     dc[l][n] = act ? dcn : dc[l][n];
-    float* zb = dzbuf(n, l, t & 1);
+    float* zb = dzbuf(n, l, t);
     zb[slot0] = d0;
     zb[slot1] = d1;
-    const uint32_t so = rowidx(l, n, min(max(t, 0), T - 1)) * st_dg;
-    const uint32_t m = act ? vmask[n] : kOOR;
-    bstore(d0, r_dg, vo_d0 | m, so);
-    bstore(d1, r_dg, vo_d1 | m, so);
+    if constexpr (DWACC) {
+      dbs[0] += act ? d0 : 0.f;
+      dbs[1] += act ? d1 : 0.f;
+    } else {
+      const uint32_t so = rowidx(l, n, min(max(t, 0), T - 1)) * st_dg;
+      const uint32_t m = act ? vmask[n] : kOOR;
+      bstore(d0, r_dg, vo_d0 | m, so);
+      bstore(d1, r_dg, vo_d1 | m, so);
+    }
   };
   auto read_dz = [&](int l, int n, int t, float4 (&g)[16]) {
-    const float* zb = dzbuf(n, l, t & 1) + colbase;
+    const float* zb = dzbuf(n, l, t) + colbase;
 #pragma unroll
     for (int c = 0; c < 16; ++c) g[c] = ld4(zb + 4 * c);
   };
@@ -663,7 +807,8 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
         body(it + 1, opB);
       }
       if (it < iters) body(it, opA);
-    } else {
+      if constexpr (DWACC) db_store(1);
+    } else if (wv == 0) {
       const BwdCol Whh0 = load_bwd_col(a.w_hh[0], kH, u, true, u, s, a.w_bf16);
       Ops opA[NB], opB[NB];
 #pragma unroll
@@ -699,6 +844,10 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
         body(it + 1, opB);
       }
       if (it < iters) body(it, opA);
+      if constexpr (DWACC) db_store(0);
+    } else if constexpr (DWACC) {
+      if (wv == 2) dw_wave(std::integral_constant<int, 0>{});
+      else dw_wave(std::integral_constant<int, 1>{});
     }
   }
   if (a.stamps && tid == 0) {
@@ -722,7 +871,7 @@ int sw_cus() {
 }
 
 size_t fwd_lds(int NL, int nb, int T) { return sizeof(float) * ((size_t)nb * NL * 2 * kHB + (size_t)nb * T * kXS); }
-size_t bwd_lds(int NL, int nb) { return sizeof(float) * ((size_t)nb * NL * 2 * kDZ + (size_t)nb * 2 * 32); }
+size_t bwd_lds(int NL, int nb, int zr = 2) { return sizeof(float) * ((size_t)nb * NL * zr * kDZ + (size_t)nb * 2 * 32); }
 int mode_nb(int mode) { return (mode & 1) ? 2 : 1; }
 
 template <int NL, int MODE>
@@ -737,8 +886,9 @@ template <int NL, int MODE>
 hipError_t launch_bwd(const PdrnnLstmSmallBwdArgs* a, hipStream_t st) {
   constexpr int NB = (MODE & 1) ? 2 : 1;
   const int grid = (a->B + NB - 1) / NB;
-  const int block = MODE >= 2 ? 64 * NL : 64;
-  hipLaunchKernelGGL((lstm_sw_bwd_kernel<NL, MODE>), dim3(grid), dim3(block), bwd_lds(NL, NB), st, *a);
+  const int block = MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64;
+  hipLaunchKernelGGL((lstm_sw_bwd_kernel<NL, MODE>), dim3(grid), dim3(block), bwd_lds(NL, NB, MODE == 4 ? 8 : 2), st,
+                     *a);
   return hipGetLastError();
 }
 
@@ -755,7 +905,11 @@ extern "C" int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell) {
 // Measured (bench/sw_probe.cpp, profiles/r5/sw): two-layer stacks run one
 // wave per layer up to one wave per SIMD (mode 2); above, the forward keeps
 // that map at three waves per SIMD (mode 6) and the backward takes two
-// sequences per wave (mode 3).  One layer: one wave per sequence (mode 0),
+// sequences per wave (mode 3).  Up to two workgroups per CU the backward
+// forms the weight gradients itself (mode 4: two more waves per workgroup on
+// the matrix cores, no dW launch; 55.7 us against 54.7 + 16.9 at B = 180,
+// profiles/r5/sw/dw4_probe.log; T % 4 == 0, the caller falls back to mode 2
+// otherwise).  One layer: one wave per sequence (mode 0),
 // two above one wave per SIMD (mode 1).  PDRNN_SW_MODE / PDRNN_SW_BWD_MODE
 // override.
 extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
@@ -763,9 +917,11 @@ extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
   if (!(e && *e) && backward) e = getenv("PDRNN_SW_MODE");
   if (e && *e) {
     const int m = atoi(e);
-    if (m >= 0 && m <= 6 && m != 4 && m != 5 && (m < 2 || NL == 2) && (m != 6 || !backward)) return m;
+    if (m >= 0 && m <= 6 && m != 5 && (m < 2 || NL == 2) && (m != 6 || !backward) && (m != 4 || backward)) return m;
   }
   const int simds = 4 * sw_cus();
+  // (mode 4: four waves of <= 256 VGPRs per workgroup, two workgroups per CU)
+  if (NL == 2 && backward && 2 * B <= simds) return 4;
   if (NL == 2) return B <= simds ? 2 : backward ? 3 : 6;
   return B <= simds ? 0 : 1;
 }
@@ -803,5 +959,9 @@ extern "C" hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode
   if (mode == 1) return launch_bwd<2, 1>(a, st);
   if (mode == 2) return launch_bwd<2, 2>(a, st);
   if (mode == 3) return launch_bwd<2, 3>(a, st);
+  if (mode == 4) {  // register dW: one slab row per workgroup; reads the x rows and the h sequence
+    if (a->T % 4 || !a->slab || !a->xg_out || a->xg_ld > 16 || !a->hseq) return hipErrorInvalidValue;
+    return launch_bwd<2, 4>(a, st);
+  }
   return hipErrorInvalidValue;
 }
