@@ -390,6 +390,27 @@ int main(int argc, char** argv) {
            mode, old ? " (lstm_small)" : mb ? " (bf16 mfma)" : "", uf, uf * 2400.0 / (T + NL - 1), ub,
            ub * 2400.0 / (T + NL - 1), uw, e_act, e_h, e_dht, e_dz,
            (e_act < tol && e_h < tol && e_dht < tol && e_dz < tol) ? "OK" : "MISMATCH");
+    if (mode != 4 && getenv("PROBE_OVERLAP")) {
+      // the backward and the dW kernel side by side on two streams (timing
+      // only: the dW reads the previous backward's gate gradients)
+      static hipStream_t st2 = nullptr;
+      static hipEvent_t fk = nullptr, jn = nullptr;
+      if (!st2) { CK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking)); CK(hipEventCreate(&fk)); CK(hipEventCreate(&jn)); }
+      CK(hipEventRecord(e0, st));
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(fk, st));
+        CK(hipStreamWaitEvent(st2, fk, 0));
+        run_bwd();
+        CK(pdrnn_lstm_small_dw(&dw, H, st2));
+        CK(hipEventRecord(jn, st2));
+        CK(hipStreamWaitEvent(st, jn, 0));
+      }
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float to = 0;
+      CK(hipEventElapsedTime(&to, e0, e1));
+      printf("  overlap: bwd || dW %7.1f us (serial %7.1f)\n", 1e3 * to / reps, ub + uw);
+    }
     fflush(stdout);
     if (want_stamps) {
       std::vector<uint64_t> hs((size_t)B * 8);
