@@ -1694,12 +1694,10 @@ hipError_t dispatch_fwd(const PdrnnLstmSmallFwdArgs* a, int nb, int split, int s
     if (save) return nb == 2 ? launch_fwd_gs<H, 2, true>(a, st) : launch_fwd_gs<H, 1, true>(a, st);
     return nb == 2 ? launch_fwd_gs<H, 2, false>(a, st) : launch_fwd_gs<H, 1, false>(a, st);
   }
-  switch (split) {
-    case 2: return dispatch_fwd_s<H, 2>(a, nb, save, st);
-    case 4: return dispatch_fwd_s<H, 4>(a, nb, save, st);
-    case 8: return dispatch_fwd_s<H, 8>(a, nb, save, st);
-    default: return hipErrorInvalidValue;
-  }
+  // (K splits of 4 / 8 lanes per unit are never the widest valid map -- a
+  // stack that fits them fits the gate-split map -- and are not built)
+  if (split == 2) return dispatch_fwd_s<H, 2>(a, nb, save, st);
+  return hipErrorInvalidValue;
 }
 
 template <int H, int S2>
@@ -1750,11 +1748,9 @@ hipError_t dispatch_bwd(const PdrnnLstmSmallBwdArgs* a, int nb, int split, hipSt
     }
     return hipErrorInvalidConfiguration;
   }
-  switch (split) {
-    case 2: return dispatch_bwd_s<H, 2>(a, nb, st);
-    case 4: return dispatch_bwd_s<H, 4>(a, nb, st);
-    default: return hipErrorInvalidValue;
-  }
+  // (likewise the 4-slice row split: a stack that fits it fits the unit-group map)
+  if (split == 2) return dispatch_bwd_s<H, 2>(a, nb, st);
+  return hipErrorInvalidValue;
 }
 
 template <int H>
@@ -1950,13 +1946,11 @@ int pdrnn_lstm_small_supported(int H, int I, int NL) {
 int pdrnn_lstm_small_max_split(int H, int NL, int backward) {
   if (backward) {
     if (NL * H * (H >= 64 ? 8 : 4) <= 512) return 1;  // unit-group map
-    for (int s2 = 4; s2 >= 2; s2 /= 2)
-      if (NL * 2 * H * s2 <= 512 && (4 * H / s2) % 16 == 0) return s2;
+    if (NL * 4 * H <= 512 && (2 * H) % 16 == 0) return 2;  // 2-slice row split
     return 0;
   }
   if (NL * 4 * H <= 512) return 1;  // gate-split map
-  for (int s = 8; s >= 2; s /= 2)
-    if (NL * H * s <= 512 && (H * s) % 64 == 0 && (2 * H / s) % 4 == 0 && H % (2 * H / s) == 0) return s;
+  if (NL * H * 2 <= 512 && (H * 2) % 64 == 0) return 2;  // 2-lane K split
   return 0;
 }
 

@@ -76,7 +76,9 @@ class MotionTrainStep:
     Single process (no gradient sync): the optimizer step is fused into the
     one-pass gradient reduction (``slab_reduce_adam`` kernel), so one step is
     four launches: forward+head+CE, BPTT, the matrix-core weight gradients
-    (deferred dW) and the reduction + Adam.
+    (deferred dW) and the reduction + Adam -- three up to two sequences per CU
+    (B <= 512 on 256 CUs), where the BPTT workgroups form the weight gradients
+    themselves (kernels/lstm_sw.hip, backward mode 4).
 
     With gradient sync (multi-GPU) the step is forward+BPTT+reductions, the
     inline RCCL all-reduce and the flat Adam.  ``cuda_graph=True`` (or
