@@ -20,6 +20,10 @@ tail -1 gpurun_out/${tag}_bench.log | cut -c1-400
 # config 2 (bf16 motion) and the GRU cell at the headline shape
 timeout -k 10 300 python bench.py --dtype bf16 > gpurun_out/${tag}_bench_bf16.log 2>&1 || { tail -20 gpurun_out/${tag}_bench_bf16.log; exit 1; }
 tail -1 gpurun_out/${tag}_bench_bf16.log | python tools/bench_line.py "bf16"
+timeout -k 10 300 python bench.py --layers 1 --dtype bf16 > gpurun_out/${tag}_bench_bf16_l1.log 2>&1 || { tail -20 gpurun_out/${tag}_bench_bf16_l1.log; exit 1; }
+tail -1 gpurun_out/${tag}_bench_bf16_l1.log | python tools/bench_line.py "bf16 1 layer (config 2)"
+timeout -k 10 300 python bench.py --layers 1 > gpurun_out/${tag}_bench_fp32_l1.log 2>&1 || { tail -20 gpurun_out/${tag}_bench_fp32_l1.log; exit 1; }
+tail -1 gpurun_out/${tag}_bench_fp32_l1.log | python tools/bench_line.py "fp32 1 layer"
 timeout -k 10 300 python bench.py --cell gru > gpurun_out/${tag}_bench_gru.log 2>&1 || { tail -20 gpurun_out/${tag}_bench_gru.log; exit 1; }
 tail -1 gpurun_out/${tag}_bench_gru.log | python tools/bench_line.py "gru"
 for B in 1440 720 360 180; do
