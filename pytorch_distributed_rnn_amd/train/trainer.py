@@ -309,6 +309,15 @@ class Trainer:
                                                          cuda_graph=self.cuda_graph, comm=self._grad_comm())
         return self._fused
 
+    def _graphed_step(self):
+        """The autograd step replayed from a HIP graph (train/graphed_step.py),
+        or None (not requested, multi-process, CPU, other optimizers)."""
+        if getattr(self, "_graphed", False) is not False:
+            return self._graphed
+        from . import graphed_step
+        self._graphed = graphed_step.make(self)
+        return self._graphed
+
     def train_batch(self, batch) -> Tuple[Tensor, int]:
         """One optimizer step on one batch; returns (stats [loss, n, correct], batch size).
 
@@ -322,6 +331,16 @@ class Trainer:
                 return fused(features, labels_all, idx), idx.numel()
             data, labels = batch
             return fused(data, labels.reshape(-1).contiguous(), None), labels.shape[0]
+        graphed = self._graphed_step()
+        if graphed is not None and self.model.training and len(batch) == 3:
+            try:
+                return graphed(*batch)
+            except RuntimeError as e:
+                if graphed.replays:
+                    raise
+                # (a capture that fails leaves the eager step in charge)
+                logging.warning("graph capture of the training step failed, running it eagerly: %s", e)
+                self._graphed = None
         self.optimizer.zero_grad()
         with trace_range("pdrnn.forward"):
             output, labels = self._forward(batch)
