@@ -45,6 +45,7 @@ constexpr int kN = 16;                      // sequences per workgroup (MFMA col
 constexpr int kXK = 16;                     // staged x columns (I <= 16, zero-padded)
 constexpr float kL2E = 1.4426950408889634f;
 constexpr uint32_t kOOR = 0x80000000u;      // buffer offset past the range: the store is dropped
+constexpr int kSR = 6 * kH + 4;             // staging row: i f g o c h (+ pad: 16-byte rows, fewer bank conflicts)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -82,6 +83,10 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
   uint16_t* hb16 = reinterpret_cast<uint16_t*>(smem);
   float* htop = smem + HBF;                  // [16][32] fp32: the top layer's h_T for the head
   uint16_t* xs = reinterpret_cast<uint16_t*>(htop + kN * kH);  // [T][16][16] bf16
+  // [2 parity][NL][16 seq][kSR] fp32: a step's act rows (i f g o c) and h,
+  // written by the cells in MFMA-accumulator order and stored row-coalesced
+  // after the step's barrier (direct stores spanned 16 sequences per
+  // instruction: the CU's vector-memory pipe set the step time)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -91,6 +96,7 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
   const bool valid = b0 + n < B;
   const int bn = valid ? b0 + n : B - 1;
   auto hbuf = [&](int l, int p) { return hb16 + (l * 2 + p) * kN * kH; };
+  float* stg = reinterpret_cast<float*>(xs + (size_t)T * kN * kXK);
 
   // ---- prologue: zero the h images (h_{-1} = 0), stage x as bf16 ---------
   for (int e = tid; e < HBF; e += 256) smem[e] = 0.f;
@@ -161,13 +167,6 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
   }
   __syncthreads();
 
-  const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
-  const __amdgpu_buffer_rsrc_t r_h = uniform_rsrc(a.hseq);
-  uint32_t rowbase[NL];  // this lane's row (l, b, 0)
-#pragma unroll
-  for (int l = 0; l < NL; ++l) rowbase[l] = (uint32_t)((l * B + bn) * T);
-  const uint32_t vmask = valid ? 0u : kOOR;
-
   float cst[NL][2], hst[NL][2];
 #pragma unroll
   for (int l = 0; l < NL; ++l)
@@ -177,8 +176,9 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
   uint64_t st0 = 0, sr0 = 0;
   if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
 
-  // epilogue of layer l's M-tile m at time t (active: commit + store)
-  auto cell = [&](int l, int m, int t, bool act, f32x4 acc) {
+  // epilogue of layer l's M-tile m at time t (active: commit; the outputs go
+  // to the step's staging rows, parity p)
+  auto cell = [&](int l, int m, int t, bool act, f32x4 acc, int p) {
     const int mt = 2 * w + m;
     const int u = 8 * g + mt;
     const float ig = sgm(acc[0] + bias[l][m][0]);
@@ -189,16 +189,30 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
     const float h = og * tnh(cn);
     cst[l][m] = act ? cn : cst[l][m];
     hst[l][m] = act ? h : hst[l][m];
-    const uint32_t row = rowbase[l] + (uint32_t)min(max(t, 0), T - 1);
-    const uint32_t m_ = act ? vmask : kOOR;
-    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)0);
-    const uint32_t ra = row * (5 * kH * 4);
-    bst(ig, r_act, (ra + (0 * kH + u) * 4) | m_, so);
-    bst(fg, r_act, (ra + (1 * kH + u) * 4) | m_, so);
-    bst(gg, r_act, (ra + (2 * kH + u) * 4) | m_, so);
-    bst(og, r_act, (ra + (3 * kH + u) * 4) | m_, so);
-    bst(cn, r_act, (ra + (4 * kH + u) * 4) | m_, so);
-    bst(h, r_h, (row * (kH * 4) + u * 4) | m_, so);
+    (void)t;
+    float* sr = stg + ((p * NL + l) * kN + n) * kSR;
+    sr[0 * kH + u] = ig;
+    sr[1 * kH + u] = fg;
+    sr[2 * kH + u] = gg;
+    sr[3 * kH + u] = og;
+    sr[4 * kH + u] = cn;
+    sr[5 * kH + u] = h;
+  };
+  // the staged rows of iteration `it` (layer l at t = it - l) to act / hseq:
+  // 48 float4 per (layer, sequence) row, 6 per thread
+  auto flush = [&](int it, int p) {
+#pragma unroll
+    for (int j = 0; j < NL * kN * 48 / 256; ++j) {
+      const int e = tid + 256 * j;
+      const int l = e / (kN * 48), rem = e - l * (kN * 48);
+      const int nn = rem / 48, c4 = rem - nn * 48;
+      const int t = it - l;
+      if (t < 0 || t >= T || b0 + nn >= B) continue;
+      const float4 v = *reinterpret_cast<const float4*>(stg + ((p * NL + l) * kN + nn) * kSR + 4 * c4);
+      const int64_t row = ((int64_t)l * B + b0 + nn) * T + t;
+      float* dst = c4 < 40 ? a.act + row * (5 * kH) + 4 * c4 : a.hseq + row * kH + 4 * (c4 - 40);
+      *reinterpret_cast<float4*>(dst) = v;
+    }
   };
   auto publish = [&](int l, int t) {  // this lane's two h (units 8g + 2w, + 1) into the step-t image
     uint32_t* dst = reinterpret_cast<uint32_t*>(hbuf(l, t & 1) + n * kH + 8 * g + 2 * w);
@@ -236,15 +250,17 @@ __global__ void __launch_bounds__(256) lstm_mb_fwd_kernel(PdrnnLstmSmallFwdArgs 
 #pragma unroll
       for (int m = 0; m < 2; ++m) acc1[m] = mfma32(ahh1[m], bh1, mfma32(aih1[m], bh0, z4));
     }
+    const int p = it & 1;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) cell(0, m, t0, t0 < T, acc0[m]);
+    for (int m = 0; m < 2; ++m) cell(0, m, t0, t0 < T, acc0[m], p);
     publish(0, t0);
     if constexpr (NL == 2) {
 #pragma unroll
-      for (int m = 0; m < 2; ++m) cell(1, m, t1, t1 >= 0, acc1[m]);
+      for (int m = 0; m < 2; ++m) cell(1, m, t1, t1 >= 0, acc1[m], p);
       publish(1, t1);
     }
     lds_barrier();
+    flush(it, p);
   }
   if (a.stamps && tid == 0) {
     uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
@@ -435,7 +451,8 @@ __global__ void __launch_bounds__(256 * NL) lstm_mb_bwd_kernel(PdrnnLstmSmallBwd
 }
 
 size_t fwd_lds(int NL, int T) {
-  return sizeof(float) * ((size_t)NL * 2 * kN * kH / 2 + kN * kH) + sizeof(uint16_t) * (size_t)T * kN * kXK;
+  return sizeof(float) * ((size_t)NL * 2 * kN * kH / 2 + kN * kH) + sizeof(uint16_t) * (size_t)T * kN * kXK +
+         sizeof(float) * (size_t)2 * NL * kN * kSR;
 }
 size_t bwd_lds(int NL) { return sizeof(float) * (size_t)(2 * NL * 4 + 2 * 4) * kN * kH; }
 
