@@ -233,7 +233,7 @@ def _epoch_of(step, feats, labels, idx_list):
     return [r.clone() for r in res], replayed
 
 
-@pytest.mark.parametrize("mode", ["ddp", "horovod", "ddp-bf16", "ddp-gru"])
+@pytest.mark.parametrize("mode", ["ddp", "horovod", "ddp-bf16", "ddp-gru", "ddp-r8"])
 def test_epoch_graph_replay_matches_local(rccl_group, mode):
     """every step of an epoch (4 full batches + the short
     last one, indices as consecutive views of one tensor like the loader's)
@@ -249,7 +249,11 @@ def test_epoch_graph_replay_matches_local(rccl_group, mode):
     from pytorch_distributed_rnn_amd.train.fused_step import MotionTrainStep
     from pytorch_distributed_rnn_amd.utils.flat import flatten_module
     torch.manual_seed(5)
-    train, _, _ = synthetic_motion(n_train=448, n_validation=1, n_test=1, seed=5)
+    # ddp-r8: one rank's epoch of the 8-GPU run (6912 / 8 = 864 sequences:
+    # four batches of 180 and one of 144, the sizes the BPTT forms its own
+    # weight gradients at -- backward mode 4)
+    n_train, bs = (864, 180) if mode == "ddp-r8" else (448, 96)
+    train, _, _ = synthetic_motion(n_train=n_train, n_validation=1, n_test=1, seed=5)
     bf16 = mode.endswith("bf16")  # BASELINE config 2: weights rounded to bf16 in-kernel, graph-replayed too
     feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
     if bf16:
@@ -276,8 +280,8 @@ def test_epoch_graph_replay_matches_local(rccl_group, mode):
     g = torch.Generator().manual_seed(2)
     outs, replays = [], 0
     for e in range(5):
-        idx_list = list(torch.split(torch.randperm(448, generator=g).cuda(), 96))
-        assert [i.numel() for i in idx_list] == [96, 96, 96, 96, 64]
+        idx_list = list(torch.split(torch.randperm(n_train, generator=g).cuda(), bs))
+        assert [i.numel() for i in idx_list] == [bs] * 4 + [n_train - 4 * bs]
         if e == 4:  # ring slots out of step with the captured mapping: the copy fallback
             s1._slot = (s1._slot + 5) % s1.RING
         n0 = comm.tracked
