@@ -326,6 +326,50 @@ def test_ddp_autograd_hooks_rccl(rccl_group):
     assert ddp.comm.tracked - n0 == len(ddp.bucket_layout()) >= 2
 
 
+def test_bucket_allreduce_beside_persistent_recurrence(rccl_group):
+    """DDP bucket all-reduces (forced through RCCL on the
+    comm stream, launched by the autograd hooks while the backward is still
+    running) beside the grid-synced persistent recurrences of a 16-bit
+    H = 1024 stack at the char-LM batch.  The communicator is created with
+    maxCTAs = PDRNN_RCCL_MAX_CTAS and the persistent grids are planned on the
+    CUs that leaves (rccl_cta_reserve), so every persistent launch -- each one
+    verified here (mode 1: host check after the launch, a timeout would be
+    counted and re-run) -- keeps its co-residency: zero fallbacks."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.models.charlm import CharLM
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
+    mod = _ext.native(torch.device("cuda", 0))
+    B, T, H, V = 128, 48, 1024, 64
+    torch.manual_seed(3)
+    m = CharLM(V, 32, H, 2, 0.0, torch.bfloat16).cuda()
+    ddp = DistributedDataParallel(m, bucket_cap_mb=4, first_bucket_cap_mb=1)
+    assert mod.rccl_max_ctas() > 0 and mod.rccl_cta_reserve() == mod.rccl_max_ctas()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count - int(mod.rccl_cta_reserve())
+    assert mod.large_persist_mt(B, H, 1, 0, cus) > 0, "the persistent recurrence does not cover this shape"
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    tok = torch.randint(0, V, (B, T + 1), device="cuda")
+    old = mod.persist_verify_mode()
+    mod.set_persist_verify(1)
+    f0 = mod.persist_fallbacks()
+    n0 = ddp.comm.tracked
+    try:
+        for _ in range(3):
+            opt.zero_grad()
+            logits = ddp(tok[:, :-1])
+            loss = torch.nn.functional.cross_entropy(logits.float().reshape(-1, V), tok[:, 1:].t().reshape(-1))
+            loss.backward()
+            opt.step()
+        torch.cuda.synchronize()
+        mod.persist_check()
+    finally:
+        mod.set_persist_verify(old)
+    assert mod.persist_fallbacks() == f0 and not mod.persist_disabled()
+    nb = len(ddp.bucket_layout())
+    assert nb >= 4 and ddp.comm.tracked - n0 == 3 * nb
+    assert bool(torch.isfinite(loss))
+
+
 _WATCHDOG_CHILD = textwrap.dedent("""
     import os, sys, time, torch
     sys.path.insert(0, os.environ["PDRNN_ROOT"])
