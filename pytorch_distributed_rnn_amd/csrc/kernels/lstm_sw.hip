@@ -140,8 +140,13 @@ PDRNN_DEVICE FwdW<NC> load_fwd_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, i
 template <int NC>
 PDRNN_DEVICE void fwd_dot(const FwdW<NC>& W, const float4 (&v)[NC], float (&p)[4]) {
   pdrnn_f2 acc[4] = {{W.bias[0], 0.f}, {0.f, 0.f}, {W.bias[1], 0.f}, {0.f, 0.f}};
+#ifdef SW_PROBE_HALF_K  // timing probe only (wrong numerics): half the products
+#pragma unroll
+  for (int c = 0; c < NC / 2; ++c) {
+#else
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       acc[j] = pfma(W.w[j][2 * c], lo2(v[c]), acc[j]);
