@@ -37,4 +37,7 @@ for B in 720 360 180; do
   PDRNN_FORCE_GRAD_SYNC=1 PDRNN_FORCE_COLLECTIVE=1 timeout -k 10 180 python bench.py --steps 200 --warmup 20 --global-batch $B --epoch-sequences $E --cuda-graph > gpurun_out/${tag}_synced$B.log 2>&1 || { tail -20 gpurun_out/${tag}_synced$B.log; exit 1; }
   tail -1 gpurun_out/${tag}_synced$B.log | python tools/bench_line.py "B=$B synced-graph"
 done
+# the GRU's synced step, graph-replayed per epoch
+PDRNN_FORCE_GRAD_SYNC=1 PDRNN_FORCE_COLLECTIVE=1 timeout -k 10 180 python bench.py --cell gru --steps 200 --warmup 20 --global-batch 180 --epoch-sequences 864 --cuda-graph > gpurun_out/${tag}_synced180_gru.log 2>&1 || { tail -20 gpurun_out/${tag}_synced180_gru.log; exit 1; }
+tail -1 gpurun_out/${tag}_synced180_gru.log | python tools/bench_line.py "GRU B=180 synced-graph"
 bash tools/gpu_windows.sh ${tag}
