@@ -17,7 +17,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // the MFMA work per barrier) measured no faster at H = 32: 67-69 vs 68 us at
 // B = 1440, 16.5 vs 14.1 at B = 180 (profiles/r5/sw/sw13_dw32.log) -- the
 // kernel sits near both its HBM (~280 MB a step) and its MFMA floor at ~50 %
-// of each (profiles/r5/pmc/dw_b1440.md).
+// of each (profiles/r5/pmc/dw_b1440.md).  Twice the chunks (two workgroups
+// per CU, two MFMA waves per SIMD) is slower too: 72.8 vs 68.7 us at B = 1440,
+// 40.8 vs 37.3 at 720 (profiles/r5/sw/dw_chunks_256_vs_512.log).
 template <int H>
 constexpr int dw_rows() { return 16; }
 static_assert(dw_rows<32>() <= PDRNN_DW_PAD_ROWS, "dW stages read past the padding");
