@@ -325,7 +325,15 @@ def lstm_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Te
     from . import lstm_large
     if lstm_large.supported(x, hidden, num_layers):
         if idx is not None:
-            x = x.index_select(0 if batch_first else 1, idx)
+            if batch_first:  # gather the batch straight into the time-major layout: one launch
+                x = x.transpose(0, 1).index_select(1, idx)
+                batch_first = False
+                out, hn, cn = lstm_large.lstm_large_forward(x, weights, h0, c0, hidden=hidden,
+                                                            num_layers=num_layers, batch_first=False,
+                                                            bidirectional=bidirectional, dropout=dropout,
+                                                            training=training)
+                return (out.transpose(0, 1) if out is not None else None), hn, cn
+            x = x.index_select(1, idx)
         return lstm_large.lstm_large_forward(x, weights, h0, c0, hidden=hidden,
                                              num_layers=num_layers, batch_first=batch_first,
                                              bidirectional=bidirectional, dropout=dropout,

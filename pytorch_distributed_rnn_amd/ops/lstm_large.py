@@ -183,10 +183,13 @@ def _bias_cat(weights, ndir: int, hidden: int, device) -> Tensor:
         t = ent[1] if ent is not None else torch.empty(ndir * n4, device=device, dtype=torch.float32)
         for d in range(ndir):
             b = t[d * n4:(d + 1) * n4].view(hidden, 4)  # interleaved: [u][q] = row q*H + u
-            b.zero_()
-            for src in bs[2 * d:2 * d + 2]:
-                if src is not None:
-                    b.add_(src.detach().view(4, hidden).t())
+            srcs = [src.detach().view(4, hidden).t() for src in bs[2 * d:2 * d + 2] if src is not None]
+            if len(srcs) == 2:  # one launch: the sum written interleaved
+                torch.add(srcs[0], srcs[1], out=b)
+            elif srcs:
+                b.copy_(srcs[0])
+            else:
+                b.zero_()
     cache[key] = (ver, t)
     return t
 
@@ -847,7 +850,7 @@ def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optio
     ndir = 2 if bidirectional else 1
     per = len(weights) // (num_layers * ndir)
     seq = x.transpose(0, 1) if batch_first else x
-    seq = seq.contiguous()
+    seq = seq.contiguous()  # (a no-op for an index-gathered batch: see lstm_forward)
     B = seq.shape[1]
     if pipeline_ok(seq, hidden, num_layers, bidirectional, dropout, training):
         out, hn, cn = _PipelinedLSTMStack.apply(seq, h0, c0, (hidden, num_layers, per, pipeline_chunks(seq.shape[0])),
