@@ -439,3 +439,17 @@ def test_graphed_autograd_step_matches_eager(cell, hidden):
         assert torch.allclose(p, q, atol=3e-5, rtol=1e-4), k
     st1, st2 = t1.optimizer.state_dict(), t2.optimizer.state_dict()
     assert float(st1["state"][0]["step"]) == float(st2["state"][0]["step"]) == 2 * len(t1.train_loader)
+
+
+@pytest.mark.parametrize("T", [126, 61])
+def test_seq_in_wave_short_sequences_fall_back_from_mode4(T, monkeypatch):
+    """Backward mode 4 (the BPTT workgroups form their own weight gradients)
+    takes K steps of 4 time steps: at T % 4 != 0 the binding runs mode 2 plus
+    the dW kernel instead -- gradients against fp64 at B = 180 for such T."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    for var in ("PDRNN_SW", "PDRNN_SW_MODE", "PDRNN_SW_BWD_MODE"):
+        monkeypatch.delenv(var, raising=False)
+    torch.manual_seed(21)
+    train, _, _ = synthetic_motion(n_train=180, n_validation=2, n_test=2, seq_length=T, seed=22)
+    _fp64_check(MotionModel(9, 32, 2, 6), train, 180)
