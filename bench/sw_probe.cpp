@@ -293,7 +293,7 @@ int main(int argc, char** argv) {
     auto run_bwd = [&]() {
       if (old) CK(pdrnn_lstm_small_bwd_dwout(&bk, H, grid_old_b, nb_old_b, st));
       else if (mb) CK(pdrnn_lstm_mb_bwd(&bk, st));
-      else CK(pdrnn_lstm_sw_bwd(&bk, mode == 6 ? 3 : mode, st));  // 6: forward-only map
+      else CK(pdrnn_lstm_sw_bwd(&bk, mode == 6 ? 3 : mode == 5 ? 2 : mode, st));  // 5, 6: forward-only maps
     };
     // correctness: one forward, check; one backward, check
     CK(hipMemsetAsync(act, 0, n_act * 4, st));
@@ -415,7 +415,7 @@ int main(int argc, char** argv) {
     if (want_stamps) {
       std::vector<uint64_t> hs((size_t)B * 8);
       CK(hipMemcpy(hs.data(), stamps, hs.size() * 8, hipMemcpyDeviceToHost));
-      const int g = mode == 5 || mode == 3 || mode == 1 ? (B + 1) / 2 : B;
+      const int g = mode == 3 || mode == 1 ? (B + 1) / 2 : B;
       double lp[2] = {0, 0}, wt[2] = {0, 0}, lo = 0;
       for (int i = 0; i < g; ++i) {
         lo += (double)(hs[i * 8 + 1] - hs[i * 8 + 0]);

@@ -518,8 +518,9 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   Tensor xg;
   if (dwout) xg = at::empty({(B * T + PADR) * xg_ld + 256}, opts);  // + one DMA job past the last stage
   if (sw) { f.xg_out = xg.data_ptr<float>(); f.xg_ld = (int)xg_ld; }
-  // sequences per sequence-in-wave workgroup: two in the odd modes
-  const int sw_fnb = sw_fmode & 1 ? 2 : 1, sw_bnb = sw_bmode & 1 ? 2 : 1;
+  // sequences per sequence-in-wave workgroup: two in modes 1 / 3 (mode 5,
+  // the four-wave forward, runs one)
+  const int sw_fnb = (sw_fmode == 1 || sw_fmode == 3) ? 2 : 1, sw_bnb = (sw_bmode == 1 || sw_bmode == 3) ? 2 : 1;
   Tensor st_f, st_b;
   if (stamps_enabled()) {
     st_f = at::zeros({sw ? (B + sw_fnb - 1) / sw_fnb : (B + nb_fwd - 1) / nb_fwd, 8}, opts.dtype(at::kLong));

@@ -393,6 +393,206 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Forward, four waves per sequence (mode 5, two-layer stacks in the latency
+// regime): wave w runs layer w >> 1, units 16 (w & 1) .. + 15.  lane =
+// (unit ul = lane >> 2, K quarter q = lane & 3): a lane holds the four gate
+// rows of its unit over a quarter of the operand vector (layer 0: x | h[0,12)
+// | h[12,24) | h[24,32) + zero pad, 3 float4 chunks; layer 1: h^0[0,16) |
+// h^0[16,32) | h^1[0,16) | h^1[16,32), 4 chunks), half of mode 2's products
+// per lane.  A quad reduce-scatter (xor 2, then xor 1) leaves lane q with the
+// full pre-activation of gate q (i, f, g, o): one activation per lane; quad
+// broadcasts give every lane of the unit i, f, g, o for c and h.  The two
+// waves of a layer meet in the per-layer h slots: one barrier per step, as in
+// mode 2.
+// ---------------------------------------------------------------------------
+template <int NC>
+struct Fwd4W {
+  pdrnn_f2 w[4][2 * NC];
+};
+
+PDRNN_DEVICE float quad_bcast(float v, int k) {
+  switch (k) {
+    case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x00, 0xF, 0xF, false));
+    case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x55, 0xF, 0xF, false));
+    case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xAA, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xFF, 0xF, 0xF, false));
+  }
+}
+
+// column of layer l, quarter q, chunk c, element e (-1: zero)
+PDRNN_DEVICE int fwd4_col(int l, int q, int c, int e, int Iin, bool& from_ih) {
+  const int k = 4 * c + e;
+  if (l == 0) {
+    if (q == 0) { from_ih = true; return k < Iin ? k : -1; }
+    from_ih = false;
+    const int hk = 12 * (q - 1) + k;
+    return hk < kH ? hk : -1;
+  }
+  from_ih = q < 2;
+  return 16 * (q & 1) + k;
+}
+
+template <int NC>
+PDRNN_DEVICE Fwd4W<NC> load_fwd4_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, int q, float (&bias)[4]) {
+  Fwd4W<NC> W;
+  const int Iin = l == 0 ? a.I : kH;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = j * kH + u;
+    const float sc = kA * (j == 2 ? 2.f : 1.f);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bool ih = false;
+        const int k = fwd4_col(l, q, c, e, Iin, ih);
+        float x = 0.f;
+        if (k >= 0) x = ih ? a.w_ih[l][(int64_t)r * Iin + k] : a.w_hh[l][(int64_t)r * kH + k];
+        v[e] = wround(x, a.w_bf16) * sc;
+      }
+      W.w[j][2 * c] = pdrnn_f2{v[0], v[1]};
+      W.w[j][2 * c + 1] = pdrnn_f2{v[2], v[3]};
+    }
+    bias[j] = q == 0 ? ((a.b_ih[l] ? wround(a.b_ih[l][r], a.w_bf16) : 0.f) +
+                        (a.b_hh[l] ? wround(a.b_hh[l][r], a.w_bf16) : 0.f)) * sc
+                     : 0.f;
+  }
+  return W;
+}
+
+__global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = wv >> 1;
+  const int ul = lane >> 2, q = lane & 3;
+  const int u = 16 * (wv & 1) + ul;
+  const int B = a.B, T = a.T, I = a.I;
+  const int b = blockIdx.x;  // one sequence per workgroup
+  const int bsrc = a.idx ? (int)a.idx[b] : b;
+  float* hb = smem;                                  // [layer][parity][kHB]
+  float* xs = smem + 2 * 2 * kHB;                    // [T][kXS]
+  auto hbuf = [&](int ll, int p) { return hb + (ll * 2 + p) * kHB; };
+
+  for (int e = tid; e < 2 * 2 * kHB; e += 256) hb[e] = 0.f;
+  for (int e = tid; e < T * kXS; e += 256) {
+    const int t = e / kXS, k = e - t * kXS;
+    const float x = ldx(a.x, (int64_t)bsrc * a.x_sb + (int64_t)t * a.x_st + min(k, I - 1), a.x_bf16);
+    const float v = k < I ? x : 0.f;
+    xs[e] = v;
+    if (a.xg_out && k < a.xg_ld) a.xg_out[((int64_t)b * T + t) * a.xg_ld + k] = v;
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
+  const __amdgpu_buffer_rsrc_t r_h = uniform_rsrc(a.hseq);
+  const uint32_t vo_a = (q * kH + u) * 4, vo_c = (4 * kH + u) * 4, vo_h = u * 4;
+  const uint32_t lead = q == 0 ? 0u : kOOR;  // c / h stored by lane q = 0 of the unit
+  const pdrnn_f2 gk = q == 2 ? pdrnn_f2{2.f, -1.f} : pdrnn_f2{1.f, 0.f};
+  float cst = 0.f, hst = 0.f;
+
+  uint64_t st0 = 0, sr0 = 0;
+  if (a.stamps && tid == 0) { st0 = stamp_cycles(); sr0 = stamp_real(); }
+
+  // quad reduce-scatter of the four gate partials -> this lane's gate (q)
+  auto gate_sum = [&](const float (&p)[4]) {
+    const bool hi = q >= 2;
+    const float k0 = hi ? p[2] : p[0], k1 = hi ? p[3] : p[1];
+    const float s0 = hi ? p[0] : p[2], s1 = hi ? p[1] : p[3];
+    const float m0 = k0 + dpp_swap2(s0), m1 = k1 + dpp_swap2(s1);
+    const bool od = (q & 1) != 0;
+    return (od ? m1 : m0) + dpp_swap1(od ? m0 : m1);
+  };
+  auto cell = [&](int t, bool act, float z) {
+    const float av = fmaf(sig2(z), gk.x, gk.y);  // i, f, tanh g or o of this lane
+    const float ig = quad_bcast(av, 0), fg = quad_bcast(av, 1), gg = quad_bcast(av, 2), og = quad_bcast(av, 3);
+    const float cn = fmaf(fg, cst, ig * gg);
+    const float hn = og * tanh_c(cn);
+    cst = act ? cn : cst;
+    hst = act ? hn : hst;
+    if (q == 0) hbuf(l, t & 1)[u] = hst;
+    const uint32_t rw = __builtin_amdgcn_readfirstlane((uint32_t)((l * B + b) * T + min(max(t, 0), T - 1)));
+    const uint32_t m = act ? 0u : kOOR;
+    bstore(av, r_act, vo_a | m, rw * (5 * kH * 4));
+    bstore(cn, r_act, vo_c | m | lead, rw * (5 * kH * 4));
+    bstore(hn, r_h, vo_h | m | lead, rw * (kH * 4));
+  };
+
+  if (l == 0) {
+    float bias[4];
+    const Fwd4W<3> W = load_fwd4_w<3>(a, 0, u, q, bias);
+    for (int it = 0; it <= T; ++it) {
+      if (it < T) {
+        const int t = it;
+        const float* src = q == 0 ? xs + t * kXS : hbuf(0, (t - 1) & 1) + 12 * (q - 1);
+        float4 v[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = ld4(src + 4 * c);
+        __builtin_amdgcn_sched_barrier(0);
+        pdrnn_f2 acc[4] = {{bias[0], 0.f}, {bias[1], 0.f}, {bias[2], 0.f}, {bias[3], 0.f}};
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] = pfma(W.w[j][2 * c], lo2(v[c]), acc[j]);
+            acc[j] = pfma(W.w[j][2 * c + 1], hi2(v[c]), acc[j]);
+          }
+        float p[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] = acc[j].x + acc[j].y;
+        cell(t, true, gate_sum(p));
+      }
+      lds_barrier();
+    }
+  } else {
+    float bias[4];
+    const Fwd4W<4> W = load_fwd4_w<4>(a, 1, u, q, bias);
+    for (int it = 0; it <= T; ++it) {
+      if (it > 0) {
+        const int t = it - 1;
+        const float* src = q < 2 ? hbuf(0, t & 1) + 16 * q : hbuf(1, (t - 1) & 1) + 16 * (q - 2);
+        float4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = ld4(src + 4 * c);
+        __builtin_amdgcn_sched_barrier(0);
+        pdrnn_f2 acc[4] = {{bias[0], 0.f}, {bias[1], 0.f}, {bias[2], 0.f}, {bias[3], 0.f}};
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] = pfma(W.w[j][2 * c], lo2(v[c]), acc[j]);
+            acc[j] = pfma(W.w[j][2 * c + 1], hi2(v[c]), acc[j]);
+          }
+        float p[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] = acc[j].x + acc[j].y;
+        cell(t, true, gate_sum(p));
+      }
+      lds_barrier();
+    }
+  }
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+  }
+  // ---- epilogue: h_n / c_n; the head reads the top layer's h_T from its slot
+  if (q == 0) {
+    if (a.hn) a.hn[((int64_t)l * B + b) * kH + u] = hst;
+    if (a.cn) a.cn[((int64_t)l * B + b) * kH + u] = cst;
+  }
+  if (a.head_w) {
+    // (the last barrier of the loop ordered every h_T write before this read:
+    // layer 1's last step t = T-1 went to slot (T-1) & 1)
+    if (wv == 2) {
+      const int hu = lane >> 1;
+      motion_head(a, b, hbuf(1, (T - 1) & 1)[hu], hu, (lane & 1) != 0);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Backward (lean contract: zero initial state, dL/dh_T of the top layer only,
 // weight gradients deferred to pdrnn_lstm_small_dw)
 // ---------------------------------------------------------------------------
@@ -877,7 +1077,7 @@ int sw_cus() {
 
 size_t fwd_lds(int NL, int nb, int T) { return sizeof(float) * ((size_t)nb * NL * 2 * kHB + (size_t)nb * T * kXS); }
 size_t bwd_lds(int NL, int nb, int zr = 2) { return sizeof(float) * ((size_t)nb * NL * zr * kDZ + (size_t)nb * 2 * 32); }
-int mode_nb(int mode) { return (mode & 1) ? 2 : 1; }
+int mode_nb(int mode) { return (mode == 1 || mode == 3) ? 2 : 1; }
 
 template <int NL, int MODE>
 hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
@@ -885,6 +1085,11 @@ hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   const int grid = (a->B + NB - 1) / NB;
   const int block = MODE >= 2 ? 64 * NL : 64;
   hipLaunchKernelGGL((lstm_sw_fwd_kernel<NL, MODE>), dim3(grid), dim3(block), fwd_lds(NL, NB, a->T), st, *a);
+  return hipGetLastError();
+}
+hipError_t launch_fwd4(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
+  hipLaunchKernelGGL(lstm_sw_fwd4_kernel, dim3(a->B), dim3(256), sizeof(float) * (2 * 2 * kHB + (size_t)a->T * kXS), st,
+                     *a);
   return hipGetLastError();
 }
 template <int NL, int MODE>
@@ -908,7 +1113,9 @@ extern "C" int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell) {
 }
 
 // Measured (bench/sw_probe.cpp, profiles/r5/sw): two-layer stacks run one
-// wave per layer up to one wave per SIMD (mode 2); above, the forward keeps
+// wave per layer up to one wave per SIMD (mode 2) -- the forward two waves
+// per layer up to half a wave per SIMD (mode 5: 56.5 vs 62.0 us at B = 180,
+// 73.1 vs 81.8 at 512, slower above, profiles/r5/sw/fwd4_probe.log); above, the forward keeps
 // that map at three waves per SIMD (mode 6) and the backward takes two
 // sequences per wave (mode 3).  Up to two workgroups per CU the backward
 // forms the weight gradients itself (mode 4: two more waves per workgroup on
@@ -922,11 +1129,11 @@ extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
   if (!(e && *e) && backward) e = getenv("PDRNN_SW_MODE");
   if (e && *e) {
     const int m = atoi(e);
-    if (m >= 0 && m <= 6 && m != 5 && (m < 2 || NL == 2) && (m != 6 || !backward) && (m != 4 || backward)) return m;
+    if (m >= 0 && m <= 6 && (m < 2 || NL == 2) && (m < 5 || !backward) && (m != 4 || backward)) return m;
   }
   const int simds = 4 * sw_cus();
-  // (mode 4: four waves of <= 256 VGPRs per workgroup, two workgroups per CU)
-  if (NL == 2 && backward && 2 * B <= simds) return 4;
+  // (modes 4 / 5: four waves per workgroup, two workgroups per CU)
+  if (NL == 2 && 2 * B <= simds) return backward ? 4 : 5;
   if (NL == 2) return B <= simds ? 2 : backward ? 3 : 6;
   return B <= simds ? 0 : 1;
 }
@@ -947,6 +1154,7 @@ extern "C" hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode
   if (mode == 2) return launch_fwd<2, 2>(a, st);
   if (mode == 3) return launch_fwd<2, 3>(a, st);
   if (mode == 6) return launch_fwd<2, 6>(a, st);
+  if (mode == 5) return launch_fwd4(a, st);
   return hipErrorInvalidValue;
 }
 

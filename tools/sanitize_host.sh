@@ -16,7 +16,11 @@ unset PDRNN_SANITIZE
 export PDRNN_EXT_SO=$so
 case $flav in
   thread) rt=$(gcc -print-file-name=libtsan.so)
-          export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 report_signal_unsafe=0" ;;
+          # (die_after_fork=0: the gloo tests fork rank processes from a
+          # multi-threaded interpreter; one OpenMP thread: libgomp is not
+          # instrumented and its barriers read as races / stall the runtime)
+          export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 report_signal_unsafe=0 die_after_fork=0"
+          export OMP_NUM_THREADS=1 ;;
   *)      rt="$(gcc -print-file-name=libasan.so)"
           case $flav in *undefined*) rt="$rt:$(gcc -print-file-name=libubsan.so)";; esac
           # the interpreter and torch are not instrumented: leaks at exit are theirs
