@@ -280,6 +280,7 @@ int main(int argc, char** argv) {
   for (int mode : modes) {
     const bool old = mode == 9;
     const bool mb = mode == 7;
+    const bool rdw = mode == 4 || mode == 8;  // the backward forms the dW itself (no dz stores, no dW launch)
     const Ref& RR = mb ? Rb : R;
     const double tol = mb ? 3e-2 : 1e-4;
     const int nb_old_f = 1, sp_old_f = B > 1024 ? 2 : 1;
@@ -288,12 +289,12 @@ int main(int argc, char** argv) {
     auto run_fwd = [&]() {
       if (old) CK(pdrnn_lstm_small_fwd(&f, H, nb_old_f, sp_old_f, 1, st));
       else if (mb) CK(pdrnn_lstm_mb_fwd(&f, st));
-      else CK(pdrnn_lstm_sw_fwd(&f, mode == 4 ? 2 : mode, st));  // 4: backward-only map
+      else CK(pdrnn_lstm_sw_fwd(&f, mode == 4 ? 2 : mode == 8 ? 5 : mode, st));  // 4: backward-only map
     };
     auto run_bwd = [&]() {
       if (old) CK(pdrnn_lstm_small_bwd_dwout(&bk, H, grid_old_b, nb_old_b, st));
       else if (mb) CK(pdrnn_lstm_mb_bwd(&bk, st));
-      else CK(pdrnn_lstm_sw_bwd(&bk, mode == 6 ? 3 : mode == 5 ? 2 : mode, st));  // 5, 6: forward-only maps
+      else CK(pdrnn_lstm_sw_bwd(&bk, mode == 6 ? 3 : mode == 8 ? 5 : mode == 5 ? 2 : mode, st));  // 8: fwd 5 + bwd 5
     };
     // correctness: one forward, check; one backward, check
     CK(hipMemsetAsync(act, 0, n_act * 4, st));
@@ -351,11 +352,11 @@ int main(int argc, char** argv) {
     run_bwd();
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(h_act.data(), act, n_act * 4, hipMemcpyDeviceToHost));
-    const double e_dz = mode == 4 ? 0.0 : maxrel(h_act, RR.dz, rows, 5 * H, 4 * H, 4 * H);  // (4: no dz stores)
+    const double e_dz = rdw ? 0.0 : maxrel(h_act, RR.dz, rows, 5 * H, 4 * H, 4 * H);  // (4: no dz stores)
     // the summed weight gradients (slab rows), against the first mode's
     {
       int nrows = B;
-      if (mode != 4) {
+      if (!rdw) {
         CK(pdrnn_lstm_small_dw(&dw, H, st));
         nrows = chunks;
       }
@@ -372,14 +373,14 @@ int main(int argc, char** argv) {
       printf("  dW sum vs first mode: max rel %.2e\n", mx > 0 ? err / mx : err);
     }
     // timing
-    for (int w = 0; w < 3; ++w) { run_fwd(); run_bwd(); if (mode != 4) CK(pdrnn_lstm_small_dw(&dw, H, st)); }
+    for (int w = 0; w < 3; ++w) { run_fwd(); run_bwd(); if (!rdw) CK(pdrnn_lstm_small_dw(&dw, H, st)); }
     CK(hipEventRecord(e0, st));
     for (int r = 0; r < reps; ++r) run_fwd();
     CK(hipEventRecord(e1, st));
     for (int r = 0; r < reps; ++r) run_bwd();
     CK(hipEventRecord(e2, st));
     for (int r = 0; r < reps; ++r)
-      if (mode != 4) CK(pdrnn_lstm_small_dw(&dw, H, st));
+      if (!rdw) CK(pdrnn_lstm_small_dw(&dw, H, st));
     CK(hipEventRecord(e3, st));
     CK(hipEventSynchronize(e3));
     float tf = 0, tb = 0, tw = 0;
@@ -390,7 +391,7 @@ int main(int argc, char** argv) {
            mode, old ? " (lstm_small)" : mb ? " (bf16 mfma)" : "", uf, uf * 2400.0 / (T + NL - 1), ub,
            ub * 2400.0 / (T + NL - 1), uw, e_act, e_h, e_dht, e_dz,
            (e_act < tol && e_h < tol && e_dht < tol && e_dz < tol) ? "OK" : "MISMATCH");
-    if (mode != 4 && getenv("PROBE_OVERLAP")) {
+    if (!rdw && getenv("PROBE_OVERLAP")) {
       // the backward and the dW kernel side by side on two streams (timing
       // only: the dW reads the previous backward's gate gradients)
       static hipStream_t st2 = nullptr;

@@ -471,7 +471,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
                   pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T) != 0 && T <= 640;
   const int sw_fmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 0) : -1;
   int sw_bmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 1) : -1;
-  if (sw_bmode == 4 && T % 4) sw_bmode = 2;  // register dW: whole 4-step K steps
+  if ((sw_bmode == 4 || sw_bmode == 5) && T % 4) sw_bmode = 2;  // register dW: whole 4-step K steps
   // Above one residency round the BPTT defers its weight gradients: the
   // recurrence writes the gate gradients (into `act`, in place) and the
   // matrix-core kernel lstm_small_dw forms dW / db over all B*T rows, one slab
@@ -484,7 +484,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const int nb_dw = dwout ? pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B) : (int)nb_bwd;
   // (sequence-in-wave mode 4: the BPTT waves form dW on the matrix cores, one
   // slab row per sequence, no dW launch)
-  const bool sw_rdw = sw && sw_bmode == 4;
+  const bool sw_rdw = sw && (sw_bmode == 4 || sw_bmode == 5);
   const int slab_rows = sw_rdw ? (int)B : dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
   Tensor slab = at::empty({slab_rows, L.P}, opts);
 
