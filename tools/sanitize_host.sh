@@ -16,10 +16,12 @@ unset PDRNN_SANITIZE
 export PDRNN_EXT_SO=$so
 case $flav in
   thread) rt=$(gcc -print-file-name=libtsan.so)
-          # (die_after_fork=0: the gloo tests fork rank processes from a
+          # (report_mutex_bugs=0: the interpreter's and torch's static
+          # destructors unlock already-destroyed mutexes at exit; data races are
+          # still reported.  die_after_fork=0: the gloo tests fork rank processes from a
           # multi-threaded interpreter; one OpenMP thread: libgomp is not
           # instrumented and its barriers read as races / stall the runtime)
-          export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 report_signal_unsafe=0 die_after_fork=0 suppressions=$PWD/tools/tsan.supp"
+          export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 report_signal_unsafe=0 die_after_fork=0 report_mutex_bugs=0 suppressions=$PWD/tools/tsan.supp"
           export OMP_NUM_THREADS=1 ;;
   *)      rt="$(gcc -print-file-name=libasan.so)"
           case $flav in *undefined*) rt="$rt:$(gcc -print-file-name=libubsan.so)";; esac
