@@ -652,8 +652,11 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
   constexpr bool SPLIT = MODE >= 2;
   // mode 4: the mode-2 map plus two waves that accumulate the weight
   // gradients on the matrix cores (no gate-gradient stores, no dW launch);
-  // mode 5: the same with two BPTT waves per layer (the four-wave forward's
-  // lane map: unit x row quarter), layer 0 two steps behind layer 1
+  // mode 5 (opt-in, PDRNN_SW_BWD_MODE=5): the same with two BPTT waves per
+  // layer (the four-wave forward's lane map: unit x row quarter), layer 0 two
+  // steps behind layer 1 -- correct but slower: 92.7 vs 55.3 us at B = 180
+  // (1,724 cycles a step: the column phase now waits behind the barrier for
+  // the other wave's dz; profiles/r5/sw/bwd5_probe.log)
   constexpr bool DWACC = MODE == 4 || MODE == 5;
   constexpr bool W4 = MODE == 5;
   constexpr int ZR = DWACC ? 8 : 2;  // dz slots per (sequence, layer): a ring that holds a dW K step
