@@ -168,14 +168,26 @@ class _LinearNarrow(torch.autograd.Function):
         ctx.save_for_backward(x2, w16)
         ctx.has_bias = bias is not None
         ctx.shp = shp
+        from . import gradsink
+        ctx.params = (weight, bias)  # (gradsink: the backward may accumulate into their .grad)
+        ctx.direct = gradsink.enabled()
         return y.view(*shp[:-1], w16.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
+        from . import gradsink
         x2, w16 = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype).contiguous()
         o16 = x2.dtype != torch.float32
         dx = gemm_f32(dy2, False, w16, True, out16=o16)[0].view(ctx.shp) if ctx.needs_input_grad[0] else None
+        sw, sb = gradsink.sink(ctx.params[0], ctx.direct), gradsink.sink(ctx.params[1], ctx.direct)
+        if sw is not None and (not ctx.has_bias or sb is not None):
+            # direct mode: dW accumulated into the flat gradient view by the GEMM
+            # epilogue, db (its row sums) added: nothing for autograd to add
+            _, rs = gemm_f32(dy2, True, x2, True, rowsum=ctx.has_bias, out=sw, accumulate=True)
+            if ctx.has_bias:
+                sb.add_(rs)
+            return dx, None, None
         dw = db = None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dw, db = gemm_f32(dy2, True, x2, True, rowsum=ctx.has_bias)

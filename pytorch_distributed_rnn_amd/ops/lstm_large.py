@@ -29,6 +29,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
+from . import gradsink
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
@@ -571,6 +572,8 @@ class _PipelinedLSTMStack(torch.autograd.Function):
         ctx.save_for_backward(x, *hseq, *cseq, *acts, *[shadow(w[0], "p", f32, H) for w in lw],
                               *[shadow(w[1], "t", f32, H) for w in lw])
         ctx.states = (h0s, c0s)
+        ctx.params = lw  # (gradsink: the backward may accumulate into their .grad itself)
+        ctx.direct = gradsink.enabled()
         ctx.cfg = (H, L, per, chunks, [[w is not None for w in ws] for ws in lw],
                    h0.dtype if h0 is not None else None, c0.dtype if c0 is not None else None)
         return hseq[L - 1], hn, cn
@@ -595,8 +598,13 @@ class _PipelinedLSTMStack(torch.autograd.Function):
         dhn_l = [dhn[l].float().contiguous() if dhn is not None else None for l in range(L)]
         dcn_l = [dcn[l].float().contiguous() if dcn is not None else None for l in range(L)]
         ins = [x] + list(hseq[:-1])  # each layer's input sequence
-        dwih = [x.new_empty(4 * H, t.shape[2]) for t in ins]
-        dwhh = [x.new_empty(4 * H, H) for _ in range(L)]
+        # direct mode (ops/gradsink.py): a layer whose w_ih / w_hh (and biases)
+        # all have flat .grad views accumulates into them in the GEMM epilogue
+        sinks = [[gradsink.sink(w, ctx.direct) for w in ctx.params[l]] for l in range(L)]
+        direct = [all(sk is not None for sk, w in zip(sinks[l], ctx.params[l]) if w is not None)
+                  for l in range(L)]
+        dwih = [sinks[l][0] if direct[l] else x.new_empty(4 * H, t.shape[2]) for l, t in enumerate(ins)]
+        dwhh = [sinks[l][1] if direct[l] else x.new_empty(4 * H, H) for l in range(L)]
         db = [x.new_empty(4 * H) for _ in range(L)]
         rec = pipeline_streams(dev, L)
 
@@ -612,7 +620,12 @@ class _PipelinedLSTMStack(torch.autograd.Function):
                                     cseq[l], acts[l], c0s[l], dgates[l], dhb[l], dcb[l], carry[l], t0, t1, 0)
 
         def finish(l):  # the layer's recurrence is done: its weight gradients, on its stream
-            _chunk_weight_grads(dwih[l], dwhh[l], db[l], dgates[l], hseq[l], h0s[l], ins[l], 0, T, True)
+            _chunk_weight_grads(dwih[l], dwhh[l], db[l], dgates[l], hseq[l], h0s[l], ins[l], 0, T, not direct[l],
+                                db_first=True)
+            if direct[l]:
+                for bg in sinks[l][2:4]:
+                    if bg is not None:
+                        bg.add_(db[l])
 
         pipeline_backward(rec, chunks, project, recur, finish)
         dx = None
@@ -621,6 +634,9 @@ class _PipelinedLSTMStack(torch.autograd.Function):
         pipeline_join(rec)
         grads: List[Optional[Tensor]] = []
         for l in range(L):
+            if direct[l]:  # already accumulated into the parameters' .grad
+                grads += [None, None] + ([None, None] if per == 4 else [])
+                continue
             grads += [dwih[l], dwhh[l]]
             if per == 4:
                 grads += [db[l] if has_w[l][2] else None, db[l] if has_w[l][3] else None]
@@ -811,7 +827,7 @@ def padded_cols(x2: Tensor, mult: int = 32) -> Tensor:
 
 
 def _chunk_weight_grads(dwih: Tensor, dwhh: Tensor, db: Tensor, G3: Tensor, hd: Tensor, h0: Optional[Tensor],
-                        xin: Tensor, t0: int, t1: int, first: bool) -> None:
+                        xin: Tensor, t0: int, t1: int, first: bool, db_first: Optional[bool] = None) -> None:
     """Steps [t0, t1) of one unidirectional fp32 layer's dW_ih, dW_hh and db,
     written (first chunk) or accumulated into the fp32 outputs: dW_hh pairs
     dgates_t with h_{t-1} (h0 at t = 0), dW_ih dgates_t with the layer input,
@@ -833,7 +849,7 @@ def _chunk_weight_grads(dwih: Tensor, dwhh: Tensor, db: Tensor, G3: Tensor, hd: 
         dwih.copy_(c[:, :x2.shape[1]]) if first else dwih.add_(c[:, :x2.shape[1]])
     else:
         _, rs = gemm_f32(G3[t0:t1].view(-1, H4), True, x2, True, rowsum=True, out=dwih, accumulate=not first)
-    if first:
+    if first if db_first is None else db_first:
         db.copy_(rs)
     else:
         db.add_(rs)

@@ -32,6 +32,7 @@ from typing import Callable, List, Optional, Tuple
 import torch
 from torch import Tensor, nn
 
+from ..ops import gradsink
 from ..data.loader import DeviceBatchLoader, ShardedSampler
 from ..ops.adam import FusedAdam
 from ..ops.xent import CrossEntropyLoss
@@ -309,6 +310,14 @@ class Trainer:
                                                          cuda_graph=self.cuda_graph, comm=self._grad_comm())
         return self._fused
 
+    def _direct_grads_ok(self) -> bool:
+        """The in-tree Functions may accumulate weight gradients straight into
+        the flat .grad views (ops/gradsink.py): one process and no forced
+        collectives -- nothing observes the per-parameter accumulation."""
+        if self.device.type != "cuda" or self.world_size() != 1:
+            return False
+        return not any(os.environ.get(k, "0") == "1" for k in ("PDRNN_FORCE_COLLECTIVE", "PDRNN_FORCE_GRAD_SYNC"))
+
     def _graphed_step(self):
         """The autograd step replayed from a HIP graph (train/graphed_step.py),
         or None (not requested, multi-process, CPU, other optimizers)."""
@@ -342,13 +351,14 @@ class Trainer:
                 logging.warning("graph capture of the training step failed, running it eagerly: %s", e)
                 self._graphed = None
         self.optimizer.zero_grad()
-        with trace_range("pdrnn.forward"):
-            output, labels = self._forward(batch)
-            labels = labels.long().reshape(-1)
-            loss = self.loss_fn(output, labels)
-            stats = self.loss_fn.last_stats
-        with trace_range("pdrnn.backward"):
-            loss.backward()
+        with gradsink.direct_grads(self._direct_grads_ok()):
+            with trace_range("pdrnn.forward"):
+                output, labels = self._forward(batch)
+                labels = labels.long().reshape(-1)
+                loss = self.loss_fn(output, labels)
+                stats = self.loss_fn.last_stats
+            with trace_range("pdrnn.backward"):
+                loss.backward()
         with trace_range("pdrnn.optimizer"):
             self.optimizer.step()
         return stats, labels.shape[0]

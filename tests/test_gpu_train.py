@@ -453,3 +453,43 @@ def test_seq_in_wave_short_sequences_fall_back_from_mode4(T, monkeypatch):
     torch.manual_seed(21)
     train, _, _ = synthetic_motion(n_train=180, n_validation=2, n_test=2, seq_length=T, seed=22)
     _fp64_check(MotionModel(9, 32, 2, 6), train, 180)
+
+
+@pytest.mark.parametrize("cell", ["lstm"])
+def test_direct_grads_match_autograd_accumulation(cell):
+    """fp32 H = 128 motion model on the autograd path: the stacked-layer
+    pipeline and the narrow head accumulating their weight gradients straight
+    into the flat .grad views (ops/gradsink.py, single process) against the
+    same steps with autograd adding returned gradients -- equal parameters
+    after a few steps and equal gradients of one backward."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.ops import gradsink
+    from pytorch_distributed_rnn_amd.train.trainer import Trainer
+    torch.manual_seed(6)
+    train, _, _ = synthetic_motion(n_train=160, n_validation=2, n_test=2, seed=9)
+    m1 = MotionModel(9, 128, 2, 6, cell=cell)
+    m2 = copy.deepcopy(m1)
+    t1 = Trainer(m1, train, batch_size=64, learning_rate=2.5e-3, device=torch.device("cuda"))
+    t2 = Trainer(m2, train, batch_size=64, learning_rate=2.5e-3, device=torch.device("cuda"))
+    t1._fused = t2._fused = None
+    assert t1._direct_grads_ok()
+    t2._direct_grads_ok = lambda: False
+    for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
+        s1, _ = t1.train_batch(x1)
+        s2, _ = t2.train_batch(x2)
+        assert abs(float(s1[0]) - float(s2[0])) < 1e-5
+    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=1e-6, rtol=1e-5), k
+    # the Functions wrote the flat views themselves: with direct mode on, a
+    # backward leaves exactly the reference gradient in them
+    x = next(iter(t1.train_loader))
+    grads = []
+    for on in (True, False):
+        t1.optimizer.zero_grad()
+        with gradsink.direct_grads(on):
+            out, lab = t1._forward(x)
+            t1.loss_fn(out, lab.long().reshape(-1)).backward()
+        grads.append([p.grad.clone() for p in m1.parameters()])
+    for (k, _), g1, g2 in zip(m1.named_parameters(), *grads):
+        assert torch.allclose(g1, g2, atol=1e-7, rtol=1e-5), k
