@@ -564,11 +564,8 @@ class _PipelinedLSTMStack(torch.autograd.Function):
 
         pipeline_forward(rec, chunks, project, recur)
         pipeline_join(rec)
-        hn = x.new_empty(L, B, H)
-        cn = x.new_empty(L, B, H)
-        for l in range(L):
-            hn[l].copy_(hseq[l][T - 1])
-            cn[l].copy_(cseq[l][T - 1])
+        hn = torch.stack([hq[T - 1] for hq in hseq])  # (one launch each instead of L copies)
+        cn = torch.stack([cq[T - 1] for cq in cseq])
         ctx.save_for_backward(x, *hseq, *cseq, *acts, *[shadow(w[0], "p", f32, H) for w in lw],
                               *[shadow(w[1], "t", f32, H) for w in lw])
         ctx.states = (h0s, c0s)
@@ -623,9 +620,14 @@ class _PipelinedLSTMStack(torch.autograd.Function):
             _chunk_weight_grads(dwih[l], dwhh[l], db[l], dgates[l], hseq[l], h0s[l], ins[l], 0, T, not direct[l],
                                 db_first=True)
             if direct[l]:
-                for bg in sinks[l][2:4]:
-                    if bg is not None:
-                        bg.add_(db[l])
+                bi, bh = sinks[l][2], sinks[l][3]
+                if bi is not None and bh is not None and bh.data_ptr() == bi.data_ptr() + bi.numel() * 4:
+                    # b_ih, b_hh adjacent in the flat gradient: one launch for both
+                    torch.as_strided(bi, (2, bi.numel()), (bi.numel(), 1)).add_(db[l])
+                else:
+                    for bg in (bi, bh):
+                        if bg is not None:
+                            bg.add_(db[l])
 
         pipeline_backward(rec, chunks, project, recur, finish)
         dx = None
