@@ -132,24 +132,46 @@ def main(argv=None):
             yield from loader.batch_indices()
             epoch += 1
 
+    # PDRNN_BENCH_TRACE=1: where the wall time of a timed run goes (stderr):
+    # host time to the first step's launch, host enqueue time, device time
+    # between events bracketing the run, the final synchronize and barrier
+    trace = os.environ.get("PDRNN_BENCH_TRACE") == "1" and dev.type == "cuda"
+
     def timed_run(batches, per_step=False):
         env.barrier()
         if dev.type == "cuda":
             torch.cuda.synchronize()
         t0 = time.perf_counter()
+        if trace:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            t_first = None
         stats = None
         # one trainer call per epoch's worth of steps (the multi-GPU fused
         # step replays them from one HIP graph, like the CLI's epoch loop)
         if per_step:
             for b in batches:
                 stats, _ = trainer.train_batch(loader.make_batch(b))
+                if trace and t_first is None:
+                    t_first = time.perf_counter() - t0
         for k in range(0, 0 if per_step else len(batches), steps_per_epoch):
             res = trainer.train_batches([loader.make_batch(b) for b in batches[k:k + steps_per_epoch]])
             stats = res[-1][0]
+            if trace and t_first is None:
+                t_first = time.perf_counter() - t0
+        if trace:
+            t_enq = time.perf_counter() - t0
+            ev[1].record()
         if dev.type == "cuda":
             torch.cuda.synchronize()
+        t_sync = time.perf_counter() - t0
         env.barrier()
-        return _max_over_ranks(time.perf_counter() - t0, dev), stats
+        elapsed = time.perf_counter() - t0
+        if trace:
+            print(f"[bench trace] steps {len(batches)} wall {elapsed * 1e3:.3f} ms: first epoch enqueued "
+                  f"{t_first * 1e3:.3f}, all enqueued {t_enq * 1e3:.3f}, synced {t_sync * 1e3:.3f}; "
+                  f"device events {ev[0].elapsed_time(ev[1]):.3f} ms", file=sys.stderr, flush=True)
+        return _max_over_ranks(elapsed, dev), stats
 
     trainer.model.train()
     # one-time device setup (kernel code-object load, workspace sizing): the

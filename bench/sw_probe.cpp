@@ -4,9 +4,10 @@
 // seconds and runs on a fresh GPU box without the torch import.
 //
 //   bench/sw_probe.sh            (build + run: B=180 and 1440, every mode)
-//   sw_probe B [reps] [modes...]  mode 0-3, 6 = sequence-in-wave (lstm_sw.hip), 7 = bf16
-//                                 matrix-core (lstm_mb.hip, vs a bf16-weight reference),
+//   sw_probe B [reps] [modes...]  mode 0-3, 6 = sequence-in-wave (lstm_sw.hip),
 //                                 9 = lstm_small (gate-split / K-split family)
+//   (mode 7, the bf16 matrix-core recurrence lstm_mb.hip, was removed in round 6:
+//   1.2-3.3x slower than these fp32 VALU kernels, docs/DESIGN.md §2b)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -279,7 +280,7 @@ int main(int argc, char** argv) {
   printf("B=%d T=%d NL=%d CUs=%d reps=%d\n", B, T, NL, cus, reps);
   for (int mode : modes) {
     const bool old = mode == 9;
-    const bool mb = mode == 7;
+    const bool mb = false;
     const bool rdw = mode == 4 || mode == 8;  // the backward forms the dW itself (no dz stores, no dW launch)
     const Ref& RR = mb ? Rb : R;
     const double tol = mb ? 3e-2 : 1e-4;
@@ -288,13 +289,11 @@ int main(int argc, char** argv) {
     const int grid_old_b = old ? pdrnn_lstm_small_bwd_dwout_grid(H, NL, T, B, nb_old_b) : 0;
     auto run_fwd = [&]() {
       if (old) CK(pdrnn_lstm_small_fwd(&f, H, nb_old_f, sp_old_f, 1, st));
-      else if (mb) CK(pdrnn_lstm_mb_fwd(&f, st));
       else CK(pdrnn_lstm_sw_fwd(&f, mode == 4 ? 2 : mode == 8 ? 5 : mode, st));  // 4: backward-only map
     };
     auto run_bwd = [&]() {
       if (old) CK(pdrnn_lstm_small_bwd_dwout(&bk, H, grid_old_b, nb_old_b, st));
-      else if (mb) CK(pdrnn_lstm_mb_bwd(&bk, st));
-      else CK(pdrnn_lstm_sw_bwd(&bk, mode == 6 ? 3 : mode == 8 ? 5 : mode == 5 ? 2 : mode, st));  // 8: fwd 5 + bwd 5
+      else CK(pdrnn_lstm_sw_bwd(&bk, mode == 6 ? 3 : mode == 8 ? 4 : mode == 5 ? 2 : mode, st));  // 8: fwd 5 + bwd 4
     };
     // correctness: one forward, check; one backward, check
     CK(hipMemsetAsync(act, 0, n_act * 4, st));

@@ -14,7 +14,6 @@ if [ "$1" = build ]; then
   # the gate-split family only when its source changed
   # SW_SRC: an alternative lstm_sw.hip (A/B against another revision)
   /opt/rocm/bin/hipcc -c $FL -mllvm -amdgpu-mfma-vgpr-form=1 ${SW_SRC:-$K/lstm_sw.hip} -o $OUT/lstm_sw.o 2>/dev/null &
-  /opt/rocm/bin/hipcc -c $FL $K/lstm_mb.hip -o $OUT/lstm_mb.o 2>/dev/null &
   for f in lstm_small lstm_small_dw; do
     if [ ! -f $OUT/$f.o ] || [ $K/$f.hip -nt $OUT/$f.o ]; then
       /opt/rocm/bin/hipcc -c -O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics \

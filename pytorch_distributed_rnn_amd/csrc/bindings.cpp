@@ -467,11 +467,14 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   // Sequence-in-wave kernels (lstm_sw.hip: a sequence's recurrence never
   // leaves its wave) for the motion shape; PDRNN_SW=0 keeps the gate-split /
   // K-split family below (A/B).  Weight gradients deferred to lstm_small_dw.
+  // (their act / hseq byte offsets are 32-bit buffer offsets under one
+  // 2 GiB descriptor: larger batches take the per-sequence-rebased family)
   const bool sw = sw_enabled() && pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, (int)cell) == 1 &&
-                  pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T) != 0 && T <= 640;
+                  pdrnn_lstm_small_dwout_ok((int)H, (int)NL, (int)T) != 0 && T <= 640 &&
+                  pdrnn_lstm_sw_fits((int)NL, (int)B, (int)T) == 1;
   const int sw_fmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 0) : -1;
   int sw_bmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 1) : -1;
-  if ((sw_bmode == 4 || sw_bmode == 5) && T % 4) sw_bmode = 2;  // register dW: whole 4-step K steps
+  if (sw_bmode == 4 && T % 4) sw_bmode = 2;  // register dW: whole 4-step K steps
   // Above one residency round the BPTT defers its weight gradients: the
   // recurrence writes the gate gradients (into `act`, in place) and the
   // matrix-core kernel lstm_small_dw forms dW / db over all B*T rows, one slab
@@ -484,7 +487,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const int nb_dw = dwout ? pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B) : (int)nb_bwd;
   // (sequence-in-wave mode 4: the BPTT waves form dW on the matrix cores, one
   // slab row per sequence, no dW launch)
-  const bool sw_rdw = sw && (sw_bmode == 4 || sw_bmode == 5);
+  const bool sw_rdw = sw && sw_bmode == 4;
   const int slab_rows = sw_rdw ? (int)B : dwout ? pdrnn_lstm_small_dw_chunks((int)H, (int)NL, (int)B, (int)T) : gridb;
   Tensor slab = at::empty({slab_rows, L.P}, opts);
 
@@ -520,7 +523,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   if (sw) { f.xg_out = xg.data_ptr<float>(); f.xg_ld = (int)xg_ld; }
   // sequences per sequence-in-wave workgroup: two in modes 1 / 3 (mode 5,
   // the four-wave forward, runs one)
-  const int sw_fnb = (sw_fmode == 1 || sw_fmode == 3) ? 2 : 1, sw_bnb = (sw_bmode == 1 || sw_bmode == 3) ? 2 : 1;
+  const int sw_fnb = sw ? pdrnn_lstm_sw_nb(sw_fmode) : 1, sw_bnb = sw ? pdrnn_lstm_sw_nb(sw_bmode) : 1;
   Tensor st_f, st_b;
   if (stamps_enabled()) {
     st_f = at::zeros({sw ? (B + sw_fnb - 1) / sw_fnb : (B + nb_fwd - 1) / nb_fwd, 8}, opts.dtype(at::kLong));
@@ -1112,138 +1115,6 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
   return {dgates, dh0, dc0};
 }
 
-// ---------------------------------------------------------------------------
-// Step ranges of a unidirectional 16-bit layer on the persistent kernels, into
-// preallocated full-length tensors (ops/lstm_large.py _PipelinedLSTMStack16:
-// layer l + 1 runs chunk c while layer l runs chunk c + 1, each grid planned
-// for half the CUs so two co-reside).  `sync` (int32 [large_persist_sync_len])
-// is zeroed before a layer's first range and carries the per-step counters
-// across its ranges.  A grid that cannot launch runs the range on the
-// per-step kernels; a grid-sync timeout sets the device's sticky flag (the
-// trainers' persistent-path checks).  Returns true when the persistent kernel ran.
-int64_t large_persist_sync_len(int64_t B, int64_t mt) { return (B + 16 * mt - 1) / (16 * mt) + 4; }
-
-int* persist_sticky_ptr(const at::TensorOptions& opts) {
-  int dev = 0;
-  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
-  TORCH_CHECK(dev >= 0 && dev < 64, "device index");
-  std::vector<Tensor>& sticky = persist_sticky();
-  if (!sticky[dev].defined()) {
-    sticky[dev] = at::zeros({1}, opts.dtype(at::kInt));
-    persist_sticky_host()[dev] = pinned_word();
-  }
-  return sticky[dev].data_ptr<int>();
-}
-
-bool lstm_large_fwd_range(const Tensor& xp, const Tensor& w, const optional<Tensor>& h0, const optional<Tensor>& c0,
-                          const Tensor& hseq, const Tensor& cseq, const Tensor& acts, int64_t H, int64_t s0,
-                          int64_t s1, const Tensor& sync, int64_t mt) {
-  CHECK_HIP_TENSOR(xp);
-  const c10::DeviceGuard guard(xp.device());
-  const int dt = large_dtype(xp);
-  TORCH_CHECK(dt != 2, "16-bit storage");
-  const int64_t T = xp.size(0), B = xp.size(1);
-  TORCH_CHECK(xp.is_contiguous() && xp.size(2) == 4 * H, "xp [T, B, 4H] contiguous");
-  TORCH_CHECK(w.is_contiguous() && w.size(0) == 4 * H && w.size(1) == H && large_dtype(w) == dt, "w [4H, H]");
-  TORCH_CHECK(hseq.is_contiguous() && hseq.numel() == T * B * H && large_dtype(hseq) == dt, "hseq [T, B, H]");
-  TORCH_CHECK(cseq.is_contiguous() && cseq.numel() == T * B * H && cseq.scalar_type() == at::kFloat, "cseq f32");
-  TORCH_CHECK(acts.is_contiguous() && acts.numel() == T * B * 4 * H && large_dtype(acts) == dt, "acts");
-  TORCH_CHECK(0 <= s0 && s0 < s1 && s1 <= T, "step range");
-  TORCH_CHECK(sync.is_contiguous() && sync.scalar_type() == at::kInt && sync.numel() >= large_persist_sync_len(B, mt),
-              "sync int32");
-  const bool has_h0 = h0.has_value() && h0->defined(), has_c0 = c0.has_value() && c0->defined();
-  if (has_h0) TORCH_CHECK(h0->is_contiguous() && large_dtype(*h0) == dt && h0->numel() == B * H, "h0 [1, B, H]");
-  if (has_c0) TORCH_CHECK(c0->is_contiguous() && c0->scalar_type() == at::kFloat && c0->numel() == B * H, "c0");
-  PdrnnLstmLargeStepArgs a{};
-  a.B = (int)B; a.H = (int)H; a.T = (int)T;
-  a.s0 = (int)s0; a.s1 = (int)s1;
-  PdrnnLstmLargeDir& d = a.dir[0];
-  d.w = eptr(w);
-  d.xp = eptr(xp); d.xp_sb = 4 * H; d.xp_st = B * 4 * H;
-  d.h0 = has_h0 ? eptr(*h0) : nullptr;
-  d.c0 = has_c0 ? c0->data_ptr<float>() : nullptr;
-  d.hseq = eptrm(hseq); d.hseq_sb = H; d.hseq_st = B * H;
-  d.cseq = cseq.data_ptr<float>();
-  d.acts = eptrm(acts);
-  hipStream_t st = cur_stream();
-  int* cnt = sync.data_ptr<int>();
-  const int nmb = (int)((B + 16 * mt - 1) / (16 * mt));
-  if (mt >= 1 && !g_persist_disabled.load() &&
-      pdrnn_lstm_large_persist(&a, 1, 0, dt, (int)mt, cnt, cnt + nmb, persist_sticky_ptr(xp.options()), 0, st) ==
-          hipSuccess)
-    return true;
-  (void)hipGetLastError();
-  for (int64_t s = s0; s < s1; ++s) {
-    a.step = (int)s;
-    HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, 1, 0, dt, -1, st));
-  }
-  return false;
-}
-
-bool lstm_large_bwd_range(const optional<Tensor>& dout, const optional<Tensor>& dhn, const optional<Tensor>& dcn,
-                          const Tensor& wt, const Tensor& cseq, const Tensor& acts, const optional<Tensor>& c0,
-                          const Tensor& dgates, const Tensor& carry, const Tensor& dh0, const Tensor& dc0, int64_t H,
-                          int64_t s0, int64_t s1, const Tensor& sync, int64_t mt) {
-  CHECK_HIP_TENSOR(acts);
-  const c10::DeviceGuard guard(acts.device());
-  const int dt = large_dtype(acts);
-  TORCH_CHECK(dt != 2, "16-bit storage");
-  TORCH_CHECK(acts.is_contiguous() && acts.dim() == 4 && acts.size(0) == 1 && acts.size(3) == 4 * H, "acts [1, T, B, 4H]");
-  const int64_t T = acts.size(1), B = acts.size(2);
-  TORCH_CHECK(wt.is_contiguous() && wt.size(0) == H && wt.size(1) == 4 * H && large_dtype(wt) == dt, "wt [H, 4H]");
-  TORCH_CHECK(cseq.is_contiguous() && cseq.numel() == T * B * H && cseq.scalar_type() == at::kFloat, "cseq f32");
-  TORCH_CHECK(dgates.is_contiguous() && dgates.numel() == T * B * 4 * H && large_dtype(dgates) == dt, "dgates");
-  for (const Tensor* t : {&carry, &dh0, &dc0})
-    TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kFloat && t->numel() == B * H, "carry / dh0 / dc0 f32");
-  TORCH_CHECK(0 <= s0 && s0 < s1 && s1 <= T, "step range");
-  TORCH_CHECK(sync.is_contiguous() && sync.scalar_type() == at::kInt && sync.numel() >= large_persist_sync_len(B, mt),
-              "sync int32");
-  const bool has_dout = dout.has_value() && dout->defined();
-  if (has_dout) TORCH_CHECK(dout->is_contiguous() && large_dtype(*dout) == dt && dout->numel() == T * B * H, "dout");
-  auto f32p = [&](const optional<Tensor>& t) -> const float* {
-    if (!(t.has_value() && t->defined())) return nullptr;
-    TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kFloat && t->numel() == B * H, "f32 [1, B, H] state");
-    return t->data_ptr<float>();
-  };
-  PdrnnLstmLargeStepArgs a{};
-  a.B = (int)B; a.H = (int)H; a.T = (int)T;
-  a.s0 = (int)s0; a.s1 = (int)s1;
-  PdrnnLstmLargeDir& d = a.dir[0];
-  d.wt = eptr(wt);
-  d.c0 = f32p(c0);
-  d.cseq = cseq.data_ptr<float>();
-  d.acts = eptrm(acts);
-  d.dgates = eptrm(dgates);
-  if (has_dout) { d.dout = eptr(*dout); d.dout_sb = H; d.dout_st = B * H; }
-  d.dhn = f32p(dhn);
-  d.dcn = f32p(dcn);
-  d.dc_carry = carry.data_ptr<float>();
-  d.dh0 = dh0.data_ptr<float>();
-  d.dc0 = dc0.data_ptr<float>();
-  int big = 0;
-  a.splitk = pdrnn_lstm_large_bwd_splitk((int)B, (int)H, 1, &big);
-  a.splitk_big = big;
-  a.bwd_pp = a.splitk == 1 ? pdrnn_lstm_large_bwd_pp((int)B, (int)H, 1, dt) : 0;
-  Tensor ws;
-  if (a.splitk > 1 || a.bwd_pp) {
-    ws = at::empty({a.splitk, 2, B, H}, acts.options().dtype(at::kFloat));
-    a.ws = ws.data_ptr<float>();
-  }
-  hipStream_t st = cur_stream();
-  if (s0 == 0) HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, 1, dt, st));
-  int* cnt = sync.data_ptr<int>();
-  const int nmb = (int)((B + 16 * mt - 1) / (16 * mt));
-  if (mt >= 1 && !g_persist_disabled.load() &&
-      pdrnn_lstm_large_persist(&a, 1, 1, dt, (int)mt, cnt, cnt + nmb, persist_sticky_ptr(acts.options()), 0, st) ==
-          hipSuccess)
-    return true;
-  (void)hipGetLastError();
-  for (int64_t s = s0; s < s1; ++s) {
-    a.step = (int)s;
-    HIP_LAUNCH_CHECK(pdrnn_lstm_large_step(&a, 1, 1, dt, -1, st));
-  }
-  return false;
-}
 
 // Time ranges of a unidirectional fp32 H = 128 layer on the row-owning
 // kernels, into preallocated full-length tensors (the stacked-layer pipeline
@@ -1588,6 +1459,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "(sequences per workgroup, grid) of the deferred-dW backward for this shape");
   m.def("lstm_sw_ok", [](int64_t H, int64_t I, int64_t NL) { return pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, 0) == 1; },
         "the sequence-in-wave kernels (lstm_sw.hip) cover this LSTM stack in the fused train step");
+  m.def("lstm_sw_fits", [](int64_t NL, int64_t B, int64_t T) { return pdrnn_lstm_sw_fits((int)NL, (int)B, (int)T) == 1; },
+        "every act / hseq row of this batch fits the sequence-in-wave kernels' 2 GiB buffer descriptor");
   m.def("lstm_sw_mode", [](int64_t NL, int64_t B, bool backward) { return pdrnn_lstm_sw_mode((int)NL, (int)B, backward ? 1 : 0); },
         "wave map of the sequence-in-wave kernels for B sequences (0/1: a wave per 1/2 sequences, 2/3: a wave "
         "per layer of 1/2 sequences, 6: mode 2 at three waves per SIMD, forward only)",
@@ -1683,12 +1556,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     a.c_16bit = out16; a.ldc = N; a.A2 = a.B2 = K2 ? (const void*)1 : nullptr;
     return M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && pdrnn_gemm_supported(&a) != 0;
   });
-  m.def("large_persist_sync_len", &large_persist_sync_len, "int32 words of a step-range sync buffer (B, mt)");
   m.def("large_persist_mt", [](int64_t B, int64_t H, int64_t ndir, int64_t dtype, int64_t cus) {
     return g_persist_disabled.load() ? 0 : pdrnn_lstm_large_persist_mt((int)B, (int)H, (int)ndir, (int)dtype, (int)cus);
   }, "row tiles of the persistent recurrence for a grid of at most `cus` workgroups (0: not covered / turned off)");
-  m.def("lstm_large_fwd_range", &lstm_large_fwd_range, "persistent forward over processing steps [s0, s1)");
-  m.def("lstm_large_bwd_range", &lstm_large_bwd_range, "persistent BPTT over processing steps [s0, s1)");
   m.def("embedding_fwd", &embedding_fwd, py::arg("weight"), py::arg("idx"), py::arg("out_dtype") = py::none());
   m.def("embedding_sort", [](const Tensor& idx, int64_t V) {
     CHECK_HIP_TENSOR(idx);

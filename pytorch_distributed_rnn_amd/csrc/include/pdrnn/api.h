@@ -172,18 +172,13 @@ hipError_t pdrnn_lstm_small_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstm
 // activations (dg_out = act, dg_st = 5H) for pdrnn_lstm_small_dw.
 // ----------------------------------------------------------------------------
 int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell);
+int pdrnn_lstm_sw_fits(int NL, int B, int T);
+// sequences per wave (and per workgroup) of a sequence-in-wave mode
+int pdrnn_lstm_sw_nb(int mode);
 // mode for a batch of B sequences (PDRNN_SW_MODE overrides): 0, 1 or 2
 int pdrnn_lstm_sw_mode(int NL, int B, int backward);
 hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode, hipStream_t stream);
 hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode, hipStream_t stream);
-
-// bf16 matrix-core recurrence (kernels/lstm_mb.hip) for bf16 models: same
-// shapes and contracts as the sequence-in-wave kernels, 16 sequences per
-// workgroup, the recurrent products on v_mfma_f32_16x16x32_bf16 (h_t, x_t and
-// the gate gradients rounded to bf16 as operands, fp32 accumulation / state).
-int pdrnn_lstm_mb_ok(int H, int I, int NL, int cell, int T);
-hipError_t pdrnn_lstm_mb_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t stream);
-hipError_t pdrnn_lstm_mb_bwd(const PdrnnLstmSmallBwdArgs* a, hipStream_t stream);
 
 // Column sums of a [rows, P] fp32 slab into out[P] (out = beta*out + sum).
 // Two deterministic passes through `work` ([split, P] floats, split <= 64).

@@ -1,6 +1,5 @@
 // Fused classifier head + softmax cross-entropy of the motion training step,
-// one wave per sequence, H = 32 (shared by kernels/lstm_sw.hip and
-// kernels/lstm_mb.hip).
+// one wave per sequence, H = 32 (kernels/lstm_sw.hip).
 #pragma once
 
 #include "pdrnn/api.h"

@@ -345,8 +345,17 @@ hipError_t pdrnn_embedding_sort(const int64_t* idx, int64_t n, int64_t V, int* s
                      scratch);
   hipLaunchKernelGGL(pdrnn::emb_scan_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)V, stream, scratch, nb,
                      (int)V, offsets);
-  hipLaunchKernelGGL(pdrnn::emb_scatter_kernel, dim3(nb), dim3(pdrnn::kSortTile),
-                     sizeof(int) * ((size_t)V + pdrnn::kSortTile), stream, idx, n, (int)V, scratch, perm);
+  // the scatter stages V counters + one tile of keys: past 64 KiB of dynamic
+  // LDS (V > 16384 - kSortTile) the launch needs the opt-in limit (160 KiB
+  // per CU on gfx950), else it fails where the old at::sort path worked
+  const size_t lds_scatter = sizeof(int) * ((size_t)V + pdrnn::kSortTile);
+  if (lds_scatter > 64 * 1024) {
+    const hipError_t ea = hipFuncSetAttribute((const void*)pdrnn::emb_scatter_kernel,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_scatter);
+    if (ea != hipSuccess) return ea;
+  }
+  hipLaunchKernelGGL(pdrnn::emb_scatter_kernel, dim3(nb), dim3(pdrnn::kSortTile), lds_scatter, stream, idx, n,
+                     (int)V, scratch, perm);
   return hipGetLastError();
 }
 

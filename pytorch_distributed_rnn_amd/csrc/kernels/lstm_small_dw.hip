@@ -27,7 +27,7 @@
 //   * db: the first h_prev wave also sums its A fragments on the VALU (free
 //     beside the MFMAs) and reduces them over the 4 row lanes at the end.
 //   * Operands reach LDS by DMA (global_load_lds, no VGPR staging): a ring
-//     of 32-row stages (16 at H = 64), stages in flight past the one being consumed,
+//     of 16-row stages (dw_rows, small_dw.h), stages in flight past the one being consumed,
 //     retired by a counted vmcnt + raw barrier (a __syncthreads() would drain
 //     the ring); every wave issues an equal share of a stage's DMA jobs.
 // Chunk c writes its partial sums to slab row c; pdrnn_slab_reduce_adam sums

@@ -71,8 +71,12 @@ PDRNN_DEVICE float pair_sum(float v) { return v + dpp_swap1(v); }
 template <int NB>
 PDRNN_DEVICE int pick(const int (&v)[NB], int n) {
   if constexpr (NB == 1) return v[0];
-  else return n == 0 ? v[0] : v[1];
+  else if constexpr (NB == 2) return n == 0 ? v[0] : v[1];
+  else return n == 0 ? v[0] : n == 1 ? v[1] : v[2];
 }
+// sequences per wave of a mode: 1 (0, 2, 4, 5, 6), 2 (1, 3), 3 (7: the
+// layer-split map of mode 2 with three sequences per layer wave)
+constexpr int sw_nb(int mode) { return mode == 7 ? 3 : (mode == 1 || mode == 3) ? 2 : 1; }
 
 // ---------------------------------------------------------------------------
 // Forward
@@ -190,7 +194,7 @@ PDRNN_DEVICE constexpr int fwd_lds_floats_hb() { return NB * NL * 2 * kHB; }
 template <int NL, int MODE>
 __global__ void __launch_bounds__(MODE >= 2 ? 64 * NL : 64) __attribute__((amdgpu_waves_per_eu(MODE == 6 ? 3 : 1)))
 lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
-  constexpr int NB = (MODE & 1) ? 2 : 1;
+  constexpr int NB = sw_nb(MODE);
   constexpr bool SPLIT = MODE >= 2;
   static_assert(NL == 1 || NL == 2, "one or two layers");
   static_assert(!SPLIT || NL == 2, "layer-split mode needs two layers");
@@ -207,12 +211,13 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   float* xs = smem + fwd_lds_floats_hb<NL, NB>();
   auto hbuf = [&](int n, int l, int p) { return hb + ((n * NL + l) * 2 + p) * kHB; };
 
-  int bidx[NB], bsrc[NB];
+  int bidx[NB], bsrc[NB], vint[NB];
   bool valid[NB];
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     const int b = bbase + n;
     valid[n] = b < B;
+    vint[n] = valid[n] ? 1 : 0;
     bidx[n] = valid[n] ? b : B - 1;  // an empty slot recomputes the last sequence, stores nothing
     bsrc[n] = a.idx ? (int)a.idx[bidx[n]] : bidx[n];
   }
@@ -239,7 +244,7 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
           const int n = e / per, rem = e - n * per;
           const int t = rem / kXS, k = rem - t * kXS;
           xs[e] = v[r];
-          if (a.xg_out && k < xg_ld && (n == 0 ? valid[0] : valid[NB - 1]))
+          if (a.xg_out && k < xg_ld && pick<NB>(vint, n))
             a.xg_out[((int64_t)pick<NB>(bidx, n) * T + t) * xg_ld + k] = v[r];
         }
       }
@@ -646,19 +651,17 @@ PDRNN_DEVICE float col_dot(const BwdCol& W, const float4 (&g)[16]) {
 // (no occupancy target: at 168 VGPRs the split backward spills, and it only
 // runs at B <= one wave per SIMD)
 template <int NL, int MODE>
-__global__ void __launch_bounds__(MODE == 5 ? 384 : MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64)
+__global__ void __launch_bounds__(MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64)
 lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
-  constexpr int NB = (MODE == 1 || MODE == 3) ? 2 : 1;
+  constexpr int NB = sw_nb(MODE);
   constexpr bool SPLIT = MODE >= 2;
   // mode 4: the mode-2 map plus two waves that accumulate the weight
-  // gradients on the matrix cores (no gate-gradient stores, no dW launch);
-  // mode 5 (opt-in, PDRNN_SW_BWD_MODE=5): the same with two BPTT waves per
-  // layer (the four-wave forward's lane map: unit x row quarter), layer 0 two
-  // steps behind layer 1 -- correct but slower: 92.7 vs 55.3 us at B = 180
-  // (1,724 cycles a step: the column phase now waits behind the barrier for
-  // the other wave's dz; profiles/r5/sw/bwd5_probe.log)
-  constexpr bool DWACC = MODE == 4 || MODE == 5;
-  constexpr bool W4 = MODE == 5;
+  // gradients on the matrix cores (no gate-gradient stores, no dW launch).
+  // (A four-wave BPTT map -- two waves per layer, unit x row quarter -- was
+  // correct but slower: 92.7 vs 55.3 us at B = 180, the column phase waiting
+  // behind the barrier for the other wave's dz; profiles/r5/sw/bwd5_probe.log;
+  // removed in round 6.)
+  constexpr bool DWACC = MODE == 4;
   constexpr int ZR = DWACC ? 8 : 2;  // dz slots per (sequence, layer): a ring that holds a dW K step
   static_assert(NL == 1 || NL == 2, "one or two layers");
   static_assert(!SPLIT || NL == 2, "layer-split mode needs two layers");
@@ -826,7 +829,7 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
     // T % 4 == 0.  Layer 1's group g (times g .. g+3) is complete after
     // iteration T-1-g, layer 0's after T-g: capture at it = T-g (layer 1) or
     // T-g+1 (layer 0), i.e. at it % 4 == LAG, then one quarter per iteration.
-    constexpr int LAG = L == 1 ? 0 : (W4 ? 2 : 1);
+    constexpr int LAG = L == 1 ? 0 : 1;
     auto pos = [&](int it, auto pc) {
       constexpr int p = decltype(pc)::value;
       constexpr int q = (p - LAG + 4) & 3;
@@ -836,7 +839,7 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
       lds_barrier();
     };
     __syncthreads();
-    const int iters = T + (W4 ? 2 : 1);
+    const int iters = T + 1;
     int it = 0;
     for (; it + 3 < iters; it += 4) {
       pos(it, Q0{});
@@ -845,11 +848,9 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
       pos(it + 3, Q3{});
     }
     pos(it, Q0{});  // it = T
-    if constexpr (W4) pos(it + 1, Q1{});  // it = T + 1
     // (after the last barrier every dz is in the ring)
     if constexpr (L == 1) {
-      if constexpr (!W4) quarter(Q1{});
-      quarter(Q2{}); quarter(Q3{});
+      quarter(Q1{}); quarter(Q2{}); quarter(Q3{});
     } else {
       capture(0, true);
       quarter(Q0{}); quarter(Q1{}); quarter(Q2{}); quarter(Q3{});
@@ -978,118 +979,6 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
       body(it + 1, opB);
     }
     if (it < iters) body(it, opA);
-  } else if constexpr (W4) {
-    // mode 5: waves 0 / 1 = layer 0, waves 2 / 3 = layer 1, units 16 (wv & 1)
-    // .. + 15; lane = (unit ul = lane >> 2, row quarter rq = lane & 3).  An
-    // iteration first finishes the previous step's dh (the column phase over
-    // the dz written before the last barrier: both waves of the layer wrote
-    // it), then runs this step's row phase: one barrier per step.  Layer 1
-    // at t = T-1-it, layer 0 at t = T+1-it (its input gradient dx(t) comes
-    // from layer 1's column phase of the previous iteration).
-    if (wv < 4) {
-      const int lw = wv >> 1;
-      const int ul = lane >> 2, rq = lane & 3;
-      const int uu = 16 * (wv & 1) + ul;
-      const int64_t bq = bidx[0];
-      // W_hh (and W_ih of layer 1) column uu over rows [32 rq, 32 rq + 32)
-      pdrnn_f2 wh[16], wx[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int r = 32 * rq + 2 * j;
-        wh[j] = pdrnn_f2{wround(a.w_hh[lw][(int64_t)r * kH + uu], a.w_bf16),
-                         wround(a.w_hh[lw][(int64_t)(r + 1) * kH + uu], a.w_bf16)};
-        wx[j] = lw == 1 ? pdrnn_f2{wround(a.w_ih[1][(int64_t)r * kH + uu], a.w_bf16),
-                                   wround(a.w_ih[1][(int64_t)(r + 1) * kH + uu], a.w_bf16)}
-                        : pdrnn_f2{0.f, 0.f};
-      }
-      const uint32_t v_i = uu * 4, v_f = (kH + uu) * 4, v_g = (2 * kH + uu) * 4, v_o = (3 * kH + uu) * 4;
-      const uint32_t v_c = (4 * kH + uu) * 4;
-      auto ld = [&](int t) {
-        const int tc = min(max(t, 0), T - 1);
-        const uint32_t ra = __builtin_amdgcn_readfirstlane((uint32_t)((lw * B + bq) * T + tc)) * st_act;
-        const uint32_t rp = __builtin_amdgcn_readfirstlane(tc > 0 ? ra - st_act : ra);
-        Ops o;
-        o.i = bload(r_act, v_i, ra);
-        o.f = bload(r_act, v_f, ra);
-        o.g = bload(r_act, v_g, ra);
-        o.o = bload(r_act, v_o, ra);
-        o.c = bload(r_act, v_c, ra);
-        o.cp = bload(r_act, v_c, rp);
-        return o;
-      };
-      const float dtop = lw == 1 ? a.dhn[bq * kH + uu] : 0.f;
-      const int zslot = dz_slot(32 * rq);
-      const int wslot = dz_slot(rq * kH + uu);
-      float dcs = 0.f, dbq = 0.f;
-      auto tstep = [&](int it) { return lw == 1 ? T - 1 - it : T + 1 - it; };
-      Ops opA = ld(tstep(0));
-      __builtin_amdgcn_sched_barrier(0);
-      Ops opB = ld(tstep(1));
-      __builtin_amdgcn_sched_barrier(0);
-      __syncthreads();
-      auto body = [&](int it, Ops& op) {
-        const int t = tstep(it);
-        const bool act = t >= 0 && t < T;
-        // column phase: dh of step t (= W^T dz(t + 1)), layer 1 also dx(t + 1)
-        const float4* zg = reinterpret_cast<const float4*>(dzbuf(0, lw, t + 1) + zslot);
-        float4 g[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) g[c] = zg[c];
-        pdrnn_f2 ah = {0.f, 0.f}, ax = {0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          ah = pfma(wh[2 * c], lo2(g[c]), ah);
-          ah = pfma(wh[2 * c + 1], hi2(g[c]), ah);
-          if (lw == 1) {
-            ax = pfma(wx[2 * c], lo2(g[c]), ax);
-            ax = pfma(wx[2 * c + 1], hi2(g[c]), ax);
-          }
-        }
-        float vh = ah.x + ah.y;
-        vh += dpp_swap1(vh);
-        vh += dpp_swap2(vh);
-        const bool next_ok = t + 1 < T && it > 0;  // dz(t + 1) was written (and is a real step)
-        float dht = next_ok ? vh : 0.f;
-        if (lw == 1) {
-          float vx = ax.x + ax.y;
-          vx += dpp_swap1(vx);
-          vx += dpp_swap2(vx);
-          if (rq == 0) dxb[((t + 1) & 1) * 32 + uu] = next_ok ? vx : 0.f;
-          if (it == 0) dht += dtop;
-        } else {
-          dht += act ? dxb[(t & 1) * 32 + uu] : 0.f;  // layer 1's input gradient of step t
-        }
-        // row phase: this lane's gate gradient (rq: i, f, g, o)
-        const float cp = t > 0 ? op.cp : 0.f;
-        const float tcv = tanh_c(op.c);
-        const float dcp = fmaf(dht * op.o, fmaf(-tcv, tcv, 1.f), dcs);
-        const float A = rq == 3 ? dht * tcv : dcp;
-        const float Bv = rq == 0 ? op.g : rq == 1 ? cp : rq == 2 ? op.i : 1.f;
-        const float Cv = rq == 0 ? fmaf(-op.i, op.i, op.i) : rq == 1 ? fmaf(-op.f, op.f, op.f)
-                         : rq == 2 ? fmaf(-op.g, op.g, 1.f) : fmaf(-op.o, op.o, op.o);
-        const float dz = act ? A * Bv * Cv : 0.f;
-        dcs = act ? dcp * op.f : dcs;
-        dbq += dz;
-        dzbuf(0, lw, t)[wslot] = dz;
-        op = ld(tstep(it + 2));
-        lds_barrier();
-      };
-      const int iters4 = T + 2;
-      int it = 0;
-      for (; it + 1 < iters4; it += 2) {
-        body(it, opA);
-        body(it + 1, opB);
-      }
-      if (it < iters4) body(it, opA);
-      float* srow = a.slab + (int64_t)blockIdx.x * a.P;
-      const float db = valid[0] ? dbq : 0.f;
-      if (a.off_bih[lw] >= 0) srow[a.off_bih[lw] + rq * kH + uu] = db;
-      if (a.off_bhh[lw] >= 0) srow[a.off_bhh[lw] + rq * kH + uu] = db;
-    } else if (wv == 4) {
-      dw_wave(std::integral_constant<int, 0>{});
-    } else {
-      dw_wave(std::integral_constant<int, 1>{});
-    }
   } else {
     // modes 2/3: wave 1 = layer 1 (t = T-1-it), wave 0 = layer 0 (t = T-it),
     // one barrier per iteration; layer 1's input gradient of step t reaches
@@ -1197,11 +1086,11 @@ int sw_cus() {
 
 size_t fwd_lds(int NL, int nb, int T) { return sizeof(float) * ((size_t)nb * NL * 2 * kHB + (size_t)nb * T * kXS); }
 size_t bwd_lds(int NL, int nb, int zr = 2) { return sizeof(float) * ((size_t)nb * NL * zr * kDZ + (size_t)nb * 2 * 32); }
-int mode_nb(int mode) { return (mode == 1 || mode == 3) ? 2 : 1; }
+int mode_nb(int mode) { return sw_nb(mode); }
 
 template <int NL, int MODE>
 hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
-  constexpr int NB = (MODE & 1) ? 2 : 1;
+  constexpr int NB = sw_nb(MODE);
   const int grid = (a->B + NB - 1) / NB;
   const int block = MODE >= 2 ? 64 * NL : 64;
   hipLaunchKernelGGL((lstm_sw_fwd_kernel<NL, MODE>), dim3(grid), dim3(block), fwd_lds(NL, NB, a->T), st, *a);
@@ -1214,9 +1103,9 @@ hipError_t launch_fwd4(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
 }
 template <int NL, int MODE>
 hipError_t launch_bwd(const PdrnnLstmSmallBwdArgs* a, hipStream_t st) {
-  constexpr int NB = (MODE == 1 || MODE == 3) ? 2 : 1;
+  constexpr int NB = sw_nb(MODE);
   const int grid = (a->B + NB - 1) / NB;
-  const int block = MODE == 5 ? 384 : MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64;
+  const int block = MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64;
   hipLaunchKernelGGL((lstm_sw_bwd_kernel<NL, MODE>), dim3(grid), dim3(block), bwd_lds(NL, NB, MODE >= 4 ? 8 : 2), st,
                      *a);
   return hipGetLastError();
@@ -1230,6 +1119,17 @@ using namespace pdrnn;
 
 extern "C" int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell) {
   return (H == kH && I >= 1 && I <= kXS && (NL == 1 || NL == 2) && cell == 0) ? 1 : 0;
+}
+
+// Every (layer, sequence, step) row of `act` (5H floats) and `hseq` is
+// addressed as a 32-bit byte offset under ONE buffer descriptor whose range
+// is 2 GiB (uniform_rsrc): past it loads return 0 and stores are dropped.
+// The launchers refuse batches whose last row (plus the deferred-dW padding
+// rows) would not fit; the caller then takes the gate-split family, which
+// rebases its descriptors per sequence.
+extern "C" int pdrnn_lstm_sw_fits(int NL, int B, int T) {
+  const int64_t rows = (int64_t)NL * B * T + PDRNN_DW_PAD_ROWS;
+  return (NL >= 1 && B >= 1 && T >= 1 && rows * 5 * kH * 4 < ((int64_t)1 << 31)) ? 1 : 0;
 }
 
 // Measured (bench/sw_probe.cpp, profiles/r5/sw): two-layer stacks run one
@@ -1249,7 +1149,9 @@ extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
   if (!(e && *e) && backward) e = getenv("PDRNN_SW_MODE");
   if (e && *e) {
     const int m = atoi(e);
-    if (m >= 0 && m <= 6 && (m < 2 || NL == 2) && (m != 6 || !backward) && (m != 4 || backward)) return m;
+    if (m >= 0 && m <= 7 && (m < 2 || NL == 2) && (m != 6 || !backward) && (m != 4 || backward) &&
+        (m != 5 || !backward))
+      return m;
   }
   const int simds = 4 * sw_cus();
   // (modes 4 / 5: four waves per workgroup, two workgroups per CU)
@@ -1258,9 +1160,12 @@ extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
   return B <= simds ? 0 : 1;
 }
 
+extern "C" int pdrnn_lstm_sw_nb(int mode) { return mode_nb(mode); }
+
 extern "C" hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode, hipStream_t st) {
   if (!pdrnn_lstm_sw_ok(kH, a->I, a->NL, a->cell) || a->h0 || a->c0) return hipErrorInvalidValue;
   if (!a->act || !a->hseq || a->B <= 0 || a->T <= 0) return hipErrorInvalidValue;
+  if (!pdrnn_lstm_sw_fits(a->NL, a->B, a->T)) return hipErrorInvalidValue;  // 2 GiB descriptor range
   if (a->head_w && (a->C > 16 || a->C < 1 || !a->labels || !a->slab || !a->dh_top)) return hipErrorInvalidValue;
   if (a->xg_out && (a->xg_ld < a->I || a->xg_ld > kXS)) return hipErrorInvalidValue;
   if (fwd_lds(a->NL, mode_nb(mode), a->T) > 64 * 1024) return hipErrorInvalidConfiguration;
@@ -1274,6 +1179,7 @@ extern "C" hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode
   if (mode == 2) return launch_fwd<2, 2>(a, st);
   if (mode == 3) return launch_fwd<2, 3>(a, st);
   if (mode == 6) return launch_fwd<2, 6>(a, st);
+  if (mode == 7) return launch_fwd<2, 7>(a, st);
   if (mode == 5) return launch_fwd4(a, st);
   return hipErrorInvalidValue;
 }
@@ -1283,6 +1189,7 @@ extern "C" hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode
   if (a->h0 || a->c0 || a->dout || a->dcn || a->dx || a->dh0 || a->dc0 || !a->dhn || !a->dhn_top_only)
     return hipErrorInvalidValue;  // lean contract only
   if (!a->act || !a->dg_out || a->dg_st < 4 * kH || a->B <= 0 || a->T <= 0) return hipErrorInvalidValue;
+  if (!pdrnn_lstm_sw_fits(a->NL, a->B, a->T)) return hipErrorInvalidValue;  // 2 GiB descriptor range
   if (a->NL == 1) {
     if (mode == 0) return launch_bwd<1, 0>(a, st);
     if (mode == 1) return launch_bwd<1, 1>(a, st);
@@ -1292,9 +1199,10 @@ extern "C" hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode
   if (mode == 1) return launch_bwd<2, 1>(a, st);
   if (mode == 2) return launch_bwd<2, 2>(a, st);
   if (mode == 3) return launch_bwd<2, 3>(a, st);
-  if (mode == 4 || mode == 5) {  // register dW: one slab row per workgroup; reads the x rows and the h sequence
+  if (mode == 7) return launch_bwd<2, 7>(a, st);
+  if (mode == 4) {  // register dW: one slab row per workgroup; reads the x rows and the h sequence
     if (a->T % 4 || !a->slab || !a->xg_out || a->xg_ld > 16 || !a->hseq) return hipErrorInvalidValue;
-    return mode == 4 ? launch_bwd<2, 4>(a, st) : launch_bwd<2, 5>(a, st);
+    return launch_bwd<2, 4>(a, st);
   }
   return hipErrorInvalidValue;
 }

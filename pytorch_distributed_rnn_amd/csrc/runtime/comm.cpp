@@ -456,7 +456,12 @@ class RcclComm final : public Comm {
     hipEvent_t ev;
     HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(ev, st));
-    int spins = 0;
+    // poll without sleeping for the first 2 ms (a barrier normally completes
+    // in tens of us: a fixed 200 us sleep after 64 polls made every world-1
+    // barrier cost ~0.3 ms, profiles/r6/bench_trace.md), then back off to
+    // 200 us sleeps so a long wait does not burn a core
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t nap_us = 10;
     for (;;) {
       const hipError_t q = hipEventQuery(ev);
       if (q == hipSuccess) break;
@@ -468,7 +473,10 @@ class RcclComm final : public Comm {
         hipEventDestroy(ev);
         live();
       }
-      if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(200));
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+        std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
+        nap_us = std::min<int64_t>(200, nap_us * 2);
+      }
     }
     hipEventDestroy(ev);
   }

@@ -621,7 +621,10 @@ class _PipelinedLSTMStack(torch.autograd.Function):
                                 db_first=True)
             if direct[l]:
                 bi, bh = sinks[l][2], sinks[l][3]
-                if bi is not None and bh is not None and bh.data_ptr() == bi.data_ptr() + bi.numel() * 4:
+                # (same storage too: two separately allocated gradients can sit
+                # side by side in the caching allocator -- ADVICE r5)
+                if bi is not None and bh is not None and bh.data_ptr() == bi.data_ptr() + bi.numel() * 4 and \
+                        bi.untyped_storage().data_ptr() == bh.untyped_storage().data_ptr():
                     # b_ih, b_hh adjacent in the flat gradient: one launch for both
                     torch.as_strided(bi, (2, bi.numel()), (bi.numel(), 1)).add_(db[l])
                 else:
@@ -644,175 +647,6 @@ class _PipelinedLSTMStack(torch.autograd.Function):
                 grads += [db[l] if has_w[l][2] else None, db[l] if has_w[l][3] else None]
         dh0 = torch.stack(dhb).to(h0_dtype) if h0_dtype is not None else None
         dc0 = torch.stack(dcb).to(c0_dtype) if c0_dtype is not None else None
-        return (dx, dh0, dc0, None, *grads)
-
-
-# ---------------------------------------------------------------------------
-# Stacked-layer pipeline for 16-bit unidirectional stacks on the persistent
-# recurrence (char-LM, BASELINE config 4).  Same chunk schedule as the fp32
-# pipeline above, with each layer's persistent grid planned for half the CUs
-# (pdrnn_lstm_large_persist_mt(..., cus / 2)) so that layer l + 1's grid on
-# chunk c and layer l's on chunk c + 1 are co-resident; a layer's ranges share
-# one sync buffer (kernels/lstm_large.hip: args.s0 / s1 resume from the state
-# the previous range left in hseq / cseq or dgates / dc_carry).  Only with the
-# persistent-path verification off (single process, PDRNN_LSTM_PERSIST_VERIFY
-# unset): a multi-rank run keeps the layer-by-layer path, whose launches are
-# checked and re-run one by one.
-#
-# Opt-in (PDRNN_LARGE_PIPE16=1), measured slower at the char-LM shape
-# (profiles/r5/charlm/): the persistent step is bound by each CU's share of
-# the work, not by the grid sync alone -- two layers' grids side by side (two
-# per CU, or one each on half the CUs) run 1.3x / 1.8x slower per step, and
-# the chunk projections (131 KB of LDS per GEMM workgroup) cannot share a CU
-# with a persistent forward workgroup: 15.2-16.3 ms/step against 15.1
-# layer by layer.
-def pipeline16_chunks(T: int) -> List[Tuple[int, int]]:
-    """[s0, s1) processing-step chunks (PDRNN_LARGE16_CHUNKS, default 4)."""
-    try:
-        c = int(os.environ.get("PDRNN_LARGE16_CHUNKS", "4"))
-    except ValueError:
-        c = 4
-    c = max(1, min(c, T))
-    return [(T * i // c, T * (i + 1) // c) for i in range(c)]
-
-
-def pipeline16_plan(x: Tensor, hidden: int, num_layers: int, bidirectional: bool, dropout: float,
-                    training: bool) -> int:
-    """Row tiles of each layer's persistent grid when the 16-bit stacked-layer
-    pipeline is on (PDRNN_LARGE_PIPE16=1) and covers this call (0: it does not)."""
-    if os.environ.get("PDRNN_LARGE_PIPE16", "0") != "1" or os.environ.get("PDRNN_LSTM_PERSIST", "1") == "0":
-        return 0
-    if _tile() >= 0 or x.dtype not in (torch.bfloat16, torch.float16) or not x.is_cuda or bidirectional or \
-            num_layers < 2 or (dropout > 0 and training):
-        return 0
-    mod = _ext.native(x.device)
-    if mod is None or not hasattr(mod, "lstm_large_fwd_range") or mod.persist_verify_mode() != 0:
-        return 0
-    cus = torch.cuda.get_device_properties(x.device).multi_processor_count - int(mod.rccl_cta_reserve())
-    dt = 0 if x.dtype == torch.bfloat16 else 1
-    try:  # CU share each layer's grid is planned for (PDRNN_LARGE16_SHARE: 1 = all CUs, 2 = half)
-        share = max(1, int(os.environ.get("PDRNN_LARGE16_SHARE", "1")))
-    except ValueError:
-        share = 1
-    return int(mod.large_persist_mt(x.shape[1], hidden, 1, dt, cus // share))
-
-
-class _PipelinedLSTMStack16(torch.autograd.Function):
-    """All layers of a unidirectional 16-bit stack on the persistent kernels,
-    chunk-pipelined across layers (see above).  x: [T, B, I] compute dtype;
-    h0 / c0: [L, B, H] or None; weights: nn.LSTM ``_all_weights`` order."""
-
-    @staticmethod
-    def forward(ctx, x, h0, c0, cfg, *weights):
-        ctx.set_materialize_grads(False)
-        H, L, per, chunks, mt = cfg
-        cdt = x.dtype
-        T, B, I = x.shape
-        dev = x.device
-        mod = _ext.native(dev)
-        lw = [list(weights[l * per:(l + 1) * per]) + ([None, None] if per == 2 else []) for l in range(L)]
-        wih_i = [shadow(w[0], "i", cdt, H) for w in lw]               # [4H, I_l] gate-interleaved
-        whh_i = [shadow(w[1], "i", cdt, H) for w in lw]
-        bias = [_bias_cat(w, 1, H, dev) for w in lw]                    # fp32, interleaved
-        h0s = [h0[l].to(cdt).contiguous() if h0 is not None else None for l in range(L)]
-        c0s = [c0[l].float().contiguous() if c0 is not None else None for l in range(L)]
-        hseq = [x.new_empty(T, B, H) for _ in range(L)]
-        cseq = [x.new_empty(1, T, B, H, dtype=torch.float32) for _ in range(L)]
-        acts = [x.new_empty(1, T, B, 4 * H) for _ in range(L)]
-        xps = [linear16(x.reshape(T * B, I), wih_i[0], bias[0]).view(T, B, 4 * H)]
-        xps += [x.new_empty(T, B, 4 * H) for _ in range(1, L)]
-        syncs = [torch.zeros(mod.large_persist_sync_len(B, mt), dtype=torch.int32, device=dev) for _ in range(L)]
-        rec = pipeline_streams(dev, L)
-
-        def project(l, t0, t1):  # this chunk's input projection
-            mod.gemm16(hseq[l - 1][t0:t1].view(-1, H), False, wih_i[l], False, bias=bias[l], out16=True,
-                       out=xps[l][t0:t1].view(-1, 4 * H))
-
-        def recur(l, t0, t1):
-            mod.lstm_large_fwd_range(xps[l], whh_i[l], h0s[l], c0s[l], hseq[l], cseq[l], acts[l], H, t0, t1,
-                                     syncs[l], mt)
-
-        pipeline_forward(rec, chunks, project, recur)
-        pipeline_join(rec)
-        hn = x.new_empty(L, B, H)
-        cn = x.new_empty(L, B, H)
-        for l in range(L):
-            hn[l].copy_(hseq[l][T - 1])
-            cn[l].copy_(cseq[l][0, T - 1])
-        ctx.save_for_backward(x, *hseq, *cseq, *acts, *[shadow(w[0], "p", cdt, H) for w in lw],
-                              *[shadow(w[1], "t", cdt, H) for w in lw])
-        ctx.states = (h0s, c0s)
-        ctx.cfg = (H, L, per, chunks, mt, [[w is not None for w in ws] for ws in lw],
-                   h0.dtype if h0 is not None else None, c0.dtype if c0 is not None else None)
-        return hseq[L - 1], hn, cn
-
-    @staticmethod
-    def backward(ctx, dhseq, dhn, dcn):
-        H, L, per, chunks, mt, has_w, h0_dtype, c0_dtype = ctx.cfg
-        h0s, c0s = ctx.states
-        sv = ctx.saved_tensors
-        x = sv[0]
-        hseq, cseq, acts = sv[1:1 + L], sv[1 + L:1 + 2 * L], sv[1 + 2 * L:1 + 3 * L]
-        wp, wt = sv[1 + 3 * L:1 + 4 * L], sv[1 + 4 * L:1 + 5 * L]
-        cdt = x.dtype
-        T, B, I = x.shape
-        dev = x.device
-        mod = _ext.native(dev)
-        f32 = torch.float32
-        dgates = [x.new_empty(1, T, B, 4 * H) for _ in range(L)]
-        douts = [x.new_empty(T, B, H) for _ in range(L - 1)]
-        douts.append(dhseq.to(cdt).contiguous() if dhseq is not None else None)
-        carry = [x.new_empty(B, H, dtype=f32) for _ in range(L)]
-        dh0s = [x.new_empty(B, H, dtype=f32) for _ in range(L)]
-        dc0s = [x.new_empty(B, H, dtype=f32) for _ in range(L)]
-        dhn_l = [dhn[l].float().contiguous() if dhn is not None else None for l in range(L)]
-        dcn_l = [dcn[l].float().contiguous() if dcn is not None else None for l in range(L)]
-        syncs = [torch.zeros(mod.large_persist_sync_len(B, mt), dtype=torch.int32, device=dev) for _ in range(L)]
-        ins = [x] + list(hseq[:-1])
-        grads_l: List[List[Optional[Tensor]]] = [[] for _ in range(L)]
-        rec = pipeline_streams(dev, L)
-        done = [[None] * len(chunks) for _ in range(L)]
-        last = len(chunks) - 1
-
-        def finish(l):  # the layer's recurrence is done: its weight gradients, on its stream
-            G = dgates[l][0].view(T * B, 4 * H)
-            pairs = []
-            if T > 1:
-                pairs.append((G[B:], hseq[l][:-1].reshape((T - 1) * B, H)))
-            if h0s[l] is not None:
-                pairs.append((G[:B], h0s[l]))
-            dwhh = mm_kk(pairs) if pairs else torch.zeros(4 * H, H, device=dev, dtype=f32)
-            dwih = mm_kk([(G, ins[l].reshape(T * B, -1))])
-            db = col_sum(G)
-            grads_l[l] = [dwih, dwhh] + ([db if has_w[l][2] else None, db if has_w[l][3] else None]
-                                         if per == 4 else [])
-
-        for k, (s0, s1) in enumerate(chunks):
-            for l in range(L - 1, -1, -1):
-                with torch.cuda.stream(rec[l]):
-                    if l < L - 1:
-                        # layer l + 1's dX for the times this chunk reads (the
-                        # step-s cell backward reads dout_{T-2-s}; the first
-                        # chunk's first-step kernel dout_{T-1})
-                        rec[l].wait_event(done[l + 1][k])
-                        lo, hi = max(T - 1 - s1, 0), (T - 1 if s0 == 0 else T - 2 - s0)
-                        if hi >= lo:
-                            mod.gemm16(dgates[l + 1][0][lo:hi + 1].view(-1, 4 * H), False, wp[l + 1], True,
-                                       out16=True, out=douts[l][lo:hi + 1].view(-1, H))
-                    mod.lstm_large_bwd_range(douts[l], dhn_l[l], dcn_l[l], wt[l], cseq[l], acts[l], c0s[l],
-                                             dgates[l], carry[l], dh0s[l], dc0s[l], H, s0, s1, syncs[l], mt)
-                    done[l][k] = _event(rec[l])
-                    if k == last:
-                        finish(l)
-        dx = None
-        if ctx.needs_input_grad[0]:  # (layer 0's stream is the caller's)
-            dx = mm_nk16([(dgates[0][0].view(T * B, 4 * H), wp[0])]).view(T, B, I)
-        pipeline_join(rec)
-        grads: List[Optional[Tensor]] = []
-        for l in range(L):
-            grads += grads_l[l]
-        dh0 = torch.stack(dh0s).to(h0_dtype) if h0_dtype is not None and ctx.needs_input_grad[1] else None
-        dc0 = torch.stack(dc0s).to(c0_dtype) if c0_dtype is not None and ctx.needs_input_grad[2] else None
         return (dx, dh0, dc0, None, *grads)
 
 
@@ -873,11 +707,6 @@ def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optio
     if pipeline_ok(seq, hidden, num_layers, bidirectional, dropout, training):
         out, hn, cn = _PipelinedLSTMStack.apply(seq, h0, c0, (hidden, num_layers, per, pipeline_chunks(seq.shape[0])),
                                                 *weights)
-        return (out.transpose(0, 1) if batch_first else out), hn, cn
-    mt = pipeline16_plan(seq, hidden, num_layers, bidirectional, dropout, training)
-    if mt:
-        out, hn, cn = _PipelinedLSTMStack16.apply(seq, h0, c0, (hidden, num_layers, per,
-                                                                pipeline16_chunks(seq.shape[0]), mt), *weights)
         return (out.transpose(0, 1) if batch_first else out), hn, cn
     tile = _tile()
     hns, cns = [], []

@@ -175,7 +175,9 @@ def get_world_size() -> int:
 
 
 def barrier() -> None:
-    if is_distributed():
+    # one rank has nobody to wait for: a world-1 barrier (an RCCL all-reduce
+    # plus a host wait, ~0.3 ms on MI355X -- profiles/r6/bench_trace.md) is skipped
+    if is_distributed() and dist.get_world_size() > 1:
         from .comm import native_world_comm
         c = native_world_comm()
         if c is not None:  # the gradient communicator (torch's RCCL comm stays unborn)

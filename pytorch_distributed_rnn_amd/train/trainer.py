@@ -318,15 +318,6 @@ class Trainer:
             return False
         return not any(os.environ.get(k, "0") == "1" for k in ("PDRNN_FORCE_COLLECTIVE", "PDRNN_FORCE_GRAD_SYNC"))
 
-    def _graphed_step(self):
-        """The autograd step replayed from a HIP graph (train/graphed_step.py),
-        or None (not requested, multi-process, CPU, other optimizers)."""
-        if getattr(self, "_graphed", False) is not False:
-            return self._graphed
-        from . import graphed_step
-        self._graphed = graphed_step.make(self)
-        return self._graphed
-
     def train_batch(self, batch) -> Tuple[Tensor, int]:
         """One optimizer step on one batch; returns (stats [loss, n, correct], batch size).
 
@@ -340,16 +331,6 @@ class Trainer:
                 return fused(features, labels_all, idx), idx.numel()
             data, labels = batch
             return fused(data, labels.reshape(-1).contiguous(), None), labels.shape[0]
-        graphed = self._graphed_step()
-        if graphed is not None and self.model.training and len(batch) == 3:
-            try:
-                return graphed(*batch)
-            except RuntimeError as e:
-                if graphed.replays:
-                    raise
-                # (a capture that fails leaves the eager step in charge)
-                logging.warning("graph capture of the training step failed, running it eagerly: %s", e)
-                self._graphed = None
         self.optimizer.zero_grad()
         with gradsink.direct_grads(self._direct_grads_ok()):
             with trace_range("pdrnn.forward"):

@@ -209,6 +209,21 @@ def test_embedding_matches_torch():
     assert torch.allclose(dw.double().cpu(), ref, atol=1e-4)
 
 
+@pytest.mark.parametrize("V", [16129, 16384])
+def test_embedding_backward_at_the_in_tree_sort_limit(V):
+    """the in-tree counting sort serves V <= 16384; its scatter
+    stages V counters plus a key tile in LDS, past 64 KiB from V = 16129 (the
+    launch opts into the larger limit)."""
+    C = _C()
+    D, N = 32, 20000
+    torch.manual_seed(V)
+    idx = torch.randint(0, V, (N,))
+    g = torch.randn(N, D)
+    dw = C.embedding_bwd(g.cuda(), idx.cuda(), V, -1)
+    ref = torch.zeros(V, D, dtype=torch.float64).index_add_(0, idx, g.double())
+    assert torch.allclose(dw.double().cpu(), ref, atol=1e-4)
+
+
 @pytest.mark.parametrize("H,NL,I,B,T,bf", [(32, 2, 9, 37, 40, True), (16, 1, 5, 8, 33, False),
                                           (64, 2, 64, 6, 12, True), (32, 3, 32, 5, 20, True)])
 def test_fused_gru_matches_torch(H, NL, I, B, T, bf):

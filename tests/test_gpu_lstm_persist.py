@@ -248,42 +248,3 @@ def test_step_verified_charlm_reruns_timed_out_step(monkeypatch):
         mod.persist_reset()
     torch.testing.assert_close(losses[0], losses[1], rtol=1e-3, atol=1e-5)
     torch.testing.assert_close(results[0], results[1], rtol=1e-3, atol=1e-5)
-
-
-@pytest.mark.parametrize("chunks,B,T,state,share", [("4", 128, 24, False, "1"), ("3", 40, 21, True, "2"),
-                                                    ("1", 16, 5, True, "1"), ("4", 96, 24, True, "2")])
-def test_layer_pipeline16_matches_layer_by_layer(chunks, B, T, state, share, monkeypatch):
-    """The 16-bit stacked-layer pipeline (ops/lstm_large.py
-    _PipelinedLSTMStack16: each layer's persistent grid on half the CUs, layer
-    1 on chunk c beside layer 0 on chunk c + 1, step ranges resuming from the
-    saved state) against the layer-by-layer persistent path on the same
-    weights: outputs, final states and every gradient, with and without an
-    initial state, chunk counts that do not divide T.  (Half the CUs at
-    B = 96: 96 workgroups, which still fit when an RCCL communicator created
-    by an earlier test of the session reserves its CUs -- B = 128 needs 128.)"""
-    from pytorch_distributed_rnn_amd.ops import lstm_large
-    torch.manual_seed(7)
-    dt = torch.bfloat16
-    m = LSTM(64, H, 2, batch_first=True).cuda()
-    x = torch.randn(B, T, 64, device="cuda").to(dt)
-    st = (torch.randn(2, B, H, device="cuda").to(dt), torch.randn(2, B, H, device="cuda").to(dt)) if state else None
-    g = torch.randn(B, T, H, device="cuda")
-
-    monkeypatch.setenv("PDRNN_LARGE_PIPE16", "1")
-    monkeypatch.setenv("PDRNN_LARGE16_SHARE", share)
-
-    def run(pipe):
-        monkeypatch.setenv("PDRNN_LARGE_PIPE16", "1" if pipe else "0")
-        monkeypatch.setenv("PDRNN_LARGE16_CHUNKS", chunks)
-        m.zero_grad(set_to_none=True)
-        xi = x.clone().requires_grad_(True)
-        out, (hn, cn) = m(xi, st)
-        (out.float() * g).sum().backward()
-        return [out, hn, cn, xi.grad] + [p.grad.clone() for p in m.parameters()]
-
-    seq = torch.transpose(x, 0, 1).contiguous()
-    assert lstm_large.pipeline16_plan(seq, H, 2, False, 0.0, True) > 0, "pipeline not selected"
-    a = run(True)
-    b = run(False)
-    for u, v in zip(a, b):
-        assert _rel(u, v) < 1e-3, (_rel(u, v), u.shape)

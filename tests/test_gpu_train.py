@@ -288,6 +288,24 @@ def test_seq_in_wave_step_gradients_match_fp64(B, layers, mode, monkeypatch):
     _fp64_check(MotionModel(9, 32, layers, 6), train, B)
 
 
+def test_seq_in_wave_batch_past_descriptor_range_falls_back(monkeypatch):
+    """the sequence-in-wave kernels address every act / hseq row as
+    a 32-bit offset under one 2 GiB buffer descriptor.  A batch whose rows
+    pass that range (NL * B * T * 640 B >= 2^31: B = 13200 at T = 128) must
+    take the per-sequence-rebased kernel family, and its gradients must still
+    match fp64 autograd."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.delenv("PDRNN_SW", raising=False)
+    mod = _ext.native(torch.device("cuda", 0))
+    B = 13200
+    assert mod.lstm_sw_fits(2, 13000, 128) and not mod.lstm_sw_fits(2, B, 128)
+    torch.manual_seed(17)
+    train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=18)
+    _fp64_check(MotionModel(9, 32, 2, 6), train, B, tol=4e-6)
+
+
 @pytest.mark.parametrize("cell,B", [("gru", 180), ("gru", 144), ("lstm", 180), ("lstm", 144)])
 def test_one_launch_gradients_match_fp64(cell, B, monkeypatch):
     """the one-launch step kernel (lstm_small_step_gs_kernel,
@@ -401,44 +419,6 @@ def test_bf16_lstm_matches_rounded_fp64_reference():
     out_r, (hn_r, _) = ref(x.double())
     torch.testing.assert_close(out.double(), out_r, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(hn.double(), hn_r, rtol=1e-4, atol=1e-5)
-
-
-@pytest.mark.parametrize("cell,hidden", [("lstm", 128), ("gru", 128), ("lstm", 64)])
-def test_graphed_autograd_step_matches_eager(cell, hidden):
-    """The autograd step replayed from HIP graphs (train/graphed_step.py: one
-    capture per batch shape, device Adam step count, shadow weights refreshed
-    inside the graph) against the same step run eagerly, over two epochs that
-    include the short last batch; a validation pass in between (eager forward
-    on the replay-updated weights) must see the current parameters."""
-    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
-    from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    from pytorch_distributed_rnn_amd.train.trainer import Trainer
-    torch.manual_seed(4)
-    train, _, _ = synthetic_motion(n_train=200, n_validation=2, n_test=2, seed=8)
-    m1 = MotionModel(9, hidden, 2, 6, cell=cell)
-    m2 = copy.deepcopy(m1)
-    t1 = Trainer(m1, train, batch_size=64, learning_rate=2.5e-3, device=torch.device("cuda"), cuda_graph=True)
-    t2 = Trainer(m2, train, batch_size=64, learning_rate=2.5e-3, device=torch.device("cuda"))
-    t1._fused = t2._fused = None
-    assert t2._graphed_step() is None  # opt-in
-    g = t1._graphed_step()
-    assert g is not None, "graphed step not selected"
-    x_probe = train.features[:16].cuda()
-    for epoch in range(2):
-        for x1, x2 in zip(list(t1.train_loader), list(t2.train_loader)):
-            s1, n1 = t1.train_batch(x1)
-            s2, n2 = t2.train_batch(x2)
-            assert n1 == n2
-            assert abs(float(s1[0]) - float(s2[0])) < 2e-5, (epoch, float(s1[0]), float(s2[0]))
-        with torch.no_grad():
-            m1.eval(), m2.eval()
-            assert torch.allclose(m1(x_probe), m2(x_probe), atol=1e-4, rtol=1e-4)
-            m1.train(), m2.train()
-    assert g.replays == 2 * len(t1.train_loader) and len(g.entries) == 2
-    for (k, p), q in zip(m1.named_parameters(), m2.parameters()):
-        assert torch.allclose(p, q, atol=3e-5, rtol=1e-4), k
-    st1, st2 = t1.optimizer.state_dict(), t2.optimizer.state_dict()
-    assert float(st1["state"][0]["step"]) == float(st2["state"][0]["step"]) == 2 * len(t1.train_loader)
 
 
 @pytest.mark.parametrize("T", [126, 61])

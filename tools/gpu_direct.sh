@@ -1,7 +1,7 @@
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_lstm_pipeline.py tests/test_gpu_lstm_large.py tests/test_gpu_coverage.py -x -q --timeout 200 --timeout-method thread -k "direct or graphed or pipeline or large or coverage" > gpurun_out/dg_tests.log 2>&1 || { tail -30 gpurun_out/dg_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_lstm_pipeline.py tests/test_gpu_lstm_large.py tests/test_gpu_coverage.py -x -q --timeout 200 --timeout-method thread -k "direct or pipeline or large or coverage" > gpurun_out/dg_tests.log 2>&1 || { tail -30 gpurun_out/dg_tests.log; exit 1; }
 tail -1 gpurun_out/dg_tests.log
 for cell in lstm gru; do
   timeout -k 10 300 python bench.py --hidden 128 --cell $cell --steps 20 --warmup 10 > gpurun_out/dg_h128_$cell.log 2>&1
