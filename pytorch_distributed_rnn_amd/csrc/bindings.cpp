@@ -405,7 +405,7 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
                           const optional<std::vector<Tensor>>& adam_state,
                           const optional<std::vector<double>>& adam_hp, int64_t cell,
                           const optional<Tensor>& grad_colmap, const optional<Tensor>& stats_slot_step,
-                          int64_t stats_slot_offset, bool round_bf16) {
+                          int64_t stats_slot_offset, bool round_bf16, const optional<Tensor>& adam_ticket) {
   CHECK_HIP_TENSOR(x);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be float32 or bfloat16");
   TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1, "x must be [N, T, I] with contiguous rows");
@@ -608,6 +608,15 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     ad.bias_correction1 = (float)(1.0 - std::pow(hp[1], hp[5]));
     ad.bias_correction2_sqrt = (float)std::sqrt(1.0 - std::pow(hp[2], hp[5]));
     ad.grad_scale = 1.f; ad.decoupled = hp[6] != 0.0 ? 1 : 0; ad.maximize = 0;
+    // graph-replayed single-process epoch: the step count lives on the device
+    // (the stats ring's slot step), advanced by the reduction's last workgroup
+    if (adam_ticket.has_value() && adam_ticket->defined()) {
+      TORCH_CHECK(slot_step != nullptr, "adam_ticket needs stats_slot_step (the device step count)");
+      TORCH_CHECK(adam_ticket->is_cuda() && adam_ticket->scalar_type() == at::kInt && adam_ticket->numel() >= 1,
+                  "adam_ticket: int32 device word");
+      ad.step_advance = const_cast<float*>(slot_step);
+      ad.ticket = reinterpret_cast<unsigned int*>(adam_ticket->data_ptr<int>());
+    }
   }
   HIP_LAUNCH_CHECK(pdrnn_slab_reduce_adam(fold_adam ? &ad : nullptr, slab.data_ptr<float>(), slab_rows, P_rnn, L.P,
                                           colmap, head_slab.data_ptr<float>(), B, PH, P_params,
@@ -1473,7 +1482,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("flat_grad"), py::arg("stats"), py::arg("H"), py::arg("NL"), py::arg("split_fwd"),
         py::arg("split_bwd"), py::arg("nb_fwd"), py::arg("nb_bwd"), py::arg("adam_state") = py::none(),
         py::arg("adam_hp") = py::none(), py::arg("cell") = 0, py::arg("grad_colmap") = py::none(),
-        py::arg("stats_slot_step") = py::none(), py::arg("stats_slot_offset") = 0, py::arg("round_bf16") = false);
+        py::arg("stats_slot_step") = py::none(), py::arg("stats_slot_offset") = 0, py::arg("round_bf16") = false,
+        py::arg("adam_ticket") = py::none());
   m.def("gemm_f32", &gemm_f32, "fp32-product MFMA GEMM: (C, rowsum of op(A) over K)", py::arg("A"),
         py::arg("a_kmajor"), py::arg("B"), py::arg("b_kmajor"), py::arg("A2") = py::none(), py::arg("B2") = py::none(),
         py::arg("bias") = py::none(), py::arg("out16") = false, py::arg("out") = py::none(),

@@ -157,6 +157,10 @@ __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
   __shared__ float red[1024];
   const int tid = threadIdx.x;
   const bool inA = (int)blockIdx.x < nblkA;
+  // a.step_advance (single-process graph replay): the step used is the
+  // device count + 1, published by the last workgroup to arrive (ticket);
+  // the count also names the statistics ring row (slot_step, same buffer)
+  const float st_new = a.step_advance ? *a.step_advance + 1.f : 0.f;
   const int cw = inA ? 64 : 16;
   const int nrg = 1024 / cw;
   const int ci = tid % cw, rg = tid / cw;
@@ -188,7 +192,7 @@ __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
   for (int k = 0; k < 8; ++k) acc[k] += acc[k + 8];
   red[tid] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
-  if (tid >= cw || !live) return;
+  if (tid < cw && live) {
   float g = 0.f;
   for (int k = 0; k < nrg; ++k) g += red[k * cw + tid];
   if (p < n_out) {
@@ -196,7 +200,12 @@ __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
     if (adam) {
       AdamScalars s;
       s.lr = a.lr; s.b1 = a.beta1; s.b2 = a.beta2; s.eps = a.eps; s.wd = a.weight_decay;
-      s.bc1 = a.bias_correction1; s.bc2_sqrt = a.bias_correction2_sqrt;
+      if (a.step_advance) {
+        s.bc1 = 1.f - powf(a.beta1, st_new);
+        s.bc2_sqrt = sqrtf(1.f - powf(a.beta2, st_new));
+      } else {
+        s.bc1 = a.bias_correction1; s.bc2_sqrt = a.bias_correction2_sqrt;
+      }
       s.gscale = a.grad_scale; s.decoupled = a.decoupled; s.maximize = a.maximize;
       s.amsgrad = 0;
       adam_elem(pv, g, m, v, nullptr, s);
@@ -214,6 +223,17 @@ __global__ void __launch_bounds__(1024) slab_reduce_adam_kernel(
     }
     const int64_t nt = PA + PB - n_out;
     tail_out[row * nt + p - n_out] = g;
+  }
+  }
+  if (a.step_advance) {
+    // every workgroup has read the old count (bias corrections, ring row)
+    // before it arrives; the last one publishes the new count and re-arms
+    // the ticket (kernel-boundary visibility for the next launch)
+    __syncthreads();
+    if (tid == 0 && atomicAdd(a.ticket, 1u) == gridDim.x - 1) {
+      *a.step_advance = st_new;
+      *a.ticket = 0u;
+    }
   }
 }
 

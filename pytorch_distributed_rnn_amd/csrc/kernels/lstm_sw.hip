@@ -74,9 +74,11 @@ PDRNN_DEVICE int pick(const int (&v)[NB], int n) {
   else if constexpr (NB == 2) return n == 0 ? v[0] : v[1];
   else return n == 0 ? v[0] : n == 1 ? v[1] : v[2];
 }
-// sequences per wave of a mode: 1 (0, 2, 4, 5, 6), 2 (1, 3), 3 (7: the
-// layer-split map of mode 2 with three sequences per layer wave)
-constexpr int sw_nb(int mode) { return mode == 7 ? 3 : (mode == 1 || mode == 3) ? 2 : 1; }
+// sequences per wave of a mode: 1 (0, 2, 4, 5, 6), 2 (1, 3).  (Three per
+// layer wave -- the mode-2 map at 960 waves for B = 1440, one per SIMD --
+// measured slower in both passes: forward +28 us, BPTT +20 us against modes
+// 6 / 3, profiles/r6/m7_ab.md; removed.)
+constexpr int sw_nb(int mode) { return (mode == 1 || mode == 3) ? 2 : 1; }
 
 // ---------------------------------------------------------------------------
 // Forward
@@ -1149,7 +1151,7 @@ extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
   if (!(e && *e) && backward) e = getenv("PDRNN_SW_MODE");
   if (e && *e) {
     const int m = atoi(e);
-    if (m >= 0 && m <= 7 && (m < 2 || NL == 2) && (m != 6 || !backward) && (m != 4 || backward) &&
+    if (m >= 0 && m <= 6 && (m < 2 || NL == 2) && (m != 6 || !backward) && (m != 4 || backward) &&
         (m != 5 || !backward))
       return m;
   }
@@ -1179,7 +1181,6 @@ extern "C" hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode
   if (mode == 2) return launch_fwd<2, 2>(a, st);
   if (mode == 3) return launch_fwd<2, 3>(a, st);
   if (mode == 6) return launch_fwd<2, 6>(a, st);
-  if (mode == 7) return launch_fwd<2, 7>(a, st);
   if (mode == 5) return launch_fwd4(a, st);
   return hipErrorInvalidValue;
 }
@@ -1199,7 +1200,6 @@ extern "C" hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode
   if (mode == 1) return launch_bwd<2, 1>(a, st);
   if (mode == 2) return launch_bwd<2, 2>(a, st);
   if (mode == 3) return launch_bwd<2, 3>(a, st);
-  if (mode == 7) return launch_bwd<2, 7>(a, st);
   if (mode == 4) {  // register dW: one slab row per workgroup; reads the x rows and the h sequence
     if (a->T % 4 || !a->slab || !a->xg_out || a->xg_ld > 16 || !a->hseq) return hipErrorInvalidValue;
     return launch_bwd<2, 4>(a, st);

@@ -137,15 +137,21 @@ class MotionTrainStep:
             # default: graph replay for the synced multi-GPU step (RCCL's eager
             # enqueue leaves ~13 us idle on each side of the all-reduce; at the
             # 8-GPU per-rank batch that is ~10 % of a step --
-            # profiles/r1_v5_graph_step.md); PDRNN_CUDA_GRAPH=0/1 overrides
+            # profiles/r1_v5_graph_step.md).  A single process replays its
+            # epochs from a graph only on request (PDRNN_CUDA_GRAPH=1 /
+            # cuda_graph=True): at B = 1440 the replay ran 1.5 % slower than
+            # the eager launches (0.3364 vs 0.3313 ms/step,
+            # profiles/r6/epoch_graph_world1.md)
             env = os.environ.get("PDRNN_CUDA_GRAPH")
             if env is not None:
                 cuda_graph = env == "1"
+            elif grad_sync is None:
+                cuda_graph = False
             else:
                 import torch.distributed as dist
                 # RCCL only: a gloo collective copies through the host and
                 # cannot be captured
-                cuda_graph = grad_sync is not None and dist.is_available() and dist.is_initialized() \
+                cuda_graph = dist.is_available() and dist.is_initialized() \
                     and dist.get_world_size() > 1 and dist.get_backend() == "nccl"
         self.cuda_graph = bool(cuda_graph)
         self._graph = None       # last replayed synced step (torch.cuda.CUDAGraph = hipGraph)
@@ -179,9 +185,11 @@ class MotionTrainStep:
         host copy sits between the steps: the batch indices of all steps reach
         the graph's static buffer in one copy before the replay.  Returns each
         step's statistics row, or None when this configuration runs per step
-        (no gradient sync / no graph replay, host-gathered batches, the first
-        two calls of a configuration)."""
-        if self.grad_sync is None or not self.cuda_graph:
+        (no graph replay, host-gathered batches, the first two calls of a
+        configuration).  Without gradient sync (one process) each captured
+        step is the fused step with Adam folded into its reduction, the
+        device step count advanced by that kernel's last workgroup."""
+        if not self.cuda_graph:
             return None
         if not idx_list or any(i is None for i in idx_list):
             return None
@@ -239,12 +247,15 @@ class MotionTrainStep:
         ent["step_host"] = c0 + n
         self._slot = (self._slot + n) % self.RING
         rows = [(int(c0) + k + ent["slot_off"]) % self.RING for k in range(n)]
-        out = []
-        for row, slot in zip(rows, slots):
-            if row != slot:
-                self.ring[slot].copy_(self.ring[row], non_blocking=True)
-            out.append(self.ring[slot])
-        return out
+        if rows != slots:
+            # the host's ring slots are out of step with the captured mapping:
+            # move the rows as one gather (the two ranges may overlap, so a
+            # row-by-row copy could overwrite a row before it is read)
+            dev = self.ring.device
+            src = torch.tensor(rows, dtype=torch.long).to(dev, non_blocking=True)
+            dst = torch.tensor(slots, dtype=torch.long).to(dev, non_blocking=True)
+            self.ring.index_copy_(0, dst, self.ring.index_select(0, src))
+        return [self.ring[slot] for slot in slots]
 
     def _epoch_key(self, features: Tensor, labels: Tensor, sizes, idx_dtype, adam):
         from ..ops.lstm import fused_bwd_nb, small_launch_config
@@ -268,7 +279,7 @@ class MotionTrainStep:
         capture -- then the capture itself, which runs nothing.  Parameters
         and optimizer state are untouched; the flat gradient (rewritten by
         every step) is left zeroed.  True when the graph is ready."""
-        if self.grad_sync is None or not self.cuda_graph or not sizes:
+        if not self.cuda_graph or not sizes:
             return False
         adam = self._flat_adam_peek()
         if adam is None:
@@ -280,7 +291,8 @@ class MotionTrainStep:
         if key in graphs and graphs[key]["graph"] is not None:
             return True
         self.flat.attach_grads()
-        self.grad_sync()
+        if self.grad_sync is not None:
+            self.grad_sync()
         self.flat.grad.zero_()
         ent = {"graph": None, "eager": 0}
         try:
@@ -314,6 +326,16 @@ class MotionTrainStep:
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for view, ((nb, sp), nb_bwd) in zip(views, cfgs):
                 ws, feats, cell = self._operands(features)  # GRU: re-packed from the updated parameters
+                if self.grad_sync is None:
+                    # one process: Adam folded into the reduction, which
+                    # advances the device step count (the hyper-parameters'
+                    # step slot is unused)
+                    self.mod.lstm_head_train_step(feats, view, labels, ws, hw, hb, self.flat.grad, self.ring,
+                                                  self.H, self.NL, sp, 0, nb, nb_bwd, [p, m, v],
+                                                  [lr, b1, b2, eps, wd, 1.0, dec], cell, self.colmap,
+                                                  ent["step"], ent["slot_off"], round_bf16=self.bf16,
+                                                  adam_ticket=ent["ticket"])
+                    continue
                 self.mod.lstm_head_train_step(feats, view, labels, ws, hw, hb, self.flat.grad, self.ring,
                                               self.H, self.NL, sp, 0, nb, nb_bwd, None, None, cell, self.colmap,
                                               ent["step"], ent["slot_off"], round_bf16=self.bf16)

@@ -435,3 +435,79 @@ def test_horovod_mode_rccl(rccl_group):
     t = torch.ones(10, device="cuda")
     hvd.allreduce_(t, average=True)
     torch.testing.assert_close(t, torch.ones(10, device="cuda"))
+
+
+def _fail_inside_capture(step):
+    """Make every later graph capture of ``step`` raise part-way through: its
+    gradient sync raises while the stream is capturing (after the fused
+    step's kernels are already in the graph), as a first world > 1 RCCL
+    capture might; eager calls are untouched."""
+    orig = step.grad_sync
+    hits = []
+
+    def grad_sync():
+        if torch.cuda.is_current_stream_capturing():
+            hits.append(1)
+            raise RuntimeError("injected capture failure")
+        return orig()
+    step.grad_sync = grad_sync
+    return hits
+
+
+@pytest.mark.parametrize("site", ["run_steps", "prepare_epoch", "per_step"])
+def test_graph_capture_failure_falls_back_to_eager(rccl_group, site):
+    """a HIP-graph capture that fails mid-capture on the
+    synced path -- the epoch graph of ``run_steps``, its ahead-of-time
+    capture in ``prepare_epoch``, and the per-step ``_capture`` -- leaves the
+    stream out of capture mode, turns graph replay off for good (or, for
+    ``prepare_epoch``, reports False) and the eager steps that follow
+    reproduce the local fp32 trajectory (statistics, parameters, step count)."""
+    import warnings
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_rnn_amd.train.fused_step import MotionTrainStep
+    from pytorch_distributed_rnn_amd.utils.flat import flatten_module
+    torch.manual_seed(9)
+    n_train, bs = 448, 96
+    train, _, _ = synthetic_motion(n_train=n_train, n_validation=1, n_test=1, seed=9)
+    feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
+    m1 = MotionModel(9, 32, 2, 6).cuda()
+    m2 = copy.deepcopy(m1)
+    flatten_module(m2)
+    ddp = DistributedDataParallel(m1)
+    o1, o2 = FusedAdam(m1.parameters(), lr=2.5e-3), FusedAdam(m2.parameters(), lr=2.5e-3)
+    s1 = MotionTrainStep(ddp, o1, ddp.reducer.all_reduce_inline, cuda_graph=True)
+    s2 = MotionTrainStep(m2, o2, None, cuda_graph=False)
+    hits = _fail_inside_capture(s1)
+    g = torch.Generator().manual_seed(4)
+    epochs = [list(torch.split(torch.randperm(n_train, generator=g).cuda(), bs)) for _ in range(4)]
+    if site == "prepare_epoch":
+        with warnings.catch_warnings(record=True):
+            warnings.simplefilter("always")
+            assert s1.prepare_epoch(feats, labels, [i.numel() for i in epochs[0]]) is False
+        assert hits and not torch.cuda.is_current_stream_capturing()
+    outs = []
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        for idx_list in epochs:
+            if site == "per_step":
+                a = [s1(feats, labels, i).clone() for i in idx_list]
+            else:
+                res = s1.run_steps(feats, labels, idx_list)
+                assert res is None, "a failed capture must leave the epoch to the eager steps"
+                a = [s1(feats, labels, i).clone() for i in idx_list]
+            assert not torch.cuda.is_current_stream_capturing()
+            b = [s2(feats, labels, i).clone() for i in idx_list]
+            outs.append((a, b))
+    assert hits, "the capture was never attempted"
+    assert any("capture" in str(w.message) for w in caught)
+    assert s1.cuda_graph is False and not s1._graphs
+    for a, b in outs:
+        for x, y in zip(a, b):
+            torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+    steps = sum(len(e) for e in epochs)
+    assert o1.state_dict()["state"][0]["step"] == o2.state_dict()["state"][0]["step"] == steps

@@ -473,3 +473,49 @@ def test_direct_grads_match_autograd_accumulation(cell):
         grads.append([p.grad.clone() for p in m1.parameters()])
     for (k, _), g1, g2 in zip(m1.named_parameters(), *grads):
         assert torch.allclose(g1, g2, atol=1e-7, rtol=1e-5), k
+
+
+@pytest.mark.parametrize("n_train,bs", [(448, 96), (6912, 1440)])
+def test_single_process_epoch_graph_matches_eager(n_train, bs):
+    """One process: every step of an epoch replayed as ONE HIP graph (fused
+    step with Adam folded into the reduction, whose last workgroup advances
+    the device step count) equals the eager per-step launches -- statistics,
+    parameters and the optimizer's step count -- over five epochs, the ring
+    slots shifted out of step once (the copy fallback)."""
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    from pytorch_distributed_rnn_amd.ops.adam import FusedAdam
+    from pytorch_distributed_rnn_amd.train.fused_step import MotionTrainStep
+    from pytorch_distributed_rnn_amd.utils.flat import flatten_module
+    torch.manual_seed(6)
+    train, _, _ = synthetic_motion(n_train=n_train, n_validation=1, n_test=1, seed=6)
+    feats, labels = train.features.cuda(), train.labels.cuda().reshape(-1)
+    m1 = MotionModel(9, 32, 2, 6).cuda()
+    m2 = copy.deepcopy(m1)
+    flatten_module(m1)
+    flatten_module(m2)
+    o1, o2 = FusedAdam(m1.parameters(), lr=2.5e-3), FusedAdam(m2.parameters(), lr=2.5e-3)
+    s1 = MotionTrainStep(m1, o1, None, cuda_graph=True)
+    s2 = MotionTrainStep(m2, o2, None)
+    assert s1.cuda_graph and not s2.cuda_graph
+    g = torch.Generator().manual_seed(3)
+    replays = 0
+    for e in range(5):
+        idx_list = list(torch.split(torch.randperm(n_train, generator=g).cuda(), bs))
+        if e == 4:
+            s1._slot = (s1._slot + 3) % s1.RING
+        res = s1.run_steps(feats, labels, idx_list)
+        if res is None:
+            res = [s1(feats, labels, i) for i in idx_list]
+        else:
+            replays += 1
+        a = [r.clone() for r in res]
+        assert s2.run_steps(feats, labels, idx_list) is None
+        b = [s2(feats, labels, i).clone() for i in idx_list]
+        for k, (x, y) in enumerate(zip(a, b)):
+            torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6, msg=lambda m: f"epoch {e} step {k}: {m}")
+    assert replays == 3, "the epoch was never replayed from a graph"
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+    steps = 5 * len(idx_list)
+    assert o1.state_dict()["state"][0]["step"] == o2.state_dict()["state"][0]["step"] == steps
