@@ -132,10 +132,10 @@ def main(argv=None):
             yield from loader.batch_indices()
             epoch += 1
 
-    # PDRNN_BENCH_TRACE=1: where the wall time of a timed run goes (stderr):
+    # PDRNN_TRACE=bench: where the wall time of a timed run goes (stderr):
     # host time to the first step's launch, host enqueue time, device time
     # between events bracketing the run, the final synchronize and barrier
-    trace = os.environ.get("PDRNN_BENCH_TRACE") == "1" and dev.type == "cuda"
+    trace = os.environ.get("PDRNN_TRACE") == "bench" and dev.type == "cuda"
 
     def timed_run(batches, per_step=False):
         env.barrier()

@@ -58,8 +58,7 @@ def main():
             out, (hn, cn) = ref(x)
             hn[-1].sum().backward()
 
-        r = dict(B=B, nb_fwd=os.environ.get("PDRNN_LSTM_NB_FWD", "auto"),
-                 nb_bwd=os.environ.get("PDRNN_LSTM_NB_BWD", "auto"),
+        r = dict(B=B, tune=os.environ.get("PDRNN_TUNE", ""),
                  fused_fwd_ms=timeit(fused_fwd), fused_fwd_save_ms=timeit(fused_fwd_save),
                  fused_train_ms=timeit(fused_fwdbwd),
                  torch_fwd_ms=timeit(ref_fwd), torch_train_ms=timeit(ref_fwdbwd))

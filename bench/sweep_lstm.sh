@@ -5,7 +5,7 @@ out=${1:-gpurun_out/sweep.log}
 for sb in 2 4; do
   for sf in 2 4 8; do
     for nb in 1 2; do
-      PDRNN_LSTM_SPLIT_FWD=$sf PDRNN_LSTM_SPLIT_BWD=$sb PDRNN_LSTM_NB_FWD=$nb \
+      PDRNN_TUNE=split_fwd=$sf,split_bwd=$sb,nb_fwd=$nb \
         timeout -k 10 120 python bench/kernels.py --batches 1440,720,360,180 | sed "s/^/sf=$sf sb=$sb nb=$nb /" >> $out
     done
   done

@@ -6,6 +6,6 @@ out=${1:-gpurun_out/sweep_nb.log}
 for nbf in 1 2; do
   for nbb in 1 2 3; do
     echo "nb_fwd=$nbf nb_bwd=$nbb" >> $out
-    PDRNN_LSTM_NB_FWD=$nbf PDRNN_LSTM_NB_BWD=$nbb timeout -k 10 120 python bench.py --steps 50 --warmup 10 2>/dev/null | tail -1 >> $out
+    PDRNN_TUNE=nb_fwd=$nbf,nb_bwd=$nbb timeout -k 10 120 python bench.py --steps 50 --warmup 10 2>/dev/null | tail -1 >> $out
   done
 done

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <atomic>
 #include <map>
+#include <mutex>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 
@@ -24,10 +25,16 @@ bool stamps_enabled() {
   return on;
 }
 // PDRNN_SW=0: the fused motion step runs the gate-split / K-split kernel family
-// instead of the sequence-in-wave kernels (A/B); read per call (tests flip it)
+// instead of the sequence-in-wave kernels (A/B); PDRNN_SW=2 keeps the
+// sequence-in-wave kernels but launches the latency regime's forward and
+// BPTT separately (no one-launch step); read per call
 bool sw_enabled() {
   const char* e = std::getenv("PDRNN_SW");
   return !(e && e[0] == '0');
+}
+bool sw_one_launch_enabled() {
+  const char* e = std::getenv("PDRNN_SW");
+  return !(e && (e[0] == '0' || e[0] == '2'));
 }
 void report_stamps(const char* what, const Tensor& st, int iters) {
   // [grid, 8]: loop start / end shader cycles, loop start / end real time,
@@ -131,11 +138,10 @@ void report_stamps(const char* what, const Tensor& st, int iters) {
   }
   fprintf(stderr, "\n");
 }
-// progress-ordered wave priority in the small-H recurrences (PDRNN_PRIO=0 off):
+// progress-ordered wave priority in the small-H recurrences (PDRNN_TUNE prio=0 off):
 // B = 1440: 0.403 -> 0.387 ms/step (profiles/r3p_prio.md); rotation every 2^3 step pairs
 int prio_env() {
-  const char* e = std::getenv("PDRNN_PRIO");
-  const int mode = e ? std::atoi(e) : 2;
+  const int mode = pdrnn_tune_int("prio", 2);
   const int sh = 3;
   static int cus = 0;  // one GPU model per process
   if (!cus) {
@@ -454,7 +460,6 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   Tensor act = at::empty({NL * B * T * 5 * H + PADR * 5 * H}, opts);
   Tensor hn = at::empty({NL, B, H}, opts), cn = at::empty({NL, B, H}, opts);
   Tensor dh_top = at::empty({B, H}, opts);
-  Tensor head_slab = at::empty({B, PH}, opts);
   if (split_fwd <= 0) split_fwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 0);
   if (split_bwd <= 0) split_bwd = pdrnn_lstm_small_max_split((int)H, (int)NL, 1);
   if (cell == 1) split_fwd = 1;  // GRU: gate-split forward only
@@ -475,6 +480,11 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const int sw_fmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 0) : -1;
   int sw_bmode = sw ? pdrnn_lstm_sw_mode((int)NL, (int)B, 1) : -1;
   if (sw_bmode == 4 && T % 4) sw_bmode = 2;  // register dW: whole 4-step K steps
+  // sequence-in-wave latency regime (forward mode 5, backward mode 4): one
+  // launch for forward + BPTT per step (lstm_sw_step_kernel)
+  const bool sw_step = sw && sw_fmode == 5 && sw_bmode == 4 && !stamps_enabled() && sw_one_launch_enabled() &&
+                       pdrnn_lstm_sw_step_ok((int)NL, (int)B, (int)T) == 1;
+  Tensor head_slab = at::empty({B, PH}, opts);
   // Above one residency round the BPTT defers its weight gradients: the
   // recurrence writes the gate gradients (into `act`, in place) and the
   // matrix-core kernel lstm_small_dw forms dW / db over all B*T rows, one slab
@@ -535,7 +545,9 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   const bool one_launch = !dwout && !st_f.defined() &&
       pdrnn_lstm_small_step_ok((int)H, (int)NL, (int)B, (int)nb_fwd, (int)split_fwd, (int)nb_bwd, (int)split_bwd,
                                gridb) == 1;
-  if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_fwd(&f, sw_fmode, st));
+  if (sw_step) {
+    // (launched with the backward below)
+  } else if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_fwd(&f, sw_fmode, st));
   else if (!one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_fwd(&f, (int)H, (int)nb_fwd, (int)split_fwd, 1, st));
 
   PdrnnLstmSmallBwdArgs bk{};
@@ -577,7 +589,8 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
     }
     dw.B = (int)B; dw.T = (int)T; dw.I = (int)I; dw.NL = (int)NL; dw.chunks = slab_rows;
   }
-  if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_bwd(&bk, sw_bmode, st));
+  if (sw_step) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_step(&f, &bk, st));
+  else if (sw) HIP_LAUNCH_CHECK(pdrnn_lstm_sw_bwd(&bk, sw_bmode, st));
   else if (one_launch) HIP_LAUNCH_CHECK(pdrnn_lstm_small_step(&f, &bk, (int)H, st));
   else if (dwout) HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd_dwout(&bk, (int)H, grid_dw, nb_dw, st));
   else HIP_LAUNCH_CHECK(pdrnn_lstm_small_bwd(&bk, (int)H, (int)nb_bwd, (int)split_bwd, gridb, st));
@@ -950,11 +963,10 @@ Tensor persist_sticky_flag() {
 }
 
 // Row-owning fp32 recurrence at H = 128 (kernels/lstm_rows_f32.hip) instead of
-// the per-step / persistent kernels; PDRNN_LSTM_ROWS=0 turns it off (A/B).
+// the per-step / persistent kernels; PDRNN_TUNE rows=0 turns it off (A/B).
 bool rows_f32_on() {
   static const bool on = [] {
-    const char* e = std::getenv("PDRNN_LSTM_ROWS");
-    return !(e && std::atoi(e) == 0);
+    return pdrnn_tune_int("rows", 1) != 0;
   }();
   return on;
 }
@@ -1468,6 +1480,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "(sequences per workgroup, grid) of the deferred-dW backward for this shape");
   m.def("lstm_sw_ok", [](int64_t H, int64_t I, int64_t NL) { return pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, 0) == 1; },
         "the sequence-in-wave kernels (lstm_sw.hip) cover this LSTM stack in the fused train step");
+  m.def("lstm_sw_step_ok", [](int64_t NL, int64_t B, int64_t T) {
+    return pdrnn_lstm_sw_step_ok((int)NL, (int)B, (int)T) == 1;
+  }, "the one-launch sequence-in-wave step (forward + BPTT in one kernel) covers this batch");
   m.def("lstm_sw_fits", [](int64_t NL, int64_t B, int64_t T) { return pdrnn_lstm_sw_fits((int)NL, (int)B, (int)T) == 1; },
         "every act / hseq row of this batch fits the sequence-in-wave kernels' 2 GiB buffer descriptor");
   m.def("lstm_sw_mode", [](int64_t NL, int64_t B, bool backward) { return pdrnn_lstm_sw_mode((int)NL, (int)B, backward ? 1 : 0); },

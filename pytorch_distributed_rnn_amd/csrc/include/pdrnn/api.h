@@ -175,7 +175,7 @@ int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell);
 int pdrnn_lstm_sw_fits(int NL, int B, int T);
 // sequences per wave (and per workgroup) of a sequence-in-wave mode
 int pdrnn_lstm_sw_nb(int mode);
-// mode for a batch of B sequences (PDRNN_SW_MODE overrides): 0, 1 or 2
+// mode for a batch of B sequences (PDRNN_TUNE sw_mode / sw_bwd_mode override)
 int pdrnn_lstm_sw_mode(int NL, int B, int backward);
 hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode, hipStream_t stream);
 hipError_t pdrnn_lstm_sw_bwd(const PdrnnLstmSmallBwdArgs* a, int mode, hipStream_t stream);
@@ -222,6 +222,15 @@ hipError_t pdrnn_xent_bwd(const float* dlogits, const float* grad_out, const flo
                           int64_t n, hipStream_t stream);
 
 // ----------------------------------------------------------------------------
+// Tuning overrides (runtime/tune.cpp): PDRNN_TUNE="key=value,...".  _str
+// copies the value of `key` into out (NUL-terminated) and returns 1 when the
+// key is present; _int returns its integer value, or dflt when absent / not
+// an integer.
+// ----------------------------------------------------------------------------
+int pdrnn_tune_str(const char* key, char* out, int out_len);
+int pdrnn_tune_int(const char* key, int dflt);
+
+// ----------------------------------------------------------------------------
 // Fused Adam / AdamW over flat fp32 buffers (torch.optim.Adam semantics).
 // ----------------------------------------------------------------------------
 typedef struct {
@@ -248,6 +257,12 @@ typedef struct {
   const int* skip;
 } PdrnnAdamArgs;
 hipError_t pdrnn_adam_flat(const PdrnnAdamArgs* a, hipStream_t stream);
+
+// One launch per training step in the latency regime (two layers, B <= two
+// workgroups per CU, T % 4 == 0): forward mode 5 + head/CE, then BPTT mode 4
+// with its matrix-core dW waves (kernels/lstm_sw.hip lstm_sw_step_kernel).
+int pdrnn_lstm_sw_step_ok(int NL, int B, int T);
+hipError_t pdrnn_lstm_sw_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBwdArgs* b, hipStream_t stream);
 // g *= min(1, max_norm / (||g|| + eps)) with no host sync; work: [nparts]
 // floats (nparts <= 1024 partial sums of squares), out: [2] = (scale, norm).
 hipError_t pdrnn_clip_flat(float* g, int64_t n, float max_norm, float eps, float* work, int nparts, float* out,

@@ -33,7 +33,11 @@ PDRNN_DEVICE void motion_head(const PdrnnLstmSmallFwdArgs& a, int b, float h, in
     if (cc < C) se += expf(lg[cc] - m);
   const float lse = m + logf(se);
   const float inv_se = 1.f / se;
-  float* srow = a.slab + (int64_t)b * a.slab_P;
+  const __amdgpu_buffer_rsrc_t r_slab = uniform_rsrc(a.slab);
+  const uint32_t srow = (uint32_t)b * (uint32_t)a.slab_P;
+  auto sst = [&](int e, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r_slab, (srow + (uint32_t)e) * 4u, 0, 0);
+  };
   float dh = 0.f;
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -41,15 +45,15 @@ PDRNN_DEVICE void motion_head(const PdrnnLstmSmallFwdArgs& a, int b, float h, in
     if (cc < C) {
       const float d = (expf(lg[cc] - m) * inv_se - (cc == lab ? 1.f : 0.f)) * a.inv_batch;
       dh = fmaf(a.head_w[cc * 32 + u], d, dh);
-      if (!odd) srow[a.head_off_w + cc * 32 + u] = d * h;
-      if (lane == 0 && a.head_b) srow[a.head_off_b + cc] = d;
+      if (!odd) sst(a.head_off_w + cc * 32 + u, d * h);
+      if (lane == 0 && a.head_b) sst(a.head_off_b + cc, d);
     }
   }
   if (!odd) a.dh_top[(int64_t)b * 32 + u] = dh;
   if (lane == 0) {
-    srow[a.stat_off + 0] = (lse - logit_y) * a.inv_batch;
-    srow[a.stat_off + 1] = 1.f;
-    srow[a.stat_off + 2] = amax == lab ? 1.f : 0.f;
+    sst(a.stat_off + 0, (lse - logit_y) * a.inv_batch);
+    sst(a.stat_off + 1, 1.f);
+    sst(a.stat_off + 2, amax == lab ? 1.f : 0.f);
   }
 }
 

@@ -865,11 +865,10 @@ __global__ void __launch_bounds__(512) lstm_large_bwd_gemm_pp_kernel(PdrnnLstmLa
 // The same fused form for the backward step measured 2353 us (its two-pass
 // cell epilogue kept too many registers live beside the accumulators and the
 // fp16 build spilled inside the main loop; profiles/r3_pp_step/) and was
-// replaced by the GEMM + cell pair below.  PDRNN_LSTM_LARGE_PP=0 opts out,
+// replaced by the GEMM + cell pair below.  PDRNN_TUNE large_pp=0 opts out,
 // =2 takes it at any legal shape (tests).
 inline bool use_pp_step(int B, int N, int ndir, int dsize, bool backward) {
-  const char* e = getenv("PDRNN_LSTM_LARGE_PP");
-  const int env = e ? atoi(e) : 1;
+  const int env = pdrnn_tune_int("large_pp", 1);
   if (!env || backward || dsize != 2 || N % 256) return false;
   if (env == 2) return true;
   return B >= 128 && (int64_t)(N / 256) * ((B + 255) / 256) * ndir >= 256;
@@ -1522,8 +1521,7 @@ int pdrnn_lstm_large_supported(int H) { return H >= 64 && H % 64 == 0; }
 // -6 % step time); small batches: 32x32 tiles, slices while < 512 workgroups
 // and each slice keeps >= 8 k-tiles (char-LM h1024 B128: 4 slices).
 int pdrnn_lstm_large_bwd_pp(int B, int H, int ndir, int dtype) {
-  const char* e = getenv("PDRNN_LSTM_LARGE_PP_BWD");
-  const int env = e ? atoi(e) : 1;
+  const int env = pdrnn_tune_int("large_pp_bwd", 1);  // (0 off, 2 at any legal shape)
   if (!env || (dtype != 0 && dtype != 1) || H % 256) return 0;
   if (env == 2) return 1;
   return B >= 128 && (int64_t)(H / 256) * ((B + 255) / 256) * ndir >= 256;

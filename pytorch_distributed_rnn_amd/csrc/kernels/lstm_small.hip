@@ -1807,12 +1807,11 @@ int bwd_dwout_cap(int NL, int T, int cell) {
 
 // Sequences per workgroup of the deferred-dW backward: 2 when pairing the
 // sequences takes fewer residency rounds than one per workgroup (B = 1152 /
-// 1440 at H = 32: one round instead of two), else 1.  PDRNN_DWOUT_NB=1|2
+// 1440 at H = 32: one round instead of two), else 1.  PDRNN_TUNE dwout_nb=1|2
 // forces one (A/B measurements).
 template <int H>
 int bwd_dwout_nb(int NL, int T, int B, int cell) {
-  const char* e = getenv("PDRNN_DWOUT_NB");  // per call: tests flip it in-process
-  const int env = e ? atoi(e) : 0;
+  const int env = pdrnn_tune_int("dwout_nb", 0);  // per call: tests flip it in-process
   if (env == 1 || env == 2) return env;
   if (H > 32 || NL * H * dwout_lanes<H>() > 512) return 1;
   const int cap1 = bwd_dwout_cap<H, 1>(NL, T, cell), cap2 = bwd_dwout_cap<H, 2>(NL, T, cell);
@@ -1864,13 +1863,13 @@ hipError_t launch_bwd_dwout(const PdrnnLstmSmallBwdArgs* a, hipStream_t st, int 
 
 extern "C" {
 
-// PDRNN_LSTM_DWOUT=0 disables the deferred-dW backward, =force selects it at
+// PDRNN_TUNE dwout=0 disables the deferred-dW backward, dwout=force selects it at
 // every batch size (tests: the one-launch step would otherwise take B <= one
 // residency round).  Returns 0 (not covered), 1 (covered), 2 (covered, forced).
 int pdrnn_lstm_small_dwout_ok(int H, int NL, int T) {
   // read per call (one host query per training step): tests flip it in-process
-  const char* e = getenv("PDRNN_LSTM_DWOUT");
-  const int mode = !e ? 1 : (e[0] == '0' ? 0 : (strcmp(e, "force") == 0 ? 2 : 1));
+  char e[16];
+  const int mode = !pdrnn_tune_str("dwout", e, (int)sizeof(e)) ? 1 : (e[0] == '0' ? 0 : (strcmp(e, "force") == 0 ? 2 : 1));
   if (mode == 0 || T < 4 || NL < 1 || NL > PDRNN_MAX_LAYERS) return 0;
   if (H != 16 && H != 32 && H != 64) return 0;
   if ((size_t)T * H * sizeof(float) > (size_t)pdrnn::kXldsBytes) return 0;  // LDS-resident x only

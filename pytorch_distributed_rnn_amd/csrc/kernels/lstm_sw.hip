@@ -38,6 +38,7 @@
 #include "pdrnn/common.h"
 #include "pdrnn/motion_head.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -468,7 +469,7 @@ PDRNN_DEVICE Fwd4W<NC> load_fwd4_w(const PdrnnLstmSmallFwdArgs& a, int l, int u,
   return W;
 }
 
-__global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs a) {
+PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -598,6 +599,7 @@ __global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs
     }
   }
 }
+__global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs a) { fwd4_body(a); }
 
 // ---------------------------------------------------------------------------
 // Backward (lean contract: zero initial state, dL/dh_T of the top layer only,
@@ -653,8 +655,7 @@ PDRNN_DEVICE float col_dot(const BwdCol& W, const float4 (&g)[16]) {
 // (no occupancy target: at 168 VGPRs the split backward spills, and it only
 // runs at B <= one wave per SIMD)
 template <int NL, int MODE>
-__global__ void __launch_bounds__(MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64)
-lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
+PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
   constexpr int NB = sw_nb(MODE);
   constexpr bool SPLIT = MODE >= 2;
   // mode 4: the mode-2 map plus two waves that accumulate the weight
@@ -859,7 +860,11 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
     }
     // this workgroup's slab row (an empty slot recomputed sequence B - 1: its
     // row must still be written, as zeros, since the reduction sums every row)
-    float* srow = a.slab + (int64_t)blockIdx.x * a.P;
+    const __amdgpu_buffer_rsrc_t r_slab = uniform_rsrc(a.slab);
+    const uint32_t srow = (uint32_t)blockIdx.x * (uint32_t)a.P;  // (element offsets; the slab is far below 2 GiB)
+    auto sst = [&](int64_t e, float v) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r_slab, (uint32_t)(srow + e) * 4u, 0, 0);
+    };
     const int Iin = L == 0 ? a.I : kH;
     const int c = lane & 15, r4 = 4 * (lane >> 4);
     const float keep = valid[0] ? 1.f : 0.f;
@@ -869,20 +874,24 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * mt + r4 + r;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) srow[a.off_whh[L] + (int64_t)row * kH + 16 * nt + c] = keep * ahh[mt][nt][r];
+        for (int nt = 0; nt < 2; ++nt) sst(a.off_whh[L] + (int64_t)row * kH + 16 * nt + c, keep * ahh[mt][nt][r]);
 #pragma unroll
         for (int nt = 0; nt < NI; ++nt) {
           const int col = 16 * nt + c;
-          if (col < Iin) srow[a.off_wih[L] + (int64_t)row * Iin + col] = keep * aih[mt][nt][r];
+          if (col < Iin) sst(a.off_wih[L] + (int64_t)row * Iin + col, keep * aih[mt][nt][r]);
         }
       }
   };
   auto db_store = [&](int l) {
-    float* srow = a.slab + (int64_t)blockIdx.x * a.P;
+    const __amdgpu_buffer_rsrc_t r_slab = uniform_rsrc(a.slab);
+    const uint32_t srow = (uint32_t)blockIdx.x * (uint32_t)a.P;
+    auto sst = [&](int64_t e, float v) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r_slab, (uint32_t)(srow + e) * 4u, 0, 0);
+    };
     const float d0 = valid[0] ? dbs[0] : 0.f, d1 = valid[0] ? dbs[1] : 0.f;
     const int r0 = 2 * s * kH + u, r1 = r0 + kH;
-    if (a.off_bih[l] >= 0) { srow[a.off_bih[l] + r0] = d0; srow[a.off_bih[l] + r1] = d1; }
-    if (a.off_bhh[l] >= 0) { srow[a.off_bhh[l] + r0] = d0; srow[a.off_bhh[l] + r1] = d1; }
+    if (a.off_bih[l] >= 0) { sst(a.off_bih[l] + r0, d0); sst(a.off_bih[l] + r1, d1); }
+    if (a.off_bhh[l] >= 0) { sst(a.off_bhh[l] + r0, d0); sst(a.off_bhh[l] + r1, d1); }
   };
 
   // layer-generic pieces
@@ -1071,6 +1080,31 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
     st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
   }
 }
+template <int NL, int MODE>
+__global__ void __launch_bounds__(MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64)
+lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
+  bwd_body<NL, MODE>(a);
+}
+
+// ---------------------------------------------------------------------------
+// One-launch step (latency regime: B <= two workgroups per CU, two layers).
+// Workgroup b runs sequence b's four-wave forward (mode 5) with the head/CE,
+// then -- no grid-wide dependency between the passes -- the same sequence's
+// BPTT with its two matrix-core dW waves (mode 4): each sequence's backward
+// starts the moment its own forward ends instead of after the slowest
+// workgroup of a forward launch.  Every operand the backward reads (act,
+// hseq, the staged x rows, dh_T) was written by the same workgroup: a
+// __syncthreads() (which drains vmcnt on gfx950) orders them.  The slab
+// reduction stays a launch of its own: inside this one (device-coherent slab
+// stores, an arrival counter, every workgroup summing a column slice) it cost
+// 15 us against 7 for the separate launch, and a release fence instead of
+// the coherent stores 35 (profiles/r6/one_launch_step.md).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) lstm_sw_step_kernel(PdrnnLstmSmallFwdArgs f, PdrnnLstmSmallBwdArgs bk) {
+  fwd4_body(f);
+  __syncthreads();  // the forward's outputs (act, hseq, x rows, dh_T) before the backward reads them
+  bwd_body<2, 4>(bk);
+}
 
 // ---- host side -------------------------------------------------------------
 int sw_cus() {
@@ -1144,13 +1178,12 @@ extern "C" int pdrnn_lstm_sw_fits(int NL, int B, int T) {
 // the matrix cores, no dW launch; 55.7 us against 54.7 + 16.9 at B = 180,
 // profiles/r5/sw/dw4_probe.log; T % 4 == 0, the caller falls back to mode 2
 // otherwise).  One layer: one wave per sequence (mode 0),
-// two above one wave per SIMD (mode 1).  PDRNN_SW_MODE / PDRNN_SW_BWD_MODE
-// override.
+// two above one wave per SIMD (mode 1).  PDRNN_TUNE sw_mode / sw_bwd_mode
+// override (sw_mode alone: both passes).
 extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
-  const char* e = getenv(backward ? "PDRNN_SW_BWD_MODE" : "PDRNN_SW_MODE");
-  if (!(e && *e) && backward) e = getenv("PDRNN_SW_MODE");
-  if (e && *e) {
-    const int m = atoi(e);
+  int m = pdrnn_tune_int(backward ? "sw_bwd_mode" : "sw_mode", -1);
+  if (m < 0 && backward) m = pdrnn_tune_int("sw_mode", -1);
+  if (m >= 0) {
     if (m >= 0 && m <= 6 && (m < 2 || NL == 2) && (m != 6 || !backward) && (m != 4 || backward) &&
         (m != 5 || !backward))
       return m;
@@ -1163,6 +1196,33 @@ extern "C" int pdrnn_lstm_sw_mode(int NL, int B, int backward) {
 }
 
 extern "C" int pdrnn_lstm_sw_nb(int mode) { return mode_nb(mode); }
+
+namespace {
+size_t step_lds(int T) { return std::max(sizeof(float) * (2 * 2 * kHB + (size_t)T * kXS), bwd_lds(2, 1, 8)); }
+}  // namespace
+
+extern "C" int pdrnn_lstm_sw_step_ok(int NL, int B, int T) {
+  if (NL != 2 || B <= 0 || T <= 0 || T % 4 || !pdrnn_lstm_sw_fits(NL, B, T)) return 0;
+  if (pdrnn_lstm_sw_mode(NL, B, 0) != 5 || pdrnn_lstm_sw_mode(NL, B, 1) != 4) return 0;
+  return step_lds(T) <= 64 * 1024 ? 1 : 0;
+}
+
+extern "C" hipError_t pdrnn_lstm_sw_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBwdArgs* b,
+                                         hipStream_t st) {
+  if (!pdrnn_lstm_sw_ok(kH, f->I, f->NL, f->cell) || f->NL != 2 || f->h0 || f->c0) return hipErrorInvalidValue;
+  if (!f->act || !f->hseq || f->B <= 0 || f->T <= 0 || f->T % 4 || !pdrnn_lstm_sw_fits(f->NL, f->B, f->T))
+    return hipErrorInvalidValue;
+  if (!f->head_w || f->C > 16 || f->C < 1 || !f->labels || !f->slab || !f->dh_top) return hipErrorInvalidValue;
+  if (!f->xg_out || f->xg_ld < f->I || f->xg_ld > 16) return hipErrorInvalidValue;
+  if (b->B != f->B || b->T != f->T || b->NL != 2 || b->act != f->act || b->hseq != f->hseq || b->dhn != f->dh_top ||
+      !b->dhn_top_only || !b->slab || b->xg_out != f->xg_out || b->h0 || b->c0 || b->dout || b->dcn || b->dx ||
+      b->dh0 || b->dc0)
+    return hipErrorInvalidValue;
+  const size_t lds = step_lds(f->T);
+  if (lds > 64 * 1024) return hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(lstm_sw_step_kernel, dim3(f->B), dim3(256), lds, st, *f, *b);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t pdrnn_lstm_sw_fwd(const PdrnnLstmSmallFwdArgs* a, int mode, hipStream_t st) {
   if (!pdrnn_lstm_sw_ok(kH, a->I, a->NL, a->cell) || a->h0 || a->c0) return hipErrorInvalidValue;

@@ -20,13 +20,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
-
-
-def _env_int(name: str, default: int) -> int:
-    try:
-        return int(os.environ.get(name, default))
-    except ValueError:
-        return default
+from ..utils.tune import tune_int
 
 
 def small_launch_config(batch: int, hidden: int, num_layers: int = 2) -> Tuple[int, int, int, int]:
@@ -35,12 +29,12 @@ def small_launch_config(batch: int, hidden: int, num_layers: int = 2) -> Tuple[i
     ``nb``: sequences per workgroup (weights in VGPRs are shared by them);
     ``split``: lanes per hidden unit (more lanes = shorter per-timestep
     critical path).  Small batches are latency-bound -> widest split, one
-    sequence per workgroup.  Env overrides (for sweeps): PDRNN_LSTM_NB_FWD,
-    PDRNN_LSTM_SPLIT_FWD, PDRNN_LSTM_NB_BWD, PDRNN_LSTM_SPLIT_BWD."""
-    nb_fwd = _env_int("PDRNN_LSTM_NB_FWD", 0)
-    nb_bwd = _env_int("PDRNN_LSTM_NB_BWD", 0)
-    sp_fwd = _env_int("PDRNN_LSTM_SPLIT_FWD", 0)
-    sp_bwd = _env_int("PDRNN_LSTM_SPLIT_BWD", 0)
+    sequence per workgroup.  Overrides (for sweeps, PDRNN_TUNE): nb_fwd,
+    split_fwd, nb_bwd, split_bwd."""
+    nb_fwd = tune_int("nb_fwd", 0)
+    nb_bwd = tune_int("nb_bwd", 0)
+    sp_fwd = tune_int("split_fwd", 0)
+    sp_bwd = tune_int("split_bwd", 0)
     if nb_fwd not in (1, 2):
         # Large batches are LDS-bandwidth bound in the gate-split forward
         # (every lane reads the whole [x | h] operand vector): above one
@@ -62,8 +56,8 @@ def gru_fwd_nb(batch: int, hidden: int, device=None) -> int:
     sequence per 4-wave workgroup holds ~150 VGPRs at H = 32, three
     workgroups per CU; above that residency round two sequences share a
     workgroup (one round instead of two, like the LSTM's K-split choice at
-    B > 1024).  PDRNN_LSTM_NB_FWD overrides."""
-    env = _env_int("PDRNN_LSTM_NB_FWD", 0)
+    B > 1024).  PDRNN_TUNE nb_fwd overrides."""
+    env = tune_int("nb_fwd", 0)
     if env in (1, 2):
         return env
     if hidden != 32 or not torch.cuda.is_available():
@@ -79,10 +73,10 @@ def fused_bwd_nb(batch: int, hidden: int, num_layers: int) -> int:
     1 = one sequence per workgroup (the default: above one residency round
     the deferred-dW backward, lstm_small.hip DWOUT + lstm_small_dw.hip).
     2..3 interleave sequences in one workgroup of the register-dW backward
-    (sweeps via PDRNN_LSTM_NB_BWD); a multi-sequence variant with LDS-DMA
+    (sweeps via PDRNN_TUNE nb_bwd); a multi-sequence variant with LDS-DMA
     staged operands was measured slower at every motion batch and removed
     (profiles/r2_tp_backward_tried.md)."""
-    env = _env_int("PDRNN_LSTM_NB_BWD", 0)
+    env = tune_int("nb_bwd", 0)
     if env in (1, 2, 3):
         return env
     return 1

@@ -29,15 +29,14 @@ import torch
 from torch import Tensor
 
 from .. import _ext
+from ..utils.tune import tune, tune_int
 from . import gradsink
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
 def _tile() -> int:
-    try:
-        return int(os.environ.get("PDRNN_LSTM_LARGE_TILE", "-1"))
-    except ValueError:
-        return -1
+    """Forced step-kernel tile (PDRNN_TUNE large_tile; -1: the heuristic)."""
+    return tune_int("large_tile", -1)
 
 
 def supported(x: Tensor, hidden: int, num_layers: int, bidirectional: bool = False) -> bool:
@@ -215,7 +214,7 @@ def _side_stream(device) -> "torch.cuda.Stream":
 
 
 def overlap_on() -> bool:
-    return os.environ.get("PDRNN_LARGE_OVERLAP", "1") != "0"
+    return tune("large_overlap", "1") != "0"
 
 
 def run_recurrence(dhseq: Optional[Tensor], fn, inputs: Sequence[Optional[Tensor]], persistent: bool = False):
@@ -446,22 +445,18 @@ def _pipe_stream(device, l: int) -> "torch.cuda.Stream":
 
 
 def pipeline_chunks(T: int) -> List[Tuple[int, int]]:
-    """[t0, t1) time chunks of the stacked-layer pipeline (PDRNN_LARGE_CHUNKS,
+    """[t0, t1) time chunks of the stacked-layer pipeline (PDRNN_TUNE large_chunks,
     default 3: at T = 128 4.54-4.57 ms/step against 4.69-4.79 with 2, 4 or 5
     chunks and 4.92 with 6, profiles/r4/pipe/p6_*)."""
-    try:
-        c = int(os.environ.get("PDRNN_LARGE_CHUNKS", "3"))
-    except ValueError:
-        c = 3
-    c = max(1, min(c, T))
+    c = max(1, min(tune_int("large_chunks", 3), T))
     return [(T * i // c, T * (i + 1) // c) for i in range(c)]
 
 
 def pipeline_ok(x: Tensor, hidden: int, num_layers: int, bidirectional: bool, dropout: float,
                 training: bool) -> bool:
     """The stacked-layer pipeline covers unidirectional fp32 stacks of >= 2
-    layers at the row-owning kernels' H (PDRNN_LARGE_PIPE=0 turns it off)."""
-    if os.environ.get("PDRNN_LARGE_PIPE", "1") == "0" or _tile() >= 0:
+    layers at the row-owning kernels' H (PDRNN_TUNE large_pipe=0 turns it off)."""
+    if tune("large_pipe", "1") == "0" or _tile() >= 0:
         return False
     if x.dtype != torch.float32 or not x.is_cuda or bidirectional or num_layers < 2 or (dropout > 0 and training):
         return False

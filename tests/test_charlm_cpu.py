@@ -9,6 +9,8 @@ from _mp import ROOT, run, torchrun
 from pytorch_distributed_rnn_amd.data.charlm import CharCorpus
 from pytorch_distributed_rnn_amd.models.charlm import BiLSTMEncoder, CharLM
 
+from _tune import set_tune
+
 _STEP = re.compile(r"Rank: (\d+)\s+Epoch 0 Step (\d+)\tLoss: ([\d.]+)")
 
 
@@ -98,12 +100,12 @@ def test_lm_trainer_settle_is_a_no_op_on_cpu():
 
 
 def test_gru_forward_sequences_per_workgroup_override(monkeypatch):
-    """ops/lstm.py gru_fwd_nb: PDRNN_LSTM_NB_FWD overrides the residency rule
+    """ops/lstm.py gru_fwd_nb: PDRNN_TUNE nb_fwd overrides the residency rule
     (which needs a GPU to count CUs; 1 without one)."""
     from pytorch_distributed_rnn_amd.ops.lstm import gru_fwd_nb
-    monkeypatch.setenv("PDRNN_LSTM_NB_FWD", "2")
+    set_tune(monkeypatch, nb_fwd="2")
     assert gru_fwd_nb(100, 32) == 2
-    monkeypatch.delenv("PDRNN_LSTM_NB_FWD")
+    set_tune(monkeypatch, nb_fwd=None)
     import torch
     if not torch.cuda.is_available():
         assert gru_fwd_nb(1440, 32) == 1

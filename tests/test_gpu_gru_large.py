@@ -7,6 +7,8 @@ import torch
 from pytorch_distributed_rnn_amd.models.rnn import GRU
 from pytorch_distributed_rnn_amd.ops import gru_large
 
+from _tune import set_tune
+
 pytestmark = pytest.mark.gpu
 
 
@@ -63,7 +65,7 @@ def test_large_gru_matches_torch(dt, H, L, bi, B, T, I):
 
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
 def test_large_gru_every_tile(tile, monkeypatch):
-    monkeypatch.setenv("PDRNN_LSTM_LARGE_TILE", str(tile))
+    set_tune(monkeypatch, large_tile=str(tile))
     m, ref = _pair(64, 128, 1, True, torch.bfloat16, seed=4)
     x = torch.randn(5, 37, 64, device="cuda").to(torch.bfloat16)
     h0 = torch.zeros(2, 5, 128, device="cuda", dtype=torch.bfloat16)
@@ -73,8 +75,8 @@ def test_large_gru_every_tile(tile, monkeypatch):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("bwd", ["0", "2"])
 def test_large_gru_pingpong_step_matches_torch(dt, bwd, monkeypatch):
-    monkeypatch.setenv("PDRNN_LSTM_LARGE_PP", "2")
-    monkeypatch.setenv("PDRNN_LSTM_LARGE_PP_BWD", bwd)
+    set_tune(monkeypatch, large_pp="2")
+    monkeypatch.setenv("PDRNN_TUNE large_pp_BWD", bwd)
     test_large_gru_matches_torch(dt, 256, 1, True, 300, 3, 64)
 
 

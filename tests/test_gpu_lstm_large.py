@@ -6,6 +6,8 @@ import torch
 from pytorch_distributed_rnn_amd import _ext
 from pytorch_distributed_rnn_amd.models.rnn import LSTM
 
+from _tune import set_tune
+
 pytestmark = pytest.mark.gpu
 
 
@@ -30,7 +32,7 @@ def test_gemm_nt_core(dt, M, N, K, tile):
 
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
 def test_large_lstm_every_tile(tile, monkeypatch):
-    monkeypatch.setenv("PDRNN_LSTM_LARGE_TILE", str(tile))
+    set_tune(monkeypatch, large_tile=str(tile))
     torch.manual_seed(4)
     m = LSTM(64, 128, 1, batch_first=True, bidirectional=True).cuda()
     with torch.no_grad():
@@ -94,8 +96,8 @@ def test_large_lstm_pingpong_step_matches_torch(dt, H, L, bi, B, T, I, mode, mon
     occupancy threshold (batch not a multiple of 256): forward with the
     two-pass cell epilogue, backward either on the fused GemmPipe step kernel
     or as the ping-pong GEMM into the dh workspace + the cell kernel."""
-    monkeypatch.setenv("PDRNN_LSTM_LARGE_PP", "2")
-    monkeypatch.setenv("PDRNN_LSTM_LARGE_PP_BWD", "2" if mode == "gemm+cell" else "0")
+    set_tune(monkeypatch, large_pp="2")
+    monkeypatch.setenv("PDRNN_TUNE large_pp_BWD", "2" if mode == "gemm+cell" else "0")
     test_large_lstm_matches_torch(dt, H, L, bi, B, T, I)
 
 

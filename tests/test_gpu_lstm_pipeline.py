@@ -8,6 +8,8 @@ from pytorch_distributed_rnn_amd import _ext
 from pytorch_distributed_rnn_amd.models.rnn import LSTM
 from pytorch_distributed_rnn_amd.ops import lstm_large
 
+from _tune import set_tune
+
 pytestmark = pytest.mark.gpu
 
 
@@ -45,13 +47,13 @@ def test_pipeline_matches_whole_sequence_and_fp64(L, chunks, B, T, I, bias, stat
     h0 = torch.randn(L, B, H, device="cuda") if state else None
     c0 = torch.randn(L, B, H, device="cuda") if state else None
     g = torch.randn(B, T, H, device="cuda")
-    monkeypatch.setenv("PDRNN_LARGE_CHUNKS", str(chunks))
+    set_tune(monkeypatch, large_chunks=str(chunks))
     calls = []
     orig = lstm_large._PipelinedLSTMStack.apply
     monkeypatch.setattr(lstm_large._PipelinedLSTMStack, "apply", lambda *a: calls.append(1) or orig(*a))
     pipe = _run(m, x, h0, c0, g)
     assert calls, "the pipelined stack did not run"
-    monkeypatch.setenv("PDRNN_LARGE_PIPE", "0")
+    set_tune(monkeypatch, large_pipe="0")
     whole = _run(m, x, h0, c0, g)
     assert len(calls) == 1
     ref_m = torch.nn.LSTM(I, H, L, batch_first=True, bias=bias).double().cuda()
@@ -89,7 +91,9 @@ def test_pipeline_runs_beside_the_default_stream(cell):
     torch.manual_seed(3)
     ref = MotionModel(9, 128, 2, 6, cell=cell).cuda()
     import os
-    os.environ["PDRNN_LARGE_PIPE"] = "0"
+    from pytorch_distributed_rnn_amd.utils.tune import tune_string
+    saved = os.environ.get("PDRNN_TUNE")
+    os.environ["PDRNN_TUNE"] = tune_string({"large_pipe": "0"})
     try:
         opt = torch.optim.SGD(ref.parameters(), lr=0.5)
         ref_losses = []
@@ -100,7 +104,10 @@ def test_pipeline_runs_beside_the_default_stream(cell):
             opt.step()
             ref_losses.append(float(loss))
     finally:
-        del os.environ["PDRNN_LARGE_PIPE"]
+        if saved is None:
+            del os.environ["PDRNN_TUNE"]
+        else:
+            os.environ["PDRNN_TUNE"] = saved
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 1e-5 * max(1.0, abs(b))
     assert losses[-1] < losses[0]
@@ -131,13 +138,13 @@ def test_gru_pipeline_matches_whole_sequence_and_fp64(L, chunks, B, T, I, bias, 
     x = torch.randn(B, T, I, device="cuda")
     h0 = torch.randn(L, B, H, device="cuda") if state else None
     g = torch.randn(B, T, H, device="cuda")
-    monkeypatch.setenv("PDRNN_LARGE_CHUNKS", str(chunks))
+    set_tune(monkeypatch, large_chunks=str(chunks))
     calls = []
     orig = gru_large._PipelinedGRUStack.apply
     monkeypatch.setattr(gru_large._PipelinedGRUStack, "apply", lambda *a: calls.append(1) or orig(*a))
     pipe = _run_gru(m, x, h0, g)
     assert calls, "the pipelined GRU stack did not run"
-    monkeypatch.setenv("PDRNN_LARGE_PIPE", "0")
+    set_tune(monkeypatch, large_pipe="0")
     whole = _run_gru(m, x, h0, g)
     assert len(calls) == 1
     ref_m = torch.nn.GRU(I, H, L, batch_first=True, bias=bias).double().cuda()
@@ -161,7 +168,7 @@ def test_layer_by_layer_overlap_matches_serial(cell, monkeypatch):
     materialising zero gradients, that zero fill was queued on the main stream
     after the event and the side stream sometimes read it first."""
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    monkeypatch.setenv("PDRNN_LARGE_PIPE", "0")
+    set_tune(monkeypatch, large_pipe="0")
     torch.manual_seed(5)
     model = MotionModel(9, 128, 2, 6, cell=cell).cuda()
     x = torch.randn(96, 40, 9, device="cuda")
@@ -172,9 +179,9 @@ def test_layer_by_layer_overlap_matches_serial(cell, monkeypatch):
         torch.nn.functional.cross_entropy(model(x), y).backward()
         return [p.grad.clone() for p in model.parameters()]
 
-    monkeypatch.setenv("PDRNN_LARGE_OVERLAP", "0")
+    set_tune(monkeypatch, large_overlap="0")
     ref = grads()
-    monkeypatch.setenv("PDRNN_LARGE_OVERLAP", "1")
+    set_tune(monkeypatch, large_overlap="1")
     for _ in range(4):
         for a, b in zip(grads(), ref):
             assert torch.equal(a, b)

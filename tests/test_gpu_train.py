@@ -4,6 +4,8 @@ import copy
 import pytest
 import torch
 
+from _tune import set_tune
+
 pytestmark = pytest.mark.gpu
 
 
@@ -82,12 +84,12 @@ def test_one_launch_step_selected_in_latency_regime():
 @pytest.mark.parametrize("nb", [2, 3])
 def test_fused_multi_sequence_backward_matches_autograd(cell, nb, monkeypatch):
     """Sequences interleaved in one workgroup of the fused step's register-dW
-    backward (PDRNN_LSTM_NB_BWD; the GRU stays single-sequence) against the
+    backward (PDRNN_TUNE nb_bwd; the GRU stays single-sequence) against the
     autograd path; 380 samples in batches of 96 leave a last batch of 92, so
     tiles with unused slots run."""
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    monkeypatch.setenv("PDRNN_LSTM_NB_BWD", str(nb))
+    set_tune(monkeypatch, nb_bwd=str(nb))
     torch.manual_seed(1)
     train, _, _ = synthetic_motion(n_train=380, n_validation=2, n_test=2, seed=4)
     m1 = MotionModel(9, 32, 2, 6, cell=cell)
@@ -109,7 +111,7 @@ def test_fused_step_headline_batch_matches_autograd(nb, monkeypatch):
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     from pytorch_distributed_rnn_amd.train.trainer import Trainer
-    monkeypatch.setenv("PDRNN_LSTM_NB_BWD", str(nb))
+    set_tune(monkeypatch, nb_bwd=str(nb))
     torch.manual_seed(2)
     train, _, _ = synthetic_motion(n_train=2880, n_validation=2, n_test=2, seed=5)
     m1 = MotionModel(9, 32, 2, 6)
@@ -161,7 +163,7 @@ def test_deferred_dw_backward_matches_autograd(cell, hidden, layers, seq, featur
     from pytorch_distributed_rnn_amd import _ext
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    monkeypatch.setenv("PDRNN_LSTM_DWOUT", "force")
+    set_tune(monkeypatch, dwout="force")
     assert _ext.native(torch.device("cuda")).lstm_small_step_deferred_dw(hidden, layers, seq, 96)
     torch.manual_seed(3)
     train, _, _ = synthetic_motion(n_train=382, n_validation=2, n_test=2, seq_length=seq, num_features=features,
@@ -211,7 +213,7 @@ def test_deferred_dw_gradients_match_fp64(cell, hidden, layers, seq, monkeypatch
     so elements whose gradient is at rounding level flip either way)."""
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    monkeypatch.setenv("PDRNN_LSTM_DWOUT", "force")
+    set_tune(monkeypatch, dwout="force")
     torch.manual_seed(3)
     train, _, _ = synthetic_motion(n_train=190, n_validation=2, n_test=2, seq_length=seq, seed=6)
     m0 = MotionModel(9, hidden, layers, 6, cell=cell)
@@ -234,9 +236,9 @@ def test_headline_batch_gradients_match_fp64(B, nb, monkeypatch):
     from pytorch_distributed_rnn_amd import _ext
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    monkeypatch.delenv("PDRNN_LSTM_DWOUT", raising=False)
+    set_tune(monkeypatch, dwout=None)
     monkeypatch.setenv("PDRNN_SW", "0")  # the gate-split / K-split family (sequence-in-wave: test below)
-    monkeypatch.setenv("PDRNN_DWOUT_NB", nb)
+    set_tune(monkeypatch, dwout_nb=nb)
     mod = _ext.native(torch.device("cuda", 0))
     assert mod.lstm_small_step_deferred_dw(32, 2, 128, B)
     torch.manual_seed(11)
@@ -276,16 +278,42 @@ def test_seq_in_wave_step_gradients_match_fp64(B, layers, mode, monkeypatch):
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     monkeypatch.delenv("PDRNN_SW", raising=False)
     fm, _, bm = mode.partition("/")  # "F/B": forward and backward maps forced apart
-    for var, val in (("PDRNN_SW_MODE", fm), ("PDRNN_SW_BWD_MODE", bm)):
-        if val:
-            monkeypatch.setenv(var, val)
-        else:
-            monkeypatch.delenv(var, raising=False)
+    set_tune(monkeypatch, sw_mode=fm or None, sw_bwd_mode=bm or None)
     mod = _ext.native(torch.device("cuda", 0))
     assert mod.lstm_sw_ok(32, 9, layers)
     torch.manual_seed(13 + B)
     train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=14)
     _fp64_check(MotionModel(9, 32, layers, 6), train, B)
+
+
+@pytest.mark.parametrize("B", [512, 180, 97])
+def test_seq_in_wave_latency_regime_separate_launches_match_fp64(B, monkeypatch):
+    """The latency regime (forward mode 5, backward mode 4) as separate
+    forward / BPTT launches (PDRNN_SW=2) against fp64 autograd; the default
+    one-launch step runs at every B <= 512 of the parametrisation above."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    set_tune(monkeypatch, sw_mode=None, sw_bwd_mode=None)
+    monkeypatch.setenv("PDRNN_SW", "2")
+    mod = _ext.native(torch.device("cuda", 0))
+    assert mod.lstm_sw_step_ok(2, B, 128)
+    torch.manual_seed(31 + B)
+    train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=32)
+    _fp64_check(MotionModel(9, 32, 2, 6), train, B)
+
+
+def test_one_launch_sw_step_selection():
+    """The one-launch step (forward + BPTT in one kernel) covers two-layer
+    stacks up to two workgroups per CU (B <= 512 on 256 CUs) at T % 4 == 0;
+    the headline batch keeps the separate launches."""
+    from pytorch_distributed_rnn_amd import _ext
+    mod = _ext.native(torch.device("cuda", 0))
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    for B in (97, 144, 180, 360, 2 * cus):
+        assert mod.lstm_sw_step_ok(2, B, 128), B
+    for B, T in ((2 * cus + 1, 128), (720, 128), (1440, 128), (180, 126)):
+        assert not mod.lstm_sw_step_ok(2, B, T), (B, T)
 
 
 def test_seq_in_wave_batch_past_descriptor_range_falls_back(monkeypatch):
@@ -317,7 +345,7 @@ def test_one_launch_gradients_match_fp64(cell, B, monkeypatch):
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
     from pytorch_distributed_rnn_amd.ops.lstm import fused_bwd_nb, small_launch_config
     monkeypatch.setenv("PDRNN_SW", "0")
-    monkeypatch.delenv("PDRNN_LSTM_DWOUT", raising=False)
+    set_tune(monkeypatch, dwout=None)
     mod = _ext.native(torch.device("cuda", 0))
     nb_f, sp_f, _, sp_b = small_launch_config(B, 32, 2)
     if cell == "gru":
@@ -332,7 +360,7 @@ def test_deferred_dw_pairs_sequences_at_headline_batch(monkeypatch):
     """B = 1440 / 1152: two sequences per workgroup of the deferred-dW BPTT,
     all of them resident in one round (the grid fits the occupancy)."""
     from pytorch_distributed_rnn_amd import _ext
-    monkeypatch.delenv("PDRNN_DWOUT_NB", raising=False)
+    set_tune(monkeypatch, dwout_nb=None)
     mod = _ext.native(torch.device("cuda", 0))
     for B in (1440, 1152):
         nb, grid = mod.lstm_small_dwout_geometry(32, 2, 128, B)
@@ -344,11 +372,11 @@ def test_deferred_dw_selected_above_one_round(monkeypatch):
     register-dW backward) takes the deferred-dW path, the 8-GPU per-rank batch
     (180, one round) keeps the one-launch step."""
     from pytorch_distributed_rnn_amd import _ext
-    monkeypatch.delenv("PDRNN_LSTM_DWOUT", raising=False)
+    set_tune(monkeypatch, dwout=None)
     mod = _ext.native(torch.device("cuda", 0))
     assert mod.lstm_small_step_deferred_dw(32, 2, 128, 1440)
     assert not mod.lstm_small_step_deferred_dw(32, 2, 128, 180)
-    monkeypatch.setenv("PDRNN_LSTM_DWOUT", "0")
+    set_tune(monkeypatch, dwout="0")
     assert not mod.lstm_small_step_deferred_dw(32, 2, 128, 1440)
 
 
@@ -357,7 +385,7 @@ def test_deferred_dw_bf16_inputs_match_autograd(monkeypatch):
     kernel widens the gathered bf16 x rows itself."""
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    monkeypatch.setenv("PDRNN_LSTM_DWOUT", "force")
+    set_tune(monkeypatch, dwout="force")
     torch.manual_seed(0)
     train, _, _ = synthetic_motion(n_train=384, n_validation=2, n_test=2, seed=3)
     m1 = MotionModel(9, 32, 1, 6, compute_dtype=torch.bfloat16)
@@ -428,8 +456,8 @@ def test_seq_in_wave_short_sequences_fall_back_from_mode4(T, monkeypatch):
     the dW kernel instead -- gradients against fp64 at B = 180 for such T."""
     from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
     from pytorch_distributed_rnn_amd.models.motion import MotionModel
-    for var in ("PDRNN_SW", "PDRNN_SW_MODE", "PDRNN_SW_BWD_MODE"):
-        monkeypatch.delenv(var, raising=False)
+    monkeypatch.delenv("PDRNN_SW", raising=False)
+    set_tune(monkeypatch, sw_mode=None, sw_bwd_mode=None)
     torch.manual_seed(21)
     train, _, _ = synthetic_motion(n_train=180, n_validation=2, n_test=2, seq_length=T, seed=22)
     _fp64_check(MotionModel(9, 32, 2, 6), train, 180)

@@ -6,10 +6,12 @@ import torch
 
 from pytorch_distributed_rnn_amd.ops.lstm_large import _chunk_weight_grads, pipeline_chunks
 
+from _tune import set_tune
+
 
 def test_pipeline_chunks_cover_the_sequence(monkeypatch):
     for c, T in [(4, 128), (3, 10), (16, 12), (1, 5)]:
-        monkeypatch.setenv("PDRNN_LARGE_CHUNKS", str(c))
+        set_tune(monkeypatch, large_chunks=str(c))
         ch = pipeline_chunks(T)
         assert len(ch) == min(c, T) and ch[0][0] == 0 and ch[-1][1] == T
         assert all(a[1] == b[0] and a[0] < a[1] for a, b in zip(ch, ch[1:]))
@@ -24,7 +26,7 @@ def test_chunked_weight_grads_match_whole_sequence(chunks, with_h0, monkeypatch)
     hd = torch.randn(T, B, H)
     x = torch.randn(T, B, I)
     h0 = torch.randn(B, H) if with_h0 else None
-    monkeypatch.setenv("PDRNN_LARGE_CHUNKS", str(chunks))
+    set_tune(monkeypatch, large_chunks=str(chunks))
     dwih, dwhh, db = torch.full((4 * H, I), float("nan")), torch.full((4 * H, H), float("nan")), torch.empty(4 * H)
     for k, (t0, t1) in enumerate(reversed(pipeline_chunks(T))):  # the backward's order: last chunk first
         _chunk_weight_grads(dwih, dwhh, db, G, hd, h0, x, t0, t1, k == 0)

@@ -11,7 +11,7 @@ from pytorch_distributed_rnn_amd.models.motion import MotionModel  # noqa: E402
 
 
 def run(cell, pipe, steps=3, B=64, T=32):
-    os.environ["PDRNN_LARGE_PIPE"] = "1" if pipe else "0"
+    os.environ["PDRNN_TUNE"] = "large_pipe=" + ("1" if pipe else "0")
     torch.manual_seed(3)
     model = MotionModel(9, 128, 2, 6, cell=cell).cuda()
     opt = torch.optim.SGD(model.parameters(), lr=0.5)
