@@ -1478,8 +1478,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     const int nb = pdrnn_lstm_small_bwd_dwout_nb((int)H, (int)NL, (int)T, (int)B);
     return py::make_tuple(nb, pdrnn_lstm_small_bwd_dwout_grid((int)H, (int)NL, (int)T, (int)B, nb));
   }, "(sequences per workgroup, grid) of the deferred-dW backward for this shape");
-  m.def("lstm_sw_ok", [](int64_t H, int64_t I, int64_t NL) { return pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, 0) == 1; },
-        "the sequence-in-wave kernels (lstm_sw.hip) cover this LSTM stack in the fused train step");
+  m.def("lstm_sw_ok", [](int64_t H, int64_t I, int64_t NL, int64_t cell) {
+    return pdrnn_lstm_sw_ok((int)H, (int)I, (int)NL, (int)cell) == 1;
+  }, "the sequence-in-wave kernels (lstm_sw.hip) cover this LSTM (cell 0) / GRU (cell 1) stack in the fused train step",
+        py::arg("H"), py::arg("I"), py::arg("NL"), py::arg("cell") = 0);
   m.def("lstm_sw_step_ok", [](int64_t NL, int64_t B, int64_t T) {
     return pdrnn_lstm_sw_step_ok((int)NL, (int)B, (int)T) == 1;
   }, "the one-launch sequence-in-wave step (forward + BPTT in one kernel) covers this batch");

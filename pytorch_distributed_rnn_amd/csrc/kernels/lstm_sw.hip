@@ -110,7 +110,11 @@ PDRNN_DEVICE int fwd_col(int l, int s, int c, int e, int Iin, bool& from_ih) {
   return 4 * c + e;
 }
 
-template <int NC>
+// CELL 1 = GRU, packed by the host as a 4-row-block stack with zero blocks
+// (W_ih: [W_ir; W_iz; W_in; 0], W_hh: [W_hr; W_hz; 0; W_hn], ops/gru_fused.py),
+// so the products are the LSTM's: rows (r, z, n_x, n_h) with n_x / n_h scaled
+// by 2 kA (tanh(n_x + r n_h) = 2 sigma(2 (n_x + r n_h)) - 1 is linear in both).
+template <int NC, int CELL = 0>
 PDRNN_DEVICE FwdW<NC> load_fwd_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, int s) {
   FwdW<NC> W;
   const int Iin = l == 0 ? a.I : kH;
@@ -121,7 +125,7 @@ PDRNN_DEVICE FwdW<NC> load_fwd_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, i
   for (int j = 0; j < 4; ++j) {
     const int q = gq[j];
     const int r = q * kH + u;
-    const float sc = kA * (q == 2 ? 2.f : 1.f);
+    const float sc = kA * ((CELL == 0 ? q == 2 : q >= 2) ? 2.f : 1.f);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       float v[4];
@@ -186,6 +190,28 @@ PDRNN_DEVICE Cell fwd_cell(const float (&p)[4], pdrnn_f2 gk, float c, bool odd) 
   r.h = from_odd(r.a1) * tanh_c(r.c);
   return r;
 }
+// GRU: lane s = 0 holds r and n_x, s = 1 z and n_h (2 kA-scaled); one DPP
+// swap each gives both lanes all four, then n = tanh(n_x + r n_h) and
+// h = n + z (h_prev - n) on both.  Saved slots: a0 = r | z, a1 = n_x | n_h
+// (unscaled; the BPTT reads n_h), c = n.
+PDRNN_DEVICE Cell fwd_cell_gru(const float (&p)[4], float hprev, bool odd) {
+  const float z0 = p[0] + dpp_swap1(p[1]);
+  const float z1 = p[2] + dpp_swap1(p[3]);
+  Cell r;
+  r.a0 = sig2(z0);
+  const float a0p = dpp_swap1(r.a0), z1p = dpp_swap1(z1);
+  const float rg = odd ? a0p : r.a0, zg = odd ? r.a0 : a0p;
+  const float nx = odd ? z1p : z1, nh = odd ? z1 : z1p;
+  r.a1 = z1 * (1.f / (2.f * kA));
+  r.c = fmaf(sig2(fmaf(rg, nh, nx)), 2.f, -1.f);
+  r.h = fmaf(zg, hprev - r.c, r.c);
+  return r;
+}
+template <int CELL>
+PDRNN_DEVICE Cell fwd_cell_any(const float (&p)[4], pdrnn_f2 gk, float c, float hprev, bool odd) {
+  if constexpr (CELL == 0) return fwd_cell(p, gk, c, odd);
+  else return fwd_cell_gru(p, hprev, odd);
+}
 template <int NL, int NB>
 PDRNN_DEVICE constexpr int fwd_lds_floats_hb() { return NB * NL * 2 * kHB; }
 
@@ -194,7 +220,7 @@ PDRNN_DEVICE constexpr int fwd_lds_floats_hb() { return NB * NL * 2 * kHB; }
 // barrier per step (layer 0's h_t handed over through parity slots).
 // mode 2 holds <= 168 VGPRs: three waves per SIMD, so B = 1440 (2880 layer
 // waves on 1024 SIMDs) is one residency round with every SIMD loaded evenly
-template <int NL, int MODE>
+template <int NL, int MODE, int CELL = 0>
 __global__ void __launch_bounds__(MODE >= 2 ? 64 * NL : 64) __attribute__((amdgpu_waves_per_eu(MODE == 6 ? 3 : 1)))
 lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   constexpr int NB = sw_nb(MODE);
@@ -320,7 +346,7 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
     for (int n = 0; n < NB; ++n) {
       float p[4];
       fwd_dot<6>(W, v[n], p);
-      commit(0, n, t, t < T, fwd_cell(p, gk, cst[0][n], odd));
+      commit(0, n, t, t < T, fwd_cell_any<CELL>(p, gk, cst[0][n], hst[0][n], odd));
     }
   };
   auto cmp1 = [&](const FwdW<8>& W, int t, const float4 (&v)[NB][8]) {
@@ -328,20 +354,20 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
     for (int n = 0; n < NB; ++n) {
       float p[4];
       fwd_dot<8>(W, v[n], p);
-      commit(NL - 1, n, t, t >= 0, fwd_cell(p, gk, cst[NL - 1][n], odd));
+      commit(NL - 1, n, t, t >= 0, fwd_cell_any<CELL>(p, gk, cst[NL - 1][n], hst[NL - 1][n], odd));
     }
   };
 
   if constexpr (NL == 1) {
-    const FwdW<6> W0 = load_fwd_w<6>(a, 0, u, odd ? 1 : 0);
+    const FwdW<6> W0 = load_fwd_w<6, CELL>(a, 0, u, odd ? 1 : 0);
     for (int t = 0; t < T; ++t) {
       float4 v0[NB][6];
       rd0(t, v0);
       cmp0(W0, t, v0);
     }
   } else if constexpr (!SPLIT) {
-    const FwdW<6> W0 = load_fwd_w<6>(a, 0, u, odd ? 1 : 0);
-    const FwdW<8> W1 = load_fwd_w<8>(a, 1, u, odd ? 1 : 0);
+    const FwdW<6> W0 = load_fwd_w<6, CELL>(a, 0, u, odd ? 1 : 0);
+    const FwdW<8> W1 = load_fwd_w<8, CELL>(a, 1, u, odd ? 1 : 0);
     // layer 0 at t = it, layer 1 at t = it - 1: both read h^0_{it-1}
     for (int it = 0; it <= T; ++it) {
       float4 v0[NB][6], v1[NB][8];
@@ -356,7 +382,7 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
     // three waves per SIMD for B > one wave per SIMD) leaves the reads to the
     // scheduler, which pairs them to stay within its registers
     if (wv == 0) {
-      const FwdW<6> W0 = load_fwd_w<6>(a, 0, u, odd ? 1 : 0);
+      const FwdW<6> W0 = load_fwd_w<6, CELL>(a, 0, u, odd ? 1 : 0);
       for (int it = 0; it <= T; ++it) {
         if (it < T) {
           float4 v0[NB][6];
@@ -367,7 +393,7 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
         lds_barrier();
       }
     } else {
-      const FwdW<8> W1 = load_fwd_w<8>(a, 1, u, odd ? 1 : 0);
+      const FwdW<8> W1 = load_fwd_w<8, CELL>(a, 1, u, odd ? 1 : 0);
       for (int it = 0; it <= T; ++it) {
         if (it > 0) {
           float4 v1[NB][8];
@@ -440,14 +466,14 @@ PDRNN_DEVICE int fwd4_col(int l, int q, int c, int e, int Iin, bool& from_ih) {
   return 16 * (q & 1) + k;
 }
 
-template <int NC>
+template <int NC, int CELL = 0>
 PDRNN_DEVICE Fwd4W<NC> load_fwd4_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, int q, float (&bias)[4]) {
   Fwd4W<NC> W;
   const int Iin = l == 0 ? a.I : kH;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int r = j * kH + u;
-    const float sc = kA * (j == 2 ? 2.f : 1.f);
+    const float sc = kA * ((CELL == 0 ? j == 2 : j >= 2) ? 2.f : 1.f);  // (GRU: see load_fwd_w)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       float v[4];
@@ -469,6 +495,7 @@ PDRNN_DEVICE Fwd4W<NC> load_fwd4_w(const PdrnnLstmSmallFwdArgs& a, int l, int u,
   return W;
 }
 
+template <int CELL = 0>
 PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -514,10 +541,20 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
     return (od ? m1 : m0) + dpp_swap1(od ? m0 : m1);
   };
   auto cell = [&](int t, bool act, float z) {
-    const float av = fmaf(sig2(z), gk.x, gk.y);  // i, f, tanh g or o of this lane
-    const float ig = quad_bcast(av, 0), fg = quad_bcast(av, 1), gg = quad_bcast(av, 2), og = quad_bcast(av, 3);
-    const float cn = fmaf(fg, cst, ig * gg);
-    const float hn = og * tanh_c(cn);
+    float av, cn, hn;
+    if constexpr (CELL == 0) {
+      av = fmaf(sig2(z), gk.x, gk.y);  // i, f, tanh g or o of this lane
+      const float ig = quad_bcast(av, 0), fg = quad_bcast(av, 1), gg = quad_bcast(av, 2), og = quad_bcast(av, 3);
+      cn = fmaf(fg, cst, ig * gg);
+      hn = og * tanh_c(cn);
+    } else {  // GRU: r, z, or the 2 kA-scaled n_x / n_h of this lane; cn carries n
+      const float sg = sig2(z);
+      const float v = q < 2 ? sg : z;
+      const float rg = quad_bcast(v, 0), zg = quad_bcast(v, 1), nx = quad_bcast(v, 2), nh = quad_bcast(v, 3);
+      cn = fmaf(sig2(fmaf(rg, nh, nx)), 2.f, -1.f);
+      hn = fmaf(zg, hst - cn, cn);
+      av = q < 2 ? sg : z * (1.f / (2.f * kA));  // saved unscaled
+    }
     cst = act ? cn : cst;
     hst = act ? hn : hst;
     if (q == 0) hbuf(l, t & 1)[u] = hst;
@@ -530,7 +567,7 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
 
   if (l == 0) {
     float bias[4];
-    const Fwd4W<3> W = load_fwd4_w<3>(a, 0, u, q, bias);
+    const Fwd4W<3> W = load_fwd4_w<3, CELL>(a, 0, u, q, bias);
     for (int it = 0; it <= T; ++it) {
       if (it < T) {
         const int t = it;
@@ -556,7 +593,7 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
     }
   } else {
     float bias[4];
-    const Fwd4W<4> W = load_fwd4_w<4>(a, 1, u, q, bias);
+    const Fwd4W<4> W = load_fwd4_w<4, CELL>(a, 1, u, q, bias);
     for (int it = 0; it <= T; ++it) {
       if (it > 0) {
         const int t = it - 1;
@@ -599,7 +636,8 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
     }
   }
 }
-__global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs a) { fwd4_body(a); }
+template <int CELL>
+__global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs a) { fwd4_body<CELL>(a); }
 
 // ---------------------------------------------------------------------------
 // Backward (lean contract: zero initial state, dL/dh_T of the top layer only,
@@ -641,6 +679,20 @@ PDRNN_DEVICE void row_phase(const Ops& o, float dht, float& dc, bool odd, bool h
   dc = dcp * o.f;
 }
 
+// GRU (saved r, z, n_h, n; cp = h_{t-1}): the gate-gradient vector is
+// [dr r(1-r) | dz z(1-z) | dpn | dpn r] with dpn = dh (1-z) (1-n^2) (s = 0:
+// the r, z blocks; s = 1: n_x, n_h), so the column phase W^T dz over the
+// packed stack is the LSTM's; dc carries the direct path dh_t z_t into t - 1.
+PDRNN_DEVICE void row_phase_gru(const Ops& o, float dht, float& dc, bool odd, bool has_prev, float& d0, float& d1) {
+  const float hp = has_prev ? o.cp : 0.f;
+  const float dh = dht + dc;
+  const float n = o.c, r = o.i, z = o.f;
+  const float dpn = dh * (1.f - z) * fmaf(-n, n, 1.f);
+  d0 = odd ? dpn : dpn * o.o * fmaf(-r, r, r);
+  d1 = odd ? dpn * r : dh * (hp - n) * fmaf(-z, z, z);
+  dc = dh * z;
+}
+
 PDRNN_DEVICE float col_dot(const BwdCol& W, const float4 (&g)[16]) {
   pdrnn_f2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
 #pragma unroll
@@ -654,7 +706,7 @@ PDRNN_DEVICE float col_dot(const BwdCol& W, const float4 (&g)[16]) {
 
 // (no occupancy target: at 168 VGPRs the split backward spills, and it only
 // runs at B <= one wave per SIMD)
-template <int NL, int MODE>
+template <int NL, int MODE, int CELL = 0>
 PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
   constexpr int NB = sw_nb(MODE);
   constexpr bool SPLIT = MODE >= 2;
@@ -703,6 +755,7 @@ PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
 
   const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
   const __amdgpu_buffer_rsrc_t r_dg = uniform_rsrc(a.dg_out);
+  const __amdgpu_buffer_rsrc_t r_hs = uniform_rsrc(a.hseq);  // GRU: h_{t-1}
   const uint32_t st_act = 5 * kH * 4, st_dg = (uint32_t)a.dg_st * 4;
   const uint32_t vo_i = u * 4, vo_f = (kH + u) * 4, vo_g = (2 * kH + u) * 4, vo_o = (3 * kH + u) * 4;
   const uint32_t vo_c = (4 * kH + u) * 4;
@@ -721,10 +774,16 @@ PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
     Ops o;
     o.i = bload(r_act, vo_i, ra);
     o.f = bload(r_act, vo_f, ra);
-    o.g = bload(r_act, vo_g, ra);
     o.o = bload(r_act, vo_o, ra);
     o.c = bload(r_act, vo_c, ra);
-    o.cp = bload(r_act, vo_c, rp);
+    if constexpr (CELL == 0) {
+      o.g = bload(r_act, vo_g, ra);
+      o.cp = bload(r_act, vo_c, rp);
+    } else {  // GRU: n_x unused; h_{t-1} of the unit from the saved h sequence
+      o.g = 0.f;
+      const uint32_t rh = rowidx(l, n, tc) * (kH * 4);
+      o.cp = bload(r_hs, u * 4, __builtin_amdgcn_readfirstlane(tc > 0 ? rh - kH * 4 : rh));
+    }
     return o;
   };
 
@@ -897,7 +956,8 @@ PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
   // layer-generic pieces
   auto rows = [&](int l, int n, int t, const Ops& o, float dh_in, bool act) {
     float d0, d1, dcn = dc[l][n];
-    row_phase(o, dhrec[l][n] + dh_in, dcn, odd, t > 0, d0, d1);
+    if constexpr (CELL == 0) row_phase(o, dhrec[l][n] + dh_in, dcn, odd, t > 0, d0, d1);
+    else row_phase_gru(o, dhrec[l][n] + dh_in, dcn, odd, t > 0, d0, d1);
     dc[l][n] = act ? dcn : dc[l][n];
     float* zb = dzbuf(n, l, t);
     zb[slot0] = d0;
@@ -1080,10 +1140,10 @@ PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
     st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
   }
 }
-template <int NL, int MODE>
+template <int NL, int MODE, int CELL = 0>
 __global__ void __launch_bounds__(MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64)
 lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
-  bwd_body<NL, MODE>(a);
+  bwd_body<NL, MODE, CELL>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1100,10 +1160,11 @@ lstm_sw_bwd_kernel(PdrnnLstmSmallBwdArgs a) {
 // 15 us against 7 for the separate launch, and a release fence instead of
 // the coherent stores 35 (profiles/r6/one_launch_step.md).
 // ---------------------------------------------------------------------------
+template <int CELL>
 __global__ void __launch_bounds__(256) lstm_sw_step_kernel(PdrnnLstmSmallFwdArgs f, PdrnnLstmSmallBwdArgs bk) {
-  fwd4_body(f);
+  fwd4_body<CELL>(f);
   __syncthreads();  // the forward's outputs (act, hseq, x rows, dh_T) before the backward reads them
-  bwd_body<2, 4>(bk);
+  bwd_body<2, 4, CELL>(bk);
 }
 
 // ---- host side -------------------------------------------------------------
@@ -1129,12 +1190,16 @@ hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   constexpr int NB = sw_nb(MODE);
   const int grid = (a->B + NB - 1) / NB;
   const int block = MODE >= 2 ? 64 * NL : 64;
-  hipLaunchKernelGGL((lstm_sw_fwd_kernel<NL, MODE>), dim3(grid), dim3(block), fwd_lds(NL, NB, a->T), st, *a);
+  if (a->cell == 1)
+    hipLaunchKernelGGL((lstm_sw_fwd_kernel<NL, MODE, 1>), dim3(grid), dim3(block), fwd_lds(NL, NB, a->T), st, *a);
+  else
+    hipLaunchKernelGGL((lstm_sw_fwd_kernel<NL, MODE, 0>), dim3(grid), dim3(block), fwd_lds(NL, NB, a->T), st, *a);
   return hipGetLastError();
 }
 hipError_t launch_fwd4(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
-  hipLaunchKernelGGL(lstm_sw_fwd4_kernel, dim3(a->B), dim3(256), sizeof(float) * (2 * 2 * kHB + (size_t)a->T * kXS), st,
-                     *a);
+  const size_t lds = sizeof(float) * (2 * 2 * kHB + (size_t)a->T * kXS);
+  if (a->cell == 1) hipLaunchKernelGGL(lstm_sw_fwd4_kernel<1>, dim3(a->B), dim3(256), lds, st, *a);
+  else hipLaunchKernelGGL(lstm_sw_fwd4_kernel<0>, dim3(a->B), dim3(256), lds, st, *a);
   return hipGetLastError();
 }
 template <int NL, int MODE>
@@ -1142,8 +1207,9 @@ hipError_t launch_bwd(const PdrnnLstmSmallBwdArgs* a, hipStream_t st) {
   constexpr int NB = sw_nb(MODE);
   const int grid = (a->B + NB - 1) / NB;
   const int block = MODE == 4 ? 256 : MODE >= 2 ? 64 * NL : 64;
-  hipLaunchKernelGGL((lstm_sw_bwd_kernel<NL, MODE>), dim3(grid), dim3(block), bwd_lds(NL, NB, MODE >= 4 ? 8 : 2), st,
-                     *a);
+  const size_t lds = bwd_lds(NL, NB, MODE >= 4 ? 8 : 2);
+  if (a->cell == 1) hipLaunchKernelGGL((lstm_sw_bwd_kernel<NL, MODE, 1>), dim3(grid), dim3(block), lds, st, *a);
+  else hipLaunchKernelGGL((lstm_sw_bwd_kernel<NL, MODE, 0>), dim3(grid), dim3(block), lds, st, *a);
   return hipGetLastError();
 }
 
@@ -1154,7 +1220,7 @@ using namespace pdrnn;
 
 
 extern "C" int pdrnn_lstm_sw_ok(int H, int I, int NL, int cell) {
-  return (H == kH && I >= 1 && I <= kXS && (NL == 1 || NL == 2) && cell == 0) ? 1 : 0;
+  return (H == kH && I >= 1 && I <= kXS && (NL == 1 || NL == 2) && (cell == 0 || cell == 1)) ? 1 : 0;
 }
 
 // Every (layer, sequence, step) row of `act` (5H floats) and `hseq` is
@@ -1209,7 +1275,8 @@ extern "C" int pdrnn_lstm_sw_step_ok(int NL, int B, int T) {
 
 extern "C" hipError_t pdrnn_lstm_sw_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstmSmallBwdArgs* b,
                                          hipStream_t st) {
-  if (!pdrnn_lstm_sw_ok(kH, f->I, f->NL, f->cell) || f->NL != 2 || f->h0 || f->c0) return hipErrorInvalidValue;
+  if (!pdrnn_lstm_sw_ok(kH, f->I, f->NL, f->cell) || f->NL != 2 || f->h0 || f->c0 || b->cell != f->cell)
+    return hipErrorInvalidValue;
   if (!f->act || !f->hseq || f->B <= 0 || f->T <= 0 || f->T % 4 || !pdrnn_lstm_sw_fits(f->NL, f->B, f->T))
     return hipErrorInvalidValue;
   if (!f->head_w || f->C > 16 || f->C < 1 || !f->labels || !f->slab || !f->dh_top) return hipErrorInvalidValue;
@@ -1220,7 +1287,8 @@ extern "C" hipError_t pdrnn_lstm_sw_step(const PdrnnLstmSmallFwdArgs* f, const P
     return hipErrorInvalidValue;
   const size_t lds = step_lds(f->T);
   if (lds > 64 * 1024) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL(lstm_sw_step_kernel, dim3(f->B), dim3(256), lds, st, *f, *b);
+  if (f->cell == 1) hipLaunchKernelGGL(lstm_sw_step_kernel<1>, dim3(f->B), dim3(256), lds, st, *f, *b);
+  else hipLaunchKernelGGL(lstm_sw_step_kernel<0>, dim3(f->B), dim3(256), lds, st, *f, *b);
   return hipGetLastError();
 }
 

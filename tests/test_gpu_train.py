@@ -280,14 +280,40 @@ def test_seq_in_wave_step_gradients_match_fp64(B, layers, mode, monkeypatch):
     fm, _, bm = mode.partition("/")  # "F/B": forward and backward maps forced apart
     set_tune(monkeypatch, sw_mode=fm or None, sw_bwd_mode=bm or None)
     mod = _ext.native(torch.device("cuda", 0))
-    assert mod.lstm_sw_ok(32, 9, layers)
+    assert mod.lstm_sw_ok(32, 9, layers, 0)
     torch.manual_seed(13 + B)
     train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=14)
     _fp64_check(MotionModel(9, 32, layers, 6), train, B)
 
 
+@pytest.mark.parametrize("B,layers,mode", [(1440, 2, ""), (1152, 2, ""), (720, 2, ""), (512, 2, ""), (180, 2, ""),
+                                           (144, 2, ""), (97, 2, ""), (1440, 2, "2"), (180, 2, "3"), (97, 2, "6/3"),
+                                           (180, 2, "2/2"), (360, 2, "5/3"), (512, 2, "2/4"),
+                                           (180, 1, ""), (1440, 1, ""), (97, 1, "1")])
+def test_seq_in_wave_gru_step_gradients_match_fp64(B, layers, mode, monkeypatch):
+    """The GRU on the sequence-in-wave map (kernels/lstm_sw.hip, CELL = 1:
+    the packed 4-block stack's products on the LSTM lanes, n = tanh(n_x + r
+    n_h) and h = n + z (h_prev - n) after two DPP swaps; BPTT row phase with
+    the direct dh z path; deferred matrix-core dW) at the headline / short /
+    per-rank batches (B <= 512: the one-launch four-wave forward + register-dW
+    BPTT) and forced wave maps: gradients before Adam against fp64 nn.GRU
+    autograd on the same weights and batch."""
+    from pytorch_distributed_rnn_amd import _ext
+    from pytorch_distributed_rnn_amd.data.motion import synthetic_motion
+    from pytorch_distributed_rnn_amd.models.motion import MotionModel
+    monkeypatch.delenv("PDRNN_SW", raising=False)
+    fm, _, bm = mode.partition("/")
+    set_tune(monkeypatch, sw_mode=fm or None, sw_bwd_mode=bm or None)
+    mod = _ext.native(torch.device("cuda", 0))
+    assert mod.lstm_sw_ok(32, 9, layers, 1)
+    torch.manual_seed(17 + B)
+    train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=18)
+    _fp64_check(MotionModel(9, 32, layers, 6, cell="gru"), train, B)
+
+
+@pytest.mark.parametrize("cell", ["lstm", "gru"])
 @pytest.mark.parametrize("B", [512, 180, 97])
-def test_seq_in_wave_latency_regime_separate_launches_match_fp64(B, monkeypatch):
+def test_seq_in_wave_latency_regime_separate_launches_match_fp64(B, cell, monkeypatch):
     """The latency regime (forward mode 5, backward mode 4) as separate
     forward / BPTT launches (PDRNN_SW=2) against fp64 autograd; the default
     one-launch step runs at every B <= 512 of the parametrisation above."""
@@ -300,7 +326,7 @@ def test_seq_in_wave_latency_regime_separate_launches_match_fp64(B, monkeypatch)
     assert mod.lstm_sw_step_ok(2, B, 128)
     torch.manual_seed(31 + B)
     train, _, _ = synthetic_motion(n_train=B, n_validation=2, n_test=2, seed=32)
-    _fp64_check(MotionModel(9, 32, 2, 6), train, B)
+    _fp64_check(MotionModel(9, 32, 2, 6, cell=cell), train, B)
 
 
 def test_one_launch_sw_step_selection():
