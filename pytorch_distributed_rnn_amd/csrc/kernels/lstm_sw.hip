@@ -954,6 +954,8 @@ PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
   };
 
   // layer-generic pieces
+  // (carrying c_{t-1} into the next step instead of re-loading it as that
+  // step's c_t measured slower: BPTT 141 vs 128 us at B = 1440)
   auto rows = [&](int l, int n, int t, const Ops& o, float dh_in, bool act) {
     float d0, d1, dcn = dc[l][n];
     if constexpr (CELL == 0) row_phase(o, dhrec[l][n] + dh_in, dcn, odd, t > 0, d0, d1);
