@@ -397,6 +397,34 @@ std::vector<Tensor> lstm_small_bwd(const Tensor& x, const optional<Tensor>& idx,
   return {dparams, dx, dh0, dc0};
 }
 
+// Per-phase cycles per step of the phase-stamped four-wave forward (rows of
+// 24: 8 loop stamps, then waves 0 / 2: five phase sums and the step count),
+// averaged over the workgroups.
+void report_phase_stamps(const Tensor& st) {
+  auto h = st.cpu();
+  const int64_t g = h.size(0);
+  const int64_t* p = h.data_ptr<int64_t>();
+  static const char* names[5] = {"reads", "products", "quad-reduce", "cell+stores", "barrier"};
+  for (int w = 0; w < 2; ++w) {
+    double m[5] = {0, 0, 0, 0, 0};
+    int64_t used = 0;
+    for (int64_t i = 0; i < g; ++i) {
+      const int64_t* r = p + i * 24 + 8 + 8 * w;
+      if (r[5] <= 0) continue;
+      for (int k = 0; k < 5; ++k) m[k] += (double)r[k] / (double)r[5];
+      ++used;
+    }
+    double tot = 0;
+    fprintf(stderr, "[stamps] fwd4 phases layer %d (wave %d, %lld workgroups, cycles/step):", w, 2 * w, (long long)used);
+    for (int k = 0; k < 5; ++k) {
+      const double v = used ? m[k] / used : 0.0;
+      tot += v;
+      fprintf(stderr, " %s %.0f", names[k], v);
+    }
+    fprintf(stderr, " | total %.0f\n", tot);
+  }
+}
+
 // Fused motion training step on the native path: LSTM stack forward with the
 // classifier head + cross-entropy fused into its epilogue, BPTT backward, and
 // one deterministic reduction that writes every parameter gradient straight
@@ -535,8 +563,13 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   // the four-wave forward, runs one)
   const int sw_fnb = sw ? pdrnn_lstm_sw_nb(sw_fmode) : 1, sw_bnb = sw ? pdrnn_lstm_sw_nb(sw_bmode) : 1;
   Tensor st_f, st_b;
+  // PDRNN_TUNE sw_phase=1 (with PDRNN_LSTM_STAMPS): the phase-stamped build
+  // of the four-wave forward, rows of 24 (report_phase_stamps)
+  const bool phase = stamps_enabled() && sw && sw_fmode == 5 && cell == 0 && pdrnn_tune_int("sw_phase", 0) != 0;
   if (stamps_enabled()) {
-    st_f = at::zeros({sw ? (B + sw_fnb - 1) / sw_fnb : (B + nb_fwd - 1) / nb_fwd, 8}, opts.dtype(at::kLong));
+    st_f = at::zeros({sw ? (B + sw_fnb - 1) / sw_fnb : (B + nb_fwd - 1) / nb_fwd, phase ? 24 : 8},
+                     opts.dtype(at::kLong));
+    f.phase_stamps = phase ? 1 : 0;
     st_b = at::zeros({sw ? (B + sw_bnb - 1) / sw_bnb : gridb, 8}, opts.dtype(at::kLong));
     f.stamps = reinterpret_cast<uint64_t*>(st_f.data_ptr<int64_t>());
   }
@@ -598,7 +631,9 @@ void lstm_head_train_step(const Tensor& x, const optional<Tensor>& idx, const Te
   if (st_f.defined()) {
     const int bw_iters = sw ? (int)(T + NL - 1)
                             : (int)(T + 2 * (NL - 1)) * (int)((B + (int64_t)grid_dw * nb_dw - 1) / ((int64_t)grid_dw * nb_dw));
-    report_stamps(sw ? "fwd(head step, seq-in-wave)" : "fwd(head step)", st_f, (int)(T + NL - 1));
+    if (phase) report_phase_stamps(st_f);
+    report_stamps(sw ? "fwd(head step, seq-in-wave)" : "fwd(head step)",
+                  phase ? st_f.narrow(1, 0, 8).contiguous() : st_f, (int)(T + NL - 1));
     report_stamps(sw ? "bwd(head step, seq-in-wave, deferred dW)"
                      : dwout ? "bwd(head step, lean, deferred dW)" : "bwd(head step, lean)",
                   st_b, bw_iters);

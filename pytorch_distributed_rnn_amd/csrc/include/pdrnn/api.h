@@ -60,6 +60,9 @@ typedef struct {
   // rows [B*T][xg_ld] for the deferred-dW kernel (NULL: not written)
   float* xg_out;
   int xg_ld;
+  // sequence-in-wave mode 5 with stamps: the phase-stamped build (stamps rows
+  // of 24: the loop stamps, then per-step cycle sums of waves 0 / 2)
+  int phase_stamps;
 } PdrnnLstmSmallFwdArgs;
 
 typedef struct {

@@ -148,6 +148,10 @@ PDRNN_DEVICE FwdW<NC> load_fwd_w(const PdrnnLstmSmallFwdArgs& a, int l, int u, i
 }
 
 // p[0] / p[2]: own partials of m0 / m1 (+ bias), p[1] / p[3]: the partner's
+// (eight accumulators instead of four -- a gate's lo / hi halves apart, no
+// back-to-back dependent v_pk_fma_f32 -- measured no faster: a wave alone on
+// its SIMD issues v_pk_fma_f32 at ~8 cycles, so the products are issue-bound,
+// profiles/r6/fwd_phase_stamps.md)
 template <int NC>
 PDRNN_DEVICE void fwd_dot(const FwdW<NC>& W, const float4 (&v)[NC], float (&p)[4]) {
   pdrnn_f2 acc[4] = {{W.bias[0], 0.f}, {0.f, 0.f}, {W.bias[1], 0.f}, {0.f, 0.f}};
@@ -495,7 +499,12 @@ PDRNN_DEVICE Fwd4W<NC> load_fwd4_w(const PdrnnLstmSmallFwdArgs& a, int l, int u,
   return W;
 }
 
-template <int CELL = 0>
+// PH: per-phase stamps (diagnostics build, PDRNN_TUNE sw_phase=1 with
+// PDRNN_LSTM_STAMPS): s_memtime at the loop top (after the barrier), after the
+// operand reads landed, after the products, after the quad reduce, after the
+// cell and its stores; per-phase cycle sums over steps [16, T - 16) of waves 0
+// (layer 0) and 2 (layer 1), written behind the loop stamps (row of 24).
+template <int CELL = 0, bool PH = false>
 PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -564,6 +573,42 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
     bstore(cn, r_act, vo_c | m | lead, rw * (5 * kH * 4));
     bstore(hn, r_h, vo_h | m | lead, rw * (kH * 4));
   };
+  // phase stamps (PH only; compiled out otherwise)
+  uint64_t ph_t[5] = {0, 0, 0, 0, 0}, ph_sum[5] = {0, 0, 0, 0, 0}, ph_prev = 0, ph_n = 0;
+  auto ph_now = [&]() -> uint64_t {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t v = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    return v;
+  };
+  auto ph_mark = [&](int k, float dep) {
+    if constexpr (PH) {
+      asm volatile("" ::"v"(dep));  // (the value this phase produced exists before the stamp)
+      ph_t[k] = ph_now();
+    }
+  };
+  auto ph_reads = [&]() {
+    if constexpr (PH) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ph_t[1] = ph_now();
+    }
+  };
+  auto ph_step = [&](int it) {  // after the barrier: close step it, open it + 1
+    if constexpr (PH) {
+      const uint64_t now = ph_now();
+      if (it >= 16 && it < T - 16) {
+        ph_sum[0] += ph_t[1] - ph_t[0];  // barrier -> operand reads landed
+        ph_sum[1] += ph_t[2] - ph_t[1];  // products
+        ph_sum[2] += ph_t[3] - ph_t[2];  // quad reduce (DPP)
+        ph_sum[3] += ph_t[4] - ph_t[3];  // activations, cell, stores issued
+        ph_sum[4] += now - ph_t[4];      // barrier wait
+        ++ph_n;
+      }
+      (void)ph_prev;
+      ph_t[0] = now;
+    }
+  };
+  if constexpr (PH) ph_t[0] = ph_now();
 
   if (l == 0) {
     float bias[4];
@@ -576,6 +621,7 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) v[c] = ld4(src + 4 * c);
         __builtin_amdgcn_sched_barrier(0);
+        ph_reads();
         pdrnn_f2 acc[4] = {{bias[0], 0.f}, {bias[1], 0.f}, {bias[2], 0.f}, {bias[3], 0.f}};
 #pragma unroll
         for (int c = 0; c < 3; ++c)
@@ -587,9 +633,14 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
         float p[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) p[j] = acc[j].x + acc[j].y;
-        cell(t, true, gate_sum(p));
+        ph_mark(2, p[3]);
+        const float z = gate_sum(p);
+        ph_mark(3, z);
+        cell(t, true, z);
+        ph_mark(4, 0.f);
       }
       lds_barrier();
+      ph_step(it);
     }
   } else {
     float bias[4];
@@ -602,6 +653,7 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = ld4(src + 4 * c);
         __builtin_amdgcn_sched_barrier(0);
+        ph_reads();
         pdrnn_f2 acc[4] = {{bias[0], 0.f}, {bias[1], 0.f}, {bias[2], 0.f}, {bias[3], 0.f}};
 #pragma unroll
         for (int c = 0; c < 4; ++c)
@@ -613,14 +665,27 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
         float p[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) p[j] = acc[j].x + acc[j].y;
-        cell(t, true, gate_sum(p));
+        ph_mark(2, p[3]);
+        const float z = gate_sum(p);
+        ph_mark(3, z);
+        cell(t, true, z);
+        ph_mark(4, 0.f);
       }
       lds_barrier();
+      ph_step(it);
     }
   }
   if (a.stamps && tid == 0) {
-    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * (PH ? 24 : 8);
     st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+  }
+  if constexpr (PH) {
+    if ((wv == 0 || wv == 2) && lane == 0) {
+      uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 24 + 8 + (wv == 2 ? 8 : 0);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) st[k] = ph_sum[k];
+      st[5] = ph_n;
+    }
   }
   // ---- epilogue: h_n / c_n; the head reads the top layer's h_T from its slot
   if (q == 0) {
@@ -636,8 +701,8 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
     }
   }
 }
-template <int CELL>
-__global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs a) { fwd4_body<CELL>(a); }
+template <int CELL, bool PH = false>
+__global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs a) { fwd4_body<CELL, PH>(a); }
 
 // ---------------------------------------------------------------------------
 // Backward (lean contract: zero initial state, dL/dh_T of the top layer only,
@@ -1200,7 +1265,9 @@ hipError_t launch_fwd(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
 }
 hipError_t launch_fwd4(const PdrnnLstmSmallFwdArgs* a, hipStream_t st) {
   const size_t lds = sizeof(float) * (2 * 2 * kHB + (size_t)a->T * kXS);
-  if (a->cell == 1) hipLaunchKernelGGL(lstm_sw_fwd4_kernel<1>, dim3(a->B), dim3(256), lds, st, *a);
+  if (a->phase_stamps && a->stamps && a->cell == 0)
+    hipLaunchKernelGGL((lstm_sw_fwd4_kernel<0, true>), dim3(a->B), dim3(256), lds, st, *a);
+  else if (a->cell == 1) hipLaunchKernelGGL(lstm_sw_fwd4_kernel<1>, dim3(a->B), dim3(256), lds, st, *a);
   else hipLaunchKernelGGL(lstm_sw_fwd4_kernel<0>, dim3(a->B), dim3(256), lds, st, *a);
   return hipGetLastError();
 }

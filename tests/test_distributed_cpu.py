@@ -9,6 +9,7 @@ weights in their checkpoints).
 """
 import json
 import os
+import re
 
 import pytest
 import torch
@@ -111,7 +112,8 @@ def test_rccl_uid_exchange_through_store(tmp_path):
         "print('uid-ok', r, flush=True)\n"
         "dist.destroy_process_group()\n")
     out = torchrun([str(script)], nproc=3, cwd=str(tmp_path))
-    assert sorted(int(ln.split()[-1]) for ln in out.splitlines() if ln.startswith("uid-ok")) == [0, 1, 2]
+    # (the ranks' lines can interleave mid-line on the shared stdout)
+    assert sorted(int(r) for r in re.findall(r"uid-ok (\d)", out)) == [0, 1, 2], out
 
 
 def test_parameter_server_payload_mode_is_agreed(tmp_path):
