@@ -791,7 +791,9 @@ Tensor embedding_fwd(const Tensor& weight, const Tensor& idx, optional<at::Scala
   return out;
 }
 
-Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddings, int64_t padding_idx) {
+// out: accumulate into this fp32 [V, dim] gradient instead of returning a new one
+Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddings, int64_t padding_idx,
+                     const optional<Tensor>& out) {
   CHECK_HIP_TENSOR(dout);
   const c10::DeviceGuard guard(dout.device());
   const int64_t dim = dout.size(-1);
@@ -818,19 +820,28 @@ Tensor embedding_bwd(const Tensor& dout, const Tensor& idx, int64_t num_embeddin
     perm = std::get<1>(sorted).contiguous();
     offsets = at::searchsorted(vals, at::arange(num_embeddings + 1, flat.options())).contiguous();
   }
-  Tensor dw = at::empty({num_embeddings, dim}, dout.options().dtype(at::kFloat));
+  const bool acc = out.has_value() && out->defined();
+  if (acc)
+    TORCH_CHECK(out->scalar_type() == at::kFloat && out->is_contiguous() && out->size(0) == num_embeddings &&
+                out->numel() == num_embeddings * dim, "embedding_bwd: out must be the fp32 [V, dim] gradient");
   // small vocabulary, many contributions per row: split each row's list
   const int64_t per_row = g.size(0) / std::max<int64_t>(num_embeddings, 1);
   if (num_embeddings <= 4096 && per_row >= 64) {
+    Tensor dw = acc ? *out : at::empty({num_embeddings, dim}, dout.options().dtype(at::kFloat));
     const int pieces = (int)std::min<int64_t>(32, std::max<int64_t>(2, per_row / 32));
     Tensor part = at::empty({num_embeddings, pieces, dim}, dout.options().dtype(at::kFloat));
     HIP_LAUNCH_CHECK(pdrnn_embedding_bwd_pieces(g.data_ptr(), dt, perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(),
                                                 part.data_ptr<float>(), pieces, dw.data_ptr<float>(), num_embeddings,
-                                                dim, padding_idx, cur_stream()));
+                                                dim, padding_idx, acc ? 1 : 0, cur_stream()));
     return dw;
   }
+  Tensor dw = at::empty({num_embeddings, dim}, dout.options().dtype(at::kFloat));
   HIP_LAUNCH_CHECK(pdrnn_embedding_bwd_csr2(g.data_ptr(), dt, perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(),
                                             dw.data_ptr<float>(), num_embeddings, dim, padding_idx, cur_stream()));
+  if (acc) {
+    out->add_(dw.view_as(*out));
+    return *out;
+  }
   return dw;
 }
 
@@ -1451,18 +1462,30 @@ std::vector<Tensor> gemm_f32(const Tensor& A, bool a_kmajor, const Tensor& B, bo
 }
 
 // column sums of a 2-D tensor (fp32 or 16-bit; unit column stride) -> fp32 [cols]
-Tensor col_sum(const Tensor& X) {
+// accumulate_into: add the sums into each of these fp32 [cols] tensors (the
+// bias gradients themselves, ops/gradsink.py) instead of returning them
+Tensor col_sum(const Tensor& X, const optional<std::vector<Tensor>>& accumulate_into) {
   CHECK_HIP_TENSOR(X);
   const c10::DeviceGuard guard(X.device());
   TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "col_sum: 2-D tensor with unit column stride");
   const int64_t rows = X.size(0), cols = X.size(1);
-  Tensor out = at::empty({cols}, X.options().dtype(at::kFloat));
-  if (rows == 0) return out.zero_();
+  const bool acc = accumulate_into.has_value() && !accumulate_into->empty();
+  if (acc)
+    for (const auto& o : *accumulate_into)
+      TORCH_CHECK(o.scalar_type() == at::kFloat && o.is_contiguous() && o.numel() == cols && o.device() == X.device(),
+                  "col_sum: accumulate_into takes fp32 [cols] tensors");
+  Tensor out = acc ? (*accumulate_into)[0] : at::empty({cols}, X.options().dtype(at::kFloat));
+  if (rows == 0) return acc ? out : out.zero_();
   const int g = pdrnn_col_sum_groups(rows, cols);
   Tensor part = at::empty({g, cols}, X.options().dtype(at::kFloat));
   hipStream_t st = cur_stream();
   HIP_LAUNCH_CHECK(pdrnn_col_sum(X.data_ptr(), any_dtype(X), rows, cols, X.stride(0), part.data_ptr<float>(), g, st));
-  HIP_LAUNCH_CHECK(pdrnn_splitk_sum(part.data_ptr<float>(), g, cols, out.data_ptr<float>(), 0, st));
+  if (!acc) {
+    HIP_LAUNCH_CHECK(pdrnn_splitk_sum(part.data_ptr<float>(), g, cols, out.data_ptr<float>(), 0, st));
+    return out;
+  }
+  for (const auto& o : *accumulate_into)
+    HIP_LAUNCH_CHECK(pdrnn_splitk_sum(part.data_ptr<float>(), g, cols, o.data_ptr<float>(), 1, st));
   return out;
 }
 
@@ -1540,7 +1563,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_kmajor"), py::arg("B"), py::arg("b_kmajor"), py::arg("A2") = py::none(), py::arg("B2") = py::none(),
         py::arg("bias") = py::none(), py::arg("out16") = false, py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("splitk") = 1, py::arg("rowsum") = false);
-  m.def("col_sum", &col_sum, "deterministic fp32 column sums of a 2-D tensor");
+  m.def("col_sum", &col_sum, "deterministic fp32 column sums of a 2-D tensor (or added into accumulate_into)",
+        py::arg("X"), py::arg("accumulate_into") = py::none());
   m.def("gemm_variants", []() {
     int v[8];
     const int n = pdrnn_gemm_variants(v, 8);
@@ -1633,7 +1657,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                           perm.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), cur_stream()));
     return py::make_tuple(perm, offsets);
   }, "stable in-tree counting sort of indices by row (V <= 16384): (perm, row offsets)");
-  m.def("embedding_bwd", &embedding_bwd);
+  m.def("embedding_bwd", &embedding_bwd, py::arg("dout"), py::arg("idx"), py::arg("num_embeddings"),
+        py::arg("padding_idx"), py::arg("out") = py::none());
   m.attr("offload_arch") = "gfx950";
   pdrnn::register_runtime(m);
 }

@@ -287,9 +287,10 @@ hipError_t pdrnn_embedding_fwd16(const float* weight, const int64_t* idx, uint16
 int64_t pdrnn_embedding_sort_scratch(int64_t n, int64_t V);
 hipError_t pdrnn_embedding_sort(const int64_t* idx, int64_t n, int64_t V, int* scratch, int64_t* perm,
                                 int64_t* offsets, hipStream_t stream);
+// accumulate: dweight += the row sums instead of dweight = (a gradient buffer)
 hipError_t pdrnn_embedding_bwd_pieces(const void* dout, int dout_dtype, const int64_t* perm, const int64_t* offsets,
                                      float* partials, int pieces, float* dweight, int64_t num_embeddings, int64_t dim,
-                                     int64_t padding_idx, hipStream_t stream);
+                                     int64_t padding_idx, int accumulate, hipStream_t stream);
 hipError_t pdrnn_embedding_bwd_csr2(const void* dout, int dout_dtype, const int64_t* perm, const int64_t* offsets,
                                    float* dweight, int64_t num_embeddings, int64_t dim, int64_t padding_idx,
                                    hipStream_t stream);

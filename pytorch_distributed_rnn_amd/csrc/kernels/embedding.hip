@@ -160,16 +160,17 @@ __global__ void __launch_bounds__(256) emb_bwd_pieces_kernel(const void* __restr
   }
 }
 
+// accumulate: dw += the sum (the weight's gradient buffer itself, ops/gradsink.py)
 __global__ void __launch_bounds__(256) emb_bwd_pieces_sum_kernel(const float* __restrict__ part,
                                                                  float* __restrict__ dw, int64_t V, int64_t dim,
-                                                                 int P, int64_t padding_idx) {
+                                                                 int P, int64_t padding_idx, int accumulate) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= V * dim) return;
   const int64_t v = e / dim, c = e - v * dim;
   float acc = 0.f;
   if (v != padding_idx)
     for (int p = 0; p < P; ++p) acc += part[(v * P + p) * dim + c];
-  dw[e] = acc;
+  dw[e] = accumulate ? dw[e] + acc : acc;
 }
 
 // ---- stable counting sort of the indices by vocabulary row (in-tree) ------
@@ -306,7 +307,7 @@ hipError_t pdrnn_embedding_bwd_csr2(const void* dout, int dout_dtype, const int6
 
 hipError_t pdrnn_embedding_bwd_pieces(const void* dout, int dout_dtype, const int64_t* perm, const int64_t* offsets,
                                      float* partials, int pieces, float* dweight, int64_t num_embeddings, int64_t dim,
-                                     int64_t padding_idx, hipStream_t stream) {
+                                     int64_t padding_idx, int accumulate, hipStream_t stream) {
   if (pieces < 1) return hipErrorInvalidValue;
   const int64_t waves = num_embeddings * ((dim + 63) / 64) * pieces;
   const dim3 grid(pdrnn::blocks_for(waves)), block(256);
@@ -323,7 +324,7 @@ hipError_t pdrnn_embedding_bwd_pieces(const void* dout, int dout_dtype, const in
   if (e != hipSuccess) return e;
   const int64_t n = num_embeddings * dim;
   hipLaunchKernelGGL(pdrnn::emb_bwd_pieces_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     partials, dweight, num_embeddings, dim, pieces, padding_idx);
+                     partials, dweight, num_embeddings, dim, pieces, padding_idx, accumulate);
   return hipGetLastError();
 }
 

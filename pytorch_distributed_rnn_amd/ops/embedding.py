@@ -15,17 +15,25 @@ from .. import _ext
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, weight, idx, out_dtype, padding_idx):
+        from . import gradsink
         mod = _ext.native(weight.device)
         out = mod.embedding_fwd(weight.contiguous(), idx, out_dtype)
         ctx.save_for_backward(idx)
         ctx.meta = (weight.shape[0], -1 if padding_idx is None else padding_idx)
+        ctx.param = weight  # (gradsink: the backward may accumulate into its .grad)
+        ctx.direct = gradsink.enabled()
         return out
 
     @staticmethod
     def backward(ctx, dout):
+        from . import gradsink
         (idx,) = ctx.saved_tensors
         V, pad = ctx.meta
         mod = _ext.native(dout.device)
+        sk = gradsink.sink(ctx.param, ctx.direct)
+        if sk is not None:  # direct mode: the row sums added into the flat gradient view
+            mod.embedding_bwd(dout.contiguous(), idx, V, pad, out=sk)
+            return None, None, None, None
         return mod.embedding_bwd(dout.contiguous(), idx, V, pad), None, None, None
 
 

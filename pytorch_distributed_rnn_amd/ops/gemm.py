@@ -82,8 +82,10 @@ def linear16(x: Tensor, w: Tensor, bias: Optional[Tensor]) -> Tensor:
     return torch.addmm(bias.to(x.dtype), x, w.t())
 
 
-def mm_kk(pairs: Sequence[Tuple[Tensor, Tensor]]) -> Tensor:
-    """sum over (a [K_s, M], b [K_s, N]) of a^T b, fp32 [M, N] (1 or 2 pairs)."""
+def mm_kk(pairs: Sequence[Tuple[Tensor, Tensor]], accumulate_into: Optional[Tensor] = None) -> Tensor:
+    """sum over (a [K_s, M], b [K_s, N]) of a^T b, fp32 [M, N] (1 or 2 pairs);
+    ``accumulate_into``: added into that contiguous fp32 [M, N] tensor by the
+    GEMM's epilogue / split-K sum (a parameter's gradient, ops/gradsink.py)."""
     a, b = pairs[0]
     mod = _native(a)
     M, N = a.shape[1], b.shape[1]
@@ -93,10 +95,11 @@ def mm_kk(pairs: Sequence[Tuple[Tensor, Tensor]]) -> Tensor:
         len(pairs) <= 2 and mod.gemm16_supported(M, N, K1, K2, True, True, False)
     if ok:
         sk = _splitk(a.device, M, N, K1 + K2)
+        kw = dict(out=accumulate_into, accumulate=True) if accumulate_into is not None else {}
         if len(pairs) == 2:
-            return mod.gemm16(a, True, b, True, A2=pairs[1][0], B2=pairs[1][1], splitk=sk, variant=_variant())
-        return mod.gemm16(a, True, b, True, splitk=sk, variant=_variant())
-    out = None
+            return mod.gemm16(a, True, b, True, A2=pairs[1][0], B2=pairs[1][1], splitk=sk, variant=_variant(), **kw)
+        return mod.gemm16(a, True, b, True, splitk=sk, variant=_variant(), **kw)
+    out = accumulate_into
     for a_, b_ in pairs:
         try:
             r = torch.mm(a_.t(), b_, out_dtype=torch.float32)
@@ -132,6 +135,7 @@ class _Linear16(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias):
+        from . import gradsink
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         w16 = weight.detach().to(x.dtype)
@@ -139,13 +143,23 @@ class _Linear16(torch.autograd.Function):
         ctx.save_for_backward(x2, w16)
         ctx.has_bias = bias is not None
         ctx.shp = shp
+        ctx.params = (weight, bias)  # (gradsink: the backward may accumulate into their .grad)
+        ctx.direct = gradsink.enabled()
         return y.view(*shp[:-1], w16.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
+        from . import gradsink
         x2, w16 = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(x2.dtype).contiguous()
         dx = mm_nk16([(dy2, w16)]).view(ctx.shp) if ctx.needs_input_grad[0] else None
+        sw, sb = gradsink.sink(ctx.params[0], ctx.direct), gradsink.sink(ctx.params[1], ctx.direct)
+        if sw is not None and (not ctx.has_bias or sb is not None):
+            # direct mode: dW and db added into the flat gradient views
+            mm_kk([(dy2, x2)], accumulate_into=sw)
+            if ctx.has_bias:
+                col_sum(dy2, accumulate_into=[sb])
+            return dx, None, None
         dw = mm_kk([(dy2, x2)]) if ctx.needs_input_grad[1] else None
         db = col_sum(dy2) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db
@@ -285,11 +299,17 @@ def gemm_f32(a: Tensor, a_kmajor: bool, b: Tensor, b_kmajor: bool, pairs2=None, 
     return c, rs
 
 
-def col_sum(x: Tensor) -> Tensor:
+def col_sum(x: Tensor, accumulate_into: Optional[Sequence[Tensor]] = None) -> Tensor:
     """fp32 column sums of a 2-D tensor (fp32 or 16-bit): in-tree and
-    deterministic on the GPU, torch on the CPU."""
+    deterministic on the GPU, torch on the CPU.  ``accumulate_into``: added
+    into each of those fp32 [cols] tensors instead (bias gradients)."""
     mod = _native_f32(x)
     if mod is not None and x.dim() == 2 and x.stride(1) == 1 and x.dtype in (torch.float32, torch.bfloat16,
                                                                               torch.float16):
-        return mod.col_sum(x)
-    return x.sum(0, dtype=torch.float32)
+        return mod.col_sum(x, list(accumulate_into) if accumulate_into else None)
+    s = x.sum(0, dtype=torch.float32)
+    if accumulate_into:
+        for o in accumulate_into:
+            o.add_(s)
+        return accumulate_into[0]
+    return s

@@ -323,6 +323,8 @@ class _LargeLSTMLayer(torch.autograd.Function):
         ctx.cfg = (H, ndir, tile, rev_mask, [w is not None for w in weights], h0 is not None,
                    c0 is not None, h0.dtype if h0 is not None else None,
                    c0.dtype if c0 is not None else None)
+        ctx.params = weights  # (gradsink: the 16-bit backward may accumulate into their .grad)
+        ctx.direct = gradsink.enabled()
         return hseq, hn, cn
 
     @staticmethod
@@ -392,6 +394,7 @@ def _backward_gemms16(ctx, dgates, dh0, dc0, hseq, h0c, x2, wih):
     T, B, I = ctx.saved_tensors[0].shape
     grads: List[Optional[Tensor]] = []
     Gs = []
+    params = getattr(ctx, "params", None)
     for d in range(ndir):
         G = dgates[d].view(T * B, 4 * H)                         # gate-blocked = parameter order
         Gs.append(G)
@@ -404,6 +407,21 @@ def _backward_gemms16(ctx, dgates, dh0, dc0, hseq, h0c, x2, wih):
                 pairs.append((G[:(T - 1) * B], hd[1:].reshape((T - 1) * B, H)))
         if h0c is not None:
             pairs.append((G[:B] if d == 0 else G[(T - 1) * B:], h0c[d]))
+        # direct mode (ops/gradsink.py): this direction's weight and bias
+        # gradients accumulated into the flat gradient views by the GEMM
+        # epilogue / split-K sum and the column-sum pass -- nothing for
+        # autograd to add
+        pw = params[4 * d:4 * d + 4] if params is not None else (None,) * 4
+        sinks = [gradsink.sink(w, ctx.direct) if w is not None else None for w in pw]
+        if params is not None and pairs and all(sk is not None for sk, w in zip(sinks, pw) if w is not None) and \
+                sinks[0] is not None and sinks[1] is not None:
+            mm_kk(pairs, accumulate_into=sinks[1])
+            mm_kk([(G, x2)], accumulate_into=sinks[0])
+            bs = [sk for sk in sinks[2:] if sk is not None]
+            if bs:
+                col_sum(G, accumulate_into=bs)
+            grads += [None, None, None, None]
+            continue
         dwhh = mm_kk(pairs) if pairs else torch.zeros(4 * H, H, device=G.device, dtype=torch.float32)
         dwih = mm_kk([(G, x2)])
         db = col_sum(G)  # in-tree deterministic column sums (fp32 accumulation of the 16-bit G)

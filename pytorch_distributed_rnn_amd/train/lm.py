@@ -69,6 +69,7 @@ class LMTrainer:
         self.streams = corpus.streams(gb, self.rank, self.world).to(device)
         self.vocab = corpus.vocab_size
         self._pending: List[dict] = []  # steps not yet verified (deferred verification)
+        self.direct_grads = True  # one process: gradients written into the flat views (see _fwd_bwd)
 
     def _clip(self) -> None:
         if self.grad_clip and self.grad_clip > 0:
@@ -81,12 +82,17 @@ class LMTrainer:
             g.mul_(torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0))
 
     def _fwd_bwd(self, inp: Tensor, tgt: Tensor) -> Tensor:
+        from ..ops import gradsink
         self.optimizer.zero_grad()
-        with trace_range("pdrnn.forward"):
-            logits = self.model(inp, carry=True)                               # [T, B, V]
-            loss = cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt.t().reshape(-1))
-        with trace_range("pdrnn.backward"):
-            loss.backward()
+        # one process: the in-tree Functions add their weight gradients into
+        # the flat gradient views themselves (ops/gradsink.py: no per-parameter
+        # autograd add launches); the DDP reducer keeps the autograd path
+        with gradsink.direct_grads(self.direct_grads and self.model is self.inner and self.device.type == "cuda"):
+            with trace_range("pdrnn.forward"):
+                logits = self.model(inp, carry=True)                               # [T, B, V]
+                loss = cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt.t().reshape(-1))
+            with trace_range("pdrnn.backward"):
+                loss.backward()
         return loss
 
     # ---------------------------------------------- persistent-path verification

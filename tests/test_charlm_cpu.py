@@ -110,3 +110,22 @@ def test_gru_forward_sequences_per_workgroup_override(monkeypatch):
     if not torch.cuda.is_available():
         assert gru_fwd_nb(1440, 32) == 1
     assert gru_fwd_nb(1440, 16) == 1
+
+
+def test_gemm_helpers_accumulate_into_cpu():
+    """ops/gemm.py mm_kk / col_sum ``accumulate_into`` (the direct-gradient
+    sinks' products) on the torch fallback: the result is added into the
+    given tensors."""
+    from pytorch_distributed_rnn_amd.ops.gemm import col_sum, mm_kk
+    torch.manual_seed(0)
+    a, b, a2, b2 = torch.randn(40, 8), torch.randn(40, 6), torch.randn(10, 8), torch.randn(10, 6)
+    o = torch.randn(8, 6)
+    ref = o + a.t() @ b + a2.t() @ b2
+    assert mm_kk([(a, b), (a2, b2)], accumulate_into=o) is o
+    torch.testing.assert_close(o, ref)
+    x = torch.randn(30, 5)
+    o1, o2 = torch.randn(5), torch.randn(5)
+    r1, r2 = o1 + x.sum(0), o2 + x.sum(0)
+    col_sum(x, accumulate_into=[o1, o2])
+    torch.testing.assert_close(o1, r1)
+    torch.testing.assert_close(o2, r2)

@@ -136,6 +136,44 @@ def test_charlm_trains_on_large_path():
     assert hist[-1] < first - 0.5, (first, hist)
 
 
+def test_charlm_direct_grads_match_autograd(monkeypatch):
+    """One process: the char-LM step's in-tree Functions (16-bit LSTM layer,
+    16-bit head, embedding) add their weight gradients into the flat gradient
+    views themselves (ops/gradsink.py) instead of returning them for
+    autograd's per-parameter adds -- the same gradients, bit for bit, as the
+    autograd path, and every sink actually taken."""
+    from pytorch_distributed_rnn_amd.data.charlm import CharCorpus
+    from pytorch_distributed_rnn_amd.models.charlm import CharLM
+    from pytorch_distributed_rnn_amd.ops import gradsink
+    from pytorch_distributed_rnn_amd.train.lm import LMTrainer
+    torch.manual_seed(0)
+    corpus = CharCorpus.synthetic(100_000, 256, seed=0)
+    tr = LMTrainer(CharLM(256, 64, 256, 2, 0.0, torch.bfloat16), corpus, 32, 64, 3e-3,
+                   device=torch.device("cuda", 0), log_interval=0)
+    segs = list(CharCorpus.segments(tr.streams, 64, 2))
+    taken = []
+    real_sink = gradsink.sink
+
+    def counting_sink(p, on):
+        g = real_sink(p, on)
+        taken.append(g is not None)
+        return g
+    monkeypatch.setattr(gradsink, "sink", counting_sink)
+    grads = []
+    for direct in (True, False):
+        tr.direct_grads = direct
+        tr.inner.reset_hidden_state()
+        tr._fwd_bwd(*segs[0])
+        tr._fwd_bwd(*segs[1])  # (a carried state)
+        torch.cuda.synchronize()
+        grads.append(tr.flat.grad.clone())
+        if direct:
+            n_direct = sum(taken)
+    # embedding 1 + head 2 + 2 layers x 4 per step, two steps
+    assert n_direct == 2 * (1 + 2 + 8), n_direct
+    assert torch.equal(grads[0], grads[1])
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_embedding_bwd_csr8(dt):
     mod = _ext.require()
