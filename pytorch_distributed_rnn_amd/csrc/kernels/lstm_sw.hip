@@ -219,6 +219,73 @@ PDRNN_DEVICE Cell fwd_cell_any(const float (&p)[4], pdrnn_f2 gk, float c, float 
 template <int NL, int NB>
 PDRNN_DEVICE constexpr int fwd_lds_floats_hb() { return NB * NL * 2 * kHB; }
 
+// x staging (forward prologue): NB sequences' [T, I] input rows into the LDS
+// rows xs[(n T + t) kXS + k] (zero-padded to kXS; the caller zeroed xs) and,
+// when xg_out is set, the fp32 rows [b T + t][xg_ld] of the deferred dW (pad
+// columns written as zeros).  A sequence's rows are one contiguous block of the
+// motion batch: 16-byte loads of the block, all of a thread's rounds in flight
+// at once (element-wise loads, one dependent round per 4 elements per thread,
+// cost the single-layer forward 16 us of ~100 at B = 1440, 23 with bf16 x,
+// profiles/r6/x_staging.md).  Returns false when the layout does not allow it.
+template <int NB>
+PDRNN_DEVICE bool stage_x_vec(const PdrnnLstmSmallFwdArgs& a, float* xs, const int (&bsrc)[NB], const int (&bidx)[NB],
+                              const int (&vint)[NB], int tid, int nthr) {
+  const int T = a.T, I = a.I;
+  const int esz = a.x_bf16 ? 2 : 4;
+  const int per = T * I;
+  if (a.x_st != I || a.x_sb != (int64_t)per || (per * esz) % 16 != 0 ||
+      (reinterpret_cast<uintptr_t>(a.x) & 15) != 0)
+    return false;
+  const int cpe = 16 / esz;  // elements per 16-byte chunk
+  const int nch = per / cpe;
+  const int tot = NB * nch;
+  const int xg_ld = a.xg_ld;
+  const char* xb = reinterpret_cast<const char*>(a.x);
+  constexpr int R = 8;  // chunks per thread in flight
+  for (int c0 = tid; c0 < tot; c0 += R * nthr) {
+    uint4 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int c = min(c0 + r * nthr, tot - 1);
+      const int n = c / nch, q = c - n * nch;
+      v[r] = *reinterpret_cast<const uint4*>(xb + ((int64_t)pick<NB>(bsrc, n) * per + (int64_t)q * cpe) * esz);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int c = c0 + r * nthr;
+      if (c < tot) {
+        const int n = c / nch, q = c - n * nch;
+        const uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+        const int e0 = q * cpe;
+        int t = e0 / I, k = e0 - t * I;  // (one division per chunk, then stepped)
+        float* xrow = xs + (n * T + t) * kXS;
+        float* grow = a.xg_out ? a.xg_out + ((int64_t)pick<NB>(bidx, n) * T + t) * xg_ld : nullptr;
+        const bool gv = grow != nullptr && pick<NB>(vint, n);
+        for (int j = 0; j < cpe; ++j) {
+          const float val = esz == 2 ? __uint_as_float((j & 1 ? w[j >> 1] >> 16 : w[j >> 1] & 0xFFFFu) << 16)
+                                     : __uint_as_float(w[j]);
+          xrow[k] = val;
+          if (gv && k < xg_ld) grow[k] = val;
+          if (++k == I) {
+            k = 0;
+            xrow += kXS;
+            if (grow) grow += xg_ld;
+          }
+        }
+      }
+    }
+  }
+  if (a.xg_out && xg_ld > I) {  // the dW kernel reads xg_ld columns: zero pads
+    const int padw = xg_ld - I;
+    for (int e = tid; e < NB * T * padw; e += nthr) {
+      const int n = e / (T * padw), rem = e - n * (T * padw);
+      const int t = rem / padw, k = I + rem - t * padw;
+      if (pick<NB>(vint, n)) a.xg_out[((int64_t)pick<NB>(bidx, n) * T + t) * xg_ld + k] = 0.f;
+    }
+  }
+  return true;
+}
+
 // NL = 1 or 2.  MODE 0/1: one wave runs all layers of NB = 1 / 2 sequences.
 // MODE 2/3 (NL = 2): wave l runs layer l of NB = 1 / 2 sequences, one
 // barrier per step (layer 0's h_t handed over through parity slots).
@@ -234,6 +301,7 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
   const int tid = threadIdx.x, nthr = blockDim.x;
+  const uint64_t sr_in = (a.stamps && tid == 0) ? stamp_real() : 0;  // (entry: the prologue's cost)
   const int lane = tid & 63;
   const int wv = SPLIT ? __builtin_amdgcn_readfirstlane(tid >> 6) : 0;
   const int u = lane >> 1;
@@ -256,8 +324,11 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   }
 
   // ---- prologue: zero the h slots (h_{-1} = 0, pad chunks), stage x ------
-  for (int e = tid; e < fwd_lds_floats_hb<NL, NB>(); e += nthr) hb[e] = 0.f;
-  {
+  // (the vector staging writes only the I real columns: xs zeroed first)
+  const bool xvec = a.x_st == I && a.x_sb == (int64_t)T * I;
+  for (int e = tid; e < fwd_lds_floats_hb<NL, NB>() + (xvec ? NB * T * kXS : 0); e += nthr) hb[e] = 0.f;
+  if (xvec) __syncthreads();
+  if (!(xvec && stage_x_vec<NB>(a, xs, bsrc, bidx, vint, tid, nthr))) {
     const int per = T * kXS, tot = NB * per;
     const int xg_ld = a.xg_ld;
     for (int e0 = tid; e0 < tot; e0 += 4 * nthr) {
@@ -409,13 +480,25 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
       }
     }
   }
+  uint64_t sr1 = 0;
   if (a.stamps && tid == 0) {
     uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
-    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+    sr1 = stamp_real();
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = sr1;
   }
 
   // ---- epilogue: h_n / c_n, then the fused head on the top layer's h_T ----
+  // (two sequences per wave: both heads' operands loaded first, their
+  // dependent loads in flight together, not behind the first head's stores;
+  // one sequence loads inline -- the VGPR-capped mode 6 would spill)
   const bool top_wave = !SPLIT || wv == NL - 1;
+  HeadIn hin[NB];
+  if constexpr (NB > 1) {
+    if (a.head_w && top_wave) {
+#pragma unroll
+      for (int n = 0; n < NB; ++n) hin[n] = head_load(a, pick<NB>(bidx, n), u);
+    }
+  }
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     if (!valid[n]) continue;
@@ -426,7 +509,14 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
       if (!odd && a.hn) a.hn[((int64_t)l * B + b) * kH + u] = hst[l][n];
       if (!odd && a.cn) a.cn[((int64_t)l * B + b) * kH + u] = cst[l][n];
     }
-    if (a.head_w && top_wave) motion_head(a, b, hst[NL - 1][n], u, odd);
+    if (a.head_w && top_wave) {
+      if constexpr (NB > 1) motion_head(a, b, hst[NL - 1][n], u, odd, hin[n]);
+      else motion_head(a, b, hst[NL - 1][n], u, odd);
+    }
+  }
+  if (a.stamps && tid == 0) {
+    uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
+    st[4] = sr_in; st[5] = stamp_real(); st[6] = stamp_cu();
   }
 }
 
@@ -520,13 +610,19 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
   float* xs = smem + 2 * 2 * kHB;                    // [T][kXS]
   auto hbuf = [&](int ll, int p) { return hb + (ll * 2 + p) * kHB; };
 
-  for (int e = tid; e < 2 * 2 * kHB; e += 256) hb[e] = 0.f;
-  for (int e = tid; e < T * kXS; e += 256) {
-    const int t = e / kXS, k = e - t * kXS;
-    const float x = ldx(a.x, (int64_t)bsrc * a.x_sb + (int64_t)t * a.x_st + min(k, I - 1), a.x_bf16);
-    const float v = k < I ? x : 0.f;
-    xs[e] = v;
-    if (a.xg_out && k < a.xg_ld) a.xg_out[((int64_t)b * T + t) * a.xg_ld + k] = v;
+  // (vector staging as in lstm_sw_fwd_kernel: xs zeroed first)
+  const bool xvec = a.x_st == I && a.x_sb == (int64_t)T * I;
+  for (int e = tid; e < 2 * 2 * kHB + (xvec ? T * kXS : 0); e += 256) hb[e] = 0.f;
+  if (xvec) __syncthreads();
+  const int bsrc1[1] = {bsrc}, bidx1[1] = {b}, vint1[1] = {1};
+  if (!(xvec && stage_x_vec<1>(a, xs, bsrc1, bidx1, vint1, tid, 256))) {
+    for (int e = tid; e < T * kXS; e += 256) {
+      const int t = e / kXS, k = e - t * kXS;
+      const float x = ldx(a.x, (int64_t)bsrc * a.x_sb + (int64_t)t * a.x_st + min(k, I - 1), a.x_bf16);
+      const float v = k < I ? x : 0.f;
+      xs[e] = v;
+      if (a.xg_out && k < a.xg_ld) a.xg_out[((int64_t)b * T + t) * a.xg_ld + k] = v;
+    }
   }
   __syncthreads();
 
@@ -788,6 +884,7 @@ PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
   const int tid = threadIdx.x;
+  const uint64_t sr_in = (a.stamps && tid == 0) ? stamp_real() : 0;  // (entry: the prologue's cost)
   const int lane = tid & 63;
   const int wv = SPLIT ? __builtin_amdgcn_readfirstlane(tid >> 6) : 0;
   const int u = lane >> 1;
@@ -1204,7 +1301,9 @@ PDRNN_DEVICE void bwd_body(const PdrnnLstmSmallBwdArgs& a) {
   }
   if (a.stamps && tid == 0) {
     uint64_t* st = a.stamps + (uint64_t)blockIdx.x * 8;
-    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+    const uint64_t sr1 = stamp_real();
+    st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = sr1;
+    st[4] = sr_in; st[5] = sr1; st[6] = stamp_cu();
   }
 }
 template <int NL, int MODE, int CELL = 0>
