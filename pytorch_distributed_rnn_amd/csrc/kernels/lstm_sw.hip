@@ -327,7 +327,7 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   // (the vector staging writes only the I real columns: xs zeroed first)
   const bool xvec = a.x_st == I && a.x_sb == (int64_t)T * I;
   for (int e = tid; e < fwd_lds_floats_hb<NL, NB>() + (xvec ? NB * T * kXS : 0); e += nthr) hb[e] = 0.f;
-  if (xvec) __syncthreads();
+  if (xvec) lds_barrier();
   if (!(xvec && stage_x_vec<NB>(a, xs, bsrc, bidx, vint, tid, nthr))) {
     const int per = T * kXS, tot = NB * per;
     const int xg_ld = a.xg_ld;
@@ -354,7 +354,9 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
       }
     }
   }
-  __syncthreads();
+  // the LDS rows are in place; the xg_out stores (read by a later launch) need
+  // not drain here -- a __syncthreads() would wait for them (~1-3 us)
+  lds_barrier();
 
   const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
   const __amdgpu_buffer_rsrc_t r_h = uniform_rsrc(a.hseq);
@@ -613,7 +615,7 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
   // (vector staging as in lstm_sw_fwd_kernel: xs zeroed first)
   const bool xvec = a.x_st == I && a.x_sb == (int64_t)T * I;
   for (int e = tid; e < 2 * 2 * kHB + (xvec ? T * kXS : 0); e += 256) hb[e] = 0.f;
-  if (xvec) __syncthreads();
+  if (xvec) lds_barrier();
   const int bsrc1[1] = {bsrc}, bidx1[1] = {b}, vint1[1] = {1};
   if (!(xvec && stage_x_vec<1>(a, xs, bsrc1, bidx1, vint1, tid, 256))) {
     for (int e = tid; e < T * kXS; e += 256) {
@@ -624,7 +626,7 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
       if (a.xg_out && k < a.xg_ld) a.xg_out[((int64_t)b * T + t) * a.xg_ld + k] = v;
     }
   }
-  __syncthreads();
+  lds_barrier();  // (as in lstm_sw_fwd_kernel; the one-launch step's __syncthreads drains them before its BPTT)
 
   const __amdgpu_buffer_rsrc_t r_act = uniform_rsrc(a.act);
   const __amdgpu_buffer_rsrc_t r_h = uniform_rsrc(a.hseq);
