@@ -312,11 +312,17 @@ class Trainer:
 
     def _direct_grads_ok(self) -> bool:
         """The in-tree Functions may accumulate weight gradients straight into
-        the flat .grad views (ops/gradsink.py): one process and no forced
-        collectives -- nothing observes the per-parameter accumulation."""
-        if self.device.type != "cuda" or self.world_size() != 1:
-            return False
-        return not any(os.environ.get(k, "0") == "1" for k in ("PDRNN_FORCE_COLLECTIVE", "PDRNN_FORCE_GRAD_SYNC"))
+        the flat .grad views (ops/gradsink.py).  Multi-rank too: the
+        framework's reducers (parallel/ddp.py, parallel/horovod.py) mark a
+        parameter ready from a post-accumulate-grad hook, which autograd fires
+        after the Function has returned -- with ``.grad`` already the finished
+        view (AccumulateGrad runs with an undefined incoming gradient and
+        leaves it alone).  Proven against the plain path on gloo ranks
+        (tests/test_distributed_cpu.py::test_direct_grads_under_ddp_and_horovod_match).
+        torch's own DDP reducer is not used with the flat views.
+        (``PDRNN_TUNE=direct_grads=0``: the autograd adds, for A/B.)"""
+        from ..utils.tune import tune
+        return self.device.type == "cuda" and tune("direct_grads", "1") != "0"
 
     def train_batch(self, batch) -> Tuple[Tensor, int]:
         """One optimizer step on one batch; returns (stats [loss, n, correct], batch size).

@@ -268,3 +268,99 @@ def test_allreduce_sweep_tool_world2(tmp_path):
     rows = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
     assert [r["bytes"] for r in rows] == [4096, 8192, 16384]
     assert all(r["world"] == 2 and r["backend"] == "gloo" and r["us"] > 0 and r["busbw_GBs"] > 0 for r in rows)
+
+
+def test_direct_grads_under_ddp_and_horovod_match(tmp_path):
+    """ops/gradsink.py on multi-rank runs: a Function that
+    adds its weight gradients into the flat .grad views itself and returns
+    None for them (the pattern of the in-tree Functions) under the
+    framework's DDP reducer and Horovod optimizer on 2 gloo ranks: the
+    post-accumulate-grad hooks still fire after the view is written, every
+    bucket is reduced, and the reduced gradients equal the plain autograd
+    path's bit for bit on every rank."""
+    script = tmp_path / "direct.py"
+    script.write_text(
+        "import sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch, torch.distributed as dist\n"
+        "from torch import nn\n"
+        "from pytorch_distributed_rnn_amd.ops import gradsink\n"
+        "from pytorch_distributed_rnn_amd.ops.adam import FusedAdam\n"
+        "from pytorch_distributed_rnn_amd.parallel import env, horovod as hvd\n"
+        "from pytorch_distributed_rnn_amd.parallel.ddp import DistributedDataParallel\n"
+        "from pytorch_distributed_rnn_amd.utils.flat import flatten_module\n"
+        "class SinkLinear(torch.autograd.Function):\n"
+        "    @staticmethod\n"
+        "    def forward(ctx, x, w, b):\n"
+        "        ctx.save_for_backward(x, w)\n"
+        "        ctx.params = (w, b)\n"
+        "        ctx.direct = gradsink.enabled()\n"
+        "        return x @ w.detach().t() + b.detach()\n"
+        "    @staticmethod\n"
+        "    def backward(ctx, dy):\n"
+        "        x, w = ctx.saved_tensors\n"
+        "        dx = dy @ w.detach()\n"
+        "        sw, sb = gradsink.sink(ctx.params[0], ctx.direct), gradsink.sink(ctx.params[1], ctx.direct)\n"
+        "        if sw is not None and sb is not None:\n"
+        "            sw.add_(dy.t() @ x)\n"
+        "            sb.add_(dy.sum(0))\n"
+        "            return dx, None, None\n"
+        "        return dx, dy.t() @ x, dy.sum(0)\n"
+        "class Net(nn.Module):\n"
+        "    def __init__(self):\n"
+        "        super().__init__()\n"
+        "        self.a, self.b = nn.Linear(12, 32), nn.Linear(32, 5)\n"
+        "    def forward(self, x):\n"
+        "        h = torch.tanh(SinkLinear.apply(x, self.a.weight, self.a.bias))\n"
+        "        return SinkLinear.apply(h, self.b.weight, self.b.bias)\n"
+        "env.init_distributed('gloo')\n"
+        "r, W = dist.get_rank(), dist.get_world_size()\n"
+        "torch.manual_seed(0)\n"
+        "base = Net()\n"
+        "gx = torch.Generator().manual_seed(100 + r)\n"
+        "xs = [torch.randn(16, 12, generator=gx) for _ in range(3)]\n"
+        "def run_ddp(direct):\n"
+        "    m = Net(); m.load_state_dict(base.state_dict())\n"
+        "    d = DistributedDataParallel(m, bucket_cap_mb=0.001)\n"
+        "    out = []\n"
+        "    for x in xs:\n"
+        "        for p in m.parameters(): p.grad.zero_()\n"
+        "        with gradsink.direct_grads(direct):\n"
+        "            d(x).square().mean().backward()\n"
+        "        out.append(torch.cat([p.grad.reshape(-1).clone() for p in m.parameters()]))\n"
+        "    return out\n"
+        "def run_hvd(direct):\n"
+        "    m = Net(); m.load_state_dict(base.state_dict()); flatten_module(m)\n"
+        "    # (the trainers' FusedAdam zeroes the flat gradient in place: the views stay)\n"
+        "    opt = hvd.DistributedOptimizer(FusedAdam(m.parameters(), lr=0.0), named_parameters=m.named_parameters())\n"
+        "    out = []\n"
+        "    for x in xs:\n"
+        "        opt.zero_grad()\n"
+        "        with gradsink.direct_grads(direct):\n"
+        "            m(x).square().mean().backward()\n"
+        "        opt.synchronize()\n"
+        "        out.append(torch.cat([p.grad.reshape(-1).clone() for p in m.parameters()]))\n"
+        "    return out\n"
+        "hvd.init('gloo')\n"
+        "taken = [0]\n"
+        "real_sink = gradsink.sink\n"
+        "def counting(p, on):\n"
+        "    g = real_sink(p, on)\n"
+        "    taken[0] += g is not None\n"
+        "    return g\n"
+        "gradsink.sink = counting\n"
+        "for name, fn in (('ddp', run_ddp), ('hvd', run_hvd)):\n"
+        "    taken[0] = 0\n"
+        "    a = fn(True)\n"
+        "    assert taken[0] == 3 * 4, (name, taken[0])  # every parameter's gradient written in place\n"
+        "    b = fn(False)\n"
+        "    for ga, gb in zip(a, b):\n"
+        "        assert torch.equal(ga, gb), (name, (ga - gb).abs().max())\n"
+        "        allg = [torch.empty_like(ga) for _ in range(W)]\n"
+        "        dist.all_gather(allg, ga)\n"
+        "        assert all(torch.equal(allg[0], g) for g in allg), name\n"
+        "    open(f'direct-ok-{name}-{r}', 'w').close()  # (the ranks share stdout)\n"
+        "dist.destroy_process_group()\n")
+    out = torchrun([str(script)], nproc=2, cwd=str(tmp_path))
+    got = sorted(p.name for p in tmp_path.glob("direct-ok-*"))
+    assert got == ["direct-ok-ddp-0", "direct-ok-ddp-1", "direct-ok-hvd-0", "direct-ok-hvd-1"], out
