@@ -324,8 +324,10 @@ lstm_sw_fwd_kernel(PdrnnLstmSmallFwdArgs a) {
   }
 
   // ---- prologue: zero the h slots (h_{-1} = 0, pad chunks), stage x ------
-  // (the vector staging writes only the I real columns: xs zeroed first)
-  const bool xvec = a.x_st == I && a.x_sb == (int64_t)T * I;
+  // (the vector staging writes only the I real columns: xs zeroed first; two
+  // sequences per workgroup only -- with one, the zeroing pass and barrier
+  // cost more than the element loads: mode 6 136.2 vs 133.6 us at B = 1440)
+  const bool xvec = NB == 2 && a.x_st == I && a.x_sb == (int64_t)T * I;
   for (int e = tid; e < fwd_lds_floats_hb<NL, NB>() + (xvec ? NB * T * kXS : 0); e += nthr) hb[e] = 0.f;
   if (xvec) lds_barrier();
   if (!(xvec && stage_x_vec<NB>(a, xs, bsrc, bidx, vint, tid, nthr))) {
