@@ -602,6 +602,7 @@ template <int CELL = 0, bool PH = false>
 PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
+  const uint64_t sr_in = (a.stamps && tid == 0) ? stamp_real() : 0;  // (entry: the prologue's cost)
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = wv >> 1;
@@ -778,6 +779,7 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
   if (a.stamps && tid == 0) {
     uint64_t* st = a.stamps + (uint64_t)blockIdx.x * (PH ? 24 : 8);
     st[0] = st0; st[1] = stamp_cycles(); st[2] = sr0; st[3] = stamp_real();
+    st[4] = sr_in; st[6] = stamp_cu();  // (exit: after the head, below)
   }
   if constexpr (PH) {
     if ((wv == 0 || wv == 2) && lane == 0) {
@@ -800,6 +802,7 @@ PDRNN_DEVICE void fwd4_body(const PdrnnLstmSmallFwdArgs& a) {
       motion_head(a, b, hbuf(1, (T - 1) & 1)[hu], hu, (lane & 1) != 0);
     }
   }
+  if (a.stamps && tid == 0) a.stamps[(uint64_t)blockIdx.x * (PH ? 24 : 8) + 5] = stamp_real();
 }
 template <int CELL, bool PH = false>
 __global__ void __launch_bounds__(256) lstm_sw_fwd4_kernel(PdrnnLstmSmallFwdArgs a) { fwd4_body<CELL, PH>(a); }
