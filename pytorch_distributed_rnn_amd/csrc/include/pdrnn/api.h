@@ -165,9 +165,9 @@ hipError_t pdrnn_lstm_small_step(const PdrnnLstmSmallFwdArgs* f, const PdrnnLstm
                                  hipStream_t stream);
 
 // ----------------------------------------------------------------------------
-// Sequence-in-wave LSTM stack (kernels/lstm_sw.hip): H = 32, 1 or 2 layers,
-// input size <= 12, lean training contract (zero initial state, loss through
-// the fused head on h_T).  A sequence's whole recurrence lives in ONE wave
+// Sequence-in-wave LSTM / GRU stack (kernels/lstm_sw.hip): H = 32, 1 or 2
+// layers, input size <= 12, lean training contract (zero initial state, loss
+// through the fused head on h_T; the GRU as the packed 4-block stack, cell = 1).  A sequence's whole recurrence lives in ONE wave
 // (mode 0: one sequence per wave, mode 1: two), or in one wave per layer of a
 // 2-layer stack (mode 2), so h_t never crosses a workgroup barrier inside a
 // layer.  The forward writes act / hseq / xg_out like the gate-split forward

@@ -1,6 +1,7 @@
-// Sequence-in-wave LSTM stack (H = 32, 1-2 layers), forward and lean BPTT,
-// fp32, gfx950.  The motion model's recurrence (reference: nn.LSTM in
-// src/motion/model.py:9,14, trained by src/motion/trainer/base.py:111,116).
+// Sequence-in-wave LSTM / GRU stack (H = 32, 1-2 layers), forward and lean
+// BPTT, fp32, gfx950.  The motion model's recurrence (reference: nn.LSTM in
+// src/motion/model.py:9,14, trained by src/motion/trainer/base.py:111,116;
+// the GRU cell through the packed 4-block stack, CELL = 1, see load_fwd_w).
 //
 // Why a second small-H family (docs/DESIGN.md §2b): the gate-split kernels of
 // lstm_small.hip spread one sequence over 4 waves (a layer = 128 lanes, one

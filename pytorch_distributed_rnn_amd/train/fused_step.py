@@ -380,7 +380,7 @@ class MotionTrainStep:
         batch = idx.numel() if idx is not None else features.shape[0]
         nb_fwd, sp_fwd, _, _ = small_launch_config(batch, self.H, self.NL)
         nb_bwd = fused_bwd_nb(batch, self.H, self.NL)
-        if self.gru:  # gate-split forward only (1 or 2 sequences per workgroup)
+        if self.gru:  # (gate-split family geometry; the sequence-in-wave kernels, H = 32, ignore it)
             nb_fwd, sp_fwd = gru_fwd_nb(batch, self.H, features.device), 1
         hw, hb = self.m.fc.weight, self.m.fc.bias  # the classifier head stays fp32
         slot = self._slot
@@ -423,7 +423,7 @@ class MotionTrainStep:
         batch = idx.numel() if idx is not None else features.shape[0]
         nb_fwd, sp_fwd, _, _ = small_launch_config(batch, self.H, self.NL)
         nb_bwd = fused_bwd_nb(batch, self.H, self.NL)
-        if self.gru:  # gate-split forward only (1 or 2 sequences per workgroup)
+        if self.gru:  # (gate-split family geometry; the sequence-in-wave kernels, H = 32, ignore it)
             nb_fwd, sp_fwd = gru_fwd_nb(batch, self.H, features.device), 1
         ws, features, cell = self._operands(features)
         stats = torch.zeros(3, dtype=torch.float32, device=self.flat.grad.device)
