@@ -29,11 +29,14 @@ def _gpu_env(extra=None):
     return env
 
 
-@pytest.mark.parametrize("mode,hidden", [("distributed", 32), ("horovod", 32), ("distributed", 128)])
-def test_two_ranks_one_gpu_match_single_process(tmp_path, mode, hidden):
+@pytest.mark.parametrize("mode,hidden,cell", [("distributed", 32, "lstm"), ("horovod", 32, "lstm"),
+                                              ("distributed", 128, "lstm"), ("distributed", 32, "gru")])
+def test_two_ranks_one_gpu_match_single_process(tmp_path, mode, hidden, cell):
     """hidden 128: the fp32 large-H path (row-owning kernels, stacked-layer
-    chunk pipeline on per-layer streams) under the DDP gradient hooks."""
-    common = COMMON + ["--hidden-units", str(hidden)]
+    chunk pipeline on per-layer streams) under the DDP gradient hooks, with
+    the weight gradients written into the flat views (ops/gradsink.py); gru:
+    the GRU on the sequence-in-wave kernels at world 2."""
+    common = COMMON + ["--hidden-units", str(hidden), "--cell", cell]
     local = batch_losses(run([sys.executable, MAIN] + common + ["local"], cwd=str(tmp_path), env=_gpu_env(),
                              timeout=110))[0]
     out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
