@@ -952,11 +952,14 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     if (persist_verify_mode() == 2) return kPersistNotRun;
     TORCH_CHECK(false, "persistent LSTM recurrence: a grid-sync wait timed out in an earlier launch (results invalid)");
   }
-  // [counters | err | pad]
-  const int64_t stamp_ints = 1;
+  // [counters | err | pad | stamps]; PDRNN_TUNE persist_stamps=1: workgroup
+  // 0 records s_memtime at 7 points of steps 0..63 (kernel mode bit 8),
+  // reported per phase after the launch (diagnostics: the launch synchronises)
+  const bool pstamps = pdrnn_tune_int("persist_stamps", 0) != 0;
+  const int64_t stamp_ints = pstamps ? 2 * 64 * 8 + 2 : 1;
   Tensor sync = at::zeros({ndir * nmb + 1 + stamp_ints + 2}, opts.dtype(at::kInt));
   int* cnt = sync.data_ptr<int>();
-  int m = mode;
+  int m = mode | (pstamps ? 8 : 0);
   for (int k = g_persist_inject.load(); k > 0; k = g_persist_inject.load())
     if (g_persist_inject.compare_exchange_weak(k, k - 1)) { m |= 16; break; }
   const hipError_t e = pdrnn_lstm_large_persist(&a, ndir, backward ? 1 : 0, dt, mt, cnt, cnt + ndir * nmb,
@@ -986,6 +989,28 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
   }
   TORCH_CHECK(hipMemcpyAsync(sticky_host[dev], sticky[dev].data_ptr<int>(), sizeof(int), hipMemcpyDeviceToHost, st) ==
                   hipSuccess, "sticky copy");
+  if (pstamps) {
+    // the kernel's stamp base: (err + 1) rounded up to 8 bytes (lstm_large.hip pdrnn_lstm_large_persist)
+    const uintptr_t base = (reinterpret_cast<uintptr_t>(cnt + ndir * nmb + 1) + 7) & ~(uintptr_t)7;
+    const int64_t off = (int64_t)(base - reinterpret_cast<uintptr_t>(sync.data_ptr<int>())) / 4;
+    auto h = sync.narrow(0, off, 2 * 64 * 8).cpu();
+    const int64_t* p = reinterpret_cast<const int64_t*>(h.data_ptr<int>());
+    double d[6] = {0, 0, 0, 0, 0, 0}, step = 0;
+    int n = 0;
+    for (int s = 8; s < 63; ++s) {  // (steps 8..62: past the start-up, the next step's start closes the last phase)
+      const int64_t* r = p + s * 8;
+      const int64_t* q = p + (s + 1) * 8;
+      if (!r[0] || !q[0]) continue;
+      for (int k = 0; k < 6; ++k) d[k] += (double)(r[k + 1] - r[k]);
+      step += (double)(q[0] - r[0]);
+      ++n;
+    }
+    static const char* names[6] = {"wait", "loads+mfma", "lds partials", "cell+h store", "arrive", "acts/c stores"};
+    fprintf(stderr, "[persist stamps] %s B=%d H=%d: cycles/step %.0f |", backward ? "bwd" : "fwd", a.B, a.H,
+            n ? step / n : 0.0);
+    for (int k = 0; k < 6; ++k) fprintf(stderr, " %s %.0f", names[k], n ? d[k] / n : 0.0);
+    fprintf(stderr, "\n");
+  }
   if (check && persist_verify_mode() != 2) {  // per-step verification re-runs the step instead
     const int err = sync[ndir * nmb].item<int>();
     TORCH_CHECK(err == 0, "persistent LSTM grid sync timed out");
