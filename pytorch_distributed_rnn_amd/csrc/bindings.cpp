@@ -876,6 +876,7 @@ enum PersistResult { kPersistNotRun = 0, kPersistOk = 1, kPersistFailed = 2 };
 std::atomic<int> g_persist_verify{-1};     // -1: PDRNN_LSTM_PERSIST_VERIFY (default off); 1 launch, 2 step
 std::atomic<int> g_persist_inject{0};      // tests: flag the next N launches as timed out
 std::atomic<long long> g_persist_fallbacks{0};
+std::atomic<long long> g_persist_tagx{0};  // launches on the tagged forward exchange
 // after the first timed-out launch in a process the persistent path is off for
 // good: a lost co-residency (RCCL kernels beside it) tends to recur every step,
 // and each occurrence costs the 2 s spin bound plus the per-step re-run
@@ -957,17 +958,25 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
   // reported per phase after the launch (diagnostics: the launch synchronises)
   const bool pstamps = pdrnn_tune_int("persist_stamps", 0) != 0;
   const int64_t stamp_ints = pstamps ? 2 * 64 * 8 + 2 : 1;
-  Tensor sync = at::zeros({ndir * nmb + 1 + stamp_ints + 2}, opts.dtype(at::kInt));
+  // 16-bit forward: the tagged h exchange (lstm_large.hip ps_poll_h), a
+  // zeroed [2][ndir][B][H] dword buffer behind the counters (16-byte aligned)
+  const bool tagx = !backward && dt != 2 && a.T < 65535 && pdrnn_tune_int("persist_tagx", 0) != 0;
+  const int64_t head = (ndir * nmb + 1 + stamp_ints + 2 + 3) & ~(int64_t)3;
+  const int nslots = tagx ? std::max(2, std::min(pdrnn_tune_int("persist_tagx_slots", 2), a.T)) : 0;
+  const int64_t xints = (int64_t)nslots * ndir * a.B * a.H;
+  Tensor sync = at::zeros({head + xints}, opts.dtype(at::kInt));
   int* cnt = sync.data_ptr<int>();
+  uint32_t* xchg = tagx ? reinterpret_cast<uint32_t*>(cnt + head) : nullptr;
   int m = mode | (pstamps ? 8 : 0);
   for (int k = g_persist_inject.load(); k > 0; k = g_persist_inject.load())
     if (g_persist_inject.compare_exchange_weak(k, k - 1)) { m |= 16; break; }
   const hipError_t e = pdrnn_lstm_large_persist(&a, ndir, backward ? 1 : 0, dt, mt, cnt, cnt + ndir * nmb,
-                                                sticky[dev].data_ptr<int>(), m, st);
+                                                sticky[dev].data_ptr<int>(), m, xchg, nslots, st);
   if (e != hipSuccess) {
     (void)hipGetLastError();  // e.g. grid cannot be co-resident: per-step path
     return kPersistNotRun;
   }
+  if (tagx) g_persist_tagx++;
   if (persist_verify_on()) {
     static std::vector<int*>& flag = *new std::vector<int*>(64, nullptr);
     if (!flag[dev]) flag[dev] = pinned_word();
@@ -1633,6 +1642,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "per-step verification: True when a persistent launch timed out since the last check (synchronises)");
   m.def("persist_inject_timeouts", [](int64_t n) { g_persist_inject = (int)n; },
         "tests: flag the next n persistent launches as timed out");
+  m.def("persist_tagx_launches", []() { return (int64_t)g_persist_tagx.load(); },
+        "persistent forward launches that used the tagged h exchange (PDRNN_TUNE persist_tagx)");
   m.def("persist_fallbacks", []() { return (int64_t)g_persist_fallbacks.load(); },
         "persistent launches re-run on the per-step kernels after a timeout");
   m.def("persist_verify_on", []() { return persist_verify_mode() != 0; },

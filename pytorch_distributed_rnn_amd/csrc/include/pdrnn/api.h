@@ -358,10 +358,13 @@ hipError_t pdrnn_lstm_rows_f32(const PdrnnLstmLargeStepArgs* a, int ndir, int ba
 // W_hh register-resident.  persist_mt: rows-per-workgroup / 16 for this shape
 // (0 = not covered); counters: ndir * ceil(B / (16 mt)) zeroed ints; err: an
 // int set to 1 if a grid-sync spin timed out (sticky, if not null: also set,
-// never cleared); mode: 0 (diagnostic bits, see the kernel).
+// never cleared); mode: 0 (diagnostic bits, see the kernel); xchg: null, or for a
+// 16-bit forward nslots (>= 2) * ndir * B * H zeroed dwords (16-byte aligned): the tagged
+// h exchange instead of the arrival counters (lstm_large.hip ps_poll_h).
 int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus);
 hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int mt,
-                                    int* counters, int* err, int* sticky, int mode, hipStream_t stream);
+                                    int* counters, int* err, int* sticky, int mode, uint32_t* xchg,
+                                    int nslots, hipStream_t stream);
 // Time-batched GEMM of the large-H layers (kernels/gemm.hip), 16-bit inputs:
 //   C[M, N] (= or +=) sum over the K segments of op(A) op(B) (+ bias[n])
 // A: a_kmajor ? element (m, k) at A[k * lda + m] : A[m * lda + k]

@@ -1037,6 +1037,9 @@ struct PersistSync {
   int mode;   // diagnostics (wrong results): bit 0 no waits, bit 1 no step GEMM, bit 2 no store drain,
               // bit 4 flag the launch as timed out (tests of the host's recovery)
   long long* stamps;  // mode bit 3: workgroup 0 records s_memtime at 8 points of steps 0..63
+  uint32_t* xchg;     // tagged forward exchange (16-bit types): [nslots][ndir][B][H] dwords, zero
+                      // at launch, or null for the arrival-counter protocol (see ps_poll_h)
+  int nslots;         // exchange ring length (>= 2)
 };
 #define PS_STAMP(k)                                                                          \
   if ((sync.mode & 8) && blockIdx.x == 0 && threadIdx.x == 0 && s < 64)                      \
@@ -1105,13 +1108,85 @@ __device__ __forceinline__ void ps_coords(int NCB, int NMB, int& dir, int& cb, i
   cb = l / NMB;
 }
 
+// Tagged forward exchange (16-bit types; PersistSync::xchg non-null).  The
+// arrival-counter protocol costs a step ~43% of its cycles on the char-LM
+// shape (wait 34% + store drain and count 9%,
+// profiles/r6/persist_fwd_step_cycles.md): every producer drains its h_t
+// stores before counting, and the reader loads h_{t-1} only after it has seen
+// the count.  Here h_t travels as one dword per value -- bf16/f16 bits in the
+// low half, the step tag s + 1 in the high half -- in a parity double buffer
+// [2][ndir][B][H] that is zero at launch.  A reader of step s polls its
+// A-fragment chunks of slot (s - 1) & 1 until every dword carries tag s, so
+// the data IS the flag: no drain, no counter, and the loads that succeed are
+// the operands.  Reuse of a slot two steps later is safe: a producer writes
+// slot s & 1 again at step s + 2 only after it has read h_{s+1} of every
+// column block of its batch block, i.e. after all of them finished step s + 1
+// (whose reads of slot s & 1 precede their cell phase).  Tags are unique
+// within a launch (T < 65535, checked by the host).  The spin is bounded like
+// ps_wait (~2 s, *err releases every other poller).
+template <int MT, int KS>
+__device__ __forceinline__ void ps_poll_h(uint4 (&af)[MT][KS], const PersistSync& sync, const uint32_t* slot,
+                                          uint32_t want, int mb, int fr, int fq, int k0, int B, int H) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rx = ps_rsrc(slot);
+  const uint64_t t0 = wall_clock64();
+  // probe: re-reading the whole operand every round (8 KiB a wave, 16 MiB a
+  // grid round on the char-LM shape) congests the device-coherent path and
+  // was 30% slower than the counters; one dword a lane watches the last unit
+  // of producer block (fq mod KS) of its row, and the full load is issued
+  // when every probe shows the tag (re-polled in full if any chunk lags)
+  bool probing = true;
+  for (;;) {
+    bool ok = true;
+    if (probing) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int row = min(mb * 16 * MT + mt * 16 + fr, B - 1);
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(
+            rx, (uint32_t)((row * H + k0 + (fq % KS) * PS_NU + PS_NU - 1) * 4), 0, PS_SC1);
+        ok = ok && (v >> 16) == want;
+      }
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+        probing = false;
+        continue;
+      }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int row = min(mb * 16 * MT + mt * 16 + fr, B - 1);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const uint32_t off = (uint32_t)((row * H + k0 + ks * 32 + fq * 8) * 4);
+          const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, PS_SC1);
+          const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rx, off + 16, 0, PS_SC1);
+          ok = ok && (lo.x >> 16) == want && (lo.y >> 16) == want && (lo.z >> 16) == want && (lo.w >> 16) == want &&
+               (hi.x >> 16) == want && (hi.y >> 16) == want && (hi.z >> 16) == want && (hi.w >> 16) == want;
+          af[mt][ks] = make_uint4((lo.x & 0xffffu) | (lo.y << 16), (lo.z & 0xffffu) | (lo.w << 16),
+                                  (hi.x & 0xffffu) | (hi.y << 16), (hi.z & 0xffffu) | (hi.w << 16));
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    const int e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(sync.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (e != 0) break;
+    if (wall_clock64() - t0 > 200000000ull) {  // 100 MHz constant clock: 2 s
+      if ((threadIdx.x & 63) == 0) {
+        __hip_atomic_store(sync.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (sync.sticky) __hip_atomic_store(sync.sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      break;
+    }
+  }
+}
+
 // Per-step epilogue state lives in registers: the cell state c (forward) and
 // the carry (backward) never leave the thread that owns the (row, unit) pair;
 // the operands of the next step that do not depend on other workgroups (xp;
 // acts / c / dout) are loaded right after the arrival, so their latency hides
 // behind the wait; only the exchanged stores (h_t / dgates_t) precede the
 // arrival -- the saved activations and c_t are stored after it.
-template <class DT, int CELL, int KS, int MT>
+template <class DT, int CELL, int KS, int MT, bool TAGX>
 __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(PdrnnLstmLargeStepArgs args,
                                                                             PersistSync sync) {
   typedef typename DT::S S;
@@ -1134,6 +1209,9 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
   const int n0 = cb * 4 * PS_NU;        // first gate column (gate-interleaved)
   const int k0 = wid * (H / PS_WAVES);  // this wave's K range
   int* cnt = sync.cnt + dir * NMB + mb;
+  // exchange slot of step s: parity s & 1, this direction (TAGX)
+  const int ndirs = gridDim.x / (NCB * NMB);
+  auto xslot = [&](int s, int dr) { return sync.xchg + ((int64_t)((s % sync.nslots) * ndirs + dr)) * B * H; };
 
   // W_hh slice as MFMA B fragments, resident for the whole sequence
   uint4 wf[KS][CT];
@@ -1178,7 +1256,9 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) xcur[mt] = xpn[mt];
     PS_STAMP(0)
-    if (s > S0 && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err, sync.sticky);
+    if constexpr (!TAGX) {
+      if (s > S0 && !(sync.mode & 1)) ps_wait(cnt, s * NCB, sync.err, sync.sticky);
+    }
     PS_STAMP(1)
 
     f32x4 acc[MT][CT];
@@ -1191,12 +1271,16 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
       const int64_t lda = first ? H : d.hseq_sb;
       const __amdgpu_buffer_rsrc_t ra = ps_rsrc(hA);
       uint4 af[MT][KS];
+      if (TAGX && s > S0) {
+        ps_poll_h<MT, KS>(af, sync, xslot(s - 1, dir), (uint32_t)s, mb, fr, fq, k0, B, H);
+      } else {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int row = min(mb * 16 * MT + mt * 16 + fr, B - 1);
+        for (int mt = 0; mt < MT; ++mt) {
+          const int row = min(mb * 16 * MT + mt * 16 + fr, B - 1);
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          af[mt][ks] = ps_ld16(ra, (uint32_t)((row * lda + k0 + ks * 4 * DT::EPC + fq * DT::EPC) * sizeof(S)));
+          for (int ks = 0; ks < KS; ++ks)
+            af[mt][ks] = ps_ld16(ra, (uint32_t)((row * lda + k0 + ks * 4 * DT::EPC + fq * DT::EPC) * sizeof(S)));
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -1218,6 +1302,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
     PS_STAMP(3)
     float gs[MT][4];
     const __amdgpu_buffer_rsrc_t rh = ps_rsrc(static_cast<S*>(d.hseq) + (int64_t)t * d.hseq_st);
+    const __amdgpu_buffer_rsrc_t rxw = ps_rsrc(TAGX ? static_cast<const void*>(xslot(s, dir)) : static_cast<const void*>(sync.cnt));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const S* xv = reinterpret_cast<const S*>(&xcur[mt]);
@@ -1242,11 +1327,22 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
         cst[mt] = hv = fmaf(g[1], cst[mt] - g[2], g[2]);
       }
       const int b = mb * 16 * MT + mt * 16 + er;
-      if (b < B) ps_st(rh, (uint32_t)((b * d.hseq_sb + u) * sizeof(S)), DT::from_f(hv));
+      if constexpr (TAGX) {
+        // h_t to hseq (read after the launch: a plain store) and, tagged with
+        // s + 1, to this step's exchange slot (read by the next step's polls)
+        if (b < B) {
+          const uint16_t hb = DT::from_f(hv);
+          static_cast<S*>(d.hseq)[(int64_t)t * d.hseq_st + (int64_t)b * d.hseq_sb + u] = hb;
+          __builtin_amdgcn_raw_buffer_store_b32(((uint32_t)(s + 1) << 16) | hb, rxw, (uint32_t)((b * H + u) * 4), 0,
+                                                PS_SC1);
+        }
+      } else {
+        if (b < B) ps_st(rh, (uint32_t)((b * d.hseq_sb + u) * sizeof(S)), DT::from_f(hv));
+      }
     }
     PS_STAMP(4)
-    if (s + 1 < T) ps_arrive(cnt, sync.mode);
-    else __syncthreads();  // (LDS reuse only; nothing waits for the last step)
+    if (TAGX || s + 1 == T) __syncthreads();  // (LDS reuse only: nobody counts arrivals)
+    else ps_arrive(cnt, sync.mode);
     PS_STAMP(5)
     if (s + 1 < S1) load_xp(rev ? t - 1 : t + 1);
 #pragma unroll
@@ -1484,7 +1580,10 @@ hipError_t persist_launch(const PdrnnLstmLargeStepArgs* a, int ndir, bool backwa
     return hipErrorInvalidValue;
   } else {
     const size_t lds = (size_t)PS_WAVES * MT * 16 * (4 * PS_NU + 4) * 4;
-    return persist_go(lstm_large_persist_fwd_kernel<DT, CELL, KSF, MT>, grid, lds, st, *a, sy, &occ_fwd);
+    static int occ_fwd_tag = -1;
+    if (sy.xchg != nullptr)
+      return persist_go(lstm_large_persist_fwd_kernel<DT, CELL, KSF, MT, true>, grid, lds, st, *a, sy, &occ_fwd_tag);
+    return persist_go(lstm_large_persist_fwd_kernel<DT, CELL, KSF, MT, false>, grid, lds, st, *a, sy, &occ_fwd);
   }
 }
 
@@ -1572,11 +1671,16 @@ int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus) {
 }
 
 hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int mt,
-                                    int* counters, int* err, int* sticky, int mode, hipStream_t stream) {
+                                    int* counters, int* err, int* sticky, int mode, uint32_t* xchg,
+                                    int nslots, hipStream_t stream) {
   if ((mt != 1 && mt != 2) || dtype < 0 || dtype > 2) return hipErrorInvalidValue;
+  if (xchg != nullptr && (backward || dtype == 2 || a->T >= 65535 || nslots < 2 || (reinterpret_cast<uintptr_t>(xchg) & 15)))
+    return hipErrorInvalidValue;
   if (dtype == 2 ? (a->H != 128 && a->H != 256) : a->H != 1024) return hipErrorInvalidValue;
   if (a->cell != 0 && a->cell != 1) return hipErrorInvalidValue;
-  const pdrnn::PersistSync sy{counters, err, sticky, mode, reinterpret_cast<long long*>((reinterpret_cast<uintptr_t>(err + 1) + 7) & ~(uintptr_t)7)};
+  const pdrnn::PersistSync sy{counters, err, sticky, mode,
+                              reinterpret_cast<long long*>((reinterpret_cast<uintptr_t>(err + 1) + 7) & ~(uintptr_t)7),
+                              xchg, nslots};
   const bool bw = backward != 0;
   if (dtype == 0)
     return a->cell ? pdrnn::persist_dispatch<pdrnn::BF16, 1>(a, ndir, bw, mt, sy, stream)

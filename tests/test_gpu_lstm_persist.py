@@ -143,13 +143,42 @@ def verified():
     mod.persist_reset()
 
 
-def test_persistent_timeout_rerun_on_per_step_kernels(verified):
+@pytest.mark.parametrize("cell", [0, 1])
+@pytest.mark.parametrize("B,T,ndir,rev", [(128, 40, 1, 0),   # char-LM shape, both parities reused many times
+                                          (200, 9, 1, 0),    # 2 x 16 rows per workgroup, clamped last block
+                                          (40, 7, 2, 2),     # bidirectional: one slot per direction
+                                          (7, 5, 1, 1)])     # tiny batch, reversed
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_persistent_tagged_exchange_matches_counters(monkeypatch, cell, B, T, ndir, rev, dt):
+    """The tagged h exchange of the persistent forward (PDRNN_TUNE
+    persist_tagx=1; lstm_large.hip ps_poll_h) moves the same bits as the
+    arrival-counter protocol, so the outputs are identical -- and the launches
+    really took the tagged kernel."""
+    mod = _ext.require()
+    xp, w, wt, h0, c0, dout, dhn, dcn = _inputs(B, T, ndir, dt, 21 + B + T + cell)
+    monkeypatch.setenv("PDRNN_TUNE", "persist_tagx=0")
+    before = mod.persist_tagx_launches()
+    ref = mod.lstm_large_fwd(xp, w, h0, c0, H, rev, -1, cell)
+    torch.cuda.synchronize()
+    assert mod.persist_tagx_launches() == before
+    monkeypatch.setenv("PDRNN_TUNE", "persist_tagx=1")
+    got = mod.lstm_large_fwd(xp, w, h0, c0, H, rev, -1, cell)
+    torch.cuda.synchronize()
+    assert mod.persist_tagx_launches() == before + 1
+    mod.persist_check()
+    for name, a, b in zip(["hseq", "cseq", "acts"], got, ref):
+        assert torch.equal(a, b), (name, _rel(a, b))
+
+
+@pytest.mark.parametrize("tagx", [0, 1])
+def test_persistent_timeout_rerun_on_per_step_kernels(verified, monkeypatch, tagx):
     """ADVICE r2 / VERDICT r2 item 2b: a persistent launch whose grid sync
     timed out (here: flagged by the kernel's test hook, waiters released
     early -- invalid outputs) is detected in the same call and the layer is
     re-run on the per-step kernels, so forward AND backward still equal the
     per-step path and nothing invalid reaches the caller."""
     mod = verified
+    monkeypatch.setenv("PDRNN_TUNE", f"persist_tagx={tagx}")
     B, T, ndir, dt = 128, 9, 1, torch.bfloat16
     xp, w, wt, h0, c0, dout, dhn, dcn = _inputs(B, T, ndir, dt, 11)
     ref = _run(mod, 0, xp, w, wt, h0, c0, dout, dhn, dcn, 0, 0)
