@@ -1114,16 +1114,18 @@ __device__ __forceinline__ void ps_coords(int NCB, int NMB, int& dir, int& cb, i
 // profiles/r6/persist_fwd_step_cycles.md): every producer drains its h_t
 // stores before counting, and the reader loads h_{t-1} only after it has seen
 // the count.  Here h_t travels as one dword per value -- bf16/f16 bits in the
-// low half, the step tag s + 1 in the high half -- in a parity double buffer
-// [2][ndir][B][H] that is zero at launch.  A reader of step s polls its
-// A-fragment chunks of slot (s - 1) & 1 until every dword carries tag s, so
-// the data IS the flag: no drain, no counter, and the loads that succeed are
-// the operands.  Reuse of a slot two steps later is safe: a producer writes
-// slot s & 1 again at step s + 2 only after it has read h_{s+1} of every
-// column block of its batch block, i.e. after all of them finished step s + 1
-// (whose reads of slot s & 1 precede their cell phase).  Tags are unique
-// within a launch (T < 65535, checked by the host).  The spin is bounded like
-// ps_wait (~2 s, *err releases every other poller).
+// low half, the step tag s + 1 in the high half -- in a ring of nslots >= 2
+// exchange slots [nslots][ndir][B][H], zero at launch.  A reader of step s
+// polls its A-fragment chunks of slot (s - 1) % nslots until every dword
+// carries tag s, so the data IS the flag: no drain, no counter, and the loads
+// that succeed are the operands.  Reusing a slot is safe: a producer writes
+// slot s % nslots again at step s + nslots >= s + 2 only after it has read
+// h_{s+1} of every column block of its batch block, i.e. after all of them
+// finished step s + 1, whose reads of the slot precede their cell phase.
+// Tags are unique within a launch (T < 65535, checked by the host).  The spin
+// is bounded like ps_wait (~2 s, *err releases every other poller).
+// Measured slower than the counters (PDRNN_TUNE persist_tagx, default off;
+// profiles/r6/persist_fwd_step_cycles.md).
 template <int MT, int KS>
 __device__ __forceinline__ void ps_poll_h(uint4 (&af)[MT][KS], const PersistSync& sync, const uint32_t* slot,
                                           uint32_t want, int mb, int fr, int fq, int k0, int B, int H) {
@@ -1209,7 +1211,7 @@ __global__ void __launch_bounds__(PS_THREADS) lstm_large_persist_fwd_kernel(Pdrn
   const int n0 = cb * 4 * PS_NU;        // first gate column (gate-interleaved)
   const int k0 = wid * (H / PS_WAVES);  // this wave's K range
   int* cnt = sync.cnt + dir * NMB + mb;
-  // exchange slot of step s: parity s & 1, this direction (TAGX)
+  // exchange slot of step s: s mod the ring length, this direction (TAGX)
   const int ndirs = gridDim.x / (NCB * NMB);
   auto xslot = [&](int s, int dr) { return sync.xchg + ((int64_t)((s % sync.nslots) * ndirs + dr)) * B * H; };
 
