@@ -701,13 +701,17 @@ std::vector<Tensor> xent_fwd(const Tensor& logits, const Tensor& labels, int64_t
   return {stats, dlogits};
 }
 
-Tensor xent_bwd(const Tensor& dlogits, const Tensor& grad_out, const Tensor& stats) {
+// out_dtype: the gradient's dtype (fp32 default; bf16 / fp16 for a 16-bit head)
+Tensor xent_bwd(const Tensor& dlogits, const Tensor& grad_out, const Tensor& stats, optional<at::ScalarType> out_dtype) {
   CHECK_HIP_TENSOR(dlogits);
   const c10::DeviceGuard guard(dlogits.device());
   Tensor g = grad_out.to(at::kFloat).contiguous();
-  Tensor out = at::empty_like(dlogits);
+  const at::ScalarType od = out_dtype.value_or(at::kFloat);
+  TORCH_CHECK(od == at::kFloat || od == at::kBFloat16 || od == at::kHalf, "xent_bwd: fp32 / bf16 / fp16 output");
+  Tensor out = at::empty_like(dlogits, dlogits.options().dtype(od));
+  const int code = od == at::kFloat ? 2 : (od == at::kBFloat16 ? 0 : 1);
   HIP_LAUNCH_CHECK(pdrnn_xent_bwd(dlogits.data_ptr<float>(), g.data_ptr<float>(), stats.data_ptr<float>(),
-                                  out.data_ptr<float>(), dlogits.numel(), cur_stream()));
+                                  out.data_ptr(), dlogits.numel(), code, cur_stream()));
   return out;
 }
 
@@ -928,6 +932,33 @@ int large_persist_plan(int B, int H, int ndir, bool backward, int dt, int64_t ti
   return pdrnn_lstm_large_persist_mt(B, H, ndir, dt, cus - pdrnn::rccl_cta_reserve());
 }
 
+// Zeroed sync words for persistent launches without a fill dispatch per
+// launch: slices of a per-(device, stream) pool handed out in order, the whole
+// pool re-zeroed by one memset when it wraps.  Stream order makes that safe:
+// every launch that used the pool before the memset has finished when it
+// runs.  (Graph capture and the diagnostics take fresh zeros instead.)
+int* persist_sync_words(int dev, hipStream_t st, int64_t n, const at::TensorOptions& opts) {
+  struct Pool {
+    Tensor buf;
+    int64_t cur = 0;
+  };
+  constexpr int64_t kPool = 1 << 16;  // ints
+  const int64_t need = (n + 63) & ~(int64_t)63;
+  if (need > kPool) return nullptr;
+  static std::mutex mu;
+  static auto& pools = *new std::map<std::pair<int, hipStream_t>, Pool>();  // never destroyed (exit order)
+  std::lock_guard<std::mutex> g(mu);
+  Pool& p = pools[{dev, st}];
+  if (!p.buf.defined()) p.buf = at::zeros({kPool}, opts.dtype(at::kInt));
+  if (p.cur + need > kPool) {
+    TORCH_CHECK(hipMemsetAsync(p.buf.data_ptr<int>(), 0, kPool * sizeof(int), st) == hipSuccess, "sync pool reset");
+    p.cur = 0;
+  }
+  int* r = p.buf.data_ptr<int>() + p.cur;
+  p.cur += need;
+  return r;
+}
+
 int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int dt, int64_t tile,
                   const at::TensorOptions& opts, hipStream_t st) {
   static const bool check = [] {
@@ -964,8 +995,15 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
   const int64_t head = (ndir * nmb + 1 + stamp_ints + 2 + 3) & ~(int64_t)3;
   const int nslots = tagx ? std::max(2, std::min(pdrnn_tune_int("persist_tagx_slots", 2), a.T)) : 0;
   const int64_t xints = (int64_t)nslots * ndir * a.B * a.H;
-  Tensor sync = at::zeros({head + xints}, opts.dtype(at::kInt));
-  int* cnt = sync.data_ptr<int>();
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool pooled = !pstamps && !tagx && hipStreamIsCapturing(st, &cap) == hipSuccess &&
+                      cap == hipStreamCaptureStatusNone;
+  Tensor sync;
+  int* cnt = pooled ? persist_sync_words(dev, st, head, opts) : nullptr;
+  if (cnt == nullptr) {
+    sync = at::zeros({head + xints}, opts.dtype(at::kInt));
+    cnt = sync.data_ptr<int>();
+  }
   uint32_t* xchg = tagx ? reinterpret_cast<uint32_t*>(cnt + head) : nullptr;
   int m = mode | (pstamps ? 8 : 0);
   for (int k = g_persist_inject.load(); k > 0; k = g_persist_inject.load())
@@ -1021,7 +1059,9 @@ int large_persist(const PdrnnLstmLargeStepArgs& a, int ndir, bool backward, int 
     fprintf(stderr, "\n");
   }
   if (check && persist_verify_mode() != 2) {  // per-step verification re-runs the step instead
-    const int err = sync[ndir * nmb].item<int>();
+    int err = 0;  // (the flag may live in the pooled sync words: read it through the pointer)
+    TORCH_CHECK(hipMemcpyAsync(&err, cnt + ndir * nmb, sizeof(int), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                    hipStreamSynchronize(st) == hipSuccess, "persistent LSTM: flag read failed");
     TORCH_CHECK(err == 0, "persistent LSTM grid sync timed out");
   }
   return kPersistOk;
@@ -1523,6 +1563,58 @@ Tensor col_sum(const Tensor& X, const optional<std::vector<Tensor>>& accumulate_
   return out;
 }
 
+// Weight shadows rebuilt in one launch (kernels/shadow_pack.hip; ops/shadow.py):
+// jobs are (dst, src, src2 or None) 3-D views of equal shape, bf16 / fp16 /
+// fp32 on either side, one device.  Launches ceil(n / 16).
+int64_t shadow_pack(const std::vector<std::tuple<Tensor, Tensor, optional<Tensor>>>& jobs) {
+  if (jobs.empty()) return 0;
+  const c10::DeviceGuard guard(std::get<0>(jobs[0]).device());
+  hipStream_t st = cur_stream();
+  int64_t launches = 0;
+  PdrnnPackBatch b{};
+  auto flush = [&]() {
+    if (b.njobs == 0) return;
+    HIP_LAUNCH_CHECK(pdrnn_shadow_pack(&b, st));
+    ++launches;
+    b = PdrnnPackBatch{};
+  };
+  for (const auto& jt : jobs) {
+    const Tensor& d = std::get<0>(jt);
+    const Tensor& s = std::get<1>(jt);
+    const optional<Tensor>& s2 = std::get<2>(jt);
+    CHECK_HIP_TENSOR(d);
+    CHECK_HIP_TENSOR(s);
+    TORCH_CHECK(d.dim() == 3 && s.dim() == 3 && d.sizes() == s.sizes(), "shadow_pack: 3-D views of equal shape");
+    auto code = [](const Tensor& t) {
+      TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf,
+                  "shadow_pack: bf16 / fp16 / fp32 tensors");
+      return t.scalar_type() == at::kFloat ? 2 : (t.scalar_type() == at::kBFloat16 ? 0 : 1);
+    };
+    TORCH_CHECK(d.device() == s.device(), "shadow_pack: source on dst's device");
+    PdrnnPackJob& j = b.job[b.njobs];
+    j.src = s.data_ptr();
+    j.sdtype = code(s);
+    j.src2 = nullptr;
+    if (s2.has_value() && s2->defined()) {
+      TORCH_CHECK(s2->scalar_type() == s.scalar_type() && s2->sizes() == s.sizes() && s2->strides() == s.strides() &&
+                      s2->device() == s.device(), "shadow_pack: src2 must match src's dtype, shape and strides");
+      j.src2 = s2->data_ptr();
+    }
+    j.dst = d.data_ptr();
+    for (int k = 0; k < 3; ++k) {
+      TORCH_CHECK(d.size(k) < (int64_t)1 << 31, "shadow_pack: extent");
+      j.n[k] = (int)d.size(k);
+      j.ss[k] = s.stride(k);
+      j.ds[k] = d.stride(k);
+    }
+    j.dtype = code(d);
+    if (pdrnn_shadow_pack_tiles(&j) == 0) continue;
+    if (++b.njobs == PDRNN_PACK_MAX_JOBS) flush();
+  }
+  flush();
+  return launches;
+}
+
 // C[M, N] f32 = A[M, K] Bt[N, K]^T on the MFMA core (tests).
 Tensor gemm_nt(const Tensor& A, const Tensor& Bt, int64_t tile) {
   CHECK_HIP_TENSOR(A);
@@ -1597,6 +1689,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_kmajor"), py::arg("B"), py::arg("b_kmajor"), py::arg("A2") = py::none(), py::arg("B2") = py::none(),
         py::arg("bias") = py::none(), py::arg("out16") = false, py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("splitk") = 1, py::arg("rowsum") = false);
+  m.def("shadow_pack", &shadow_pack,
+        "rebuild weight shadows: (dst, src, src2|None) 3-D views, fp32 sources, one launch per 16 jobs",
+        py::arg("jobs"));
   m.def("col_sum", &col_sum, "deterministic fp32 column sums of a 2-D tensor (or added into accumulate_into)",
         py::arg("X"), py::arg("accumulate_into") = py::none());
   m.def("gemm_variants", []() {
@@ -1605,7 +1700,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return std::vector<int>(v, v + n);
   }, "schedule variants of the in-tree GEMM compiled into this build (first = default)");
   m.def("xent_fwd", &xent_fwd, "fused softmax cross-entropy + accuracy");
-  m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
+  m.def("xent_bwd", &xent_bwd, "cross-entropy backward (gradient in out_dtype, fp32 by default)",
+        py::arg("dlogits"), py::arg("grad_out"), py::arg("stats"), py::arg("out_dtype") = py::none());
   m.def("adam_flat", &adam_flat, "fused Adam/AdamW step over a flat buffer", py::arg("param"), py::arg("grad"),
         py::arg("exp_avg"), py::arg("exp_avg_sq"), py::arg("max_exp_avg_sq"), py::arg("lr"), py::arg("beta1"),
         py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("step"), py::arg("grad_scale"),

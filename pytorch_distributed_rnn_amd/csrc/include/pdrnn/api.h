@@ -221,8 +221,8 @@ typedef struct {
 hipError_t pdrnn_xent_fwd(const PdrnnXentArgs* a, hipStream_t stream);
 int pdrnn_xent_partial_blocks(int64_t N, int64_t C);
 // dst = dlogits * (grad_out[0] / stats[1])   (stats = PdrnnXentArgs.out)
-hipError_t pdrnn_xent_bwd(const float* dlogits, const float* grad_out, const float* stats, float* dst,
-                          int64_t n, hipStream_t stream);
+hipError_t pdrnn_xent_bwd(const float* dlogits, const float* grad_out, const float* stats, void* dst,
+                          int64_t n, int out_dtype, hipStream_t stream);
 
 // ----------------------------------------------------------------------------
 // Tuning overrides (runtime/tune.cpp): PDRNN_TUNE="key=value,...".  _str
@@ -361,6 +361,28 @@ hipError_t pdrnn_lstm_rows_f32(const PdrnnLstmLargeStepArgs* a, int ndir, int ba
 // never cleared); mode: 0 (diagnostic bits, see the kernel); xchg: null, or for a
 // 16-bit forward nslots (>= 2) * ndir * B * H zeroed dwords (16-byte aligned): the tagged
 // h exchange instead of the arrival counters (lstm_large.hip ps_poll_h).
+// Weight-shadow pack (kernels/shadow_pack.hip): up to PDRNN_PACK_MAX_JOBS
+// 3-D strided gathers dst[i0,i1,i2] = src[...] (+ src2[...]) from bf16 /
+// fp16 / fp32 sources (sdtype), converted to dtype, one launch.  Strides
+// in elements; tile0 is filled in by pdrnn_shadow_pack.
+#define PDRNN_PACK_MAX_JOBS 16
+typedef struct PdrnnPackJob {
+  const void* src;
+  const void* src2;  // optional second addend (same strides and dtype), or null
+  void* dst;
+  int64_t ss[3];
+  int64_t ds[3];
+  int n[3];
+  int dtype;   // destination: 0 bf16, 1 fp16, 2 fp32
+  int sdtype;  // sources: same codes
+  int64_t tile0;
+} PdrnnPackJob;
+typedef struct PdrnnPackBatch {
+  PdrnnPackJob job[PDRNN_PACK_MAX_JOBS];
+  int njobs;
+} PdrnnPackBatch;
+int64_t pdrnn_shadow_pack_tiles(const PdrnnPackJob* j);
+hipError_t pdrnn_shadow_pack(PdrnnPackBatch* b, hipStream_t stream);
 int pdrnn_lstm_large_persist_mt(int B, int H, int ndir, int dtype, int cus);
 hipError_t pdrnn_lstm_large_persist(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, int dtype, int mt,
                                     int* counters, int* err, int* sticky, int mode, uint32_t* xchg,

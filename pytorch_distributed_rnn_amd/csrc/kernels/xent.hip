@@ -120,11 +120,24 @@ __global__ void __launch_bounds__(256) xent_finalize_kernel(const float* partial
 }
 
 // dst = src * (grad_out[0] / stats[1])
+// OD: output 0 bf16, 1 fp16, 2 fp32 -- a 16-bit head takes its logits
+// gradient in its own dtype straight from here (no separate cast dispatch)
+template <int OD>
 __global__ void xent_bwd_kernel(const float* __restrict__ src, const float* grad_out, const float* stats,
-                                float* __restrict__ dst, int64_t n) {
+                                void* __restrict__ dst, int64_t n) {
   const float scale = grad_out[0] / stats[1];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i] * scale;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = src[i] * scale;
+    if constexpr (OD == 2) {
+      static_cast<float*>(dst)[i] = v;
+    } else if constexpr (OD == 1) {
+      static_cast<uint16_t*>(dst)[i] = __builtin_bit_cast(uint16_t, (_Float16)v);
+    } else {
+      const uint32_t u = __float_as_uint(v);  // round to nearest even (finite inputs)
+      static_cast<uint16_t*>(dst)[i] = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    }
+  }
 }
 
 int rows_per_block_for(int64_t N, int64_t C) {
@@ -162,12 +175,19 @@ hipError_t pdrnn_xent_fwd(const PdrnnXentArgs* a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t pdrnn_xent_bwd(const float* dlogits, const float* grad_out, const float* stats, float* dst,
-                          int64_t n, hipStream_t stream) {
+hipError_t pdrnn_xent_bwd(const float* dlogits, const float* grad_out, const float* stats, void* dst,
+                          int64_t n, int out_dtype, hipStream_t stream) {
   int blocks = (int)((n + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(pdrnn::xent_bwd_kernel, dim3(blocks), dim3(256), 0, stream, dlogits, grad_out, stats, dst, n);
+  if (out_dtype == 0)
+    hipLaunchKernelGGL(pdrnn::xent_bwd_kernel<0>, dim3(blocks), dim3(256), 0, stream, dlogits, grad_out, stats, dst, n);
+  else if (out_dtype == 1)
+    hipLaunchKernelGGL(pdrnn::xent_bwd_kernel<1>, dim3(blocks), dim3(256), 0, stream, dlogits, grad_out, stats, dst, n);
+  else if (out_dtype == 2)
+    hipLaunchKernelGGL(pdrnn::xent_bwd_kernel<2>, dim3(blocks), dim3(256), 0, stream, dlogits, grad_out, stats, dst, n);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -22,6 +22,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
+from . import shadow as _shadow
 
 _CUS = {}
 
@@ -138,7 +139,7 @@ class _Linear16(torch.autograd.Function):
         from . import gradsink
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        w16 = weight.detach().to(x.dtype)
+        w16 = _shadow.cast(weight, x.dtype)  # converted once per optimizer step (ops/shadow.py)
         y = linear16(x2, w16, bias.detach() if bias is not None else None)
         ctx.save_for_backward(x2, w16)
         ctx.has_bias = bias is not None
@@ -176,7 +177,7 @@ class _LinearNarrow(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        w16 = weight.detach().to(x.dtype)
+        w16 = _shadow.cast(weight, x.dtype)  # converted once per optimizer step (ops/shadow.py)
         o16 = x.dtype != torch.float32
         y, _ = gemm_f32(x2, False, w16, False, bias=bias.detach().float() if bias is not None else None, out16=o16)
         ctx.save_for_backward(x2, w16)

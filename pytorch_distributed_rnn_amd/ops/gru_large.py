@@ -34,6 +34,7 @@ import torch
 from torch import Tensor
 
 from .. import _ext
+from . import shadow as _sh
 from .lstm_large import (_tile, final_hidden, mark_ready, padded_cols, pipeline_backward, pipeline_chunks,
                          pipeline_forward, pipeline_join, pipeline_ok, pipeline_streams, run_recurrence, stack_layers)
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
@@ -61,50 +62,53 @@ def _gru_shadows(weights, ndir: int, H: int, I: int, cdt, device):
     the folded projection bias.  Cached on the first weight and rebuilt only
     when a parameter's version counter or storage changes (an optimizer step),
     like the large LSTM's shadows (ops/lstm_large.py:_shadow_cat)."""
-    ver = tuple((w._version, w.data_ptr()) if w is not None else None for w in weights[:4 * ndir])
-    key = ("gru", cdt, ndir, H, I)
-    cache = getattr(weights[0], "_pdrnn_shadow", None)
-    if cache is None:
-        cache = {}
-        weights[0]._pdrnn_shadow = cache
-    ent = cache.get(key)
-    if ent is not None and ent[0] == ver:
-        return ent[1]
-    if ent is None:
+    masters = list(weights[:4 * ndir])
+    box = []
+
+    def alloc():
         # buffers allocated once: the zero blocks stay zero, a rebuild after an
-        # optimizer step only copies (and converts) the parameters into them --
-        # strided copies straight into the gate-interleaved / transposed
-        # layouts, no concatenation
+        # optimizer step only converts the parameters into them
         z = dict(device=device, dtype=cdt)
-        out = ([torch.empty(3 * H, I, **z) for _ in range(ndir)], torch.zeros(ndir * 4 * H, I, **z),
-               [torch.zeros(4 * H, H, **z) for _ in range(ndir)], [torch.zeros(4 * H, H, **z) for _ in range(ndir)],
-               [torch.zeros(H, 4 * H, **z) for _ in range(ndir)],
-               torch.zeros(ndir * 4 * H, device=device, dtype=torch.float32))
-    else:
-        out = ent[1]
-    wih, wih4_all, whh4, whh_p, wt, b4_all = out
-    with torch.no_grad():
+        box.append(([torch.empty(3 * H, I, **z) for _ in range(ndir)], torch.zeros(ndir * 4 * H, I, **z),
+                    [torch.zeros(4 * H, H, **z) for _ in range(ndir)], [torch.zeros(4 * H, H, **z) for _ in range(ndir)],
+                    [torch.zeros(H, 4 * H, **z) for _ in range(ndir)],
+                    torch.zeros(ndir * 4 * H, device=device, dtype=torch.float32)))
+        return box[0]
+
+    def build(*ms):
+        # every job reads a master, never another output of the same launch
+        wih, wih4_all, whh4, whh_p, wt, b4_all = box[0]
+        jobs = []
         for d in range(ndir):
-            w_ih, w_hh, b_ih, b_hh = (w.detach() if w is not None else None for w in weights[4 * d:4 * d + 4])
-            wih[d].copy_(w_ih)
+            w_ih, w_hh, b_ih, b_hh = ms[4 * d:4 * d + 4]
+            wh = w_hh.view(3, H, H)
+            jobs.append(_sh.job(wih[d], w_ih))
             # projection stack [r | z | n_x | 0], gate-interleaved: row 4u + q
-            wih4_all[d * 4 * H:(d + 1) * 4 * H].view(H, 4, I)[:, :3].copy_(w_ih.view(3, H, I).transpose(0, 1))
+            jobs.append(_sh.job(wih4_all[d * 4 * H:(d + 1) * 4 * H].view(H, 4, I)[:, :3],
+                                w_ih.view(3, H, I).transpose(0, 1)))
             # recurrent stack [r | z | 0 | n_h] (gate-blocked), its interleaved
             # form and its transpose
-            whh4[d][:2 * H].copy_(w_hh[:2 * H])
-            whh4[d][3 * H:].copy_(w_hh[2 * H:])
-            whh_p[d].view(H, 4, H).copy_(whh4[d].view(4, H, H).transpose(0, 1))
-            wt[d].copy_(whh4[d].t())
+            jobs.append(_sh.job(whh4[d][:2 * H], w_hh[:2 * H]))
+            jobs.append(_sh.job(whh4[d][3 * H:], w_hh[2 * H:]))
+            jobs.append(_sh.job(whh_p[d].view(H, 4, H)[:, :2], wh[:2].transpose(0, 1)))
+            jobs.append(_sh.job(whh_p[d].view(H, 4, H)[:, 3], wh[2]))
+            jobs.append(_sh.job(wt[d][:, :2 * H], w_hh[:2 * H].t()))
+            jobs.append(_sh.job(wt[d][:, 3 * H:], w_hh[2 * H:].t()))
             # folded bias [b_ir + b_hr | b_iz + b_hz | b_in | b_hn], interleaved
             b = b4_all[d * 4 * H:(d + 1) * 4 * H].view(H, 4)
-            b.zero_()
-            if b_ih is not None:
-                b[:, :3].add_(b_ih.view(3, H).t())
-            if b_hh is not None:
-                b[:, :2].add_(b_hh[:2 * H].view(2, H).t())
-                b[:, 3].add_(b_hh[2 * H:])
-    cache[key] = (ver, out)
-    return out
+            bi = b_ih.view(3, H).t() if b_ih is not None else None
+            bh = b_hh.view(3, H).t() if b_hh is not None else None
+            if bi is not None and bh is not None:
+                jobs.append(_sh.job(b[:, :2], bi[:, :2], bh[:, :2]))
+            elif bi is not None or bh is not None:
+                jobs.append(_sh.job(b[:, :2], (bi if bi is not None else bh)[:, :2]))
+            if bi is not None:
+                jobs.append(_sh.job(b[:, 2], bi[:, 2]))
+            if bh is not None:
+                jobs.append(_sh.job(b[:, 3], bh[:, 2]))
+        return jobs
+
+    return _sh.get(weights[0], ("gru", cdt, ndir, H, I), masters, alloc, build)
 
 
 class _LargeGRULayer(torch.autograd.Function):

@@ -31,6 +31,7 @@ from torch import Tensor
 from .. import _ext
 from ..utils.tune import tune, tune_int
 from . import gradsink
+from . import shadow as _sh
 from .gemm import col_sum, gemm_f32, linear16, mm_kk, mm_nk16
 
 
@@ -91,53 +92,42 @@ def _addmm_f32_(c: Tensor, a: Tensor, b: Tensor) -> Tensor:
 
 
 def shadow(w: Tensor, kind: str, cdt: torch.dtype, hidden: int) -> Tensor:
-    """Compute-dtype copy (16-bit, or fp32 for the fp32 path) of an fp32 master weight in the layout a kernel reads,
-    cached on the parameter and rebuilt only when the master changed: its
-    version counter moves on every in-place update (FusedAdam's native step
-    bumps it explicitly).  Replaces the per-forward casts / interleaves /
-    transposes (a cast, an interleave copy and a second cast for the backward
-    per weight per step before).
+    """Compute-dtype copy of an fp32 master weight in the layout a kernel reads.
+
+    The copy is 16-bit, or fp32 on the fp32 path. It is cached on the parameter
+    and rebuilt only when the master changed: the version counter moves on every
+    in-place update, and FusedAdam's native step bumps it explicitly. After an
+    optimizer step, the first stale lookup rebuilds every stale shadow of the
+    device in one pack launch (ops/shadow.py, kernels/shadow_pack.hip).
 
     kind: "i" gate-interleaved rows (forward step GEMM / input projection),
           "p" stored layout (dX GEMM), "t" transposed [I, 4H] (BPTT step GEMM)."""
-    key = (kind, cdt)
-    ver = (w._version, w.data_ptr())
-    cache = getattr(w, "_pdrnn_shadow", None)
-    if cache is None:
-        cache = {}
-        w._pdrnn_shadow = cache
-    ent = cache.get(key)
-    if ent is not None and ent[0] == ver:
-        return ent[1]
-    with torch.no_grad():
-        src = w.detach()
-        if kind == "p" and src.dtype == cdt:
-            t = src  # the master itself
-        else:
-            # rebuilt into the previous buffer (one converting strided copy)
-            if ent is not None and ent[1] is not src:
-                t = ent[1]
-            else:
-                rows, cols = src.shape
-                t = torch.empty((cols, rows) if kind == "t" else (rows, cols), device=src.device, dtype=cdt)
-            if kind == "i":
-                _interleave_into(t, src, hidden)
-            elif kind == "p":
-                t.copy_(src)
-            elif kind == "t":
-                t.copy_(src.t())
-            else:
-                raise ValueError(kind)
-    cache[key] = (ver, t)
-    return t
+    if kind == "p" and w.dtype == cdt:
+        return w.detach()  # the master itself
+    if kind not in ("i", "p", "t"):
+        raise ValueError(kind)
+    rows, cols = w.shape
+    box = []  # the output buffer, for the builder (which must not hold the master)
+
+    def alloc():
+        box.append(torch.empty((cols, rows) if kind == "t" else (rows, cols), device=w.device, dtype=cdt))
+        return box[0]
+
+    def build(src):
+        t = box[0]
+        if kind == "i":
+            return [_interleave_job(t, src, hidden)]
+        if kind == "p":
+            return [_sh.job(t, src)]
+        return [_sh.job(t, src.t())]
+
+    return _sh.get(w, (kind, cdt), [w], alloc, build)
 
 
-def _interleave_into(dst: Tensor, src: Tensor, hidden: int) -> Tensor:
-    """dst[4u + q] = src[q*H + u] (gate-blocked -> gate-interleaved rows), one
-    converting strided copy."""
+def _interleave_job(dst: Tensor, src: Tensor, hidden: int):
+    """dst[4u + q] = src[q*H + u]: gate-blocked -> gate-interleaved rows."""
     k = src.shape[1]
-    dst.view(hidden, 4, k).copy_(src.view(4, hidden, k).transpose(0, 1))
-    return dst
+    return _sh.job(dst.view(hidden, 4, k), src.view(4, hidden, k).transpose(0, 1))
 
 
 def _shadow_cat(ws: List[Tensor], cdt: torch.dtype, hidden: int) -> Tensor:
@@ -145,22 +135,19 @@ def _shadow_cat(ws: List[Tensor], cdt: torch.dtype, hidden: int) -> Tensor:
     input-projection GEMM for both), cached on the first weight."""
     if len(ws) == 1:
         return shadow(ws[0], "i", cdt, hidden)
-    key = ("icat", cdt, tuple(id(w) for w in ws))
-    ver = tuple((w._version, w.data_ptr()) for w in ws)
-    cache = getattr(ws[0], "_pdrnn_shadow", None)
-    if cache is None:
-        cache = {}
-        ws[0]._pdrnn_shadow = cache
-    ent = cache.get(key)
-    if ent is not None and ent[0] == ver:
-        return ent[1]
     n4 = 4 * hidden
-    with torch.no_grad():
-        t = ent[1] if ent is not None else torch.empty(len(ws) * n4, ws[0].shape[1], device=ws[0].device, dtype=cdt)
-        for d, w in enumerate(ws):
-            _interleave_into(t[d * n4:(d + 1) * n4], w.detach(), hidden)
-    cache[key] = (ver, t)
-    return t
+    key = ("icat", cdt, tuple(id(w) for w in ws))
+    box = []
+
+    def alloc():
+        box.append(torch.empty(len(ws) * n4, ws[0].shape[1], device=ws[0].device, dtype=cdt))
+        return box[0]
+
+    def build(*srcs):
+        t = box[0]
+        return [_interleave_job(t[d * n4:(d + 1) * n4], src, hidden) for d, src in enumerate(srcs)]
+
+    return _sh.get(ws[0], key, list(ws), alloc, build)
 
 
 def _bias_cat(weights, ndir: int, hidden: int, device) -> Tensor:
@@ -168,30 +155,27 @@ def _bias_cat(weights, ndir: int, hidden: int, device) -> Tensor:
     projection GEMM's fp32 epilogue bias), cached like the shadow weights and
     rebuilt only after the biases change."""
     bs = [weights[4 * d + k] for d in range(ndir) for k in (2, 3)]
-    anchor = weights[0]
-    ver = tuple((b._version, b.data_ptr()) if b is not None else None for b in bs)
-    cache = getattr(anchor, "_pdrnn_shadow", None)
-    if cache is None:
-        cache = {}
-        anchor._pdrnn_shadow = cache
-    key = ("bias", ndir, hidden)
-    ent = cache.get(key)
-    if ent is not None and ent[0] == ver:
-        return ent[1]
     n4 = 4 * hidden
-    with torch.no_grad():
-        t = ent[1] if ent is not None else torch.empty(ndir * n4, device=device, dtype=torch.float32)
+    box = []
+
+    def alloc():
+        box.append(torch.zeros(ndir * n4, device=device, dtype=torch.float32))
+        return box[0]
+
+    def build(*srcs):
+        t = box[0]
+        jobs = []
         for d in range(ndir):
             b = t[d * n4:(d + 1) * n4].view(hidden, 4)  # interleaved: [u][q] = row q*H + u
-            srcs = [src.detach().view(4, hidden).t() for src in bs[2 * d:2 * d + 2] if src is not None]
-            if len(srcs) == 2:  # one launch: the sum written interleaved
-                torch.add(srcs[0], srcs[1], out=b)
-            elif srcs:
-                b.copy_(srcs[0])
-            else:
-                b.zero_()
-    cache[key] = (ver, t)
-    return t
+            pair = [src.view(4, hidden).t() for src in srcs[2 * d:2 * d + 2] if src is not None]
+            if len(pair) == 2:
+                jobs.append(_sh.job(b, pair[0], pair[1]))
+            elif pair:
+                jobs.append(_sh.job(b, pair[0]))
+            # no bias at all: the buffer stays zero
+        return jobs
+
+    return _sh.get(weights[0], ("bias", ndir, hidden), bs, alloc, build)
 
 
 # ---------------------------------------------------------------------------
@@ -271,6 +255,34 @@ def final_hidden(hseq: Tensor, last: Sequence[int], H: int) -> Tensor:
     return hn
 
 
+class _StackStates(torch.autograd.Function):
+    """Per-layer final h and c ([ndir, B, H] each) stacked into nn.LSTM's
+    [layers*ndir, B, H] pair by one pack launch (ops/shadow.py) instead of a
+    slice copy per layer and state; the backward hands each layer its slices."""
+
+    @staticmethod
+    def forward(ctx, L, *states):
+        ctx.set_materialize_grads(False)
+        outs, jobs, ns = [], [], []
+        for group in (states[:L], states[L:]):
+            n = group[0].shape[0]
+            out = group[0].new_empty(n * L, *group[0].shape[1:])
+            jobs += [_sh.job(out[l * n:(l + 1) * n], s) for l, s in enumerate(group)]
+            outs.append(out)
+            ns.append(n)
+        _sh.pack(jobs, states[0].device)
+        ctx.L, ctx.ns = L, ns
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, dh, dc):
+        L = ctx.L
+        grads = []
+        for g, n in zip((dh, dc), ctx.ns):
+            grads += [g[l * n:(l + 1) * n] if g is not None else None for l in range(L)]
+        return (None, *grads)
+
+
 def stack_layers(states: List[Tensor]) -> Tensor:
     """Per-layer [ndir, B, H] states -> [layers*ndir, B, H] (slice copies,
     autograd-tracked; a single layer is returned as is)."""
@@ -312,10 +324,12 @@ class _LargeLSTMLayer(torch.autograd.Function):
         rev_mask = 2 if ndir == 2 else 0
         hseq, cseq, acts = mod.lstm_large_fwd(xp, whh_p, h0c, c0c, H, rev_mask, tile, 0)
         last = [T - 1, 0][:ndir]
-        hn = final_hidden(hseq, last, H)
+        # final h (out of hseq) and c (fp32 cseq -> compute dtype) of every
+        # direction: one pack launch instead of a copy each
+        hn = hseq.new_empty(ndir, B, H)
         cn = cseq.new_empty(ndir, B, H, dtype=cdt)
-        for d in range(ndir):
-            cn[d].copy_(cseq[d, last[d]])
+        _sh.pack([_sh.job(hn[d], hseq[last[d], :, d * H:(d + 1) * H]) for d in range(ndir)] +
+                 [_sh.job(cn[d], cseq[d, last[d]]) for d in range(ndir)], x.device)
         # backward works in torch's gate-blocked order: W_ih as stored (dX GEMM),
         # W_hh transposed (BPTT step GEMM), both 16-bit shadows
         ctx.save_for_backward(x, hseq, cseq, acts, h0c, c0c, *[shadow(w, "p", cdt, H) for w in w_ih],
@@ -738,4 +752,7 @@ def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optio
         if dropout > 0 and training and l < num_layers - 1:
             seq = torch.nn.functional.dropout(seq, dropout, True)
     out = seq.transpose(0, 1) if batch_first else seq
-    return out, stack_layers(hns), stack_layers(cns)
+    if num_layers == 1:
+        return out, hns[0], cns[0]
+    hn, cn = _StackStates.apply(num_layers, *hns, *cns)
+    return out, hn, cn

@@ -30,8 +30,9 @@ class _FusedXent(torch.autograd.Function):
     def backward(ctx, gloss, _gstats):
         dlogits, stats = ctx.saved_tensors
         mod = _ext.native(dlogits.device)
-        g = mod.xent_bwd(dlogits, gloss.reshape(1), stats)
-        if ctx.in_dtype != torch.float32:
+        od = ctx.in_dtype if ctx.in_dtype in (torch.bfloat16, torch.float16) else torch.float32
+        g = mod.xent_bwd(dlogits, gloss.reshape(1), stats, od)  # 16-bit logits: 16-bit gradient, no cast
+        if g.dtype != ctx.in_dtype:
             g = g.to(ctx.in_dtype)
         return g, None, None
 

@@ -13,7 +13,7 @@ from __future__ import annotations
 import logging
 import math
 import time
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -81,16 +81,33 @@ class LMTrainer:
             norm = torch.linalg.vector_norm(g)
             g.mul_(torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0))
 
+    @staticmethod
+    def _time_major(inp: Tensor, tgt: Tensor) -> Tuple[Tensor, Tensor]:
+        """Sequence-major contiguous [T, B] copies of the [B, T] input and
+        target windows, which the embedding gather and the loss read.  For the
+        overlapping windows of one stream (target = input shifted by one,
+        data/charlm.py segments) that is ONE copy of the [B, T + 1] window
+        instead of a transpose copy per consumer."""
+        B, T = inp.shape
+        if (tgt.shape == inp.shape and tgt.dtype == inp.dtype and tgt.device == inp.device and
+                tgt.stride() == inp.stride() and inp.untyped_storage().data_ptr() == tgt.untyped_storage().data_ptr()
+                and tgt.storage_offset() == inp.storage_offset() + inp.stride(1)):
+            win = inp.as_strided((B, T + 1), inp.stride(), inp.storage_offset())
+            both = win.t().contiguous()  # [T + 1, B]
+            return both[:T], both[1:]
+        return inp.t().contiguous(), tgt.t().contiguous()
+
     def _fwd_bwd(self, inp: Tensor, tgt: Tensor) -> Tensor:
         from ..ops import gradsink
+        inp_tb, tgt_tb = self._time_major(inp, tgt)
         self.optimizer.zero_grad()
         # one process: the in-tree Functions add their weight gradients into
         # the flat gradient views themselves (ops/gradsink.py: no per-parameter
         # autograd add launches); the DDP reducer keeps the autograd path
         with gradsink.direct_grads(self.direct_grads and self.model is self.inner and self.device.type == "cuda"):
             with trace_range("pdrnn.forward"):
-                logits = self.model(inp, carry=True)                               # [T, B, V]
-                loss = cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt.t().reshape(-1))
+                logits = self.model(inp_tb.t(), carry=True)                        # [T, B, V]
+                loss = cross_entropy(logits.reshape(-1, logits.shape[-1]), tgt_tb.reshape(-1))
             with trace_range("pdrnn.backward"):
                 loss.backward()
         return loss

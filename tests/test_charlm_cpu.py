@@ -129,3 +129,20 @@ def test_gemm_helpers_accumulate_into_cpu():
     col_sum(x, accumulate_into=[o1, o2])
     torch.testing.assert_close(o1, r1)
     torch.testing.assert_close(o2, r2)
+
+
+def test_time_major_tokens_one_copy_for_shifted_windows():
+    """LMTrainer._time_major: the overlapping (input, target) windows of one
+    stream become sequence-major [T, B] tensors out of ONE [T + 1, B] copy;
+    unrelated windows fall back to a transpose copy each."""
+    from pytorch_distributed_rnn_amd.data.charlm import CharCorpus
+    from pytorch_distributed_rnn_amd.train.lm import LMTrainer
+    streams = torch.randint(0, 256, (4, 50))
+    for inp, tgt in CharCorpus.segments(streams, 7, 3):
+        a, b = LMTrainer._time_major(inp, tgt)
+        assert torch.equal(a, inp.t()) and torch.equal(b, tgt.t())
+        assert a.is_contiguous() and b.is_contiguous()
+        assert a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()  # one buffer
+    x, y = torch.randint(0, 9, (3, 5)), torch.randint(0, 9, (3, 5))
+    a, b = LMTrainer._time_major(x, y)
+    assert torch.equal(a, x.t()) and torch.equal(b, y.t())
