@@ -591,8 +591,11 @@ class _PipelinedLSTMStack(torch.autograd.Function):
 
         pipeline_forward(rec, chunks, project, recur)
         pipeline_join(rec)
-        hn = torch.stack([hq[T - 1] for hq in hseq])  # (one launch each instead of L copies)
-        cn = torch.stack([cq[T - 1] for cq in cseq])
+        # final h and c of every layer: one pack launch (ops/shadow.py)
+        hn = hseq[0].new_empty(L, *hseq[0].shape[1:])
+        cn = cseq[0].new_empty(L, *cseq[0].shape[1:])
+        _sh.pack([_sh.job(hn[l], hq[T - 1]) for l, hq in enumerate(hseq)] +
+                 [_sh.job(cn[l], cq[T - 1]) for l, cq in enumerate(cseq)], x.device)
         ctx.save_for_backward(x, *hseq, *cseq, *acts, *[shadow(w[0], "p", f32, H) for w in lw],
                               *[shadow(w[1], "t", f32, H) for w in lw])
         ctx.states = (h0s, c0s)
