@@ -1239,11 +1239,11 @@ std::vector<Tensor> lstm_large_bwd(const optional<Tensor>& dout, const optional<
     a.ws = ws.data_ptr<float>();
   }
   hipStream_t st = cur_stream();
-  HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, ndir, dt, st));
   if (tile < 0 && rows_f32_on() && pdrnn_lstm_rows_f32_supported((int)H, dt)) {
-    HIP_LAUNCH_CHECK(pdrnn_lstm_rows_f32(&a, ndir, 1, st));
+    HIP_LAUNCH_CHECK(pdrnn_lstm_rows_f32(&a, ndir, 1, st));  // (the first step's cell backward included)
     return {dgates, dh0, dc0};
   }
+  HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, ndir, dt, st));
   const int pr = large_persist(a, ndir, true, dt, tile, o32, st);
   if (pr != kPersistOk) {
     // a failed launch may have advanced the dc carry: start the layer over
@@ -1349,9 +1349,7 @@ void lstm_rows_bwd_range(const optional<Tensor>& dout, const optional<Tensor>& d
   d.dc_carry = carry.data_ptr<float>();
   d.dh0 = dh0.data_ptr<float>();
   d.dc0 = dc0.data_ptr<float>();
-  hipStream_t st = cur_stream();
-  HIP_LAUNCH_CHECK(pdrnn_lstm_large_bwd_first(&a, 1, 2, st));
-  HIP_LAUNCH_CHECK(pdrnn_lstm_rows_f32(&a, 1, 1, st));
+  HIP_LAUNCH_CHECK(pdrnn_lstm_rows_f32(&a, 1, 1, cur_stream()));  // (the first step's cell backward included)
 }
 
 // Time-batched GEMM (kernels/gemm.hip).  A: a_kmajor ? [K, M] : [M, K];

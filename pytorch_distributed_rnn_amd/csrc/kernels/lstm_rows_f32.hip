@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(RT) lstm_rows_f32_bwd_kernel(PdrnnLstmLargeSte
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     brow[i] = min(r0 + 4 * fq + i, B - 1);
-    carry[i] = d.dc_carry[(int64_t)brow[i] * RH + u];
+    carry[i] = (CELL == 0 && d.dcn) ? d.dcn[(int64_t)brow[i] * RH + u] : 0.f;  // the dc_n flowing in
   }
   // next cell-backward operands: dout, the 4 saved gates, c_tn, c_{tn-1}
   float nd[4], ncur[4], nsp[4];
@@ -205,14 +205,47 @@ __global__ void __launch_bounds__(RT) lstm_rows_f32_bwd_kernel(PdrnnLstmLargeSte
       nsp[i] = has_prev ? d.cseq[(int64_t)tpp * B * RH + bu] : (d.c0 ? d.c0[bu] : 0.f);
     }
   };
+  // the cell backward of step tn for pair i: dgates_tn (gate-blocked) into
+  // LDS (the next step's A operand) and global, the dc carry advanced
+  auto cell_step = [&](int i, float dh, float dd, float4 act, float cc, float sp, float* dn, int tn) {
+    const int row = 4 * fq + i;
+    const int b = r0 + row;
+    dh += dd;
+    const float a0 = act.x, a1 = act.y, a2 = act.z, a3 = act.w;
+    float g0, g1, g2, g3;
+    if constexpr (CELL == 0) {
+      const float tc = r_tanh(cc);
+      const float dc = fmaf(dh * a3, 1.f - tc * tc, carry[i]);
+      g0 = dc * a2 * a0 * (1.f - a0);
+      g1 = dc * sp * a1 * (1.f - a1);
+      g2 = dc * a0 * (1.f - a2 * a2);
+      g3 = dh * tc * a3 * (1.f - a3);
+      carry[i] = dc * a1;
+    } else {
+      const float dpn = dh * (1.f - a1) * (1.f - a2 * a2);
+      g0 = dpn * a3 * a0 * (1.f - a0);
+      g1 = dh * (sp - a2) * a1 * (1.f - a1);
+      g2 = dpn;
+      g3 = dpn * a0;
+      carry[i] = dh * a1;
+    }
+    float* dr = dn + row * RLDG + u;
+    dr[0] = g0; dr[RH] = g1; dr[2 * RH] = g2; dr[3 * RH] = g3;
+    if (b < B) {
+      float* o = static_cast<float*>(d.dgates) + (int64_t)tn * B * 4 * RH + (int64_t)b * 4 * RH + u;
+      o[0] = g0; o[RH] = g1; o[2 * RH] = g2; o[3 * RH] = g3;
+    }
+  };
+  // The first processed step (the layer's last forward step) has no
+  // recurrent product: dh = dh_n.  Done here instead of a separate
+  // lstm_large_bwd_first launch before this one (a dispatch per layer and
+  // pipeline chunk on the fp32 hidden-128 model, profiles/r6/glue).
   const int t0 = rev ? 0 : T - 1, tn0 = rev ? t0 + 1 : t0 - 1;
+  load_ops(t0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    cell_step(i, d.dhn ? d.dhn[(int64_t)brow[i] * RH + u] : 0.f, nd[i], nact[i], ncur[i], nsp[i], &dl[0][0][0], t0);
   if (rev ? tn0 < T : tn0 >= 0) load_ops(tn0);
-  // dgates of the first processed step (lstm_large_bwd_first_kernel)
-  for (int e = threadIdx.x; e < 16 * 4 * RH; e += RT) {
-    const int row = e / (4 * RH), k = e - row * 4 * RH;
-    const int b = min(r0 + row, B - 1);
-    dl[0][row][k] = static_cast<const float*>(d.dgates)[(int64_t)t0 * B * 4 * RH + (int64_t)b * 4 * RH + k];
-  }
   __syncthreads();
 
   int cur = 0;
@@ -249,31 +282,7 @@ __global__ void __launch_bounds__(RT) lstm_rows_f32_bwd_kernel(PdrnnLstmLargeSte
         }
         continue;
       }
-      dh += od[i];
-      const float a0 = oact[i].x, a1 = oact[i].y, a2 = oact[i].z, a3 = oact[i].w;
-      float g0, g1, g2, g3;
-      if constexpr (CELL == 0) {
-        const float tc = r_tanh(ocur[i]);
-        const float dc = fmaf(dh * a3, 1.f - tc * tc, carry[i]);
-        g0 = dc * a2 * a0 * (1.f - a0);
-        g1 = dc * osp[i] * a1 * (1.f - a1);
-        g2 = dc * a0 * (1.f - a2 * a2);
-        g3 = dh * tc * a3 * (1.f - a3);
-        carry[i] = dc * a1;
-      } else {
-        const float dpn = dh * (1.f - a1) * (1.f - a2 * a2);
-        g0 = dpn * a3 * a0 * (1.f - a0);
-        g1 = dh * (osp[i] - a2) * a1 * (1.f - a1);
-        g2 = dpn;
-        g3 = dpn * a0;
-        carry[i] = dh * a1;
-      }
-      float* dr = dn + row * RLDG + u;
-      dr[0] = g0; dr[RH] = g1; dr[2 * RH] = g2; dr[3 * RH] = g3;
-      if (b < B) {
-        float* o = static_cast<float*>(d.dgates) + (int64_t)tn * B * 4 * RH + (int64_t)b * 4 * RH + u;
-        o[0] = g0; o[RH] = g1; o[2 * RH] = g2; o[3 * RH] = g3;
-      }
+      cell_step(i, dh, od[i], oact[i], ocur[i], osp[i], dn, tn);
     }
     lds_barrier();  // dgates_tn of every wave in LDS before the next step's reads
     cur ^= 1;
@@ -288,8 +297,9 @@ extern "C" {
 int pdrnn_lstm_rows_f32_supported(int H, int dtype) { return dtype == 2 && H == pdrnn::RH; }
 
 // One layer pass (ndir directions) of the row-owning fp32 recurrence.  The
-// backward expects dgates of the first processed step and the dc carry from
-// pdrnn_lstm_large_bwd_first (like the persistent backward).
+// backward runs the first processed step's cell backward itself (from dhn /
+// dcn; no pdrnn_lstm_large_bwd_first launch before it, unlike the persistent
+// backward).
 hipError_t pdrnn_lstm_rows_f32(const PdrnnLstmLargeStepArgs* a, int ndir, int backward, hipStream_t stream) {
   if (a->H != pdrnn::RH || ndir < 1 || ndir > 2 || a->B < 1 || a->T < 1) return hipErrorInvalidValue;
   if (a->cell != 0 && a->cell != 1) return hipErrorInvalidValue;
