@@ -647,9 +647,12 @@ class _PipelinedLSTMStack(torch.autograd.Function):
                                     cseq[l], acts[l], c0s[l], dgates[l], dhb[l], dcb[l], carry[l], t0, t1, 0)
 
         def finish(l):  # the layer's recurrence is done: its weight gradients, on its stream
-            _chunk_weight_grads(dwih[l], dwhh[l], db[l], dgates[l], hseq[l], h0s[l], ins[l], 0, T, not direct[l],
-                                db_first=True)
+            # (direct mode: the row sums are added into the bias gradients as
+            # they come out of the dW_ih pass, no copy into db first)
+            rs = _chunk_weight_grads(dwih[l], dwhh[l], None if direct[l] else db[l], dgates[l], hseq[l], h0s[l],
+                                     ins[l], 0, T, not direct[l], db_first=True)
             if direct[l]:
+                db[l] = rs
                 bi, bh = sinks[l][2], sinks[l][3]
                 # (same storage too: two separately allocated gradients can sit
                 # side by side in the caching allocator -- ADVICE r5)
@@ -687,13 +690,29 @@ def padded_cols(x2: Tensor, mult: int = 32) -> Tensor:
     loads do not overlap its MFMAs; padded, every tile is whole and aligned
     (layer 0's dW_ih 214 -> ~90 us at the motion batch, profiles/r4/gemm_probe/)."""
     n = x2.shape[1]
-    out = x2.new_zeros(x2.shape[0], -(-n // mult) * mult)
+    shape = (x2.shape[0], -(-n // mult) * mult)
+    # the padded buffer is kept per (shape, dtype, device, stream): its pad
+    # columns are zeroed once, a step only copies the data columns (one
+    # dispatch, not a fill and a copy); reuse is stream-ordered
+    if x2.is_cuda and torch.cuda.is_current_stream_capturing():  # (graph-pool memory: never cached)
+        out = x2.new_zeros(shape)
+        out[:, :n].copy_(x2)
+        return out
+    key = (shape, x2.dtype, x2.device, torch.cuda.current_stream(x2.device).cuda_stream if x2.is_cuda else 0)
+    out = _PADDED.get(key)
+    if out is None:
+        if len(_PADDED) >= 8:
+            _PADDED.clear()
+        out = _PADDED[key] = x2.new_zeros(shape)
     out[:, :n].copy_(x2)
     return out
 
 
-def _chunk_weight_grads(dwih: Tensor, dwhh: Tensor, db: Tensor, G3: Tensor, hd: Tensor, h0: Optional[Tensor],
-                        xin: Tensor, t0: int, t1: int, first: bool, db_first: Optional[bool] = None) -> None:
+_PADDED: dict = {}
+
+
+def _chunk_weight_grads(dwih: Tensor, dwhh: Tensor, db: Optional[Tensor], G3: Tensor, hd: Tensor, h0: Optional[Tensor],
+                        xin: Tensor, t0: int, t1: int, first: bool, db_first: Optional[bool] = None) -> Tensor:
     """Steps [t0, t1) of one unidirectional fp32 layer's dW_ih, dW_hh and db,
     written (first chunk) or accumulated into the fp32 outputs: dW_hh pairs
     dgates_t with h_{t-1} (h0 at t = 0), dW_ih dgates_t with the layer input,
@@ -715,10 +734,13 @@ def _chunk_weight_grads(dwih: Tensor, dwhh: Tensor, db: Tensor, G3: Tensor, hd: 
         dwih.copy_(c[:, :x2.shape[1]]) if first else dwih.add_(c[:, :x2.shape[1]])
     else:
         _, rs = gemm_f32(G3[t0:t1].view(-1, H4), True, x2, True, rowsum=True, out=dwih, accumulate=not first)
+    if db is None:  # the caller takes the row sums as they are
+        return rs
     if first if db_first is None else db_first:
         db.copy_(rs)
     else:
         db.add_(rs)
+    return db
 
 
 def lstm_large_forward(x: Tensor, weights: Sequence[Optional[Tensor]], h0: Optional[Tensor],
