@@ -375,6 +375,7 @@ typedef struct PdrnnPackJob {
   int n[3];
   int dtype;   // destination: 0 bf16, 1 fp16, 2 fp32
   int sdtype;  // sources: same codes
+  int vec;     // set by pdrnn_shadow_pack: the 4-wide path applies
   int64_t tile0;
 } PdrnnPackJob;
 typedef struct PdrnnPackBatch {

@@ -45,6 +45,47 @@ __global__ void __launch_bounds__(PK_THREADS) shadow_pack_kernel(PdrnnPackBatch 
   const int t1 = (int)((l / t2n) % t1n);
   const int64_t i0 = l / ((int64_t)t2n * t1n);
   const int a1 = t1 * PK_T, a2 = t2 * PK_T;
+  if (p.vec) {
+    // both sides unit-stride along i2, 4-element aligned (interleave / cast
+    // jobs: most of the bytes): 4 elements a thread straight through, no LDS
+    for (int e = threadIdx.x; e < PK_T * PK_T / 4; e += PK_THREADS) {
+      const int r = e / (PK_T / 4), c = (e % (PK_T / 4)) * 4;
+      if (a1 + r >= p.n[1] || a2 + c >= p.n[2]) continue;
+      const int64_t so = i0 * p.ss[0] + (int64_t)(a1 + r) * p.ss[1] + (a2 + c);
+      const int64_t dof = i0 * p.ds[0] + (int64_t)(a1 + r) * p.ds[1] + (a2 + c);
+      float v[4];
+      auto ld4 = [&](const void* base, float* o) {
+        if (p.sdtype == 2) {
+          const float4 f = *reinterpret_cast<const float4*>(static_cast<const float*>(base) + so);
+          o[0] = f.x; o[1] = f.y; o[2] = f.z; o[3] = f.w;
+        } else {
+          const uint2 h = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(base) + so);
+          const uint16_t hs[4] = {(uint16_t)h.x, (uint16_t)(h.x >> 16), (uint16_t)h.y, (uint16_t)(h.y >> 16)};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            o[q] = p.sdtype == 1 ? (float)__builtin_bit_cast(_Float16, hs[q]) : __uint_as_float((uint32_t)hs[q] << 16);
+        }
+      };
+      ld4(p.src, v);
+      if (p.src2) {
+        float w2[4];
+        ld4(p.src2, w2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += w2[q];
+      }
+      if (p.dtype == 2) {
+        *reinterpret_cast<float4*>(static_cast<float*>(p.dst) + dof) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint16_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = p.dtype == 1 ? __builtin_bit_cast(uint16_t, (_Float16)v[q]) : pk_bf16(v[q]);
+        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.dst) + dof) =
+            make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
+      }
+    }
+    return;
+  }
   // read along the source's unit-stride dimension
   const bool s_in2 = p.ss[2] == 1 || p.ss[1] != 1;
   auto ld = [&](const void* base, int64_t o) -> float {
@@ -97,6 +138,13 @@ hipError_t pdrnn_shadow_pack(PdrnnPackBatch* b, hipStream_t stream) {
     if (!p.src || !p.dst || p.dtype < 0 || p.dtype > 2 || p.sdtype < 0 || p.sdtype > 2) return hipErrorInvalidValue;
     p.tile0 = tiles;
     tiles += pdrnn_shadow_pack_tiles(&p);
+    // the vector path: unit stride along i2 on both sides, every row start and
+    // the extent a multiple of 4 elements, 16 / 8-byte aligned bases
+    const int ses = p.sdtype == 2 ? 4 : 2, des = p.dtype == 2 ? 4 : 2;
+    const uintptr_t al = (uintptr_t)p.src | (uintptr_t)p.src2 | 0;
+    p.vec = p.ss[2] == 1 && p.ds[2] == 1 && p.n[2] % 4 == 0 && p.ss[1] % 4 == 0 && p.ds[1] % 4 == 0 &&
+            p.ss[0] % 4 == 0 && p.ds[0] % 4 == 0 && (al % (4 * ses)) == 0 &&
+            ((uintptr_t)p.dst % (4 * des)) == 0;
   }
   if (tiles == 0) return hipSuccess;
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;

@@ -114,3 +114,22 @@ def test_pack_16bit_sources_and_stacked_states():
     assert x.grad is not None and torch.isfinite(x.grad.float()).all() and x.grad.float().abs().sum() > 0
     for p in m.parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all()
+
+
+def test_pack_vector_path_guards_alignment():
+    """The 4-wide path (unit stride along i2 on both sides) and its guards:
+    aligned slices take it, odd offsets / extents fall back to the LDS tile;
+    both exact."""
+    mod = _ext.require()
+    src = torch.randn(96, 260, device="cuda")
+    cases = [(slice(0, 256), slice(0, 256)),   # aligned: vector path
+             (slice(1, 257), slice(3, 259)),   # odd offsets on both sides
+             (slice(0, 255), slice(1, 256))]   # extent not a multiple of 4
+    for dt in (torch.bfloat16, torch.float32):
+        for ds_, ss_ in cases:
+            out = torch.zeros(96, 260, device="cuda", dtype=dt)
+            assert mod.shadow_pack([sh.job(out[:, ds_], src[:, ss_], src[:, ss_])]) == 1
+            torch.cuda.synchronize()
+            ref = torch.zeros(96, 260, device="cuda", dtype=dt)
+            ref[:, ds_] = (src[:, ss_] + src[:, ss_]).to(dt)
+            assert torch.equal(out, ref), (dt, ds_, ss_)
